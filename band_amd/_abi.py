@@ -1,0 +1,124 @@
+"""ctypes binding of the C ABI exported by band_amd/libband_hip.so.
+
+Mirrors include/band_hip_kernels.h (kernel layer, `bh_*`) and
+include/band_hip_backend.h (executor layer, `bhx_*`).  Loading fails loudly
+when the library has not been built: there is no CPU fallback on the product
+path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libband_hip.so")
+
+c_int, c_int32, c_void_p, c_size_t = ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t
+
+
+class ConvParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "k_h", "k_w",
+        "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "k_pad", "n_pad", "in_xor")] + [
+        (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
+        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift")]
+
+
+class DwConvParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "depth_multiplier",
+        "k_h", "k_w", "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "in_xor")] + [
+        (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
+        (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift")]
+
+
+class FcParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("rows", "depth", "depth_pad", "units", "in_xor")] + [
+        (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
+        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift")]
+
+
+class EltwiseParams(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("in_signed", c_int), ("shape_a", c_int * 4),
+                ("shape_b", c_int * 4), ("shape_o", c_int * 4)] + [
+        (n, c_int32) for n in ("a_off", "b_off", "o_off", "left_shift", "a_mult", "a_shift",
+                               "b_mult", "b_shift", "o_mult", "o_shift", "act_min", "act_max")] + [
+        (n, c_void_p) for n in ("a", "b", "out")]
+
+
+class PoolParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "kind", "in_signed", "batch", "in_h", "in_w", "channels", "out_h", "out_w",
+        "f_h", "f_w", "stride_h", "stride_w", "pad_h", "pad_w")] + [
+        (n, c_int32) for n in ("act_min", "act_max")] + [
+        (n, c_void_p) for n in ("input", "output")]
+
+
+# symbol -> (restype, argtypes)
+KERNEL_SYMBOLS = {
+    "bh_device_count": (c_int, [ctypes.POINTER(c_int)]),
+    "bh_set_device": (c_int, [c_int]),
+    "bh_get_device": (c_int, [ctypes.POINTER(c_int)]),
+    "bh_device_arch": (c_int, [c_int, ctypes.c_char_p, c_size_t]),
+    "bh_stream_create": (c_int, [ctypes.POINTER(c_void_p)]),
+    "bh_stream_destroy": (c_int, [c_void_p]),
+    "bh_stream_sync": (c_int, [c_void_p]),
+    "bh_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
+    "bh_free": (c_int, [c_void_p]),
+    "bh_host_alloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
+    "bh_host_free": (c_int, [c_void_p]),
+    "bh_memcpy_h2d_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bh_memcpy_d2h_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bh_memcpy_d2d_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bh_memset_async": (c_int, [c_void_p, c_int, c_size_t, c_void_p]),
+    "bh_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "bh_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),
+    "bh_capture_begin": (c_int, [c_void_p]),
+    "bh_capture_end": (c_int, [c_void_p, ctypes.POINTER(c_void_p)]),
+    "bh_graph_launch": (c_int, [c_void_p, c_void_p]),
+    "bh_graph_destroy": (c_int, [c_void_p]),
+    "bh_event_create": (c_int, [ctypes.POINTER(c_void_p)]),
+    "bh_event_destroy": (c_int, [c_void_p]),
+    "bh_event_record": (c_int, [c_void_p, c_void_p]),
+    "bh_event_sync": (c_int, [c_void_p]),
+    "bh_event_elapsed_ms": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ctypes.c_float)]),
+    "bh_pack_conv_weights": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                                     c_int32, c_int32, c_void_p, c_void_p]),
+    "bh_conv_packed_geometry": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "bh_conv2d_i8": (c_int, [ctypes.POINTER(ConvParams), c_void_p]),
+    "bh_dwconv2d_i8": (c_int, [ctypes.POINTER(DwConvParams), c_void_p]),
+    "bh_fc_i8": (c_int, [ctypes.POINTER(FcParams), c_void_p]),
+    "bh_eltwise_i8": (c_int, [ctypes.POINTER(EltwiseParams), c_void_p]),
+    "bh_pool_i8": (c_int, [ctypes.POINTER(PoolParams), c_void_p]),
+    "bh_last_error": (ctypes.c_char_p, []),
+}
+
+BACKEND_SYMBOLS = {}  # filled by backend.py
+
+_lib = None
+
+
+class BandHipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libband_hip.so; raises if it is missing (no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise BandHipError(
+            "libband_hip.so not built (%s); run __graft_entry__.build() / make -C band_amd/csrc" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in list(KERNEL_SYMBOLS.items()) + list(BACKEND_SYMBOLS.items()):
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().bh_last_error()
+        raise BandHipError("%s failed (rc=%d): %s" % (what, rc, msg.decode() if msg else ""))
+    return rc

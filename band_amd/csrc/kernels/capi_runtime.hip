@@ -1,0 +1,119 @@
+// Runtime plumbing of the thin C ABI (include/band_hip_kernels.h): devices,
+// streams, pinned host memory, async copies, stream capture into hipGraphs
+// and events.  Every function returns 0 or the hipError_t it hit, and
+// records a message retrievable with bh_last_error().
+#include <stdio.h>
+#include <string.h>
+
+#include "common.hpp"
+
+static thread_local char g_last_error[256] = "";
+
+extern "C" void bh_set_last_error(const char* msg) {
+  snprintf(g_last_error, sizeof(g_last_error), "%s", msg ? msg : "");
+}
+
+extern "C" const char* bh_last_error(void) { return g_last_error; }
+
+static int ck(hipError_t e, const char* what) {
+  if (e == hipSuccess) return 0;
+  snprintf(g_last_error, sizeof(g_last_error), "%s: %s", what, hipGetErrorString(e));
+  return (int)e;
+}
+
+int bh_check_launch(const char* what) { return ck(hipGetLastError(), what); }
+
+extern "C" int bh_device_count(int* count) {
+  if (!count) return BH_EINVAL;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    *count = 0;
+    return ck(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return 0;
+}
+
+extern "C" int bh_set_device(int ordinal) { return ck(hipSetDevice(ordinal), "hipSetDevice"); }
+extern "C" int bh_get_device(int* ordinal) { return ck(hipGetDevice(ordinal), "hipGetDevice"); }
+
+extern "C" int bh_device_arch(int ordinal, char* buf, size_t cap) {
+  if (!buf || cap == 0) return BH_EINVAL;
+  hipDeviceProp_t prop;
+  int rc = ck(hipGetDeviceProperties(&prop, ordinal), "hipGetDeviceProperties");
+  if (rc) return rc;
+  snprintf(buf, cap, "%s", prop.gcnArchName);
+  return 0;
+}
+
+extern "C" int bh_stream_create(bh_stream_t* stream) {
+  hipStream_t s = nullptr;
+  int rc = ck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+  *stream = (bh_stream_t)s;
+  return rc;
+}
+extern "C" int bh_stream_destroy(bh_stream_t s) { return ck(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy"); }
+extern "C" int bh_stream_sync(bh_stream_t s) { return ck(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); }
+
+extern "C" int bh_malloc(void** p, size_t bytes) { return ck(hipMalloc(p, bytes ? bytes : 16), "hipMalloc"); }
+extern "C" int bh_free(void* p) { return p ? ck(hipFree(p), "hipFree") : 0; }
+extern "C" int bh_host_alloc(void** p, size_t bytes) {
+  return ck(hipHostMalloc(p, bytes ? bytes : 16, hipHostMallocPortable), "hipHostMalloc");
+}
+extern "C" int bh_host_free(void* p) { return p ? ck(hipHostFree(p), "hipHostFree") : 0; }
+
+extern "C" int bh_memcpy_h2d_async(void* d, const void* s, size_t n, bh_stream_t st) {
+  return n ? ck(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, (hipStream_t)st), "hipMemcpyAsync H2D") : 0;
+}
+extern "C" int bh_memcpy_d2h_async(void* d, const void* s, size_t n, bh_stream_t st) {
+  return n ? ck(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)st), "hipMemcpyAsync D2H") : 0;
+}
+extern "C" int bh_memcpy_d2d_async(void* d, const void* s, size_t n, bh_stream_t st) {
+  return n ? ck(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)st), "hipMemcpyAsync D2D") : 0;
+}
+extern "C" int bh_memset_async(void* d, int v, size_t n, bh_stream_t st) {
+  return n ? ck(hipMemsetAsync(d, v, n, (hipStream_t)st), "hipMemsetAsync") : 0;
+}
+extern "C" int bh_memcpy_h2d(void* d, const void* s, size_t n) {
+  return n ? ck(hipMemcpy(d, s, n, hipMemcpyHostToDevice), "hipMemcpy H2D") : 0;
+}
+extern "C" int bh_memcpy_d2h(void* d, const void* s, size_t n) {
+  return n ? ck(hipMemcpy(d, s, n, hipMemcpyDeviceToHost), "hipMemcpy D2H") : 0;
+}
+
+extern "C" int bh_capture_begin(bh_stream_t s) {
+  return ck(hipStreamBeginCapture((hipStream_t)s, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+}
+extern "C" int bh_capture_end(bh_stream_t s, bh_graph_exec_t* exec) {
+  hipGraph_t g = nullptr;
+  int rc = ck(hipStreamEndCapture((hipStream_t)s, &g), "hipStreamEndCapture");
+  if (rc) return rc;
+  hipGraphExec_t ge = nullptr;
+  rc = ck(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+  (void)hipGraphDestroy(g);
+  *exec = (bh_graph_exec_t)ge;
+  return rc;
+}
+extern "C" int bh_graph_launch(bh_graph_exec_t e, bh_stream_t s) {
+  return ck(hipGraphLaunch((hipGraphExec_t)e, (hipStream_t)s), "hipGraphLaunch");
+}
+extern "C" int bh_graph_destroy(bh_graph_exec_t e) {
+  return e ? ck(hipGraphExecDestroy((hipGraphExec_t)e), "hipGraphExecDestroy") : 0;
+}
+
+extern "C" int bh_event_create(bh_event_t* ev) {
+  hipEvent_t e = nullptr;
+  int rc = ck(hipEventCreate(&e), "hipEventCreate");
+  *ev = (bh_event_t)e;
+  return rc;
+}
+extern "C" int bh_event_destroy(bh_event_t ev) { return ck(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy"); }
+extern "C" int bh_event_record(bh_event_t ev, bh_stream_t s) {
+  return ck(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord");
+}
+extern "C" int bh_event_sync(bh_event_t ev) { return ck(hipEventSynchronize((hipEvent_t)ev), "hipEventSynchronize"); }
+extern "C" int bh_event_elapsed_ms(bh_event_t a, bh_event_t b, float* ms) {
+  return ck(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+}

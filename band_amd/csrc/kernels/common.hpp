@@ -1,0 +1,66 @@
+// Device-side helpers shared by the gfx950 kernels.
+//
+// The fixed-point requantisation below is the device restatement of TFLite
+// 2.9.2's kernels/internal/common.h MultiplyByQuantizedMultiplier (double
+// rounding: SaturatingRoundingDoublingHighMul then RoundingDivideByPOT), the
+// arithmetic every int8 op on Band's hot path ends with
+// (band/backend/tfl/model_executor.cc:249-255 -> Interpreter::Invoke).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "band_hip_kernels.h"
+
+namespace bh {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+typedef int v2i __attribute__((ext_vector_type(2)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int32_t srdhm(int32_t a, int32_t b) {
+  const bool overflow = (a == b) && (a == INT32_MIN);
+  const int64_t ab = (int64_t)a * (int64_t)b;
+  const int64_t nudge = ab >= 0 ? (1ll << 30) : (1ll - (1ll << 30));
+  const int32_t hi = (int32_t)((ab + nudge) / (1ll << 31));
+  return overflow ? INT32_MAX : hi;
+}
+
+__device__ __forceinline__ int32_t rdbypot(int32_t x, int e) {
+  const int32_t mask = (int32_t)((1ll << e) - 1);
+  const int32_t rem = x & mask;
+  const int32_t thr = (mask >> 1) + (x < 0 ? 1 : 0);
+  return (x >> e) + (rem > thr ? 1 : 0);
+}
+
+// MultiplyByQuantizedMultiplier(x, m, shift): shift > 0 is a left shift.
+__device__ __forceinline__ int32_t requant(int32_t x, int32_t m, int32_t shift) {
+  const int left = shift > 0 ? shift : 0;
+  const int right = shift > 0 ? 0 : -shift;
+  return rdbypot(srdhm((int32_t)((uint32_t)x << left), m), right);
+}
+
+// MultiplyByQuantizedMultiplierSmallerThanOneExp(x, m, left_shift<=0)
+__device__ __forceinline__ int32_t requant_lt1(int32_t x, int32_t m, int32_t left_shift) {
+  return rdbypot(srdhm(x, m), -left_shift);
+}
+
+__device__ __forceinline__ int32_t clamp_i32(int32_t v, int32_t lo, int32_t hi) {
+  return v < lo ? lo : (v > hi ? hi : v);
+}
+
+// sign-extend byte b of a dword
+__device__ __forceinline__ int32_t sbyte(uint32_t w, int b) {
+  return (int32_t)(int8_t)((w >> (8 * b)) & 0xff);
+}
+
+__device__ __forceinline__ uint32_t splat_byte(int32_t v) {
+  return ((uint32_t)v & 0xffu) * 0x01010101u;
+}
+
+}  // namespace bh
+
+// thread-local last-error plumbing for the C ABI (defined in capi_runtime.hip)
+extern "C" void bh_set_last_error(const char* msg);
+int bh_check_launch(const char* what);

@@ -1,0 +1,206 @@
+/*
+ * band_hip_kernels.h — thin C ABI between the host-side HIP backend
+ * (band_amd/csrc/backend/hip/) and the hand-written gfx950 kernels.
+ *
+ * This is the "Thin C ABI (build-internal)" of SURVEY.md §8(b): plain
+ * pointers, sizes and POD parameter blocks, no C++ or torch types.  Every
+ * entry point returns 0 on success or a hipError_t value (>0), or BH_EINVAL
+ * (-1) for a parameter block that fails host-side validation.  Launch entry
+ * points are asynchronous on the given stream (nullptr = the calling
+ * thread's current-device null stream is NOT used: pass a real stream).
+ *
+ * Each op launcher stands in for one TFLite 2.9.2 builtin kernel that
+ * `tflite::Interpreter::Invoke` dispatches from the reference hot path
+ * `TfLiteModelExecutor::ExecuteSubgraph` (band/backend/tfl/model_executor.cc:249-255):
+ *   bh_conv2d_i8      <- CONV_2D            (reference_integer_ops::ConvPerChannel,
+ *                                            reference_ops::Conv uint8)
+ *   bh_dwconv2d_i8    <- DEPTHWISE_CONV_2D  (reference_integer_ops::DepthwiseConvPerChannel)
+ *   bh_fc_i8          <- FULLY_CONNECTED    (reference_integer_ops::FullyConnected)
+ *   bh_add_i8         <- ADD / SUB          (reference_integer_ops::Add, sub.cc)
+ *   bh_mul_i8         <- MUL                (reference_integer_ops::Mul)
+ *   bh_pool_i8        <- AVERAGE_POOL_2D / MAX_POOL_2D (reference_integer_ops::{Average,Max}Pool)
+ *
+ * Quantised tensors live on the device as raw bytes in their TFLite type
+ * (int8 or uint8).  Kernels work in the "int8 domain": a uint8 input is
+ * mapped to int8 by XOR 0x80 on load (x - 128), and every zero point handed
+ * to a kernel is already expressed in that domain.  Outputs are clamped to
+ * [act_min, act_max] of the OUTPUT tensor's own type and stored as bytes, so
+ * uint8 and int8 outputs are both bit-exact with TFLite.
+ */
+#ifndef BAND_HIP_KERNELS_H_
+#define BAND_HIP_KERNELS_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BH_EINVAL (-1)
+
+typedef void* bh_stream_t;
+typedef void* bh_graph_exec_t;
+typedef void* bh_event_t;
+
+/* ---- device / memory / stream (runtime plumbing) ------------------------ */
+int bh_device_count(int* count);
+int bh_set_device(int ordinal);
+int bh_get_device(int* ordinal);
+/* arch name of `ordinal` (e.g. "gfx950:sramecc+:xnack-"), NUL-terminated */
+int bh_device_arch(int ordinal, char* buf, size_t cap);
+int bh_stream_create(bh_stream_t* stream);
+int bh_stream_destroy(bh_stream_t stream);
+int bh_stream_sync(bh_stream_t stream);
+int bh_malloc(void** ptr, size_t bytes);
+int bh_free(void* ptr);
+int bh_host_alloc(void** ptr, size_t bytes); /* pinned, portable */
+int bh_host_free(void* ptr);
+int bh_memcpy_h2d_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
+int bh_memcpy_d2h_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
+int bh_memcpy_d2d_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
+int bh_memset_async(void* dst, int value, size_t bytes, bh_stream_t s);
+int bh_memcpy_h2d(void* dst, const void* src, size_t bytes);
+int bh_memcpy_d2h(void* dst, const void* src, size_t bytes);
+
+/* ---- stream capture -> hipGraph (one graph per prepared subgraph) ------- */
+int bh_capture_begin(bh_stream_t s);
+int bh_capture_end(bh_stream_t s, bh_graph_exec_t* exec);
+int bh_graph_launch(bh_graph_exec_t exec, bh_stream_t s);
+int bh_graph_destroy(bh_graph_exec_t exec);
+
+/* ---- events (timing) ---------------------------------------------------- */
+int bh_event_create(bh_event_t* ev);
+int bh_event_destroy(bh_event_t ev);
+int bh_event_record(bh_event_t ev, bh_stream_t s);
+int bh_event_sync(bh_event_t ev);
+int bh_event_elapsed_ms(bh_event_t start, bh_event_t end, float* ms);
+
+/* ---- op parameter blocks ------------------------------------------------ */
+
+/* CONV_2D.  Input NHWC [batch,in_h,in_w,in_c] bytes; output NHWC
+ * [batch,out_h,out_w,out_c] bytes.  `weights` is the packed operand made by
+ * bh_pack_conv_weights: int8-domain B^T [n_pad][k_pad] with
+ * k = (ky*k_w + kx)*in_c + ci, zero padded.  bias_eff[c] already folds the
+ * int32 bias and every zero-point cross term that does not depend on the
+ * activations (see bh_pack_conv_weights); when w_zp != 0 (uint8 weights) the
+ * kernel subtracts w_zp * sum_k x'[m][k] per output pixel. */
+typedef struct bh_conv_params {
+  int batch, in_h, in_w, in_c;
+  int out_h, out_w, out_c;
+  int k_h, k_w;
+  int stride_h, stride_w, dil_h, dil_w;
+  int pad_h, pad_w;               /* top / left padding (TFLite padding.h) */
+  int k_pad, n_pad;               /* packed weight geometry */
+  int in_xor;                     /* 0x80 when the input tensor is uint8 */
+  int32_t in_zp;                  /* int8-domain input zero point (pad value) */
+  int32_t w_zp;                   /* int8-domain weight zero point (0 if symmetric) */
+  int32_t out_zp;                 /* output tensor zero point (own domain) */
+  int32_t act_min, act_max;       /* output tensor domain */
+  const void* input;
+  void* output;
+  const int8_t* weights;
+  const int32_t* bias_eff;        /* [out_c] */
+  const int32_t* mult;            /* [out_c] Q31 multipliers */
+  const int32_t* shift;           /* [out_c] TFLite exponent (>0 = left) */
+} bh_conv_params;
+
+/* DEPTHWISE_CONV_2D.  weights: int8-domain [k_h][k_w][out_c] (TFLite layout
+ * [1,kh,kw,oc] with XOR applied for uint8 filters).  Exact int32 math
+ * (x'-in_zp)*(w'-w_zp) per tap, taps outside the image skipped. */
+typedef struct bh_dwconv_params {
+  int batch, in_h, in_w, in_c;
+  int out_h, out_w, out_c, depth_multiplier;
+  int k_h, k_w;
+  int stride_h, stride_w, dil_h, dil_w;
+  int pad_h, pad_w;
+  int in_xor;
+  int32_t in_zp, w_zp, out_zp;
+  int32_t act_min, act_max;
+  const void* input;
+  void* output;
+  const int8_t* weights;
+  const int32_t* bias;            /* [out_c] raw int32 bias (zeros if absent) */
+  const int32_t* mult;
+  const int32_t* shift;
+} bh_dwconv_params;
+
+/* FULLY_CONNECTED.  input [rows][depth] bytes, weights int8-domain
+ * [units][depth_pad] (depth_pad multiple of 16, zero padded); bias_eff as
+ * for conv (folds bias - in_zp*sum(w') + depth*in_zp*w_zp). */
+typedef struct bh_fc_params {
+  int rows, depth, depth_pad, units;
+  int in_xor;
+  int32_t in_zp, w_zp, out_zp;
+  int32_t act_min, act_max;
+  const void* input;
+  void* output;
+  const int8_t* weights;
+  const int32_t* bias_eff;
+  const int32_t* mult;            /* [units] */
+  const int32_t* shift;
+} bh_fc_params;
+
+/* ADD / SUB / MUL with TFLite 4-D broadcasting.  Shapes are extended to 4-D
+ * (leading 1s); a dimension of 1 in an input broadcasts.  Offsets are the
+ * NEGATED zero points in each tensor's own domain (TFLite input*_offset). */
+#define BH_ELT_ADD 0
+#define BH_ELT_MUL 1
+typedef struct bh_eltwise_params {
+  int kind;                       /* BH_ELT_ADD (also SUB) or BH_ELT_MUL */
+  int in_signed;                  /* 1 int8, 0 uint8 (both inputs, output) */
+  int shape_a[4], shape_b[4], shape_o[4];
+  int32_t a_off, b_off, o_off;
+  int32_t left_shift;             /* ADD: 20 */
+  int32_t a_mult, a_shift;        /* ADD: input1 (shift <= 0) */
+  int32_t b_mult, b_shift;        /* ADD: input2 (negated mult for SUB) */
+  int32_t o_mult, o_shift;        /* ADD: output; MUL: the only multiplier */
+  int32_t act_min, act_max;
+  const void* a;
+  const void* b;
+  void* out;
+} bh_eltwise_params;
+
+/* AVERAGE_POOL_2D / MAX_POOL_2D (no rescale: in/out share scale). */
+#define BH_POOL_AVG 0
+#define BH_POOL_MAX 1
+typedef struct bh_pool_params {
+  int kind;
+  int in_signed;
+  int batch, in_h, in_w, channels;
+  int out_h, out_w;
+  int f_h, f_w, stride_h, stride_w, pad_h, pad_w;
+  int32_t act_min, act_max;
+  const void* input;
+  void* output;
+} bh_pool_params;
+
+/* ---- host-side operand packing (pure CPU, no device calls) -------------- */
+
+/* Pack OHWI conv weights ([out_c][k_h*k_w*in_c] bytes, signed or unsigned)
+ * into the int8-domain padded B^T operand and compute bias_eff:
+ *   bias_eff[c] = bias[c] - in_zp*S_c + K*in_zp*w_zp,  S_c = sum_k w'[c][k]
+ * where w' = w (int8) or w-128 (uint8) and in_zp/w_zp are int8-domain.
+ * packed must hold n_pad*k_pad bytes; bias may be NULL. */
+int bh_pack_conv_weights(const void* w, int w_signed, int out_c, int k,
+                         int k_pad, int n_pad, const int32_t* bias,
+                         int32_t in_zp, int32_t w_zp, int8_t* packed,
+                         int32_t* bias_eff);
+
+/* Tile geometry the conv launcher expects for a layer (k_pad, n_pad). */
+int bh_conv_packed_geometry(int out_c, int k, int* k_pad, int* n_pad);
+
+/* ---- launchers ---------------------------------------------------------- */
+int bh_conv2d_i8(const bh_conv_params* p, bh_stream_t s);
+int bh_dwconv2d_i8(const bh_dwconv_params* p, bh_stream_t s);
+int bh_fc_i8(const bh_fc_params* p, bh_stream_t s);
+int bh_eltwise_i8(const bh_eltwise_params* p, bh_stream_t s);
+int bh_pool_i8(const bh_pool_params* p, bh_stream_t s);
+
+/* human-readable name of the last error set on this thread */
+const char* bh_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BAND_HIP_KERNELS_H_ */

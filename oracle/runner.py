@@ -1,0 +1,361 @@
+"""ORACLE — test infrastructure only.
+
+Whole-model CPU runner restating what `tflite::Interpreter::Invoke` computes
+for the op set on Band's hot path (`band/backend/tfl/model_executor.cc:249-255`
+-> TFLite 2.9.2 builtin kernels).  The op-level Prepare logic (quantisation
+parameter derivation) mirrors TFLite 2.9.2's `kernels/{conv,depthwise_conv,
+fully_connected,add,sub,mul,pooling,reshape}.cc`; the arithmetic runs in the C
+restatement `oracle/tflite_ref.c` (loaded via ctypes from `liboracle.so`).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may use
+this module.  It is never on the product path.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .tflite_fb import Model, OP
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+P_U8 = ctypes.POINTER(ctypes.c_uint8)
+P_I32 = ctypes.POINTER(ctypes.c_int32)
+P_F32 = ctypes.POINTER(ctypes.c_float)
+
+
+def build():
+    """Compile liboracle.so with the committed Makefile (gcc)."""
+    import subprocess
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        L.tfl_srdhm.restype = ctypes.c_int32
+        L.tfl_srdhm.argtypes = [ctypes.c_int32, ctypes.c_int32]
+        L.tfl_rdbypot.restype = ctypes.c_int32
+        L.tfl_rdbypot.argtypes = [ctypes.c_int32, ctypes.c_int]
+        L.tfl_mbqm.restype = ctypes.c_int32
+        L.tfl_mbqm.argtypes = [ctypes.c_int32, ctypes.c_int32, ctypes.c_int]
+        L.tfl_quantize_multiplier.argtypes = [ctypes.c_double, P_I32, ctypes.POINTER(ctypes.c_int)]
+        L.tfl_act_range_quantized.argtypes = [ctypes.c_int, ctypes.c_float, ctypes.c_int32,
+                                              ctypes.c_int, P_I32, P_I32]
+        L.tfl_conv_multipliers.argtypes = [ctypes.c_float, P_F32, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_float, ctypes.c_int, P_I32, P_I32]
+        L.tfl_add_params.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, P_I32]
+        L.tfl_mul_params.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, P_I32, P_I32]
+        L.tfl_out_size.restype = ctypes.c_int
+        L.tfl_padding.restype = ctypes.c_int
+        _LIB = L
+    return _LIB
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+def quantize_multiplier(m):
+    q = ctypes.c_int32()
+    s = ctypes.c_int()
+    lib().tfl_quantize_multiplier(float(m), ctypes.byref(q), ctypes.byref(s))
+    return q.value, s.value
+
+
+def act_range(act, scale, zp, signed):
+    lo = ctypes.c_int32()
+    hi = ctypes.c_int32()
+    lib().tfl_act_range_quantized(int(act), float(scale), int(zp), int(signed),
+                                  ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value
+
+
+def conv_multipliers(in_scale, w_scales, n_channels, out_scale, legacy):
+    w = np.ascontiguousarray(np.asarray(w_scales, np.float32))
+    mult = np.zeros(n_channels, np.int32)
+    shift = np.zeros(n_channels, np.int32)
+    lib().tfl_conv_multipliers(float(in_scale), _p(w, P_F32), len(w), n_channels,
+                               float(out_scale), int(legacy), _p(mult, P_I32), _p(shift, P_I32))
+    return mult, shift
+
+
+def out_size(same, n, f, s, d):
+    return lib().tfl_out_size(int(same), n, f, s, d)
+
+
+def padding(s, d, n, f, o):
+    return lib().tfl_padding(s, d, n, f, o)
+
+
+def _u8(a):
+    return np.ascontiguousarray(a).view(np.uint8)
+
+
+def _signed(dt):
+    return 1 if np.dtype(dt) == np.int8 else 0
+
+
+def conv2d(x, w, bias, *, in_zp, w_zp, out_zp, mult, shift, amin, amax,
+           stride=(1, 1), dilation=(1, 1), pad=(0, 0), out_hw=None, out_dtype=None):
+    """x NHWC, w OHWI; returns NHWC output (dtype of x unless out_dtype)."""
+    b, ih, iw, ic = x.shape
+    oc, kh, kw, _ = w.shape
+    oh, ow = out_hw
+    out = np.zeros((b, oh, ow, oc), out_dtype or x.dtype)
+    bias = None if bias is None else np.ascontiguousarray(bias, np.int32)
+    mult = np.ascontiguousarray(mult, np.int32)
+    shift = np.ascontiguousarray(shift, np.int32)
+    lib().tfl_conv2d(_p(_u8(x), P_U8), _signed(x.dtype), b, ih, iw, ic,
+                     _p(_u8(w), P_U8), _signed(w.dtype), oc, kh, kw,
+                     None if bias is None else _p(bias, P_I32), _p(out.view(np.uint8), P_U8),
+                     oh, ow, stride[0], stride[1], dilation[0], dilation[1], pad[0], pad[1],
+                     ctypes.c_int32(-in_zp), ctypes.c_int32(-w_zp), ctypes.c_int32(out_zp),
+                     _p(mult, P_I32), _p(shift, P_I32), ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def dwconv2d(x, w, bias, *, dm, in_zp, w_zp, out_zp, mult, shift, amin, amax,
+             stride=(1, 1), dilation=(1, 1), pad=(0, 0), out_hw=None):
+    b, ih, iw, ic = x.shape
+    _, kh, kw, oc = w.shape
+    oh, ow = out_hw
+    out = np.zeros((b, oh, ow, oc), x.dtype)
+    bias = None if bias is None else np.ascontiguousarray(bias, np.int32)
+    mult = np.ascontiguousarray(mult, np.int32)
+    shift = np.ascontiguousarray(shift, np.int32)
+    lib().tfl_dwconv2d(_p(_u8(x), P_U8), _signed(x.dtype), b, ih, iw, ic,
+                       _p(_u8(w), P_U8), _signed(w.dtype), dm, kh, kw,
+                       None if bias is None else _p(bias, P_I32), _p(out.view(np.uint8), P_U8),
+                       oh, ow, stride[0], stride[1], dilation[0], dilation[1], pad[0], pad[1],
+                       ctypes.c_int32(-in_zp), ctypes.c_int32(-w_zp), ctypes.c_int32(out_zp),
+                       _p(mult, P_I32), _p(shift, P_I32), ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def fully_connected(x2d, w, bias, *, in_zp, w_zp, out_zp, mult, shift, amin, amax):
+    rows, depth = x2d.shape
+    units = w.shape[0]
+    out = np.zeros((rows, units), x2d.dtype)
+    bias = None if bias is None else np.ascontiguousarray(bias, np.int32)
+    mult = np.ascontiguousarray(np.broadcast_to(mult, (units,)), np.int32)
+    shift = np.ascontiguousarray(np.broadcast_to(shift, (units,)), np.int32)
+    lib().tfl_fully_connected(_p(_u8(x2d), P_U8), _signed(x2d.dtype), rows, depth,
+                              _p(_u8(w), P_U8), _signed(w.dtype), units,
+                              None if bias is None else _p(bias, P_I32), _p(out.view(np.uint8), P_U8),
+                              ctypes.c_int32(-in_zp), ctypes.c_int32(-w_zp), ctypes.c_int32(out_zp),
+                              _p(mult, P_I32), _p(shift, P_I32), ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def _shape4(s):
+    s = list(s)
+    return [1] * (4 - len(s)) + s
+
+
+def _bshape(a, b):
+    sa, sb = _shape4(a.shape), _shape4(b.shape)
+    so = [max(x, y) for x, y in zip(sa, sb)]
+    return (np.array(sa, np.int32), np.array(sb, np.int32), np.array(so, np.int32),
+            np.broadcast_shapes(a.shape, b.shape))
+
+
+def add_params(s1, s2, so):
+    p = np.zeros(7, np.int32)
+    lib().tfl_add_params(float(s1), float(s2), float(so), _p(p, P_I32))
+    return p
+
+
+def add(a, b, *, a_zp, b_zp, out_zp, params, amin, amax, sub=False):
+    sa, sb, so, oshape = _bshape(a, b)
+    out = np.zeros(oshape, a.dtype)
+    lib().tfl_add(_p(_u8(a), P_U8), _p(sa, P_I32), _p(_u8(b), P_U8), _p(sb, P_I32),
+                  _p(out.view(np.uint8), P_U8), _p(so, P_I32), _signed(a.dtype),
+                  ctypes.c_int32(-a_zp), ctypes.c_int32(-b_zp), ctypes.c_int32(out_zp),
+                  _p(np.ascontiguousarray(params, np.int32), P_I32), int(sub),
+                  ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def mul_params(s1, s2, so):
+    m = np.zeros(1, np.int32)
+    s = np.zeros(1, np.int32)
+    lib().tfl_mul_params(float(s1), float(s2), float(so), _p(m, P_I32), _p(s, P_I32))
+    return int(m[0]), int(s[0])
+
+
+def mul(a, b, *, a_zp, b_zp, out_zp, mult, shift, amin, amax):
+    sa, sb, so, oshape = _bshape(a, b)
+    out = np.zeros(oshape, a.dtype)
+    lib().tfl_mul(_p(_u8(a), P_U8), _p(sa, P_I32), _p(_u8(b), P_U8), _p(sb, P_I32),
+                  _p(out.view(np.uint8), P_U8), _p(so, P_I32), _signed(a.dtype),
+                  ctypes.c_int32(-a_zp), ctypes.c_int32(-b_zp), ctypes.c_int32(out_zp),
+                  ctypes.c_int32(mult), ctypes.c_int32(shift), ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def pool2d(x, *, kind, filt, stride, pad, out_hw, amin, amax):
+    b, ih, iw, c = x.shape
+    oh, ow = out_hw
+    out = np.zeros((b, oh, ow, c), x.dtype)
+    fn = lib().tfl_avg_pool if kind == "avg" else lib().tfl_max_pool
+    fn(_p(_u8(x), P_U8), _signed(x.dtype), b, ih, iw, c, _p(out.view(np.uint8), P_U8),
+       oh, ow, filt[0], filt[1], stride[0], stride[1], pad[0], pad[1],
+       ctypes.c_int32(amin), ctypes.c_int32(amax))
+    return out
+
+
+def add_f32(a, b, amin=-np.inf, amax=np.inf, sub=False):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    sa, sb, so, oshape = _bshape(a, b)
+    out = np.zeros(oshape, np.float32)
+    lib().tfl_add_f32(_p(a, P_F32), _p(sa, P_I32), _p(b, P_F32), _p(sb, P_I32),
+                      _p(out, P_F32), _p(so, P_I32), ctypes.c_float(amin), ctypes.c_float(amax), int(sub))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# whole-model runner
+# ---------------------------------------------------------------------------
+
+def _q(t):
+    return float(t.scale[0]), int(t.zero_point[0])
+
+
+def _act_range_for(act, t):
+    s, z = _q(t)
+    return act_range(act, s, z, t.np_dtype == np.int8)
+
+
+def _f32_act(act):
+    return {1: (0.0, np.inf), 2: (-1.0, 1.0), 3: (0.0, 6.0)}.get(act, (-np.inf, np.inf))
+
+
+class OracleInterpreter:
+    """Runs the primary subgraph of a .tflite model op by op on the CPU."""
+
+    SUPPORTED = {OP["CONV_2D"], OP["DEPTHWISE_CONV_2D"], OP["FULLY_CONNECTED"],
+                 OP["ADD"], OP["SUB"], OP["MUL"], OP["AVERAGE_POOL_2D"],
+                 OP["MAX_POOL_2D"], OP["RESHAPE"], OP["SQUEEZE"]}
+
+    def __init__(self, model):
+        self.model = model if isinstance(model, Model) else Model.from_path(model)
+
+    def unsupported_ops(self):
+        return [i for i, o in enumerate(self.model.operators) if o.builtin not in self.SUPPORTED]
+
+    def run(self, inputs, ops=None):
+        """inputs: {tensor_index: ndarray}. Returns {tensor_index: ndarray}."""
+        m = self.model
+        vals = {}
+        for t in m.tensors:
+            if t.is_const:
+                vals[t.index] = t.data
+        for k, v in inputs.items():
+            t = m.tensors[k]
+            vals[k] = np.asarray(v, t.np_dtype).reshape(t.shape)
+        order = range(len(m.operators)) if ops is None else sorted(ops)
+        for i in order:
+            o = m.operators[i]
+            outs = self._op(o, vals)
+            for idx, val in zip(o.outputs, outs):
+                vals[idx] = np.asarray(val).reshape(m.tensors[idx].shape).astype(m.tensors[idx].np_dtype, copy=False)
+        return vals
+
+    def _op(self, o, vals):
+        m = self.model
+        T = m.tensors
+        opt = o.options
+        code = o.builtin
+        if code in (OP["CONV_2D"], OP["DEPTHWISE_CONV_2D"]):
+            dw = code == OP["DEPTHWISE_CONV_2D"]
+            x, w = vals[o.inputs[0]], vals[o.inputs[1]]
+            bias = vals.get(o.inputs[2]) if len(o.inputs) > 2 and o.inputs[2] >= 0 else None
+            ti, tw, to = T[o.inputs[0]], T[o.inputs[1]], T[o.outputs[0]]
+            pad_same = opt.scalar(0, "b", 0) == 0
+            sw, sh = opt.scalar(1, "i", 1), opt.scalar(2, "i", 1)
+            if dw:
+                dm = opt.scalar(3, "i", 1)
+                act = opt.scalar(4, "b", 0)
+                dw_, dh_ = opt.scalar(5, "i", 1), opt.scalar(6, "i", 1)
+                kh, kw, oc = w.shape[1], w.shape[2], w.shape[3]
+            else:
+                act = opt.scalar(3, "b", 0)
+                dw_, dh_ = opt.scalar(4, "i", 1), opt.scalar(5, "i", 1)
+                oc, kh, kw = w.shape[0], w.shape[1], w.shape[2]
+            ih, iw = x.shape[1], x.shape[2]
+            oh = out_size(pad_same, ih, kh, sh, dh_)
+            ow = out_size(pad_same, iw, kw, sw, dw_)
+            ph = padding(sh, dh_, ih, kh, oh)
+            pw = padding(sw, dw_, iw, kw, ow)
+            in_s, in_z = _q(ti)
+            out_s, out_z = _q(to)
+            legacy = ti.np_dtype == np.uint8
+            mult, shift = conv_multipliers(in_s, tw.scale, oc, out_s, legacy)
+            amin, amax = _act_range_for(act, to)
+            w_zp = int(tw.zero_point[0]) if legacy else 0
+            kw_args = dict(in_zp=in_z, w_zp=w_zp, out_zp=out_z, mult=mult, shift=shift,
+                           amin=amin, amax=amax, stride=(sh, sw), dilation=(dh_, dw_),
+                           pad=(ph, pw), out_hw=(oh, ow))
+            if dw:
+                return [dwconv2d(x, w, bias, dm=dm, **kw_args)]
+            return [conv2d(x, w, bias, **kw_args)]
+        if code == OP["FULLY_CONNECTED"]:
+            x, w = vals[o.inputs[0]], vals[o.inputs[1]]
+            bias = vals.get(o.inputs[2]) if len(o.inputs) > 2 and o.inputs[2] >= 0 else None
+            ti, tw, to = T[o.inputs[0]], T[o.inputs[1]], T[o.outputs[0]]
+            act = opt.scalar(0, "b", 0) if opt is not None else 0
+            depth = w.shape[1]
+            x2 = x.reshape(-1, depth)
+            in_s, in_z = _q(ti)
+            out_s, out_z = _q(to)
+            mult, shift = conv_multipliers(in_s, tw.scale[:1], 1, out_s, True)
+            amin, amax = _act_range_for(act, to)
+            return [fully_connected(x2, w, bias, in_zp=in_z, w_zp=int(tw.zero_point[0]),
+                                    out_zp=out_z, mult=mult[0], shift=shift[0], amin=amin, amax=amax)]
+        if code in (OP["ADD"], OP["SUB"]):
+            a, b = vals[o.inputs[0]], vals[o.inputs[1]]
+            ta, tb, to = T[o.inputs[0]], T[o.inputs[1]], T[o.outputs[0]]
+            act = opt.scalar(0, "b", 0) if opt is not None else 0
+            if to.np_dtype == np.float32:
+                lo, hi = _f32_act(act)
+                return [add_f32(a, b, lo, hi, sub=code == OP["SUB"])]
+            sa, za = _q(ta)
+            sb, zb = _q(tb)
+            so, zo = _q(to)
+            amin, amax = _act_range_for(act, to)
+            return [add(a, b, a_zp=za, b_zp=zb, out_zp=zo, params=add_params(sa, sb, so),
+                        amin=amin, amax=amax, sub=code == OP["SUB"])]
+        if code == OP["MUL"]:
+            a, b = vals[o.inputs[0]], vals[o.inputs[1]]
+            ta, tb, to = T[o.inputs[0]], T[o.inputs[1]], T[o.outputs[0]]
+            act = opt.scalar(0, "b", 0) if opt is not None else 0
+            sa, za = _q(ta)
+            sb, zb = _q(tb)
+            so, zo = _q(to)
+            mult, shift = mul_params(sa, sb, so)
+            amin, amax = _act_range_for(act, to)
+            return [mul(a, b, a_zp=za, b_zp=zb, out_zp=zo, mult=mult, shift=shift, amin=amin, amax=amax)]
+        if code in (OP["AVERAGE_POOL_2D"], OP["MAX_POOL_2D"]):
+            x = vals[o.inputs[0]]
+            to = T[o.outputs[0]]
+            pad_same = opt.scalar(0, "b", 0) == 0
+            sw, sh = opt.scalar(1, "i", 1), opt.scalar(2, "i", 1)
+            fw, fh = opt.scalar(3, "i", 1), opt.scalar(4, "i", 1)
+            act = opt.scalar(5, "b", 0)
+            ih, iw = x.shape[1], x.shape[2]
+            oh, ow = out_size(pad_same, ih, fh, sh, 1), out_size(pad_same, iw, fw, sw, 1)
+            ph, pw = padding(sh, 1, ih, fh, oh), padding(sw, 1, iw, fw, ow)
+            amin, amax = _act_range_for(act, to)
+            kind = "avg" if code == OP["AVERAGE_POOL_2D"] else "max"
+            return [pool2d(x, kind=kind, filt=(fh, fw), stride=(sh, sw), pad=(ph, pw),
+                           out_hw=(oh, ow), amin=amin, amax=amax)]
+        if code in (OP["RESHAPE"], OP["SQUEEZE"]):
+            return [vals[o.inputs[0]].copy()]
+        raise NotImplementedError("oracle: op %s not restated" % o.name)

@@ -1,0 +1,198 @@
+"""Op-level parity: HIP kernels (through the C ABI) vs the CPU oracle, bit-exact.
+
+Oracle = TFLite 2.9.2 integer reference kernels restated in oracle/tflite_ref.c
+(pinned by tests/test_oracle.py against the reference's own known answers).
+"""
+import ctypes
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle import runner as orc
+from tests.kernel_harness import (MNV2_DEPTHWISE, MNV2_POINTWISE, ConvCase, dom, rand_q)
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("spatial,ic,oc", MNV2_POINTWISE)
+def test_conv1x1_mnv2_shapes_int8(gpu_lib, spatial, ic, oc):
+    rng = np.random.default_rng(1000 + spatial * 7 + ic + oc)
+    c = ConvCase(rng, 1, spatial, spatial, ic, oc, 1, 1, act=3)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+def test_conv_first_layer_3x3_s2_int8(gpu_lib):
+    rng = np.random.default_rng(7)
+    c = ConvCase(rng, 1, 224, 224, 3, 32, 3, 3, stride=(2, 2), act=3)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+@pytest.mark.parametrize("spatial,ic,oc", MNV2_POINTWISE[::4])
+def test_conv1x1_uint8_per_tensor(gpu_lib, spatial, ic, oc):
+    rng = np.random.default_rng(2000 + spatial + ic + oc)
+    c = ConvCase(rng, 1, spatial, spatial, ic, oc, 1, 1, dtype=np.uint8, act=3)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+@pytest.mark.parametrize("args", [
+    dict(b=1, ih=224, iw=224, ic=3, oc=32, kh=3, kw=3, stride=(2, 2), dtype=np.uint8),
+    dict(b=2, ih=17, iw=13, ic=16, oc=40, kh=3, kw=3, stride=(1, 1)),
+    dict(b=1, ih=20, iw=20, ic=24, oc=72, kh=3, kw=3, stride=(2, 2)),
+    dict(b=1, ih=11, iw=9, ic=13, oc=21, kh=5, kw=3, stride=(1, 2), same=False),
+    dict(b=1, ih=16, iw=16, ic=32, oc=64, kh=3, kw=3, dil=(2, 2)),
+    dict(b=3, ih=8, iw=8, ic=40, oc=24, kh=1, kw=1, stride=(2, 2)),
+    dict(b=1, ih=9, iw=9, ic=20, oc=17, kh=1, kw=1, act=0),
+    dict(b=1, ih=6, iw=7, ic=8, oc=130, kh=3, kw=3, dtype=np.uint8, act=1),
+])
+def test_conv_general(gpu_lib, args):
+    rng = np.random.default_rng(zlib.crc32(repr(sorted(args.items())).encode()))
+    c = ConvCase(rng, **args)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+@pytest.mark.parametrize("spatial,ch,stride", MNV2_DEPTHWISE)
+def test_dwconv_mnv2_shapes(gpu_lib, spatial, ch, stride):
+    rng = np.random.default_rng(3000 + spatial + ch + stride)
+    c = ConvCase(rng, 1, spatial, spatial, ch, ch, 3, 3, stride=(stride, stride), depthwise=True)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+@pytest.mark.parametrize("args", [
+    dict(b=1, ih=56, iw=56, ic=144, oc=0, kh=3, kw=3, stride=(2, 2), dtype=np.uint8),
+    dict(b=2, ih=13, iw=11, ic=6, oc=0, kh=3, kw=3, depthwise=True, dm=2),
+    dict(b=1, ih=15, iw=15, ic=7, oc=0, kh=5, kw=5, stride=(2, 2), same=False),
+    dict(b=1, ih=12, iw=12, ic=16, oc=0, kh=3, kw=3, dil=(2, 2)),
+])
+def test_dwconv_general(gpu_lib, args):
+    args = dict(args)
+    args["depthwise"] = True
+    rng = np.random.default_rng(zlib.crc32(repr(sorted(args.items())).encode()))
+    c = ConvCase(rng, **args)
+    np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+def _elt(gpu_lib, a, b, kind, dtype, rng, sub=False):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    sa, sb = float(rng.uniform(0.01, 0.1)), float(rng.uniform(0.01, 0.1))
+    so = float(rng.uniform(0.02, 0.15))
+    if dtype == np.int8:
+        za, zb, zo = (int(v) for v in rng.integers(-128, 128, 3))
+    else:
+        za, zb, zo = (int(v) for v in rng.integers(0, 256, 3))
+    amin, amax = orc.act_range(1, so, zo, dtype == np.int8)
+    if kind == "add":
+        prm = orc.add_params(sa, sb, so)
+        ref = orc.add(a, b, a_zp=za, b_zp=zb, out_zp=zo, params=prm, amin=amin, amax=amax, sub=sub)
+    else:
+        m, s = orc.mul_params(sa, sb, so)
+        ref = orc.mul(a, b, a_zp=za, b_zp=zb, out_zp=zo, mult=m, shift=s, amin=amin, amax=amax)
+    s4 = lambda s: [1] * (4 - len(s)) + list(s)
+    p = _abi.EltwiseParams()
+    p.kind = 0 if kind == "add" else 1
+    p.in_signed = int(dtype == np.int8)
+    for i, (x, y, z) in enumerate(zip(s4(a.shape), s4(b.shape), s4(ref.shape))):
+        p.shape_a[i], p.shape_b[i], p.shape_o[i] = x, y, z
+    p.a_off, p.b_off, p.o_off = -za, -zb, zo
+    if kind == "add":
+        p.a_mult, p.a_shift, p.b_mult, p.b_shift, p.o_mult, p.o_shift, p.left_shift = [int(v) for v in prm]
+        if sub:
+            p.b_mult = -p.b_mult
+    else:
+        p.o_mult, p.o_shift = m, s
+    p.act_min, p.act_max = amin, amax
+    da, db = DeviceBuffer.from_array(a), DeviceBuffer.from_array(b)
+    do = DeviceBuffer(ref.nbytes)
+    p.a, p.b, p.out = da.value, db.value, do.value
+    _abi.check(gpu_lib.bh_eltwise_i8(ctypes.byref(p), None), "eltwise")
+    np.testing.assert_array_equal(do.download(dtype, ref.shape), ref)
+
+
+@pytest.mark.parametrize("dtype", [np.int8, np.uint8])
+@pytest.mark.parametrize("shape", [(1, 56, 56, 24), (1, 7, 7, 160), (1, 5, 3, 3), (2, 3, 3, 1)])
+def test_add_same_shape(gpu_lib, dtype, shape):
+    rng = np.random.default_rng(sum(shape) + (dtype == np.int8))
+    _elt(gpu_lib, rand_q(rng, shape, dtype), rand_q(rng, shape, dtype), "add", dtype, rng)
+
+
+def test_sub_and_broadcast(gpu_lib):
+    rng = np.random.default_rng(5)
+    a = rand_q(rng, (1, 16, 16, 3), np.int8)
+    _elt(gpu_lib, a, rand_q(rng, (1, 1, 1, 3), np.int8), "add", np.int8, rng, sub=True)
+    _elt(gpu_lib, a, rand_q(rng, (3,), np.int8), "add", np.int8, rng)
+
+
+@pytest.mark.parametrize("dtype", [np.int8, np.uint8])
+def test_mul(gpu_lib, dtype):
+    rng = np.random.default_rng(11)
+    _elt(gpu_lib, rand_q(rng, (1, 10, 10, 8), dtype), rand_q(rng, (1, 10, 10, 8), dtype), "mul", dtype, rng)
+    _elt(gpu_lib, rand_q(rng, (1, 10, 10, 8), dtype), rand_q(rng, (1, 1, 1, 1), dtype), "mul", dtype, rng)
+
+
+@pytest.mark.parametrize("kind", ["avg", "max"])
+@pytest.mark.parametrize("cfg", [
+    dict(shape=(1, 7, 7, 1280), f=(7, 7), s=(1, 1), same=False, dtype=np.uint8),
+    dict(shape=(1, 7, 7, 1280), f=(7, 7), s=(1, 1), same=False, dtype=np.int8),
+    dict(shape=(2, 13, 11, 6), f=(3, 3), s=(2, 2), same=True, dtype=np.int8),
+    dict(shape=(1, 9, 9, 5), f=(2, 2), s=(2, 2), same=True, dtype=np.uint8),
+])
+def test_pool(gpu_lib, kind, cfg):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(17)
+    x = rand_q(rng, cfg["shape"], cfg["dtype"])
+    b, ih, iw, c = x.shape
+    (fh, fw), (sh, sw) = cfg["f"], cfg["s"]
+    oh, ow = orc.out_size(cfg["same"], ih, fh, sh, 1), orc.out_size(cfg["same"], iw, fw, sw, 1)
+    ph, pw = orc.padding(sh, 1, ih, fh, oh), orc.padding(sw, 1, iw, fw, ow)
+    signed = cfg["dtype"] == np.int8
+    amin, amax = (-128, 127) if signed else (0, 255)
+    ref = orc.pool2d(x, kind=kind, filt=(fh, fw), stride=(sh, sw), pad=(ph, pw), out_hw=(oh, ow),
+                     amin=amin, amax=amax)
+    dx = DeviceBuffer.from_array(x)
+    dy = DeviceBuffer(ref.nbytes)
+    p = _abi.PoolParams(kind=0 if kind == "avg" else 1, in_signed=int(signed), batch=b, in_h=ih, in_w=iw,
+                        channels=c, out_h=oh, out_w=ow, f_h=fh, f_w=fw, stride_h=sh, stride_w=sw,
+                        pad_h=ph, pad_w=pw, act_min=amin, act_max=amax, input=dx.value, output=dy.value)
+    _abi.check(gpu_lib.bh_pool_i8(ctypes.byref(p), None), "pool")
+    np.testing.assert_array_equal(dy.download(x.dtype, ref.shape), ref)
+
+
+@pytest.mark.parametrize("rows,depth,units,dtype", [
+    (1, 1280, 1001, np.int8), (1, 1280, 1001, np.uint8), (3, 37, 10, np.int8), (2, 64, 5, np.uint8),
+])
+def test_fully_connected(gpu_lib, rows, depth, units, dtype):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(rows * 1000 + depth + units)
+    x = rand_q(rng, (rows, depth), dtype)
+    w = rand_q(rng, (units, depth), dtype) if dtype == np.uint8 else \
+        rng.integers(-127, 128, (units, depth)).astype(np.int8)
+    bias = rng.integers(-(1 << 15), 1 << 15, units).astype(np.int32)
+    in_zp = int(rng.integers(-128, 128)) if dtype == np.int8 else int(rng.integers(0, 256))
+    w_zp = 0 if dtype == np.int8 else int(rng.integers(90, 170))
+    in_s, w_s = 0.02, 0.005
+    out_s = in_s * w_s * np.sqrt(depth) * 74 * 74 / 40
+    out_zp = 3 if dtype == np.int8 else 130
+    mult, shift = orc.conv_multipliers(in_s, [w_s], 1, out_s, True)
+    amin, amax = orc.act_range(0, out_s, out_zp, dtype == np.int8)
+    ref = orc.fully_connected(x, w, bias, in_zp=in_zp, w_zp=w_zp, out_zp=out_zp, mult=mult[0],
+                              shift=shift[0], amin=amin, amax=amax)
+    # host packing identical to the executor's (int8 domain, bias folding)
+    depth_pad = (depth + 15) // 16 * 16
+    wd = w.astype(np.int32) - (0 if dtype == np.int8 else 128)
+    in_zd, w_zd = dom(in_zp, dtype), dom(w_zp, dtype) if dtype == np.uint8 else 0
+    packed = np.zeros((units, depth_pad), np.int8)
+    packed[:, :depth] = wd.astype(np.int8)
+    beff = (bias.astype(np.int64) - in_zd * wd.sum(1) + depth * in_zd * w_zd).astype(np.int32)
+    dx, dy = DeviceBuffer.from_array(x), DeviceBuffer(ref.nbytes)
+    dw, db = DeviceBuffer.from_array(packed), DeviceBuffer.from_array(beff)
+    dm = DeviceBuffer.from_array(np.full(units, mult[0], np.int32))
+    ds = DeviceBuffer.from_array(np.full(units, shift[0], np.int32))
+    p = _abi.FcParams(rows=rows, depth=depth, depth_pad=depth_pad, units=units,
+                      in_xor=0 if dtype == np.int8 else 0x80, in_zp=in_zd, w_zp=w_zd, out_zp=out_zp,
+                      act_min=amin, act_max=amax, input=dx.value, output=dy.value, weights=dw.value,
+                      bias_eff=db.value, mult=dm.value, shift=ds.value)
+    _abi.check(gpu_lib.bh_fc_i8(ctypes.byref(p), None), "fc")
+    np.testing.assert_array_equal(dy.download(dtype, ref.shape), ref)

@@ -94,6 +94,7 @@ KERNEL_SYMBOLS = {
 BACKEND_SYMBOLS = {}  # filled by backend.py
 
 _lib = None
+_configured = set()
 
 
 class BandHipError(RuntimeError):
@@ -103,18 +104,19 @@ class BandHipError(RuntimeError):
 def load():
     """Load libband_hip.so; raises if it is missing (no fallback)."""
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise BandHipError(
-            "libband_hip.so not built (%s); run __graft_entry__.build() / make -C band_amd/csrc" % LIB_PATH)
-    lib = ctypes.CDLL(LIB_PATH)
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise BandHipError(
+                "libband_hip.so not built (%s); run __graft_entry__.build() / make -C band_amd/csrc" % LIB_PATH)
+        _lib = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in list(KERNEL_SYMBOLS.items()) + list(BACKEND_SYMBOLS.items()):
-        fn = getattr(lib, name)
+        if name in _configured:
+            continue
+        fn = getattr(_lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
-    return lib
+        _configured.add(name)
+    return _lib
 
 
 def check(rc, what=""):

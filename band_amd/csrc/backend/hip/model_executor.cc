@@ -1,0 +1,684 @@
+#include "backend/hip/model_executor.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+#include "backend/hip/quant.h"
+
+#define RETURN_STATUS_IF(expr)      \
+  do {                              \
+    absl::Status _st = (expr);      \
+    if (!_st.ok()) return _st;      \
+  } while (0)
+
+namespace band {
+namespace hip {
+
+const std::vector<int> HipModelExecutor::kEmpty;
+
+namespace {
+
+constexpr size_t kAlign = 256;
+
+bool IsQ8(DataType t) { return t == DataType::kInt8 || t == DataType::kUInt8; }
+
+// zero point in the kernels' int8 domain (uint8 values are XOR 0x80 = x-128)
+int32_t Dom(const TflTensor& t) {
+  const int32_t zp = t.zero_point.empty() ? 0 : static_cast<int32_t>(t.zero_point[0]);
+  return t.type == DataType::kUInt8 ? zp - 128 : zp;
+}
+int32_t Zp(const TflTensor& t) { return t.zero_point.empty() ? 0 : static_cast<int32_t>(t.zero_point[0]); }
+float Scale(const TflTensor& t) { return t.scale.empty() ? 0.0f : t.scale[0]; }
+bool HasQ(const TflTensor& t) { return !t.scale.empty(); }
+
+std::string Hex(uint64_t v) {
+  char b[32];
+  std::snprintf(b, sizeof(b), "%llx", static_cast<unsigned long long>(v));
+  return b;
+}
+
+void Shape4(const std::vector<int>& s, int* out) {
+  const int pad = 4 - static_cast<int>(s.size());
+  for (int i = 0; i < 4; ++i) out[i] = i < pad ? 1 : s[i - pad];
+}
+
+absl::Status HipErr(int rc, const char* what) {
+  return absl::InternalError(std::string("HIP Error: ") + what + " (" + std::to_string(rc) + "): " + bh_last_error());
+}
+
+}  // namespace
+
+HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceFlag device_flag,
+                                   CpuSet mask, int num_threads)
+    : IModelExecutor(model_id, worker_id, device_flag, mask, num_threads) {
+  if (device_flag_ == DeviceFlag::kGPU && DeviceRegistry::Get().GpuAvailable()) {
+    ordinal_ = DeviceRegistry::Get().OrdinalForWorker(worker_id_);
+    stream_ = DeviceRegistry::Get().StreamForWorker(worker_id_);
+  }
+  const char* g = std::getenv("BAND_HIP_GRAPH");
+  if (g && g[0] == '0') use_graph_ = false;
+}
+
+HipModelExecutor::~HipModelExecutor() {
+  if (ordinal_ >= 0) {
+    bh_set_device(ordinal_);
+    if (stream_) bh_stream_sync(stream_);
+    for (auto& kv : subgraphs_)
+      if (kv.second->graph) bh_graph_destroy(kv.second->graph);
+  }
+  subgraphs_.clear();
+}
+
+bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
+  auto no = [&](const char* w) {
+    if (why) *why = w;
+    return false;
+  };
+  auto T = [&](int i) -> const TflTensor& { return m.tensors[i]; };
+  if (op.inputs.empty() || op.outputs.empty() || op.inputs[0] < 0) return no("no operands");
+  const TflTensor& in = T(op.inputs[0]);
+  const TflTensor& out = T(op.outputs[0]);
+  switch (op.builtin) {
+    case kTflConv2D:
+    case kTflDepthwiseConv2D:
+    case kTflFullyConnected: {
+      if (op.inputs.size() < 2 || op.inputs[1] < 0) return no("missing filter");
+      const TflTensor& w = T(op.inputs[1]);
+      if (!IsQ8(in.type) || w.type != in.type || out.type != in.type) return no("only int8/uint8 quantized");
+      if (!w.is_const() || !HasQ(in) || !HasQ(w) || !HasQ(out)) return no("needs constant quantized filter");
+      if (op.inputs.size() > 2 && op.inputs[2] >= 0) {
+        const TflTensor& b = T(op.inputs[2]);
+        if (!b.is_const() || b.type != DataType::kInt32) return no("bias must be constant int32");
+      }
+      if (op.builtin == kTflFullyConnected) {
+        if (w.shape.size() != 2 || w.shape[1] <= 0) return no("FC weights must be 2-D");
+        if (in.num_elements() % static_cast<size_t>(w.shape[1]) != 0) return no("FC input/depth mismatch");
+        return true;
+      }
+      if (in.shape.size() != 4 || w.shape.size() != 4 || out.shape.size() != 4) return no("conv needs 4-D");
+      if (op.builtin == kTflConv2D && w.shape[3] != in.shape[3]) return no("grouped conv unsupported");
+      if (op.builtin == kTflDepthwiseConv2D && (in.shape[3] == 0 || w.shape[3] % in.shape[3] != 0))
+        return no("bad depth multiplier");
+      return true;
+    }
+    case kTflAdd:
+    case kTflSub:
+    case kTflMul: {
+      if (op.inputs.size() != 2 || op.inputs[1] < 0) return no("binary op needs 2 inputs");
+      const TflTensor& b = T(op.inputs[1]);
+      if (!IsQ8(in.type) || b.type != in.type || out.type != in.type) return no("only int8/uint8 quantized");
+      if (!HasQ(in) || !HasQ(b) || !HasQ(out)) return no("missing quantization");
+      if (in.shape.size() > 4 || b.shape.size() > 4 || out.shape.size() > 4) return no("rank > 4");
+      int sa[4], sb[4], so[4];
+      Shape4(in.shape, sa);
+      Shape4(b.shape, sb);
+      Shape4(out.shape, so);
+      for (int d = 0; d < 4; ++d)
+        if ((sa[d] != so[d] && sa[d] != 1) || (sb[d] != so[d] && sb[d] != 1)) return no("bad broadcast");
+      return true;
+    }
+    case kTflAveragePool2D:
+    case kTflMaxPool2D:
+      if (!IsQ8(in.type) || out.type != in.type || in.shape.size() != 4) return no("only int8/uint8 4-D");
+      if (!HasQ(out)) return no("missing quantization");
+      return true;
+    case kTflReshape:
+    case kTflSqueeze:
+      if (out.type != in.type || out.num_elements() != in.num_elements()) return no("size mismatch");
+      return true;
+    default:
+      return no("op not in the HIP kernel set");
+  }
+}
+
+absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
+  if (!meta_.empty()) return absl::OkStatus();
+  const TflModel& d = model.desc();
+  meta_.reserve(d.tensors.size());
+  for (const TflTensor& t : d.tensors) {
+    auto m = std::make_unique<TensorMeta>();
+    m->type = t.type;
+    m->dims = t.shape;
+    m->name = t.name;
+    m->bytes = GetDataTypeBytes(t.type) * t.num_elements();
+    m->SetQuant(t.scale, t.zero_point, t.quantized_dimension);
+    meta_.push_back(std::move(m));
+  }
+  return absl::OkStatus();
+}
+
+absl::StatusOr<ModelSpec> HipModelExecutor::InvestigateModelSpec(interface::IModel* model) {
+  auto* hm = dynamic_cast<HipModel*>(model);
+  if (!hm || !hm->IsInitialized()) return absl::InternalError("Failed to investigate model: not a loaded HIP model");
+  const TflModel& d = hm->desc();
+  const int num_ops = static_cast<int>(d.ops.size());
+  std::vector<DataType> tensor_types;
+  std::vector<std::set<int>> op_in, op_out;
+  for (const TflOperator& op : d.ops) {
+    std::set<int> all, ins, outs;
+    for (int t : op.inputs) {
+      if (t < 0) continue;  // kTfLiteOptionalTensor
+      all.insert(t);
+      if (!d.tensors[t].is_const()) ins.insert(t);  // constants are kTfLiteMmapRo
+    }
+    for (int t : op.outputs) {
+      if (t < 0) continue;
+      all.insert(t);
+      if (!d.tensors[t].is_const()) outs.insert(t);
+    }
+    for (int t : all) tensor_types.push_back(d.tensors[t].type);
+    op_in.push_back(ins);
+    op_out.push_back(outs);
+  }
+  std::map<DeviceFlag, std::set<int>> unsupported;
+  std::set<DeviceFlag> unavailable;
+  const bool gpu = DeviceRegistry::Get().GpuAvailable();
+  for (size_t f = 0; f < EnumLength<DeviceFlag>(); ++f) {
+    const DeviceFlag flag = static_cast<DeviceFlag>(f);
+    unsupported[flag] = {};
+    if (flag == DeviceFlag::kCPU) continue;
+    if (flag != DeviceFlag::kGPU || !gpu) {
+      unavailable.insert(flag);
+      continue;
+    }
+    for (int i = 0; i < num_ops; ++i)
+      if (!GpuSupports(d, d.ops[i], nullptr)) unsupported[flag].insert(i);
+  }
+  ModelSpec spec(num_ops, static_cast<int>(d.tensors.size()), tensor_types,
+                 std::set<int>(d.inputs.begin(), d.inputs.end()),
+                 std::set<int>(d.outputs.begin(), d.outputs.end()), op_in, op_out, unsupported, unavailable);
+  spec.path = hm->GetPath();
+  return spec;
+}
+
+absl::Status HipModelExecutor::DevicePtr(const HipModel& model, int t, PreparedSubgraph* sg, void** ptr) {
+  const TflTensor& tt = model.desc().tensors[t];
+  if (!tt.is_const()) {
+    auto it = sg->offset.find(t);
+    if (it == sg->offset.end()) return absl::InternalError("tensor without arena slot");
+    *ptr = static_cast<char*>(sg->arena->ptr()) + it->second;
+    return absl::OkStatus();
+  }
+  const std::string key = "m" + Hex(model.serial()) + "/t" + std::to_string(t);
+  auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
+  if (!blob) {
+    blob = std::make_shared<DeviceBlob>(ordinal_, tt.data_size);
+    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), tt.data, tt.data_size) != 0)
+      return HipErr(1, "upload constant");
+    DeviceRegistry::Get().PutConst(ordinal_, key, blob);
+  }
+  sg->consts.push_back(blob);
+  *ptr = blob->ptr();
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubgraph* sg) {
+  const TflModel& d = model.desc();
+  const TflOperator& op = d.ops[oi];
+  std::string why;
+  if (!GpuSupports(d, op, &why))
+    return absl::InternalError("HIP backend cannot run op " + std::to_string(oi) + " (" +
+                               TflBuiltinName(op.builtin) + "): " + why);
+  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
+  const TflTensor& in = T(op.inputs[0]);
+  const TflTensor& out = T(op.outputs[0]);
+  void* in_ptr = nullptr;
+  void* out_ptr = nullptr;
+  RETURN_STATUS_IF(DevicePtr(model, op.inputs[0], sg, &in_ptr));
+  RETURN_STATUS_IF(DevicePtr(model, op.outputs[0], sg, &out_ptr));
+  const bool i8 = in.type == DataType::kInt8;
+  const std::string ckey = "m" + Hex(model.serial()) + "/op" + std::to_string(oi);
+  Launch L;
+  L.op_index = oi;
+
+  if (op.builtin == kTflConv2D || op.builtin == kTflDepthwiseConv2D) {
+    const bool dw = op.builtin == kTflDepthwiseConv2D;
+    const TflTensor& w = T(op.inputs[1]);
+    const int32_t* bias = nullptr;
+    if (op.inputs.size() > 2 && op.inputs[2] >= 0) bias = reinterpret_cast<const int32_t*>(T(op.inputs[2]).data);
+    const FbTable& o = op.options;
+    const bool same = o.Int8(0, 0) == 0;
+    const int sw = o.Int(1, 1), sh = o.Int(2, 1);
+    const int act = dw ? o.Int8(4, 0) : o.Int8(3, 0);
+    const int dlw = dw ? o.Int(5, 1) : o.Int(4, 1);
+    const int dlh = dw ? o.Int(6, 1) : o.Int(5, 1);
+    const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], ic = in.shape[3];
+    const int oc = dw ? w.shape[3] : w.shape[0];
+    const int kh = w.shape[1], kw = w.shape[2];
+    const int oh = ComputeOutSize(same, ih, kh, sh, dlh);
+    const int ow = ComputeOutSize(same, iw, kw, sw, dlw);
+    if (out.shape != std::vector<int>{b, oh, ow, oc}) return absl::InternalError("conv output shape mismatch");
+    const int ph = ComputePadding(sh, dlh, ih, kh, oh);
+    const int pw = ComputePadding(sw, dlw, iw, kw, ow);
+    std::vector<int32_t> mult, shift;
+    ConvMultipliers(Scale(in), w.scale, oc, Scale(out), !i8, &mult, &shift);
+    int32_t amin, amax;
+    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &amin, &amax);
+    const int32_t in_zp = Dom(in);
+    const int32_t w_zp = i8 ? 0 : Dom(w);  // int8 kernels ignore the filter zero point
+    const double M = static_cast<double>(b) * oh * ow;
+    if (!dw) {
+      const int K = kh * kw * ic;
+      int kp = 0, np = 0;
+      bh_conv_packed_geometry(oc, K, &kp, &np);
+      const size_t wbytes = static_cast<size_t>(kp) * np;
+      const size_t tbytes = 12ull * oc;
+      auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
+      if (!blob) {
+        std::vector<int8_t> packed(wbytes);
+        std::vector<int32_t> tables(3ull * oc);
+        if (bh_pack_conv_weights(w.data, i8 ? 1 : 0, oc, K, kp, np, bias, in_zp, w_zp, packed.data(), tables.data()) != 0)
+          return absl::InternalError("weight packing failed");
+        std::copy(mult.begin(), mult.end(), tables.begin() + oc);
+        std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
+        blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
+        if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
+            bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+          return HipErr(1, "upload conv operands");
+        DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
+      }
+      sg->consts.push_back(blob);
+      const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
+      bh_conv_params& p = L.conv;
+      p = bh_conv_params{};
+      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic;
+      p.out_h = oh; p.out_w = ow; p.out_c = oc; p.k_h = kh; p.k_w = kw;
+      p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw; p.pad_h = ph; p.pad_w = pw;
+      p.k_pad = kp; p.n_pad = np; p.in_xor = i8 ? 0 : 0x80;
+      p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out); p.act_min = amin; p.act_max = amax;
+      p.input = in_ptr; p.output = out_ptr;
+      p.weights = static_cast<const int8_t*>(blob->ptr());
+      p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+      L.kind = Launch::kConv;
+      L.kernel = "conv_mfma_kernel";
+      L.alg_ops = 2.0 * M * oc * K;
+      L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
+    } else {
+      const int dm = oc / ic;
+      const size_t wbytes = static_cast<size_t>(kh) * kw * oc;
+      const size_t wpad = (wbytes + 15) / 16 * 16;
+      const size_t tbytes = 12ull * oc;
+      auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
+      if (!blob) {
+        std::vector<uint8_t> wd(wpad, 0);
+        for (size_t i = 0; i < wbytes; ++i) wd[i] = i8 ? w.data[i] : static_cast<uint8_t>(w.data[i] ^ 0x80);
+        std::vector<int32_t> tables(3ull * oc, 0);
+        for (int c = 0; c < oc; ++c) tables[c] = bias ? bias[c] : 0;
+        std::copy(mult.begin(), mult.end(), tables.begin() + oc);
+        std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
+        blob = std::make_shared<DeviceBlob>(ordinal_, wpad + tbytes);
+        if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), wd.data(), wpad) != 0 ||
+            bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wpad, tables.data(), tbytes) != 0)
+          return HipErr(1, "upload depthwise operands");
+        DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
+      }
+      sg->consts.push_back(blob);
+      const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wpad);
+      bh_dwconv_params& p = L.dw;
+      p = bh_dwconv_params{};
+      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic;
+      p.out_h = oh; p.out_w = ow; p.out_c = oc; p.depth_multiplier = dm; p.k_h = kh; p.k_w = kw;
+      p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw; p.pad_h = ph; p.pad_w = pw;
+      p.in_xor = i8 ? 0 : 0x80; p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out);
+      p.act_min = amin; p.act_max = amax; p.input = in_ptr; p.output = out_ptr;
+      p.weights = static_cast<const int8_t*>(blob->ptr());
+      p.bias = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+      L.kind = Launch::kDwConv;
+      L.kernel = "dwconv_kernel";
+      L.alg_ops = 2.0 * M * oc * kh * kw;
+      L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(wbytes) + 12.0 * oc;
+    }
+  } else if (op.builtin == kTflFullyConnected) {
+    const TflTensor& w = T(op.inputs[1]);
+    const int32_t* bias = nullptr;
+    if (op.inputs.size() > 2 && op.inputs[2] >= 0) bias = reinterpret_cast<const int32_t*>(T(op.inputs[2]).data);
+    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
+    const int units = w.shape[0], depth = w.shape[1];
+    const int rows = static_cast<int>(in.num_elements() / depth);
+    const int depth_pad = (depth + 15) / 16 * 16;
+    int32_t mult, shift, amin, amax;
+    FullyConnectedMultiplier(Scale(in), Scale(w), Scale(out), &mult, &shift);
+    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &amin, &amax);
+    const int32_t in_zp = Dom(in), w_zp = Dom(w);
+    const size_t wbytes = static_cast<size_t>(units) * depth_pad;
+    const size_t tbytes = 12ull * units;
+    auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
+    if (!blob) {
+      std::vector<int8_t> packed(wbytes, 0);
+      std::vector<int32_t> tables(3ull * units);
+      for (int u = 0; u < units; ++u) {
+        int64_t s = 0;
+        for (int k = 0; k < depth; ++k) {
+          const uint8_t raw = w.data[static_cast<size_t>(u) * depth + k];
+          const int v = i8 ? static_cast<int>(static_cast<int8_t>(raw)) : static_cast<int>(raw) - 128;
+          packed[static_cast<size_t>(u) * depth_pad + k] = static_cast<int8_t>(v);
+          s += v;
+        }
+        tables[u] = static_cast<int32_t>((bias ? bias[u] : 0) - static_cast<int64_t>(in_zp) * s +
+                                         static_cast<int64_t>(depth) * in_zp * w_zp);
+        tables[units + u] = mult;
+        tables[2 * units + u] = shift;
+      }
+      blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
+      if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
+          bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+        return HipErr(1, "upload fc operands");
+      DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
+    }
+    sg->consts.push_back(blob);
+    const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
+    bh_fc_params& p = L.fc;
+    p = bh_fc_params{};
+    p.rows = rows; p.depth = depth; p.depth_pad = depth_pad; p.units = units;
+    p.in_xor = i8 ? 0 : 0x80; p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out);
+    p.act_min = amin; p.act_max = amax; p.input = in_ptr; p.output = out_ptr;
+    p.weights = static_cast<const int8_t*>(blob->ptr());
+    p.bias_eff = tab; p.mult = tab + units; p.shift = tab + 2 * units;
+    L.kind = Launch::kFc;
+    L.kernel = "fc_kernel";
+    L.alg_ops = 2.0 * rows * units * depth;
+    L.alg_bytes = static_cast<double>(rows) * depth + static_cast<double>(rows) * units +
+                  static_cast<double>(units) * depth + 12.0 * units;
+  } else if (op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) {
+    const TflTensor& b = T(op.inputs[1]);
+    void* b_ptr = nullptr;
+    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
+    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
+    bh_eltwise_params& p = L.elt;
+    p = bh_eltwise_params{};
+    p.in_signed = i8 ? 1 : 0;
+    Shape4(in.shape, p.shape_a);
+    Shape4(b.shape, p.shape_b);
+    Shape4(out.shape, p.shape_o);
+    p.a_off = -Zp(in);
+    p.b_off = -Zp(b);
+    p.o_off = Zp(out);
+    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &p.act_min, &p.act_max);
+    if (op.builtin == kTflMul) {
+      p.kind = BH_ELT_MUL;
+      MulMultiplier(Scale(in), Scale(b), Scale(out), &p.o_mult, &p.o_shift);
+    } else {
+      p.kind = BH_ELT_ADD;
+      const AddParams ap = AddSubParams(Scale(in), Scale(b), Scale(out), op.builtin == kTflSub);
+      p.left_shift = ap.left_shift;
+      p.a_mult = ap.m1; p.a_shift = ap.s1;
+      p.b_mult = ap.m2; p.b_shift = ap.s2;
+      p.o_mult = ap.mo; p.o_shift = ap.so;
+    }
+    p.a = in_ptr; p.b = b_ptr; p.out = out_ptr;
+    L.kind = Launch::kEltwise;
+    L.kernel = "eltwise_kernel";
+    L.alg_bytes = static_cast<double>(in.num_elements() + b.num_elements() + out.num_elements());
+  } else if (op.builtin == kTflAveragePool2D || op.builtin == kTflMaxPool2D) {
+    const FbTable& o = op.options;
+    const bool same = o.Int8(0, 0) == 0;
+    const int sw = o.Int(1, 1), sh = o.Int(2, 1), fw = o.Int(3, 1), fh = o.Int(4, 1);
+    const int act = o.Int8(5, 0);
+    bh_pool_params& p = L.pool;
+    p = bh_pool_params{};
+    p.kind = op.builtin == kTflAveragePool2D ? BH_POOL_AVG : BH_POOL_MAX;
+    p.in_signed = i8 ? 1 : 0;
+    p.batch = in.shape[0]; p.in_h = in.shape[1]; p.in_w = in.shape[2]; p.channels = in.shape[3];
+    p.out_h = ComputeOutSize(same, p.in_h, fh, sh, 1);
+    p.out_w = ComputeOutSize(same, p.in_w, fw, sw, 1);
+    p.f_h = fh; p.f_w = fw; p.stride_h = sh; p.stride_w = sw;
+    p.pad_h = ComputePadding(sh, 1, p.in_h, fh, p.out_h);
+    p.pad_w = ComputePadding(sw, 1, p.in_w, fw, p.out_w);
+    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &p.act_min, &p.act_max);
+    p.input = in_ptr; p.output = out_ptr;
+    L.kind = Launch::kPool;
+    L.kernel = "pool_kernel";
+    L.alg_bytes = static_cast<double>(in.num_elements() + out.num_elements());
+  } else {  // RESHAPE / SQUEEZE: same bytes, new dims
+    L.kind = Launch::kCopy;
+    L.kernel = "copy";
+    L.src = in_ptr;
+    L.dst = out_ptr;
+    L.bytes = meta_[op.outputs[0]]->bytes;
+    L.alg_bytes = 2.0 * L.bytes;
+  }
+  sg->launches.push_back(L);
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::set<int> ops, std::set<int> unit_indices) {
+  auto* hm = dynamic_cast<HipModel*>(model);
+  if (!hm || model->GetId() != model_id_)
+    return absl::InternalError("Failed to prepare subgraph: model id " + std::to_string(model ? model->GetId() : -1) +
+                               " != executor's model id " + std::to_string(model_id_));
+  if (!hm->IsInitialized()) return absl::InternalError("Failed to prepare subgraph: model not loaded");
+  if (model_ && model_ != hm) return absl::InternalError("executor already bound to another model object");
+  model_ = hm;
+  RETURN_STATUS_IF(EnsureMeta(*hm));
+  const TflModel& d = hm->desc();
+  const int num_ops = static_cast<int>(d.ops.size());
+  const bool whole = ops.empty();
+  if (whole)
+    for (int i = 0; i < num_ops; ++i) ops.insert(i);
+  for (int i : ops)
+    if (i < 0 || i >= num_ops) return absl::InternalError("op index out of range");
+
+  if (device_flag_ == DeviceFlag::kGPU && (ordinal_ < 0 || !stream_))
+    return absl::InternalError("Failed to create HIP executor: no gfx950 device");
+  auto sg = std::make_unique<PreparedSubgraph>();
+  sg->ops.assign(ops.begin(), ops.end());
+  std::set<int> consumed, produced, touched;
+  for (int i : sg->ops) {
+    for (int t : d.ops[i].inputs)
+      if (t >= 0 && !d.tensors[t].is_const()) { consumed.insert(t); touched.insert(t); }
+    for (int t : d.ops[i].outputs)
+      if (t >= 0 && !d.tensors[t].is_const()) { produced.insert(t); touched.insert(t); }
+  }
+  if (whole) {
+    sg->inputs = d.inputs;
+    sg->outputs = d.outputs;
+  } else {
+    for (int t : consumed)
+      if (!produced.count(t)) sg->inputs.push_back(t);
+    std::set<int> needed_outside(d.outputs.begin(), d.outputs.end());
+    for (int i = 0; i < num_ops; ++i)
+      if (!ops.count(i))
+        for (int t : d.ops[i].inputs)
+          if (t >= 0) needed_outside.insert(t);
+    for (int t : produced)
+      if (needed_outside.count(t)) sg->outputs.push_back(t);
+  }
+
+  // host-pinned boundary mirrors (Band memcpy's job I/O through these)
+  const bool pinned = device_flag_ == DeviceFlag::kGPU;
+  for (int t : sg->inputs) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
+  for (int t : sg->outputs)
+    if (!sg->host.count(t)) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
+  for (auto& kv : sg->host)
+    if (!kv.second->ok()) return absl::InternalError("pinned host allocation failed");
+
+  if (device_flag_ == DeviceFlag::kGPU) {
+    if (ordinal_ < 0 || !stream_) return absl::InternalError("Failed to create HIP executor: no gfx950 device");
+    if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
+    size_t total = 0;
+    for (int t : touched) {
+      sg->offset[t] = total;
+      total += (meta_[t]->bytes + kAlign - 1) / kAlign * kAlign;
+    }
+    sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
+    if (!sg->arena->ok()) return absl::InternalError("HBM arena allocation failed");
+    for (int i : sg->ops) RETURN_STATUS_IF(Lower(*hm, i, sg.get()));
+  } else if (device_flag_ != DeviceFlag::kCPU) {
+    return absl::InternalError(std::string("Unsupported device type ") + ToString(device_flag_));
+  }
+  SubgraphKey key(model->GetId(), worker_id_, unit_indices);
+  auto old = subgraphs_.find(key);
+  if (old != subgraphs_.end() && old->second->graph) bh_graph_destroy(old->second->graph);
+  subgraphs_[key] = std::move(sg);
+  return absl::OkStatus();
+}
+
+PreparedSubgraph* HipModelExecutor::Find(const SubgraphKey& key) const {
+  auto it = subgraphs_.find(key);
+  return it == subgraphs_.end() ? nullptr : it->second.get();
+}
+
+const std::vector<int>& HipModelExecutor::GetInputs(const SubgraphKey& key) const {
+  auto* sg = Find(key);
+  return sg ? sg->inputs : kEmpty;
+}
+const std::vector<int>& HipModelExecutor::GetOutputs(const SubgraphKey& key) const {
+  auto* sg = Find(key);
+  return sg ? sg->outputs : kEmpty;
+}
+const char* HipModelExecutor::GetInputName(const SubgraphKey& key, int index) const {
+  auto* sg = Find(key);
+  if (!sg || index < 0 || index >= static_cast<int>(sg->inputs.size())) return nullptr;
+  return meta_[sg->inputs[index]]->name.c_str();
+}
+const char* HipModelExecutor::GetOutputName(const SubgraphKey& key, int index) const {
+  auto* sg = Find(key);
+  if (!sg || index < 0 || index >= static_cast<int>(sg->outputs.size())) return nullptr;
+  return meta_[sg->outputs[index]]->name.c_str();
+}
+size_t HipModelExecutor::GetNumTensors(const SubgraphKey& key) const { return Find(key) ? meta_.size() : 0; }
+size_t HipModelExecutor::GetNumNodes(const SubgraphKey& key) const {
+  auto* sg = Find(key);
+  return sg ? sg->ops.size() : 0;
+}
+bool HipModelExecutor::HasSubgraph(const SubgraphKey& key) const { return Find(key) != nullptr; }
+
+SubgraphKey HipModelExecutor::GetLargestSubgraphKey() const {
+  SubgraphKey best;
+  size_t most = 0;
+  for (const auto& kv : subgraphs_)
+    if (kv.second->ops.size() > most) {
+      most = kv.second->ops.size();
+      best = kv.first;
+    }
+  return best;
+}
+
+void HipModelExecutor::ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) {
+  for (const auto& kv : subgraphs_) visitor(kv.first);
+}
+
+std::shared_ptr<interface::ITensorView> HipModelExecutor::GetTensorView(const SubgraphKey& key, int index) {
+  auto* sg = Find(key);
+  if (!sg || index < 0 || index >= static_cast<int>(meta_.size())) return nullptr;
+  TensorMeta* m = meta_[index].get();
+  auto h = sg->host.find(index);
+  if (h != sg->host.end()) return std::make_shared<HipTensorView>(m, h->second->data());
+  const TflTensor& t = model_->desc().tensors[index];
+  if (t.is_const())
+    return std::make_shared<HipTensorView>(m, const_cast<char*>(reinterpret_cast<const char*>(t.data)));
+  if (device_flag_ == DeviceFlag::kGPU && sg->offset.count(index)) {
+    // an intermediate of this subgraph: mirror it and copy it back on every run
+    auto buf = std::make_unique<PinnedBuffer>(m->bytes);
+    if (!buf->ok()) return nullptr;
+    char* data = buf->data();
+    sg->host[index] = std::move(buf);
+    sg->extra_d2h.insert(index);
+    if (sg->graph) {
+      bh_set_device(ordinal_);
+      bh_graph_destroy(sg->graph);
+      sg->graph = nullptr;
+    }
+    return std::make_shared<HipTensorView>(m, data);
+  }
+  return std::make_shared<HipTensorView>(m, nullptr);
+}
+
+absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
+  int rc = 0;
+  switch (l.kind) {
+    case Launch::kConv: rc = bh_conv2d_i8(&l.conv, stream_); break;
+    case Launch::kDwConv: rc = bh_dwconv2d_i8(&l.dw, stream_); break;
+    case Launch::kFc: rc = bh_fc_i8(&l.fc, stream_); break;
+    case Launch::kEltwise: rc = bh_eltwise_i8(&l.elt, stream_); break;
+    case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
+    case Launch::kCopy: rc = l.src == l.dst ? 0 : bh_memcpy_d2d_async(l.dst, l.src, l.bytes, stream_); break;
+  }
+  return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::Enqueue(PreparedSubgraph* sg) {
+  char* arena = static_cast<char*>(sg->arena->ptr());
+  for (int t : sg->inputs) {
+    int rc = bh_memcpy_h2d_async(arena + sg->offset.at(t), sg->host.at(t)->data(), meta_[t]->bytes, stream_);
+    if (rc) return HipErr(rc, "H2D input");
+  }
+  for (const Launch& l : sg->launches) RETURN_STATUS_IF(EnqueueLaunch(l));
+  for (int t : sg->outputs) {
+    int rc = bh_memcpy_d2h_async(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes, stream_);
+    if (rc) return HipErr(rc, "D2H output");
+  }
+  for (int t : sg->extra_d2h) {
+    int rc = bh_memcpy_d2h_async(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes, stream_);
+    if (rc) return HipErr(rc, "D2H intermediate");
+  }
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
+  PreparedSubgraph* sg = Find(key);
+  if (!sg) return absl::InternalError("Cannot find subgraph");
+  if (device_flag_ != DeviceFlag::kGPU)
+    return absl::InternalError("HIP backend: CPU workers host model metadata only; jobs must run on kGPU workers");
+  int rc = bh_set_device(ordinal_);
+  if (rc) return HipErr(rc, "hipSetDevice");
+  if (use_graph_ && !sg->graph && sg->runs > 0) {
+    rc = bh_capture_begin(stream_);
+    if (rc) return HipErr(rc, "capture begin");
+    absl::Status s = Enqueue(sg);
+    bh_graph_exec_t g = nullptr;
+    rc = bh_capture_end(stream_, &g);
+    if (!s.ok()) return s;
+    if (rc) return HipErr(rc, "capture end");
+    sg->graph = g;
+  }
+  if (use_graph_ && sg->graph) {
+    rc = bh_graph_launch(sg->graph, stream_);
+    if (rc) return HipErr(rc, "graph launch");
+  } else {
+    RETURN_STATUS_IF(Enqueue(sg));
+  }
+  rc = bh_stream_sync(stream_);
+  if (rc) return HipErr(rc, "stream sync");
+  ++sg->runs;
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out) {
+  PreparedSubgraph* sg = Find(key);
+  if (!sg) return absl::InternalError("Cannot find subgraph");
+  if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("profiling needs a GPU executor");
+  if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
+  const size_t n = sg->launches.size();
+  std::vector<bh_event_t> ev(n + 1, nullptr);
+  for (auto& e : ev)
+    if (bh_event_create(&e) != 0) return HipErr(1, "event create");
+  std::vector<double> acc(n, 0.0);
+  absl::Status status = absl::OkStatus();
+  for (int it = 0; it < iters && status.ok(); ++it) {
+    bh_event_record(ev[0], stream_);
+    for (size_t i = 0; i < n && status.ok(); ++i) {
+      status = EnqueueLaunch(sg->launches[i]);
+      bh_event_record(ev[i + 1], stream_);
+    }
+    if (bh_stream_sync(stream_) != 0) status = HipErr(1, "sync");
+    for (size_t i = 0; i < n && status.ok(); ++i) {
+      float ms = 0;
+      bh_event_elapsed_ms(ev[i], ev[i + 1], &ms);
+      acc[i] += ms;
+    }
+  }
+  for (auto e : ev) bh_event_destroy(e);
+  if (!status.ok()) return status;
+  out->clear();
+  for (size_t i = 0; i < n; ++i) {
+    const Launch& l = sg->launches[i];
+    out->push_back({l.op_index, l.kernel, acc[i] / std::max(iters, 1), l.alg_bytes, l.alg_ops});
+  }
+  return absl::OkStatus();
+}
+
+}  // namespace hip
+}  // namespace band

@@ -1,0 +1,123 @@
+// HipModelExecutor: the IModelExecutor of the HIP backend - the drop-in for
+// band/backend/tfl/model_executor.{h,cc} (TfLiteModelExecutor).
+//
+// Reference contract (file:line in /root/reference):
+//   InvestigateModelSpec   band/backend/tfl/model_executor.cc:48-171
+//   PrepareSubgraph        :173-192 (+ CreateTfLiteInterpreter :327-373)
+//   GetInputs/Outputs/...  :198-224
+//   GetTensorView          :226-229
+//   GetLargestSubgraphKey / HasSubgraph / ForEachSubgraph :231-262
+//   ExecuteSubgraph        :249-255  <- Engine::Invoke band/engine.cc:843-850
+//
+// MI355X design: one executor per (model, worker); weights, requantisation
+// tables and an activation arena are resident in HBM; subgraph boundary
+// tensors have host-pinned mirrors that Band memcpy's through GetData();
+// ExecuteSubgraph = H2D inputs -> kernel sequence -> D2H outputs on the
+// worker's stream, replayed from a hipGraph after the first run, and returns
+// only when the results are on the host (Band timestamps right after,
+// band/worker.cc:274-291).
+#pragma once
+
+#include <map>
+#include <memory>
+#include <set>
+#include <string>
+#include <vector>
+
+#include "backend/hip/device.h"
+#include "backend/hip/model.h"
+#include "backend/hip/tensor.h"
+#include "band/interface/model_executor.h"
+#include "band_hip_kernels.h"
+
+namespace band {
+namespace hip {
+
+struct Launch {
+  enum Kind { kConv, kDwConv, kFc, kEltwise, kPool, kCopy } kind;
+  int op_index = -1;
+  bh_conv_params conv{};
+  bh_dwconv_params dw{};
+  bh_fc_params fc{};
+  bh_eltwise_params elt{};
+  bh_pool_params pool{};
+  void* dst = nullptr;
+  const void* src = nullptr;
+  size_t bytes = 0;
+  double alg_bytes = 0;  // algorithmic HBM bytes per launch (roofline numerator)
+  double alg_ops = 0;    // algorithmic int ops (2 per MAC)
+  const char* kernel = "";
+};
+
+struct OpTiming {
+  int op_index;
+  const char* kernel;
+  double ms;
+  double alg_bytes;
+  double alg_ops;
+};
+
+struct PreparedSubgraph {
+  std::vector<int> ops;
+  std::vector<int> inputs, outputs;
+  std::map<int, size_t> offset;  // arena offset of each non-constant tensor
+  std::shared_ptr<DeviceBlob> arena;
+  std::map<int, std::unique_ptr<PinnedBuffer>> host;  // boundary mirrors
+  std::set<int> extra_d2h;                            // intermediates a view asked for
+  std::vector<Launch> launches;
+  std::vector<std::shared_ptr<DeviceBlob>> consts;
+  bh_graph_exec_t graph = nullptr;
+  int runs = 0;
+};
+
+class HipModelExecutor : public interface::IModelExecutor {
+ public:
+  HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceFlag device_flag,
+                   CpuSet thread_affinity_mask, int num_threads);
+  ~HipModelExecutor() override;
+
+  absl::StatusOr<ModelSpec> InvestigateModelSpec(interface::IModel* model) override;
+  absl::Status PrepareSubgraph(interface::IModel* model, std::set<int> ops = {},
+                               std::set<int> unit_indices = {}) override;
+  BackendType GetBackendType() const override { return BackendType::kTfLite; }
+  const std::vector<int>& GetInputs(const SubgraphKey& key) const override;
+  const std::vector<int>& GetOutputs(const SubgraphKey& key) const override;
+  const char* GetInputName(const SubgraphKey& key, int index) const override;
+  const char* GetOutputName(const SubgraphKey& key, int index) const override;
+  size_t GetNumTensors(const SubgraphKey& key) const override;
+  size_t GetNumNodes(const SubgraphKey& key) const override;
+  std::shared_ptr<interface::ITensorView> GetTensorView(const SubgraphKey& key, int index) override;
+  bool HasSubgraph(const SubgraphKey& key) const override;
+  SubgraphKey GetLargestSubgraphKey() const override;
+  absl::Status ExecuteSubgraph(const SubgraphKey& key) override;
+  void ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) override;
+
+  // --- extensions used by the C ABI / bench (not part of Band's interface) ---
+  void SetUseGraph(bool on) { use_graph_ = on; }
+  // Times every launch of `key` with HIP events on the executor's stream
+  // (eager enqueue, averaged over `iters`).
+  absl::Status ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out);
+  int ordinal() const { return ordinal_; }
+
+  // Whether the GPU kernel set covers `op` of `model` (drives unsupported_ops[kGPU]).
+  static bool GpuSupports(const TflModel& model, const TflOperator& op, std::string* why);
+
+ private:
+  PreparedSubgraph* Find(const SubgraphKey& key) const;
+  absl::Status EnsureMeta(const HipModel& model);
+  absl::Status Lower(const HipModel& model, int op_index, PreparedSubgraph* sg);
+  absl::Status DevicePtr(const HipModel& model, int tensor, PreparedSubgraph* sg, void** ptr);
+  absl::Status Enqueue(PreparedSubgraph* sg);
+  absl::Status EnqueueLaunch(const Launch& l);
+
+  const HipModel* model_ = nullptr;
+  std::vector<std::unique_ptr<TensorMeta>> meta_;
+  std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
+  int ordinal_ = -1;
+  bh_stream_t stream_ = nullptr;
+  bool use_graph_ = true;
+  static const std::vector<int> kEmpty;
+};
+
+}  // namespace hip
+}  // namespace band

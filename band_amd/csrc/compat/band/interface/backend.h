@@ -15,6 +15,7 @@ class IBackendSpecific {
 
 class IBackendUtil {
  public:
+  virtual ~IBackendUtil() = default;
   virtual std::set<DeviceFlag> GetAvailableDevices() const = 0;
 };
 }  // namespace interface

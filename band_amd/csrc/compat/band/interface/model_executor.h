@@ -17,7 +17,7 @@
 
 namespace band {
 namespace interface {
-class ITensorView;
+struct ITensorView;
 
 class IModelExecutor : public IBackendSpecific {
  public:

@@ -1,0 +1,478 @@
+"""Write TFLite schema-v3 flatbuffers and synthesise the BASELINE models.
+
+Five of the six BASELINE.json models are not in the reference's fixtures
+(band/test/data/ holds only mobilenet_v2_1.0_224_quant, retinaface, ICN and
+magenta), and there is no network, so bench and tests build
+them here as .tflite files with the same operator set a TFLite converter
+emits.  Weights are synthetic (seeded) unless converted from a real model.
+
+Nothing here is on the hot path: it produces the *input* of IModel::FromPath
+(band/backend/tfl/model.cc:25-39).  The writer is dependency-free (no
+flatbuffers package): tables are laid out front-to-back with each child
+written after its parent so every uoffset is forward, as the format needs.
+"""
+import struct
+
+import numpy as np
+
+# schema enums
+T_FLOAT32, T_INT32, T_UINT8, T_INT8 = 0, 2, 3, 9
+NP_TO_SCHEMA = {np.dtype(np.float32): T_FLOAT32, np.dtype(np.int32): T_INT32,
+                np.dtype(np.uint8): T_UINT8, np.dtype(np.int8): T_INT8}
+ACT = {"NONE": 0, "RELU": 1, "RELU_N1_TO_1": 2, "RELU6": 3}
+OPC = dict(ADD=0, AVERAGE_POOL_2D=1, CONCATENATION=2, CONV_2D=3, DEPTHWISE_CONV_2D=4,
+           FULLY_CONNECTED=9, LOGISTIC=14, MAX_POOL_2D=17, MUL=18, RESHAPE=22,
+           RESIZE_BILINEAR=23, SOFTMAX=25, CUSTOM=32, PAD=34, SUB=41, QUANTIZE=114)
+# BuiltinOptions union indices
+OPT = dict(Conv2DOptions=1, DepthwiseConv2DOptions=2, Pool2DOptions=5, FullyConnectedOptions=8,
+           SoftmaxOptions=9, ConcatenationOptions=10, AddOptions=11, ReshapeOptions=17,
+           ResizeBilinearOptions=15, MulOptions=21, PadOptions=22, SubOptions=28)
+
+
+# ---------------------------------------------------------------------------
+# minimal flatbuffer serializer
+# ---------------------------------------------------------------------------
+class Table:
+    """fields: {slot: (fmt, value)} for scalars, {slot: ('o', obj)} for children."""
+
+    def __init__(self, **kw):
+        self.fields = {}
+
+    def set(self, slot, fmt, value):
+        self.fields[slot] = (fmt, value)
+        return self
+
+
+class Vec:
+    def __init__(self, fmt, values, align=4):
+        self.fmt = fmt
+        self.values = values
+        self.align = align
+
+
+class VecT:
+    def __init__(self, items):
+        self.items = items
+
+
+class Str:
+    def __init__(self, s):
+        self.s = s.encode() if isinstance(s, str) else bytes(s)
+
+
+class _Writer:
+    def __init__(self):
+        self.buf = bytearray()
+
+    def pad_to(self, n, extra=0):
+        while (len(self.buf) + extra) % n:
+            self.buf.append(0)
+
+    def write(self, obj):
+        if isinstance(obj, Table):
+            return self._table(obj)
+        if isinstance(obj, Vec):
+            return self._vec(obj)
+        if isinstance(obj, VecT):
+            return self._vect(obj)
+        if isinstance(obj, Str):
+            self.pad_to(4)
+            pos = len(self.buf)
+            self.buf += struct.pack("<I", len(obj.s)) + obj.s + b"\0"
+            return pos
+        raise TypeError(obj)
+
+    def _vec(self, v):
+        if isinstance(v.values, (bytes, bytearray, np.ndarray)):
+            raw = bytes(np.ascontiguousarray(v.values).tobytes()) if isinstance(v.values, np.ndarray) else bytes(v.values)
+            n = len(raw) // struct.calcsize("<" + v.fmt)
+        else:
+            raw = b"".join(struct.pack("<" + v.fmt, x) for x in v.values)
+            n = len(v.values)
+        self.pad_to(max(v.align, 4), extra=4)
+        pos = len(self.buf)
+        self.buf += struct.pack("<I", n) + raw
+        return pos
+
+    def _vect(self, v):
+        self.pad_to(4)
+        pos = len(self.buf)
+        self.buf += struct.pack("<I", len(v.items))
+        slots = []
+        for _ in v.items:
+            slots.append(len(self.buf))
+            self.buf += b"\0\0\0\0"
+        for slot, item in zip(slots, v.items):
+            cpos = self.write(item)
+            struct.pack_into("<I", self.buf, slot, cpos - slot)
+        return pos
+
+    def _table(self, t):
+        slots = sorted(t.fields)
+        nslots = (max(slots) + 1) if slots else 0
+        # field layout inside the table: scalars by size (desc), then offsets
+        items = []
+        for s in slots:
+            fmt, val = t.fields[s]
+            size = 4 if fmt == "o" else struct.calcsize("<" + fmt)
+            items.append((size, s, fmt, val))
+        items.sort(key=lambda x: -x[0])
+        layout = {}
+        off = 4  # soffset to vtable
+        for size, s, fmt, val in items:
+            off = (off + size - 1) // size * size
+            layout[s] = off
+            off += size
+        tsize = off
+        vt = struct.pack("<HH", 4 + 2 * nslots, tsize) + b"".join(
+            struct.pack("<H", layout.get(i, 0)) for i in range(nslots))
+        self.pad_to(2)
+        vt_pos = len(self.buf)
+        self.buf += vt
+        self.pad_to(8)
+        tpos = len(self.buf)
+        self.buf += bytearray(tsize)
+        struct.pack_into("<i", self.buf, tpos, tpos - vt_pos)
+        children = []
+        for size, s, fmt, val in items:
+            p = tpos + layout[s]
+            if fmt == "o":
+                children.append((p, val))
+            else:
+                struct.pack_into("<" + fmt, self.buf, p, val)
+        for p, child in children:
+            cpos = self.write(child)
+            struct.pack_into("<I", self.buf, p, cpos - p)
+        return tpos
+
+
+def serialize(root):
+    w = _Writer()
+    w.buf += b"\0\0\0\0TFL3"
+    rpos = w.write(root)
+    struct.pack_into("<I", w.buf, 0, rpos)
+    return bytes(w.buf)
+
+
+# ---------------------------------------------------------------------------
+# model description -> flatbuffer
+# ---------------------------------------------------------------------------
+class ModelBuilder:
+    """Collects tensors / buffers / operators of one subgraph."""
+
+    def __init__(self, description="band_amd synthetic"):
+        self.tensors = []   # dicts
+        self.buffers = [b""]  # buffer 0 is the empty sentinel
+        self.ops = []
+        self.opcodes = []   # (builtin, custom)
+        self.inputs = []
+        self.outputs = []
+        self.description = description
+
+    def tensor(self, name, shape, dtype, scale=None, zero_point=None, qdim=0, data=None):
+        buf = 0
+        if data is not None:
+            arr = np.ascontiguousarray(np.asarray(data, dtype=dtype).reshape(shape))
+            self.buffers.append(arr.tobytes())
+            buf = len(self.buffers) - 1
+        self.tensors.append(dict(name=name, shape=list(shape), type=NP_TO_SCHEMA[np.dtype(dtype)],
+                                 buffer=buf, scale=scale, zero_point=zero_point, qdim=qdim))
+        return len(self.tensors) - 1
+
+    def op(self, builtin, inputs, outputs, options_type=0, options=None, custom=None):
+        key = (OPC[builtin] if isinstance(builtin, str) else builtin, custom)
+        if key not in self.opcodes:
+            self.opcodes.append(key)
+        self.ops.append(dict(opcode=self.opcodes.index(key), inputs=list(inputs), outputs=list(outputs),
+                             options_type=options_type, options=options))
+        return len(self.ops) - 1
+
+    def build(self):
+        tens = []
+        for t in self.tensors:
+            tt = Table().set(0, "o", Vec("i", t["shape"])).set(1, "b", t["type"]).set(2, "I", t["buffer"])
+            tt.set(3, "o", Str(t["name"]))
+            if t["scale"] is not None:
+                sc = [float(x) for x in np.atleast_1d(t["scale"])]
+                zp = [int(x) for x in np.atleast_1d(t["zero_point"] if t["zero_point"] is not None else 0)]
+                if len(zp) != len(sc):
+                    zp = zp * len(sc) if len(zp) == 1 else zp
+                q = Table().set(2, "o", Vec("f", sc)).set(3, "o", Vec("q", zp)).set(6, "i", int(t["qdim"]))
+                tt.set(4, "o", q)
+            tens.append(tt)
+        ops = []
+        for o in self.ops:
+            ot = Table().set(0, "I", o["opcode"]).set(1, "o", Vec("i", o["inputs"])).set(2, "o", Vec("i", o["outputs"]))
+            if o["options_type"]:
+                ot.set(3, "B", o["options_type"]).set(4, "o", o["options"])
+            ops.append(ot)
+        sg = (Table().set(0, "o", VecT(tens)).set(1, "o", Vec("i", self.inputs))
+              .set(2, "o", Vec("i", self.outputs)).set(3, "o", VecT(ops)).set(4, "o", Str("main")))
+        codes = []
+        for b, c in self.opcodes:
+            oc = Table().set(0, "b", min(b, 127)).set(2, "i", 1).set(3, "i", b)
+            if c:
+                oc.set(1, "o", Str(c))
+            codes.append(oc)
+        bufs = [Table() if not b else Table().set(0, "o", Vec("B", b, align=16)) for b in self.buffers]
+        root = (Table().set(0, "I", 3).set(1, "o", VecT(codes)).set(2, "o", VecT([sg]))
+                .set(3, "o", Str(self.description)).set(4, "o", VecT(bufs)))
+        return serialize(root)
+
+
+def conv_options(padding, stride, act, dilation=1):
+    return (Table().set(0, "b", 0 if padding == "SAME" else 1).set(1, "i", stride).set(2, "i", stride)
+            .set(3, "b", ACT[act]).set(4, "i", dilation).set(5, "i", dilation))
+
+
+def dw_options(padding, stride, act, dm=1, dilation=1):
+    return (Table().set(0, "b", 0 if padding == "SAME" else 1).set(1, "i", stride).set(2, "i", stride)
+            .set(3, "i", dm).set(4, "b", ACT[act]).set(5, "i", dilation).set(6, "i", dilation))
+
+
+def pool_options(padding, stride, filt, act="NONE"):
+    return (Table().set(0, "b", 0 if padding == "SAME" else 1).set(1, "i", stride).set(2, "i", stride)
+            .set(3, "i", filt[1]).set(4, "i", filt[0]).set(5, "b", ACT[act]))
+
+
+def act_options(act="NONE"):
+    return Table().set(0, "b", ACT[act])
+
+
+# ---------------------------------------------------------------------------
+# quantised graph construction with synthetic (seeded) weights
+# ---------------------------------------------------------------------------
+class QGraph:
+    """Builds an int8 (per-channel) or uint8 (per-tensor) NHWC graph.
+
+    Output scales are set analytically so activations stay spread over the
+    8-bit range (acc std ~ sqrt(K)*50*73 LSB products mapped to ~40 LSB)
+    instead of saturating, which keeps the bit-exact checks meaningful.
+    """
+
+    def __init__(self, dtype=np.int8, seed=0, name="model"):
+        self.dtype = np.dtype(dtype)
+        self.rng = np.random.default_rng(seed)
+        self.mb = ModelBuilder(name)
+        self.n = 0
+        self.meta = {}  # tensor -> (shape, scale, zp)
+
+    def _name(self, kind):
+        self.n += 1
+        return "%s_%d" % (kind, self.n)
+
+    def _act_zp(self):
+        return int(self.rng.integers(-20, 21)) if self.dtype == np.int8 else int(self.rng.integers(108, 149))
+
+    def act_tensor(self, shape, scale, zp, kind="act"):
+        t = self.mb.tensor(self._name(kind), shape, self.dtype, scale=[scale], zero_point=[zp])
+        self.meta[t] = (list(shape), scale, zp)
+        return t
+
+    def input(self, shape, scale=0.0078125, zp=None):
+        zp = (0 if self.dtype == np.int8 else 128) if zp is None else zp
+        t = self.act_tensor(shape, scale, zp, "input")
+        self.mb.inputs.append(t)
+        return t
+
+    def output(self, t):
+        self.mb.outputs.append(t)
+
+    def _weights(self, shape, out_c, qdim):
+        if self.dtype == np.int8:
+            w = self.rng.integers(-127, 128, size=shape).astype(np.int8)
+            ws = np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2), size=out_c)).astype(np.float32)
+            wt = self.mb.tensor(self._name("weights"), shape, np.int8, scale=ws, zero_point=[0] * out_c,
+                                qdim=qdim, data=w)
+            return wt, ws
+        w = self.rng.integers(0, 256, size=shape).astype(np.uint8)
+        ws = np.array([np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2)))], np.float32)
+        wt = self.mb.tensor(self._name("weights"), shape, np.uint8, scale=ws,
+                            zero_point=[int(self.rng.integers(100, 156))], data=w)
+        return wt, ws
+
+    def _bias(self, out_c, in_scale, ws):
+        b = self.rng.integers(-(1 << 12), 1 << 12, size=out_c).astype(np.int32)
+        bs = (in_scale * (ws if len(ws) > 1 else np.repeat(ws, out_c))).astype(np.float32)
+        return self.mb.tensor(self._name("bias"), [out_c], np.int32, scale=bs, zero_point=[0] * out_c, data=b)
+
+    def _out_scale(self, in_scale, ws, K):
+        return float(in_scale * float(np.mean(ws)) * np.sqrt(K) * 50.0 * 73.0 / 40.0)
+
+    def conv(self, x, out_c, k=1, stride=1, act="RELU6", padding="SAME", dilation=1):
+        shp, s_in, _ = self.meta[x]
+        b, h, w, c = shp
+        wt, ws = self._weights([out_c, k, k, c], out_c, 0)
+        bt = self._bias(out_c, s_in, ws)
+        eff = (k - 1) * dilation + 1
+        oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
+        ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
+        y = self.act_tensor([b, oh, ow, out_c], self._out_scale(s_in, ws, k * k * c), self._act_zp())
+        self.mb.op("CONV_2D", [x, wt, bt], [y], OPT["Conv2DOptions"], conv_options(padding, stride, act, dilation))
+        return y
+
+    def dwconv(self, x, k=3, stride=1, act="RELU6", padding="SAME", dm=1, dilation=1):
+        shp, s_in, _ = self.meta[x]
+        b, h, w, c = shp
+        oc = c * dm
+        wt, ws = self._weights([1, k, k, oc], oc, 3)
+        bt = self._bias(oc, s_in, ws)
+        eff = (k - 1) * dilation + 1
+        oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
+        ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
+        y = self.act_tensor([b, oh, ow, oc], self._out_scale(s_in, ws, k * k), self._act_zp())
+        self.mb.op("DEPTHWISE_CONV_2D", [x, wt, bt], [y], OPT["DepthwiseConv2DOptions"],
+                   dw_options(padding, stride, act, dm, dilation))
+        return y
+
+    def add(self, a, b, act="NONE"):
+        shp, sa, _ = self.meta[a]
+        _, sb, _ = self.meta[b]
+        y = self.act_tensor(shp, float(max(sa, sb) * 1.4), self._act_zp())
+        self.mb.op("ADD", [a, b], [y], OPT["AddOptions"], act_options(act))
+        return y
+
+    def avgpool(self, x, filt, stride=1, padding="VALID"):
+        shp, s, z = self.meta[x]
+        b, h, w, c = shp
+        oh = (h + stride - filt[0]) // stride if padding == "VALID" else (h + stride - 1) // stride
+        ow = (w + stride - filt[1]) // stride if padding == "VALID" else (w + stride - 1) // stride
+        y = self.act_tensor([b, oh, ow, c], s, z)
+        self.mb.op("AVERAGE_POOL_2D", [x], [y], OPT["Pool2DOptions"], pool_options(padding, stride, filt))
+        return y
+
+    def maxpool(self, x, filt, stride, padding="SAME"):
+        shp, s, z = self.meta[x]
+        b, h, w, c = shp
+        oh = (h + stride - filt[0]) // stride if padding == "VALID" else (h + stride - 1) // stride
+        ow = (w + stride - filt[1]) // stride if padding == "VALID" else (w + stride - 1) // stride
+        y = self.act_tensor([b, oh, ow, c], s, z)
+        self.mb.op("MAX_POOL_2D", [x], [y], OPT["Pool2DOptions"], pool_options(padding, stride, filt))
+        return y
+
+    def reshape(self, x, shape):
+        _, s, z = self.meta[x]
+        st = self.mb.tensor(self._name("shape"), [len(shape)], np.int32, data=np.array(shape, np.int32))
+        y = self.act_tensor(list(shape), s, z)
+        self.mb.op("RESHAPE", [x, st], [y], OPT["ReshapeOptions"], Table().set(0, "o", Vec("i", list(shape))))
+        return y
+
+    def fully_connected(self, x, units, act="NONE"):
+        shp, s_in, _ = self.meta[x]
+        depth = shp[-1]
+        rows = int(np.prod(shp)) // depth
+        w = (self.rng.integers(-127, 128, size=(units, depth)).astype(np.int8) if self.dtype == np.int8
+             else self.rng.integers(0, 256, size=(units, depth)).astype(np.uint8))
+        ws = np.array([np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2)))], np.float32)
+        wzp = 0 if self.dtype == np.int8 else int(self.rng.integers(100, 156))
+        wt = self.mb.tensor(self._name("fc_weights"), [units, depth], self.dtype, scale=ws, zero_point=[wzp], data=w)
+        bt = self._bias(units, s_in, ws)
+        y = self.act_tensor([rows, units], self._out_scale(s_in, ws, depth), self._act_zp())
+        self.mb.op("FULLY_CONNECTED", [x, wt, bt], [y], OPT["FullyConnectedOptions"], act_options(act))
+        return y
+
+    def build(self):
+        return self.mb.build()
+
+
+# ---------------------------------------------------------------------------
+# BASELINE models
+# ---------------------------------------------------------------------------
+MNV2_BLOCKS = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 96, 3, 1),
+               (6, 160, 3, 2), (6, 320, 1, 1)]
+
+
+def mobilenet_v2(dtype=np.int8, seed=0, size=224, batch=1, classes=1001, width=1.0):
+    """MobileNetV2-1.0 with the topology of mobilenet_v2_1.0_224_quant.tflite
+    (65 ops: 36 CONV_2D, 17 DEPTHWISE_CONV_2D, 10 ADD, AVERAGE_POOL_2D, RESHAPE)."""
+    g = QGraph(dtype, seed, "mobilenet_v2_%s" % np.dtype(dtype).name)
+    ch = lambda c: max(8, int(c * width + 4) // 8 * 8)
+    x = g.input([batch, size, size, 3])
+    x = g.conv(x, ch(32), k=3, stride=2)
+    c_in = ch(32)
+    for t, c, n, s in MNV2_BLOCKS:
+        for i in range(n):
+            inp = x
+            stride = s if i == 0 else 1
+            h = x
+            if t != 1:
+                h = g.conv(h, c_in * t, k=1)
+            h = g.dwconv(h, k=3, stride=stride)
+            h = g.conv(h, ch(c), k=1, act="NONE")
+            if stride == 1 and c_in == ch(c):
+                h = g.add(h, inp)
+            x = h
+            c_in = ch(c)
+    x = g.conv(x, 1280 if width <= 1.0 else ch(1280), k=1)
+    k = size // 32
+    x = g.avgpool(x, (k, k))
+    x = g.conv(x, classes, k=1, act="NONE")
+    x = g.reshape(x, [batch, classes])
+    g.output(x)
+    return g.build()
+
+
+def mobilenet_v1(dtype=np.int8, seed=0, size=224, batch=1, classes=1001):
+    """MobileNetV1-1.0 (config C1): conv + 13 depthwise-separable blocks."""
+    g = QGraph(dtype, seed, "mobilenet_v1_%s" % np.dtype(dtype).name)
+    x = g.input([batch, size, size, 3])
+    x = g.conv(x, 32, k=3, stride=2)
+    for c, s in [(64, 1), (128, 2), (128, 1), (256, 2), (256, 1), (512, 2), (512, 1), (512, 1),
+                 (512, 1), (512, 1), (512, 1), (1024, 2), (1024, 1)]:
+        x = g.dwconv(x, stride=s)
+        x = g.conv(x, c, k=1)
+    k = size // 32
+    x = g.avgpool(x, (k, k))
+    x = g.conv(x, classes, k=1, act="NONE")
+    x = g.reshape(x, [batch, classes])
+    g.output(x)
+    return g.build()
+
+
+def int8_from_uint8(model_bytes):
+    """Convert a uint8 per-tensor TFLite model to int8 per-channel with the
+    same float semantics (what TFLite's converter emits for int8): activations
+    shift by -128 (same scale), conv/dw filters re-quantised symmetric per
+    output channel, biases re-scaled to in_scale*w_scale[c]."""
+    from .tflite_reader_py import read  # local, dependency-free reader
+    m = read(model_bytes)
+    mb = ModelBuilder("int8 conversion of %s" % m["description"])
+    tmap = {}
+    new_w = {}
+    # per-op filter / bias conversion
+    for op in m["ops"]:
+        if op["builtin"] in (OPC["CONV_2D"], OPC["DEPTHWISE_CONV_2D"]):
+            x, w, b = op["inputs"][:3]
+            tw, tb, tx = m["tensors"][w], m["tensors"][b], m["tensors"][x]
+            wf = (tw["data"].astype(np.float32) - tw["zero_point"][0]) * tw["scale"][0]
+            qdim = 0 if op["builtin"] == OPC["CONV_2D"] else 3
+            axes = tuple(i for i in range(4) if i != qdim)
+            amax = np.max(np.abs(wf), axis=axes)
+            sc = np.where(amax > 0, amax / 127.0, 1e-8).astype(np.float32)
+            shp = [1, 1, 1, 1]
+            shp[qdim] = -1
+            wq = np.clip(np.round(wf / sc.reshape(shp)), -127, 127).astype(np.int8)
+            bf = tb["data"].astype(np.float64) * tb["scale"][0]
+            bsc = (np.float32(tx["scale"][0]) * sc).astype(np.float32)
+            bq = np.round(bf / bsc.astype(np.float64)).astype(np.int32)
+            new_w[w] = (wq, sc, qdim)
+            new_w[b] = (bq, bsc, 0)
+    for i, t in enumerate(m["tensors"]):
+        if i in new_w:
+            data, sc, qd = new_w[i]
+            tmap[i] = mb.tensor(t["name"], t["shape"], data.dtype, scale=sc, zero_point=[0] * len(sc),
+                                qdim=qd, data=data)
+        elif t["type"] == T_UINT8:
+            zp = [z - 128 for z in t["zero_point"]] if t["zero_point"] is not None else None
+            data = None if t["data"] is None else (t["data"].astype(np.int16) - 128).astype(np.int8)
+            tmap[i] = mb.tensor(t["name"], t["shape"], np.int8, scale=t["scale"], zero_point=zp, data=data)
+        else:
+            dt = {T_INT32: np.int32, T_FLOAT32: np.float32, T_INT8: np.int8}[t["type"]]
+            tmap[i] = mb.tensor(t["name"], t["shape"], dt, scale=t["scale"], zero_point=t["zero_point"],
+                                data=t["data"])
+    for op in m["ops"]:
+        mb.op(op["builtin"], [tmap[i] if i >= 0 else -1 for i in op["inputs"]], [tmap[i] for i in op["outputs"]],
+              op["options_type"], op["options"])
+    mb.inputs = [tmap[i] for i in m["inputs"]]
+    mb.outputs = [tmap[i] for i in m["outputs"]]
+    return mb.build()

@@ -1,0 +1,106 @@
+/*
+ * band_hip_backend.h - C ABI over the HIP backend's Band plugin objects.
+ *
+ * Band binds its backend through C++ virtuals (band/interface/model.h:17-38,
+ * band/interface/model_executor.h:30-180, band/interface/tensor.h:27-50,
+ * band/interface/backend.h:21-26), created by BackendFactory
+ * (band/backend_factory.h:31-70).  Inside a Band build those are used
+ * directly.  This header exposes the same objects with
+ * plain pointers and sizes so any FFI (ctypes, JNI, cgo) can drive them;
+ * each function names the interface method it forwards to.
+ *
+ * Subgraph keys are passed as (model_id, worker_id, unit_mask) where bit i of
+ * unit_mask is unit subgraph i (SubgraphKey's 64-bit BitMask,
+ * band/common.h:293-319).  Device flags use Band's DeviceFlag numbering
+ * (0 CPU, 1 GPU, 2 DSP, 3 NPU); data types use Band's DataType (== TfLiteType).
+ *
+ * Return codes: 0 = OK; otherwise the absl::StatusCode of the failing call
+ * (13 = kInternal) with the message available from bhx_last_error().
+ */
+#ifndef BAND_HIP_BACKEND_H_
+#define BAND_HIP_BACKEND_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct bhx_model bhx_model;
+typedef struct bhx_executor bhx_executor;
+
+typedef struct bhx_tensor_info {
+  int type;           /* Band DataType */
+  int ndims;
+  int dims[8];
+  void* data;         /* host-addressable view data (ITensorView::GetData) */
+  size_t bytes;       /* ITensorView::GetBytes */
+  const char* name;   /* ITensorView::GetName */
+  int quant_type;     /* QuantizationType: 0 none, 1 affine */
+  int n_quant;        /* number of scales / zero points */
+  const float* scale;
+  const int32_t* zero_point;
+  int quantized_dimension;
+} bhx_tensor_info;
+
+typedef struct bhx_op_timing {
+  int op_index;
+  const char* kernel;
+  double ms;          /* mean HIP-event time of the launch */
+  double alg_bytes;   /* algorithmic bytes per launch */
+  double alg_ops;     /* algorithmic integer ops per launch (2 per MAC) */
+} bhx_op_timing;
+
+const char* bhx_last_error(void);
+
+/* IBackendUtil::GetAvailableDevices -> bit i set = DeviceFlag i available */
+int bhx_available_devices(uint32_t* mask);
+/* pin a Band worker id to a GPU ordinal (one process per GPU launchers) */
+int bhx_set_worker_device(int worker_id, int ordinal);
+
+/* IModel (BackendFactory::CreateModel + FromPath/FromBuffer/IsInitialized) */
+int bhx_model_create(int model_id, bhx_model** out);
+int bhx_model_from_path(bhx_model* m, const char* path);
+int bhx_model_from_buffer(bhx_model* m, const char* buffer, size_t size);
+int bhx_model_is_initialized(const bhx_model* m);
+int bhx_model_get_id(const bhx_model* m);
+void bhx_model_destroy(bhx_model* m);
+
+/* IModelExecutor (BackendFactory::CreateModelExecutor) */
+int bhx_executor_create(int model_id, int worker_id, int device_flag, int num_threads, bhx_executor** out);
+void bhx_executor_destroy(bhx_executor* e);
+/* InvestigateModelSpec -> ModelSpec serialised as JSON into buf.
+ * *needed receives the full length (+1); the call fails if cap < needed. */
+int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed);
+/* PrepareSubgraph(model, ops, unit_indices); n_ops == 0 -> whole model */
+int bhx_prepare_subgraph(bhx_executor* e, bhx_model* m, const int* ops, int n_ops,
+                         const int* unit_indices, int n_units);
+int bhx_has_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask);
+/* GetInputs / GetOutputs: writes up to cap indices, *n = total count */
+int bhx_get_inputs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int* out, int cap, int* n);
+int bhx_get_outputs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int* out, int cap, int* n);
+const char* bhx_get_input_name(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int index);
+const char* bhx_get_output_name(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int index);
+size_t bhx_get_num_tensors(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask);
+size_t bhx_get_num_nodes(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask);
+/* GetTensorView: fills info; data stays valid for the executor's lifetime */
+int bhx_get_tensor_view(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int tensor_index,
+                        bhx_tensor_info* info);
+int bhx_get_largest_subgraph_key(bhx_executor* e, int* model_id, int* worker_id, uint64_t* unit_mask);
+/* ForEachSubgraph: writes up to cap keys */
+int bhx_list_subgraphs(bhx_executor* e, int* model_ids, int* worker_ids, uint64_t* unit_masks, int cap, int* n);
+/* ExecuteSubgraph (synchronous: returns when outputs are in the views) */
+int bhx_execute_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask);
+
+/* --- extensions (measurement / tuning; not part of Band's interface) --- */
+int bhx_executor_set_graph(bhx_executor* e, int enabled);
+int bhx_executor_device(bhx_executor* e, int* ordinal);
+/* per-launch HIP-event timing of a prepared subgraph, averaged over iters */
+int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
+                         bhx_op_timing* out, int cap, int* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BAND_HIP_BACKEND_H_ */

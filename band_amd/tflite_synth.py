@@ -245,9 +245,11 @@ def act_options(act="NONE"):
 class QGraph:
     """Builds an int8 (per-channel) or uint8 (per-tensor) NHWC graph.
 
-    Output scales are set analytically so activations stay spread over the
-    8-bit range (acc std ~ sqrt(K)*50*73 LSB products mapped to ~40 LSB)
-    instead of saturating, which keeps the bit-exact checks meaningful.
+    Scales mimic converter output (RELU6 tensors at 6/255) and filter scales
+    are chosen per layer so activations stay spread over the 8-bit range
+    instead of collapsing or saturating, which keeps bit-exact checks
+    meaningful (BASELINE.md's log-uniform [1e-3, 2e-2] filter scales collapse
+    a 65-op network to constants within a few layers).
     """
 
     def __init__(self, dtype=np.int8, seed=0, name="model"):
@@ -278,36 +280,47 @@ class QGraph:
     def output(self, t):
         self.mb.outputs.append(t)
 
-    def _weights(self, shape, out_c, qdim):
+    def _out_q(self, act, s_in):
+        """Output (scale, zero point) the way converted models look: RELU6/RELU
+        outputs cover [0, 6] (scale 6/255, zero point at the range bottom);
+        linear outputs keep the input scale around a small zero point."""
+        if act in ("RELU6", "RELU"):
+            return 6.0 / 255.0, (-128 if self.dtype == np.int8 else 0)
+        return float(s_in), self._act_zp()
+
+    def _weights(self, shape, out_c, qdim, s_in, s_out, K):
+        # filter scale chosen so sum_k x*w lands ~40 output LSBs wide
+        # (|x - zp| ~ 45 LSB, |w| ~ 73 LSB), jittered per channel
+        base = 40.0 * s_out / (s_in * np.sqrt(K) * 45.0 * 73.0)
         if self.dtype == np.int8:
             w = self.rng.integers(-127, 128, size=shape).astype(np.int8)
-            ws = np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2), size=out_c)).astype(np.float32)
+            ws = (base * np.exp(self.rng.uniform(-0.4, 0.4, size=out_c))).astype(np.float32)
             wt = self.mb.tensor(self._name("weights"), shape, np.int8, scale=ws, zero_point=[0] * out_c,
                                 qdim=qdim, data=w)
             return wt, ws
         w = self.rng.integers(0, 256, size=shape).astype(np.uint8)
-        ws = np.array([np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2)))], np.float32)
+        ws = np.array([base * np.exp(self.rng.uniform(-0.4, 0.4))], np.float32)
         wt = self.mb.tensor(self._name("weights"), shape, np.uint8, scale=ws,
-                            zero_point=[int(self.rng.integers(100, 156))], data=w)
+                            zero_point=[int(self.rng.integers(125, 132))], data=w)
         return wt, ws
 
-    def _bias(self, out_c, in_scale, ws):
-        b = self.rng.integers(-(1 << 12), 1 << 12, size=out_c).astype(np.int32)
-        bs = (in_scale * (ws if len(ws) > 1 else np.repeat(ws, out_c))).astype(np.float32)
+    def _bias(self, out_c, in_scale, ws, K):
+        lim = max(1, int(np.sqrt(K) * 45 * 73 / 3))
+        b = self.rng.integers(-lim, lim + 1, size=out_c).astype(np.int32)
+        bs = (np.float32(in_scale) * (ws if len(ws) > 1 else np.repeat(ws, out_c))).astype(np.float32)
         return self.mb.tensor(self._name("bias"), [out_c], np.int32, scale=bs, zero_point=[0] * out_c, data=b)
-
-    def _out_scale(self, in_scale, ws, K):
-        return float(in_scale * float(np.mean(ws)) * np.sqrt(K) * 50.0 * 73.0 / 40.0)
 
     def conv(self, x, out_c, k=1, stride=1, act="RELU6", padding="SAME", dilation=1):
         shp, s_in, _ = self.meta[x]
         b, h, w, c = shp
-        wt, ws = self._weights([out_c, k, k, c], out_c, 0)
-        bt = self._bias(out_c, s_in, ws)
+        s_out, zp = self._out_q(act, s_in)
+        K = k * k * c
+        wt, ws = self._weights([out_c, k, k, c], out_c, 0, s_in, s_out, K)
+        bt = self._bias(out_c, s_in, ws, K)
         eff = (k - 1) * dilation + 1
         oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
         ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
-        y = self.act_tensor([b, oh, ow, out_c], self._out_scale(s_in, ws, k * k * c), self._act_zp())
+        y = self.act_tensor([b, oh, ow, out_c], s_out, zp)
         self.mb.op("CONV_2D", [x, wt, bt], [y], OPT["Conv2DOptions"], conv_options(padding, stride, act, dilation))
         return y
 
@@ -315,12 +328,13 @@ class QGraph:
         shp, s_in, _ = self.meta[x]
         b, h, w, c = shp
         oc = c * dm
-        wt, ws = self._weights([1, k, k, oc], oc, 3)
-        bt = self._bias(oc, s_in, ws)
+        s_out, zp = self._out_q(act, s_in)
+        wt, ws = self._weights([1, k, k, oc], oc, 3, s_in, s_out, k * k)
+        bt = self._bias(oc, s_in, ws, k * k)
         eff = (k - 1) * dilation + 1
         oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
         ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
-        y = self.act_tensor([b, oh, ow, oc], self._out_scale(s_in, ws, k * k), self._act_zp())
+        y = self.act_tensor([b, oh, ow, oc], s_out, zp)
         self.mb.op("DEPTHWISE_CONV_2D", [x, wt, bt], [y], OPT["DepthwiseConv2DOptions"],
                    dw_options(padding, stride, act, dm, dilation))
         return y
@@ -364,10 +378,12 @@ class QGraph:
         w = (self.rng.integers(-127, 128, size=(units, depth)).astype(np.int8) if self.dtype == np.int8
              else self.rng.integers(0, 256, size=(units, depth)).astype(np.uint8))
         ws = np.array([np.exp(self.rng.uniform(np.log(1e-3), np.log(2e-2)))], np.float32)
-        wzp = 0 if self.dtype == np.int8 else int(self.rng.integers(100, 156))
+        wzp = 0 if self.dtype == np.int8 else int(self.rng.integers(125, 132))
+        s_out, zp = self._out_q(act, s_in)
+        ws = np.array([40.0 * s_out / (s_in * np.sqrt(depth) * 45.0 * 73.0)], np.float32)
         wt = self.mb.tensor(self._name("fc_weights"), [units, depth], self.dtype, scale=ws, zero_point=[wzp], data=w)
-        bt = self._bias(units, s_in, ws)
-        y = self.act_tensor([rows, units], self._out_scale(s_in, ws, depth), self._act_zp())
+        bt = self._bias(units, s_in, ws, depth)
+        y = self.act_tensor([rows, units], s_out, zp)
         self.mb.op("FULLY_CONNECTED", [x, wt, bt], [y], OPT["FullyConnectedOptions"], act_options(act))
         return y
 
@@ -448,7 +464,7 @@ def int8_from_uint8(model_bytes):
             qdim = 0 if op["builtin"] == OPC["CONV_2D"] else 3
             axes = tuple(i for i in range(4) if i != qdim)
             amax = np.max(np.abs(wf), axis=axes)
-            sc = np.where(amax > 0, amax / 127.0, 1e-8).astype(np.float32)
+            sc = np.where(amax > 0, amax / 127.0, 1.0).astype(np.float32)
             shp = [1, 1, 1, 1]
             shp[qdim] = -1
             wq = np.clip(np.round(wf / sc.reshape(shp)), -127, 127).astype(np.int8)

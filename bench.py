@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Headline benchmark: multi-DNN inferences/s + p99 job latency (BASELINE.json).
+
+Workload (N=1): BASELINE config C2 - MobileNetV2-224 int8 (synthetic seeded
+weights, TFLite-converter-shaped quantisation), GPU worker(s) on one MI355X,
+fixed-worker placement.  A "step" is one Band job: the per-job work of
+`Worker::Work` (band/worker.cc:222-323) - copy the request's input into the
+executor's input view (Engine::TryCopyInputTensors, band/engine.cc:1247-1319),
+`IModelExecutor::ExecuteSubgraph` (band/engine.cc:843-850), copy the output
+view out (TryCopyOutputTensors :1333-1365).  Job latency = end - enqueue
+(band/common.h:351-353).  Several Band GPU workers may share one GPU (each
+its own executor + HIP stream, like AddWorkers({kGPU, kGPU, ...})).
+
+N>1: one process per GPU (torchrun), jobs shard across GPUs with no
+data-path collective (weak scaling); a gloo process group only provides the
+barrier and the max-over-ranks timing.  The GPU is driven exclusively
+through libband_hip.so; torch never touches the device here.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import platform
+import tempfile
+import threading
+import time
+
+import numpy as np
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=4000, help="jobs per rank in the timed region")
+    p.add_argument("--warmup", type=int, default=400)
+    p.add_argument("--workers-per-gpu", type=int, default=4)
+    p.add_argument("--model", default="mobilenet_v2_int8",
+                   choices=["mobilenet_v2_int8", "mobilenet_v2_uint8", "mobilenet_v1_int8"])
+    p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--profile-iters", type=int, default=20)
+    return p.parse_args()
+
+
+def model_bytes(name):
+    from band_amd import tflite_synth as S
+    if name == "mobilenet_v2_int8":
+        return S.mobilenet_v2(np.int8, seed=0)
+    if name == "mobilenet_v2_uint8":
+        return S.mobilenet_v2(np.uint8, seed=0)
+    return S.mobilenet_v1(np.int8, seed=0)
+
+
+class Dist:
+    """barrier + max/gather over ranks (gloo, CPU only) when WORLD_SIZE > 1"""
+
+    def __init__(self):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, v):
+        if not self.dist:
+            return v
+        import torch
+        t = torch.tensor([v], dtype=torch.float64)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+def run_worker(ex, key, in_view, out_view, inputs, n_jobs, lat, results, idx):
+    """One Band GPU worker thread: closed-loop jobs."""
+    src_slots = inputs
+    ring_out = np.empty_like(out_view)
+    ok = True
+    for j in range(n_jobs):
+        t_enq = time.perf_counter()
+        in_view[...] = src_slots[j % len(src_slots)]       # TryCopyInputTensors
+        st = ex.ExecuteSubgraph(key)                        # Engine::Invoke
+        ring_out[...] = out_view                            # TryCopyOutputTensors
+        lat.append(time.perf_counter() - t_enq)
+        if not st.ok():
+            ok = False
+            results[idx] = st.message()
+            return
+    results[idx] = ok
+
+
+def cpu_baseline(model_buf, seconds):
+    """Oracle (scalar C port of TFLite's reference kernels) on the host."""
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model
+    m = Model(model_buf)
+    interp = OracleInterpreter(m)
+    rng = np.random.default_rng(5489)
+    t_in = m.tensors[m.inputs[0]]
+    lo, hi = (-127, 128) if t_in.np_dtype == np.int8 else (0, 255)
+    x = rng.integers(lo, hi, t_in.shape).astype(t_in.np_dtype)
+    interp.run({m.inputs[0]: x})  # warm
+    n, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        interp.run({m.inputs[0]: x})
+        n += 1
+    dt = time.perf_counter() - t0
+    return dict(value=n / dt, unit="inferences/s", cores=1, kind="port",
+                sample="%d MobileNetV2-224 %s inferences on 1 host core (%.1f s)" % (n, t_in.np_dtype.__name__, dt))
+
+
+def main():
+    args = parse()
+    D = Dist()
+    import band_amd
+    from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
+
+    buf = model_bytes(args.model)
+    tmp = tempfile.NamedTemporaryFile(prefix="band_bench_", suffix=".tflite", delete=False)
+    tmp.write(buf)
+    tmp.close()
+
+    W = max(1, args.workers_per_gpu)
+    workers = []
+    m = HipModel(0)  # one IModel shared by every worker's executor, as in Band
+    st = m.FromPath(tmp.name)
+    assert st.ok(), st
+    for w in range(W):
+        wid = 1 + w  # worker 0 is Band's CPU worker
+        band_amd.SetWorkerDevice(wid, D.local_rank)
+        ex = HipModelExecutor(0, wid, DeviceFlag.kGPU)
+        if args.no_graph:
+            ex.SetUseGraph(False)
+        spec = ex.InvestigateModelSpec(m)
+        assert not spec.unsupported_ops[DeviceFlag.kGPU], spec.unsupported_ops
+        st = ex.PrepareSubgraph(m)
+        assert st.ok(), st
+        key = SubgraphKey(0, wid)
+        iv = ex.GetTensorView(key, ex.GetInputs(key)[0])
+        ov = ex.GetTensorView(key, ex.GetOutputs(key)[0])
+        workers.append((m, ex, key, iv.GetData(), ov.GetData()))
+    os.unlink(tmp.name)
+
+    # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
+    rng = np.random.default_rng(5489 + D.rank)
+    in_arr = workers[0][3]
+    lo, hi = (-127, 128) if in_arr.dtype == np.int8 else (0, 255)
+    inputs = [rng.integers(lo, hi, in_arr.shape).astype(in_arr.dtype) for _ in range(8)]
+
+    def run(n_total):
+        lats = [[] for _ in range(W)]
+        res = [None] * W
+        share = [n_total // W + (1 if i < n_total % W else 0) for i in range(W)]
+        ths = [threading.Thread(target=run_worker, args=(ex, key, iv, ov, inputs, share[i], lats[i], res, i))
+               for i, (_, ex, key, iv, ov) in enumerate(workers)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        bad = [r for r in res if r is not True]
+        if bad:
+            raise RuntimeError("job failed: %s" % bad)
+        return [x for l in lats for x in l]
+
+    run(max(args.warmup, 2 * W))
+    D.barrier()
+    t0 = time.perf_counter()
+    lat = run(args.steps)
+    t1 = time.perf_counter()
+    D.barrier()
+    elapsed = D.max(t1 - t0)
+    all_lat = [x for part in D.gather(lat) for x in part]
+
+    # roofline of the dominant kernel: per-launch HIP events on the worker's stream
+    prof = workers[0][1].ProfileSubgraph(workers[0][2], iters=args.profile_iters)
+    by_k = {}
+    for r in prof:
+        k = by_k.setdefault(r["kernel"], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
+        k["ms"] += r["ms"]
+        k["bytes"] += r["alg_bytes"]
+        k["ops"] += r["alg_ops"]
+        k["launches"] += 1
+    dom_name = max(by_k, key=lambda k: by_k[k]["ms"])
+    dom = by_k[dom_name]
+    avg_ms = dom["ms"] / dom["launches"]
+    bytes_per_launch = dom["bytes"] / dom["launches"]
+    ops_per_launch = dom["ops"] / dom["launches"]
+    achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+    gpu_ms_total = sum(v["ms"] for v in by_k.values())
+
+    cpu = None
+    if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(buf, args.cpu_baseline_seconds)
+
+    if D.rank == 0:
+        n = D.world
+        total_jobs = args.steps * n
+        lat_ms = np.array(all_lat) * 1e3
+        line = {
+            "metric": "multi-DNN inferences/sec + p99 job latency, 4-model int8 mix @1/2/4/8 GPU",
+            "value": total_jobs / elapsed,
+            "unit": "inferences/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int8" if "int8" in args.model else "uint8",
+            "data": "synthetic (seeded int8 inputs and weights; no checkpoint)",
+            "config": {"workload": "C2: %s 224x224 batch-1 jobs, %d Band GPU worker(s) per MI355X, fixed_worker"
+                       % (args.model, W), "model": args.model, "global_batch": n * W, "seq_len": None,
+                       "parallelism": "job-sharded x%d (no collective)" % n, "hipgraph": not args.no_graph},
+            "p50_job_latency_ms": float(np.percentile(lat_ms, 50)),
+            "p99_job_latency_ms": float(np.percentile(lat_ms, 99)),
+            "gpu_kernel_ms_per_inference": gpu_ms_total,
+            "roofline": {
+                "kernel": dom_name, "bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
+                "frac": achieved_gbs / 8000.0, "traffic": None,
+                "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
+                "launches_per_inference": dom["launches"],
+                "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,
+                "mfma_i8_frac": ops_per_launch / (avg_ms * 1e-3) / 5.0e15,
+            },
+            "cpu_baseline": cpu,
+            "host": platform.node(),
+        }
+        print(json.dumps(line), flush=True)
+    D.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -19,7 +19,10 @@ class ConvParams(ctypes.Structure):
         "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "k_h", "k_w",
         "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "k_pad", "n_pad", "in_xor")] + [
         (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
-        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift")]
+        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift", "residual")] + [
+        (n, c_int32) for n in ("add_y_off", "add_r_off", "add_o_off", "add_left_shift", "add_y_mult",
+                               "add_y_shift", "add_r_mult", "add_r_shift", "add_o_mult", "add_o_shift",
+                               "add_act_min", "add_act_max")]
 
 
 class DwConvParams(ctypes.Structure):
@@ -50,6 +53,22 @@ class PoolParams(ctypes.Structure):
         "f_h", "f_w", "stride_h", "stride_w", "pad_h", "pad_w")] + [
         (n, c_int32) for n in ("act_min", "act_max")] + [
         (n, c_void_p) for n in ("input", "output")]
+
+
+class IrbParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "batch", "in_h", "in_w", "in_c", "exp_c", "out_h", "out_w", "out_c", "stride", "pad_h", "pad_w",
+        "has_expand", "tile_h", "tile_w")] + [
+        ("exp_w", c_void_p), ("exp_k_pad", c_int), ("exp_bias_eff", c_void_p), ("exp_mult", c_void_p),
+        ("exp_shift", c_void_p)] + [(n, c_int32) for n in ("x_zp", "e_zp", "e_act_min", "e_act_max")] + [
+        ("dw_w", c_void_p), ("dw_bias", c_void_p), ("dw_mult", c_void_p), ("dw_shift", c_void_p)] + [
+        (n, c_int32) for n in ("d_zp", "d_act_min", "d_act_max")] + [
+        ("proj_w", c_void_p), ("proj_k_pad", c_int), ("proj_bias_eff", c_void_p), ("proj_mult", c_void_p),
+        ("proj_shift", c_void_p)] + [(n, c_int32) for n in ("p_zp", "p_act_min", "p_act_max")] + [
+        ("has_residual", c_int)] + [(n, c_int32) for n in (
+            "add_p_off", "add_x_off", "add_o_off", "add_left_shift", "add_p_mult", "add_p_shift", "add_x_mult",
+            "add_x_shift", "add_o_mult", "add_o_shift", "add_act_min", "add_act_max")] + [
+        ("input", c_void_p), ("output", c_void_p), ("debug_stamps", c_void_p)]
 
 
 # symbol -> (restype, argtypes)
@@ -88,6 +107,8 @@ KERNEL_SYMBOLS = {
     "bh_fc_i8": (c_int, [ctypes.POINTER(FcParams), c_void_p]),
     "bh_eltwise_i8": (c_int, [ctypes.POINTER(EltwiseParams), c_void_p]),
     "bh_pool_i8": (c_int, [ctypes.POINTER(PoolParams), c_void_p]),
+    "bh_irb_i8": (c_int, [ctypes.POINTER(IrbParams), c_void_p]),
+    "bh_irb_lds_bytes": (c_size_t, [ctypes.POINTER(IrbParams)]),
     "bh_last_error": (ctypes.c_char_p, []),
 }
 

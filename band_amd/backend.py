@@ -60,9 +60,12 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_list_subgraphs": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int),
                                    ctypes.POINTER(c_uint64), c_int, ctypes.POINTER(c_int)]),
     "bhx_execute_subgraph": (c_int, _KEY),
+    "bhx_run_jobs": (c_int, _KEY + [ctypes.POINTER(c_void_p), c_int, c_size_t, c_void_p, c_size_t, c_int,
+                                    ctypes.POINTER(ctypes.c_double)]),
     "bhx_executor_set_graph": (c_int, [c_void_p, c_int]),
     "bhx_executor_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int)]),
+    "bhx_time_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(ctypes.c_double)]),
 })
 
 
@@ -382,6 +385,20 @@ class HipModelExecutor:
         return Status.from_rc(self.lib.bhx_execute_subgraph(self.handle, *key._args()))
 
     # ---- extensions -----------------------------------------------------
+    def RunJobs(self, key, inputs, n_jobs, out=None):
+        """Native Band-worker loop (bhx_run_jobs): returns per-job latency in us."""
+        arrs = [np.ascontiguousarray(a) for a in inputs]
+        slots = (c_void_p * len(arrs))(*[a.ctypes.data for a in arrs])
+        lat = np.zeros(max(n_jobs, 1), np.float64)
+        out_p = out.ctypes.data if out is not None else None
+        out_n = out.nbytes if out is not None else 0
+        rc = self.lib.bhx_run_jobs(self.handle, *key._args(), slots, len(arrs), arrs[0].nbytes, out_p, out_n,
+                                   int(n_jobs), lat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+        st = Status.from_rc(rc)
+        if not st.ok():
+            raise _abi.BandHipError("bhx_run_jobs: " + st.message())
+        return lat[:n_jobs]
+
     def SetUseGraph(self, enabled):
         _abi.check(self.lib.bhx_executor_set_graph(self.handle, int(bool(enabled))), "set_graph")
 
@@ -398,6 +415,13 @@ class HipModelExecutor:
                    "ProfileSubgraph")
         return [dict(op_index=arr[i].op_index, kernel=arr[i].kernel.decode(), ms=arr[i].ms,
                      alg_bytes=arr[i].alg_bytes, alg_ops=arr[i].alg_ops) for i in range(min(n.value, cap))]
+
+    def TimeSubgraph(self, key, iters=100):
+        """device microseconds per subgraph pass, passes issued back to back"""
+        us = ctypes.c_double(0)
+        _abi.check(self.lib.bhx_time_subgraph(self.handle, *key._args(), int(iters), ctypes.byref(us)),
+                   "TimeSubgraph")
+        return us.value
 
     def __del__(self):
         try:

@@ -2,6 +2,7 @@
 // created through Band's own BackendFactory so the registration path
 // (TfLiteRegisterCreators -> RegisterBackendCreators) is exercised exactly
 // as a Band engine would exercise it.
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -245,6 +246,29 @@ int bhx_execute_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask) {
   return s.ok() ? 0 : Fail(s);
 }
 
+int bhx_run_jobs(bhx_executor* e, int mid, int wid, uint64_t mask, const void* const* in_slots, int n_slots,
+                 size_t in_bytes, void* out, size_t out_bytes, int n_jobs, double* latency_us) {
+  if (!e || !in_slots || n_slots <= 0 || n_jobs < 0) return Fail("bad arguments");
+  const SubgraphKey key = Key(mid, wid, mask);
+  const auto& ins = e->exec->GetInputs(key);
+  const auto& outs = e->exec->GetOutputs(key);
+  if (ins.size() != 1 || outs.size() != 1) return Fail("bhx_run_jobs needs a single-input, single-output subgraph");
+  auto iv = e->exec->GetTensorView(key, ins[0]);
+  auto ov = e->exec->GetTensorView(key, outs[0]);
+  if (!iv || !ov || iv->GetBytes() != in_bytes || (out && ov->GetBytes() != out_bytes))
+    return Fail("request / view size mismatch");
+  for (int j = 0; j < n_jobs; ++j) {
+    const auto t0 = std::chrono::steady_clock::now();
+    std::memcpy(iv->GetData(), in_slots[j % n_slots], in_bytes);
+    absl::Status s = e->exec->ExecuteSubgraph(key);
+    if (!s.ok()) return Fail(s);
+    if (out) std::memcpy(out, ov->GetData(), out_bytes);
+    if (latency_us)
+      latency_us[j] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  }
+  return 0;
+}
+
 int bhx_executor_set_graph(bhx_executor* e, int enabled) {
   auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;
   if (!h) return Fail("not a HIP executor");
@@ -269,6 +293,14 @@ int bhx_profile_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int i
   if (n) *n = static_cast<int>(t.size());
   for (int i = 0; i < cap && i < static_cast<int>(t.size()); ++i)
     out[i] = bhx_op_timing{t[i].op_index, t[i].kernel, t[i].ms, t[i].alg_bytes, t[i].alg_ops};
+  return 0;
+}
+
+int bhx_time_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int iters, double* us) {
+  auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;
+  if (!h) return Fail("not a HIP executor");
+  auto s = h->TimeSubgraph(Key(mid, wid, mask), iters, us);
+  if (!s.ok()) return Fail(s);
   return 0;
 }
 

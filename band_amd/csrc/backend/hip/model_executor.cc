@@ -1,9 +1,12 @@
 #include "backend/hip/model_executor.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <unordered_map>
 
 #include "backend/hip/quant.h"
 
@@ -146,6 +149,14 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
     m->SetQuant(t.scale, t.zero_point, t.quantized_dimension);
     meta_.push_back(std::move(m));
   }
+  consumers_.assign(d.tensors.size(), {});
+  for (int i = 0; i < static_cast<int>(d.ops.size()); ++i)
+    for (int t : d.ops[i].inputs)
+      if (t >= 0) consumers_[t].push_back(i);
+  const char* f = std::getenv("BAND_HIP_FUSION");
+  if (f && f[0] == '0') allow_fusion_ = false;
+  const char* at = std::getenv("BAND_HIP_AUTOTUNE");
+  if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
 }
 
@@ -212,6 +223,285 @@ absl::Status HipModelExecutor::DevicePtr(const HipModel& model, int t, PreparedS
   sg->consts.push_back(blob);
   *ptr = blob->ptr();
   return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubgraph* sg) {
+  sg->launches.clear();
+  sg->fused_ops.clear();
+  sg->fused_tensors.clear();
+  for (int i : sg->ops) {
+    if (sg->fused_ops.count(i)) continue;
+    RETURN_STATUS_IF(Lower(model, i, sg));
+  }
+  if (allow_fusion_) FuseBlocks(model, sg);
+  return absl::OkStatus();
+}
+
+namespace {
+bool Is1x1S1(const bh_conv_params& c) {
+  return c.k_h == 1 && c.k_w == 1 && c.stride_h == 1 && c.stride_w == 1 && c.pad_h == 0 && c.pad_w == 0;
+}
+
+// Static latency model for a fused block's tile (used when it cannot be
+// measured): (workgroup rounds over 256 CUs) x (MFMA tiles + depthwise /
+// epilogue work per workgroup) / waves - halo recompute of small tiles
+// against too few workgroups of large ones.
+double IrbModelCost(const bh_irb_params& q, int t, size_t lds) {
+  const int R = ((t - 1) * q.stride + 3) * ((t - 1) * q.stride + 3);
+  const double mt1 = (R + 15) / 16, mt3 = (t * t + 15) / 16;
+  const double ks1 = (q.in_c + 63) / 64, ks3 = (q.exp_c + 63) / 64;
+  const double work = (q.has_expand ? mt1 * (q.exp_c / 16) * (1.0 + ks1) : 0.0) +  // +1: epilogue
+                      mt3 * 16 * q.exp_c / 256.0 * 3.0 +                          // depthwise
+                      mt3 * ((q.out_c + 15) / 16) * ks3 + t * t * q.out_c / 64.0;
+  const int nw = lds > 80 * 1024 ? 16 : 8;
+  const double per_cu = lds > 80 * 1024 ? 1 : 2;
+  const long wg = static_cast<long>(q.batch) * ((q.out_h + t - 1) / t) * ((q.out_w + t - 1) / t);
+  const double rounds = std::ceil(static_cast<double>(wg) / (256.0 * per_cu));
+  return rounds * (work / nw + 8.0);  // + fixed per-workgroup latency
+}
+
+// Measured choices, shared by every executor of the process: one block
+// geometry is timed once per device.  Value: tile edge, or 0 = keep unfused.
+std::mutex g_tune_mu;
+std::unordered_map<std::string, int> g_tune;
+
+std::string IrbKey(int ordinal, const bh_irb_params& q) {
+  char buf[256];
+  std::snprintf(buf, sizeof(buf), "%d:%d:%dx%dx%d:%d:%d:%dx%d:%d:%d:%d", ordinal, q.batch, q.in_h, q.in_w, q.in_c,
+                q.exp_c, q.out_c, q.out_h, q.out_w, q.stride, q.has_expand, q.has_residual);
+  return buf;
+}
+}  // namespace
+
+double HipModelExecutor::TimeLaunches(const std::vector<const Launch*>& ls, int iters) {
+  if (device_flag_ != DeviceFlag::kGPU || !stream_ || ls.empty()) return -1.0;
+  bh_event_t e0 = nullptr, e1 = nullptr;
+  if (bh_event_create(&e0) != 0) return -1.0;
+  if (bh_event_create(&e1) != 0) {
+    bh_event_destroy(e0);
+    return -1.0;
+  }
+  double us = -1.0;
+  bool ok = true;
+  for (int w = 0; w < 2 && ok; ++w)
+    for (const Launch* l : ls) ok = ok && EnqueueLaunch(*l).ok();
+  if (ok && bh_event_record(e0, stream_) == 0) {
+    for (int it = 0; it < iters && ok; ++it)
+      for (const Launch* l : ls) ok = ok && EnqueueLaunch(*l).ok();
+    float ms = 0.f;
+    if (ok && bh_event_record(e1, stream_) == 0 && bh_stream_sync(stream_) == 0 &&
+        bh_event_elapsed_ms(e0, e1, &ms) == 0)
+      us = 1e3 * ms / iters;
+  }
+  bh_stream_sync(stream_);
+  bh_event_destroy(e0);
+  bh_event_destroy(e1);
+  return us;
+}
+
+// Rewrites [conv1x1 ->] dw3x3 -> conv1x1 [+fused ADD] launch runs into one
+// bh_irb_i8 launch when the intermediates are private to the run.
+void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
+  const TflModel& d = model.desc();
+  auto private_tensor = [&](int t, int only_consumer) {
+    if (consumers_[t].size() != 1 || consumers_[t][0] != only_consumer) return false;
+    if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
+    if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
+    return std::find(d.outputs.begin(), d.outputs.end(), t) == d.outputs.end();
+  };
+  std::vector<Launch> out;
+  const auto& L = sg->launches;
+  for (size_t i = 0; i < L.size(); ++i) {
+    // candidate run: [E] D P
+    const Launch* E = nullptr;
+    size_t j = i;
+    if (L[i].kind == Launch::kConv && i + 2 < L.size() && L[i + 1].kind == Launch::kDwConv &&
+        L[i + 2].kind == Launch::kConv) {
+      E = &L[i];
+      j = i + 1;
+    } else if (!(L[i].kind == Launch::kDwConv && i + 1 < L.size() && L[i + 1].kind == Launch::kConv)) {
+      out.push_back(L[i]);
+      continue;
+    }
+    const Launch& D = L[j];
+    const Launch& P = L[j + 1];
+    const bh_dwconv_params& dw = D.dw;
+    const bh_conv_params& pc = P.conv;
+    bool ok = dw.in_xor == 0 && dw.w_zp == 0 && dw.depth_multiplier == 1 && dw.k_h == 3 && dw.k_w == 3 &&
+              dw.dil_h == 1 && dw.dil_w == 1 && dw.stride_h == dw.stride_w && pc.in_xor == 0 && pc.w_zp == 0 &&
+              Is1x1S1(pc) && pc.input == dw.output &&
+              private_tensor(d.ops[D.op_index].outputs[0], P.op_index);
+    if (ok && E) {
+      const bh_conv_params& ec = E->conv;
+      ok = ec.in_xor == 0 && ec.w_zp == 0 && Is1x1S1(ec) && !ec.residual && ec.output == dw.input &&
+           private_tensor(d.ops[E->op_index].outputs[0], D.op_index);
+    }
+    if (ok && pc.residual) {
+      const void* x = E ? E->conv.input : dw.input;
+      ok = pc.residual == x;
+    }
+    bh_irb_params q{};
+    if (ok) {
+      const bh_conv_params* ec = E ? &E->conv : nullptr;
+      q.batch = dw.batch;
+      q.in_h = dw.in_h; q.in_w = dw.in_w;
+      q.in_c = ec ? ec->in_c : dw.in_c;
+      q.exp_c = dw.in_c;
+      q.out_h = dw.out_h; q.out_w = dw.out_w; q.out_c = pc.out_c;
+      q.stride = dw.stride_h; q.pad_h = dw.pad_h; q.pad_w = dw.pad_w;
+      q.has_expand = ec ? 1 : 0;
+      if (ec) {
+        q.exp_w = ec->weights; q.exp_k_pad = ec->k_pad;
+        q.exp_bias_eff = ec->bias_eff; q.exp_mult = ec->mult; q.exp_shift = ec->shift;
+        q.x_zp = ec->in_zp;
+        q.e_zp = ec->out_zp; q.e_act_min = ec->act_min; q.e_act_max = ec->act_max;
+      }
+      q.dw_w = dw.weights; q.dw_bias = dw.bias; q.dw_mult = dw.mult; q.dw_shift = dw.shift;
+      if (!ec) q.e_zp = dw.in_zp;
+      q.d_zp = dw.out_zp; q.d_act_min = dw.act_min; q.d_act_max = dw.act_max;
+      q.proj_w = pc.weights; q.proj_k_pad = pc.k_pad;
+      q.proj_bias_eff = pc.bias_eff; q.proj_mult = pc.mult; q.proj_shift = pc.shift;
+      q.p_zp = pc.out_zp; q.p_act_min = pc.act_min; q.p_act_max = pc.act_max;
+      q.has_residual = pc.residual ? 1 : 0;
+      q.add_p_off = pc.add_y_off; q.add_x_off = pc.add_r_off; q.add_o_off = pc.add_o_off;
+      q.add_left_shift = pc.add_left_shift;
+      q.add_p_mult = pc.add_y_mult; q.add_p_shift = pc.add_y_shift;
+      q.add_x_mult = pc.add_r_mult; q.add_x_shift = pc.add_r_shift;
+      q.add_o_mult = pc.add_o_mult; q.add_o_shift = pc.add_o_shift;
+      q.add_act_min = pc.add_act_min; q.add_act_max = pc.add_act_max;
+      q.input = ec ? ec->input : dw.input;
+      q.output = pc.output;
+      // Tile edge: measured on this device when possible (each feasible
+      // tile, and the unfused launches, timed on the real buffers; the
+      // winner is cached per block geometry), else the static model.
+      int tile = 0;
+      const std::string key = IrbKey(ordinal_, q);
+      bool cached = false;
+      if (autotune_) {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        auto it = g_tune.find(key);
+        if (it != g_tune.end()) {
+          tile = it->second;
+          cached = true;
+        }
+      }
+      if (!cached) {
+        double best_model = 1e300, best_us = 1e300;
+        int model_tile = 0;
+        bool measured = autotune_;
+        if (measured) {
+          std::vector<const Launch*> unfused;
+          if (E) unfused.push_back(E);
+          unfused.push_back(&D);
+          unfused.push_back(&P);
+          const double u = TimeLaunches(unfused, 10);
+          measured = u > 0;
+          best_us = u * 0.98;  // fusion must win by > 2% to be taken
+        }
+        for (int t = 8; t >= 1; --t) {
+          q.tile_h = q.tile_w = t;
+          const size_t lds = bh_irb_lds_bytes(&q);
+          if (lds == 0) continue;
+          const double est = IrbModelCost(q, t, lds);
+          if (est < best_model * 0.97) {
+            best_model = est;
+            model_tile = t;
+          }
+          if (measured) {
+            Launch F;
+            F.kind = Launch::kIrb;
+            F.irb = q;
+            const double us = TimeLaunches({&F}, 10);
+            if (us > 0 && us < best_us) {
+              best_us = us;
+              tile = t;
+            }
+          }
+        }
+        if (!measured) tile = model_tile;
+        if (autotune_ && measured) {
+          std::lock_guard<std::mutex> lk(g_tune_mu);
+          g_tune[key] = tile;
+        }
+      }
+      q.tile_h = q.tile_w = tile;
+      ok = tile > 0 && bh_irb_lds_bytes(&q) > 0;
+    }
+    if (!ok) {
+      out.push_back(L[i]);
+      continue;
+    }
+    Launch F;
+    F.kind = Launch::kIrb;
+    F.op_index = E ? E->op_index : D.op_index;
+    F.irb = q;
+    F.kernel = "irb_kernel";
+    // algorithmic bytes: block input + block output + all filters/tables
+    const double x_bytes = static_cast<double>(q.batch) * q.in_h * q.in_w * q.in_c;
+    const double y_bytes = static_cast<double>(q.batch) * q.out_h * q.out_w * q.out_c;
+    F.alg_bytes = x_bytes + y_bytes + 12.0 * (q.exp_c + q.out_c) + 9.0 * q.exp_c +
+                  static_cast<double>(q.exp_c) * q.out_c + (E ? static_cast<double>(q.exp_c) * q.in_c + 12.0 * q.exp_c : 0);
+    F.alg_ops = (E ? E->alg_ops : 0) + D.alg_ops + P.alg_ops;
+    out.push_back(F);
+    // intermediates now live only in LDS; a later view of one re-lowers
+    sg->fused_tensors.insert(d.ops[D.op_index].outputs[0]);
+    if (E) sg->fused_tensors.insert(d.ops[E->op_index].outputs[0]);
+    i = j + 1;  // consumed [E] D P
+  }
+  sg->launches.swap(out);
+}
+
+// Folds `conv -> ADD/SUB(conv_out, residual)` into the conv epilogue when the
+// conv output has no other reader and nobody needs it materialised.  The
+// epilogue reproduces both TFLite ops exactly (conv requant + clamp to the
+// conv's 8-bit output, then add.cc's arithmetic), so the result is
+// bit-identical to running the two ops.
+bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, PreparedSubgraph* sg, Launch* L) {
+  if (!allow_fusion_) return false;
+  const TflModel& d = model.desc();
+  const int t = d.ops[oi].outputs[0];
+  if (consumers_[t].size() != 1) return false;
+  const int j = consumers_[t][0];
+  if (j <= oi || !std::binary_search(sg->ops.begin(), sg->ops.end(), j)) return false;
+  const TflOperator& add = d.ops[j];
+  if ((add.builtin != kTflAdd && add.builtin != kTflSub) || add.inputs.size() != 2) return false;
+  if (!GpuSupports(d, add, nullptr)) return false;
+  if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
+  if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
+  if (std::find(d.outputs.begin(), d.outputs.end(), t) != d.outputs.end()) return false;
+  const bool conv_is_first = add.inputs[0] == t;
+  const int other = conv_is_first ? add.inputs[1] : add.inputs[0];
+  if (other == t) return false;
+  const TflTensor& tc = d.tensors[t];
+  const TflTensor& tr = d.tensors[other];
+  const TflTensor& to = d.tensors[add.outputs[0]];
+  if (tr.shape != tc.shape || to.shape != tc.shape || tr.type != tc.type || to.type != tc.type) return false;
+  void* rptr = nullptr;
+  void* optr = nullptr;
+  if (!DevicePtr(model, other, sg, &rptr).ok() || !DevicePtr(model, add.outputs[0], sg, &optr).ok()) return false;
+  const TflTensor& t1 = d.tensors[add.inputs[0]];
+  const TflTensor& t2 = d.tensors[add.inputs[1]];
+  const AddParams ap = AddSubParams(Scale(t1), Scale(t2), Scale(to), add.builtin == kTflSub);
+  bh_conv_params& p = L->conv;
+  p.residual = rptr;
+  p.output = optr;
+  p.add_left_shift = ap.left_shift;
+  p.add_y_off = -Zp(tc);
+  p.add_r_off = -Zp(tr);
+  p.add_o_off = Zp(to);
+  p.add_y_mult = conv_is_first ? ap.m1 : ap.m2;
+  p.add_y_shift = conv_is_first ? ap.s1 : ap.s2;
+  p.add_r_mult = conv_is_first ? ap.m2 : ap.m1;
+  p.add_r_shift = conv_is_first ? ap.s2 : ap.s1;
+  p.add_o_mult = ap.mo;
+  p.add_o_shift = ap.so;
+  const int act = add.options.valid() ? add.options.Int8(0, 0) : 0;
+  ActivationRangeQuantized(act, Scale(to), Zp(to), to.type == DataType::kInt8, &p.add_act_min, &p.add_act_max);
+  L->alg_bytes += static_cast<double>(tr.num_elements());  // residual read; y never stored
+  L->kernel = "conv_mfma_kernel+add";
+  sg->fused_ops.insert(j);
+  sg->fused_tensors.insert(t);
+  return true;
 }
 
 absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubgraph* sg) {
@@ -438,6 +728,31 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.dst = out_ptr;
     L.bytes = meta_[op.outputs[0]]->bytes;
     L.alg_bytes = 2.0 * L.bytes;
+    if (L.src == L.dst) return absl::OkStatus();  // aliased slot: nothing to move
+  }
+  if (L.kind == Launch::kConv) {
+    const bh_conv_params c = L.conv;
+    const long M = static_cast<long>(c.batch) * c.out_h * c.out_w;
+    if (c.k_h == 1 && c.k_w == 1 && c.stride_h == 1 && c.stride_w == 1 && M <= 4) {
+      // a 1x1 conv over a handful of pixels (the classifier at batch 1) is
+      // a GEMV: run it on the weight-streaming FC kernel with the same
+      // packed operands (Bt rows are K-contiguous, bias_eff identical)
+      Launch F;
+      F.kind = Launch::kFc;
+      F.op_index = oi;
+      bh_fc_params& f = F.fc;
+      f = bh_fc_params{};
+      f.rows = static_cast<int>(M); f.depth = c.in_c; f.depth_pad = c.k_pad; f.units = c.out_c;
+      f.in_xor = c.in_xor; f.in_zp = c.in_zp; f.w_zp = c.w_zp; f.out_zp = c.out_zp;
+      f.act_min = c.act_min; f.act_max = c.act_max; f.input = c.input; f.output = c.output;
+      f.weights = c.weights; f.bias_eff = c.bias_eff; f.mult = c.mult; f.shift = c.shift;
+      F.kernel = "fc_kernel";
+      F.alg_bytes = L.alg_bytes;
+      F.alg_ops = L.alg_ops;
+      L = F;
+    } else {
+      TryFuseResidualAdd(model, oi, sg, &L);
+    }
   }
   sg->launches.push_back(L);
   return absl::OkStatus();
@@ -497,14 +812,28 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
   if (device_flag_ == DeviceFlag::kGPU) {
     if (ordinal_ < 0 || !stream_) return absl::InternalError("Failed to create HIP executor: no gfx950 device");
     if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
+    // RESHAPE / SQUEEZE outputs alias their input's slot (same bytes, and
+    // every tensor is immutable once produced), so they cost no launch.
+    std::map<int, int> alias;
+    for (int i : sg->ops) {
+      const TflOperator& op = d.ops[i];
+      if ((op.builtin == kTflReshape || op.builtin == kTflSqueeze) && !op.inputs.empty() && op.inputs[0] >= 0 &&
+          !d.tensors[op.inputs[0]].is_const() && meta_[op.outputs[0]]->bytes == meta_[op.inputs[0]]->bytes) {
+        int src = op.inputs[0];
+        while (alias.count(src)) src = alias[src];
+        alias[op.outputs[0]] = src;
+      }
+    }
     size_t total = 0;
     for (int t : touched) {
+      if (alias.count(t)) continue;
       sg->offset[t] = total;
       total += (meta_[t]->bytes + kAlign - 1) / kAlign * kAlign;
     }
+    for (const auto& kv : alias) sg->offset[kv.first] = sg->offset.at(kv.second);
     sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
     if (!sg->arena->ok()) return absl::InternalError("HBM arena allocation failed");
-    for (int i : sg->ops) RETURN_STATUS_IF(Lower(*hm, i, sg.get()));
+    RETURN_STATUS_IF(BuildLaunches(*hm, sg.get()));
   } else if (device_flag_ != DeviceFlag::kCPU) {
     return absl::InternalError(std::string("Unsupported device type ") + ToString(device_flag_));
   }
@@ -576,10 +905,15 @@ std::shared_ptr<interface::ITensorView> HipModelExecutor::GetTensorView(const Su
     char* data = buf->data();
     sg->host[index] = std::move(buf);
     sg->extra_d2h.insert(index);
+    bh_set_device(ordinal_);
     if (sg->graph) {
-      bh_set_device(ordinal_);
       bh_graph_destroy(sg->graph);
       sg->graph = nullptr;
+    }
+    if (sg->fused_tensors.count(index)) {
+      // the tensor was folded away by an epilogue fusion: re-lower with it materialised
+      sg->no_fuse.insert(index);
+      if (!BuildLaunches(*model_, sg).ok()) return nullptr;
     }
     return std::make_shared<HipTensorView>(m, data);
   }
@@ -594,6 +928,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kFc: rc = bh_fc_i8(&l.fc, stream_); break;
     case Launch::kEltwise: rc = bh_eltwise_i8(&l.elt, stream_); break;
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
+    case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
     case Launch::kCopy: rc = l.src == l.dst ? 0 : bh_memcpy_d2d_async(l.dst, l.src, l.bytes, stream_); break;
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
@@ -644,6 +979,35 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (rc) return HipErr(rc, "stream sync");
   ++sg->runs;
   return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, double* us) {
+  PreparedSubgraph* sg = Find(key);
+  if (!sg) return absl::InternalError("Cannot find subgraph");
+  if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("timing needs a GPU executor");
+  if (iters <= 0 || !us) return absl::InternalError("bad arguments");
+  // two ordinary runs first, so the graph (if enabled) is captured
+  for (int i = 0; i < 2; ++i) RETURN_STATUS_IF(ExecuteSubgraph(key));
+  bh_event_t e0 = nullptr, e1 = nullptr;
+  if (bh_event_create(&e0) != 0 || bh_event_create(&e1) != 0) return HipErr(1, "event create");
+  absl::Status status = absl::OkStatus();
+  bh_event_record(e0, stream_);
+  for (int i = 0; i < iters && status.ok(); ++i) {
+    if (use_graph_ && sg->graph) {
+      const int rc = bh_graph_launch(sg->graph, stream_);
+      if (rc) status = HipErr(rc, "graph launch");
+    } else {
+      status = Enqueue(sg);
+    }
+  }
+  bh_event_record(e1, stream_);
+  float ms = 0.f;
+  if (bh_stream_sync(stream_) != 0 && status.ok()) status = HipErr(1, "sync");
+  if (status.ok() && bh_event_elapsed_ms(e0, e1, &ms) != 0) status = HipErr(1, "elapsed");
+  bh_event_destroy(e0);
+  bh_event_destroy(e1);
+  if (status.ok()) *us = 1e3 * ms / iters;
+  return status;
 }
 
 absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out) {

@@ -34,13 +34,14 @@ namespace band {
 namespace hip {
 
 struct Launch {
-  enum Kind { kConv, kDwConv, kFc, kEltwise, kPool, kCopy } kind;
+  enum Kind { kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb } kind;
   int op_index = -1;
   bh_conv_params conv{};
   bh_dwconv_params dw{};
   bh_fc_params fc{};
   bh_eltwise_params elt{};
   bh_pool_params pool{};
+  bh_irb_params irb{};
   void* dst = nullptr;
   const void* src = nullptr;
   size_t bytes = 0;
@@ -64,6 +65,9 @@ struct PreparedSubgraph {
   std::shared_ptr<DeviceBlob> arena;
   std::map<int, std::unique_ptr<PinnedBuffer>> host;  // boundary mirrors
   std::set<int> extra_d2h;                            // intermediates a view asked for
+  std::set<int> fused_ops;      // ADD/SUB ops folded into the producing conv's epilogue
+  std::set<int> fused_tensors;  // conv outputs that are therefore never materialised
+  std::set<int> no_fuse;        // tensors a view needs materialised
   std::vector<Launch> launches;
   std::vector<std::shared_ptr<DeviceBlob>> consts;
   bh_graph_exec_t graph = nullptr;
@@ -97,6 +101,10 @@ class HipModelExecutor : public interface::IModelExecutor {
   // Times every launch of `key` with HIP events on the executor's stream
   // (eager enqueue, averaged over `iters`).
   absl::Status ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out);
+  // Device time of one subgraph pass (us) with `iters` passes issued back to
+  // back (replayed hipGraph when captured, else the launch sequence): no host
+  // gaps, H2D/D2H included.  The latency floor of ExecuteSubgraph's device side.
+  absl::Status TimeSubgraph(const SubgraphKey& key, int iters, double* us);
   int ordinal() const { return ordinal_; }
 
   // Whether the GPU kernel set covers `op` of `model` (drives unsupported_ops[kGPU]).
@@ -106,12 +114,21 @@ class HipModelExecutor : public interface::IModelExecutor {
   PreparedSubgraph* Find(const SubgraphKey& key) const;
   absl::Status EnsureMeta(const HipModel& model);
   absl::Status Lower(const HipModel& model, int op_index, PreparedSubgraph* sg);
+  absl::Status BuildLaunches(const HipModel& model, PreparedSubgraph* sg);
+  bool TryFuseResidualAdd(const HipModel& model, int conv_op, PreparedSubgraph* sg, Launch* l);
+  void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
+  // Mean device time (us) of one pass over `ls`, or < 0 when it cannot be
+  // measured (no GPU stream, or a launch failed).
+  double TimeLaunches(const std::vector<const Launch*>& ls, int iters);
   absl::Status DevicePtr(const HipModel& model, int tensor, PreparedSubgraph* sg, void** ptr);
   absl::Status Enqueue(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
 
   const HipModel* model_ = nullptr;
   std::vector<std::unique_ptr<TensorMeta>> meta_;
+  std::vector<std::vector<int>> consumers_;  // tensor -> ops reading it (whole model)
+  bool allow_fusion_ = true;
+  bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;
   bh_stream_t stream_ = nullptr;

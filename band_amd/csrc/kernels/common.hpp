@@ -59,6 +59,27 @@ __device__ __forceinline__ uint32_t splat_byte(int32_t v) {
   return ((uint32_t)v & 0xffu) * 0x01010101u;
 }
 
+// Division by a runtime-invariant divisor for dividends < 2^31, by the
+// multiply-high method (Granlund & Montgomery): q = umulhi(n, m) >> s.
+// CDNA has no integer divide instruction - a plain `/` or `%` by a runtime
+// value is a ~40-instruction VALU sequence, which dominates these
+// latency-bound kernels' index math.  Built on the host, passed by value.
+struct FastDiv {
+  uint32_t d = 1, m = 0, s = 0;
+  FastDiv() = default;
+  __host__ __device__ explicit FastDiv(uint32_t div) : d(div ? div : 1) {
+    if (d > 1) {
+      uint32_t l = 0;
+      while ((1u << l) < d) ++l;  // ceil(log2 d)
+      const uint64_t p = 31 + l;
+      m = (uint32_t)(((1ull << p) + d - 1) / d);
+      s = (uint32_t)(p - 32);
+    }
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t n) const { return d == 1 ? n : (__umulhi(n, m) >> s); }
+  __device__ __forceinline__ uint32_t mod(uint32_t n) const { return n - div(n) * d; }
+};
+
 }  // namespace bh
 
 // thread-local last-error plumbing for the C ABI (defined in capi_runtime.hip)

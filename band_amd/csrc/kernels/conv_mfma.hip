@@ -8,13 +8,21 @@
 //   y = clamp(MultiplyByQuantizedMultiplier(acc, M[n], shift[n]) + zp_out)
 // where x'/w' are int8-domain operands (uint8 XOR 0x80), spatial padding is
 // filled with the input zero point (so centred padding contributes exactly
-// 0, like TFLite's skipped taps) and the K tail is zero-filled.
+// 0, like TFLite's skipped taps) and the K tail is zero-filled.  An optional
+// fused epilogue applies the following residual ADD (add.cc arithmetic) to
+// y before it is stored, so y never round-trips HBM.
 //
 // GEMM view (NHWC / OHWI): M = batch*out_h*out_w pixels, N = out_c,
 // K = k_h*k_w*in_c.  Both operands are K-contiguous, so each lane's MFMA
-// fragment (16 consecutive k of one row) is a single 16-byte load for 1x1
+// fragment (16 consecutive k of one row) is one 16-byte load for 1x1
 // layers.  v_mfma_i32_16x16x64_i8: lane l supplies A[l&15][16*(l>>4)+j] and
 // B[16*(l>>4)+j][l&15]; D lands as D[4*(l>>4)+r][l&15] (r = 0..3).
+//
+// Batch-1 MobileNet layers are tiny (M*N*K ~ 1-25 MMAC), so the kernel is
+// shaped for latency: the host picks the workgroup tile per layer so that
+// enough workgroups exist, deep-K layers split K across the 4 waves of a
+// workgroup (partials reduced through LDS), and each wave issues the loads
+// of up to 4 K-steps before their MFMAs.
 #include "common.hpp"
 
 namespace bh {
@@ -42,6 +50,20 @@ __device__ __forceinline__ void load_unit(const uint8_t* src, uint32_t* w, int u
 }
 
 template <int VEC>
+__device__ __forceinline__ void xor_unit(uint32_t* w, int u, uint32_t xorw) {
+  if constexpr (VEC == 16) {
+    w[0] ^= xorw; w[1] ^= xorw; w[2] ^= xorw; w[3] ^= xorw;
+  } else if constexpr (VEC == 8) {
+    w[2 * u] ^= xorw; w[2 * u + 1] ^= xorw;
+  } else if constexpr (VEC == 4) {
+    w[u] ^= xorw;
+  } else {
+    const int d = u >> 2, b = u & 3;
+    w[d] ^= (xorw & (0xffu << (8 * b)));
+  }
+}
+
+template <int VEC>
 __device__ __forceinline__ void fill_unit(uint32_t* w, int u, uint32_t pat) {
   if constexpr (VEC == 16) {
     w[0] = w[1] = w[2] = w[3] = pat;
@@ -56,9 +78,14 @@ __device__ __forceinline__ void fill_unit(uint32_t* w, int u, uint32_t pat) {
 }
 
 // 16 int8-domain A bytes of im2col row `ri`, k in [kb, kb+16).
+// Runtime divisors of the index math, as multiply-high reciprocals (FastDiv)
+struct ConvDivs {
+  FastDiv out_w, out_h, in_c, k_w;
+};
+
 template <bool IS1X1, int VEC>
-__device__ __forceinline__ v4i load_a(const bh_conv_params& p, const RowInfo& ri, int K, int kb,
-                                      uint32_t xorw, uint32_t padw) {
+__device__ __forceinline__ v4i load_a(const bh_conv_params& p, const ConvDivs& dv, const RowInfo& ri, int K,
+                                      int kb, uint32_t xorw, uint32_t padw) {
   uint32_t w[4] = {0u, 0u, 0u, 0u};
   if (ri.valid) {
     const uint8_t* in = (const uint8_t*)p.input;
@@ -69,42 +96,19 @@ __device__ __forceinline__ v4i load_a(const bh_conv_params& p, const RowInfo& ri
         fill_unit<VEC>(w, u, 0u);
       } else if constexpr (IS1X1) {
         load_unit<VEC>(in + ri.base + k, w, u);
-        if constexpr (VEC == 1) {
-          const int d = u >> 2, b = u & 3;
-          w[d] ^= (xorw & (0xffu << (8 * b)));
-        }
+        xor_unit<VEC>(w, u, xorw);
       } else {
-        const int tap = k / p.in_c;
+        const int tap = dv.in_c.div(k);
         const int ci = k - tap * p.in_c;
-        const int fy = tap / p.k_w;
+        const int fy = dv.k_w.div(tap);
         const int fx = tap - fy * p.k_w;
         const int y = ri.y0 + fy * p.dil_h;
         const int x = ri.x0 + fx * p.dil_w;
         if (y >= 0 && y < p.in_h && x >= 0 && x < p.in_w) {
           load_unit<VEC>(in + ri.base + ((long)y * p.in_w + x) * p.in_c + ci, w, u);
-          if constexpr (VEC == 1) {
-            const int d = u >> 2, b = u & 3;
-            w[d] ^= (xorw & (0xffu << (8 * b)));
-          } else if constexpr (VEC == 8) {
-            w[2 * u] ^= xorw; w[2 * u + 1] ^= xorw;
-          } else if constexpr (VEC == 4) {
-            w[u] ^= xorw;
-          } else {
-            w[0] ^= xorw; w[1] ^= xorw; w[2] ^= xorw; w[3] ^= xorw;
-          }
+          xor_unit<VEC>(w, u, xorw);
         } else {
           fill_unit<VEC>(w, u, padw);
-        }
-      }
-    }
-    if constexpr (IS1X1 && VEC > 1) {
-      // XOR only the loaded (k < K) part; K % VEC == 0 so whole units.
-#pragma unroll
-      for (int u = 0; u < 16 / VEC; ++u) {
-        if (kb + u * VEC < K) {
-          if constexpr (VEC == 16) { w[0] ^= xorw; w[1] ^= xorw; w[2] ^= xorw; w[3] ^= xorw; }
-          else if constexpr (VEC == 8) { w[2 * u] ^= xorw; w[2 * u + 1] ^= xorw; }
-          else { w[u] ^= xorw; }
         }
       }
     }
@@ -114,18 +118,33 @@ __device__ __forceinline__ v4i load_a(const bh_conv_params& p, const RowInfo& ri
   return r;
 }
 
-template <int WM, int WN, int WAVES_M, int WAVES_N, bool IS1X1, int VEC, bool WZP>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N) {
+__device__ __forceinline__ int rowsum16(v4i a, int s) {
+  s = __builtin_amdgcn_sdot4(a.x, 0x01010101, s, false);
+  s = __builtin_amdgcn_sdot4(a.y, 0x01010101, s, false);
+  s = __builtin_amdgcn_sdot4(a.z, 0x01010101, s, false);
+  return __builtin_amdgcn_sdot4(a.w, 0x01010101, s, false);
+}
+
+constexpr int KU = 4;  // K-steps whose loads are issued together
+
+// WM x WN 16x16 tiles per wave; waves arranged WAVES_M x WAVES_N x SPLITK.
+template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv) {
+  static_assert(WAVES_M * WAVES_N * SPLITK == 4, "4 waves per workgroup");
   constexpr int TM = WAVES_M * WM * 16;
   constexpr int TN = WAVES_N * WN * 16;
+  constexpr int NACC = WM * WN * 4;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int wave_m = wave % WAVES_M;
-  const int wave_n = wave / WAVES_M;
+  const int kz = wave / (WAVES_M * WAVES_N);
+  const int wt = wave % (WAVES_M * WAVES_N);
+  const int wave_m = wt % WAVES_M;
+  const int wave_n = wt / WAVES_M;
   const int m0 = blockIdx.x * TM + wave_m * WM * 16;
   const int n0 = blockIdx.y * TN + wave_n * WN * 16;
   const int r16 = lane & 15;
   const int g = lane >> 4;
+  const bool wzp = p.w_zp != 0;
 
   const uint32_t xorw = splat_byte(p.in_xor);
   const uint32_t padw = splat_byte(p.in_zp);
@@ -136,10 +155,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
     const int m = m0 + wm * 16 + r16;
     ri[wm].valid = m < M;
     const int mm = ri[wm].valid ? m : 0;
-    const int ox = mm % p.out_w;
-    const int t = mm / p.out_w;
-    const int oy = t % p.out_h;
-    const int n = t / p.out_h;
+    const int t = dv.out_w.div(mm);
+    const int ox = mm - t * p.out_w;
+    const int n = dv.out_h.div(t);
+    const int oy = t - n * p.out_h;
     if constexpr (IS1X1) {
       ri[wm].base = (((long)n * p.in_h + (long)oy * p.stride_h) * p.in_w + (long)ox * p.stride_w) * p.in_c;
       ri[wm].y0 = 0; ri[wm].x0 = 0;
@@ -160,32 +179,67 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   for (int i = 0; i < WM; ++i) rs[i] = 0;
 
   const int8_t* wrow = p.weights + (long)(n0 + r16) * p.k_pad + g * 16;
+  const int kbeg = kz * kchunk;
+  const int kend = min(K, kbeg + kchunk);
 
-  for (int kb0 = 0; kb0 < K; kb0 += 64) {
-    const int kb = kb0 + g * 16;
-    v4i a[WM], b[WN];
+  for (int kb0 = kbeg; kb0 < kend; kb0 += 64 * KU) {
+    v4i a[KU][WM], b[KU][WN];
 #pragma unroll
-    for (int wm = 0; wm < WM; ++wm) a[wm] = load_a<IS1X1, VEC>(p, ri[wm], K, kb, xorw, padw);
+    for (int u = 0; u < KU; ++u) {
+      const int kb = kb0 + u * 64;
+      if (kb < kend) {
 #pragma unroll
-    for (int wn = 0; wn < WN; ++wn) b[wn] = *(const v4i*)(wrow + (long)wn * 16 * p.k_pad + kb0);
+        for (int wm = 0; wm < WM; ++wm) a[u][wm] = load_a<IS1X1, VEC>(p, dv, ri[wm], K, kb + g * 16, xorw, padw);
 #pragma unroll
-    for (int wm = 0; wm < WM; ++wm)
+        for (int wn = 0; wn < WN; ++wn) b[u][wn] = *(const v4i*)(wrow + (long)wn * 16 * p.k_pad + kb);
+      }
+    }
 #pragma unroll
-      for (int wn = 0; wn < WN; ++wn)
-        acc[wm][wn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[wm], b[wn], acc[wm][wn], 0, 0, 0);
-    if constexpr (WZP) {
+    for (int u = 0; u < KU; ++u) {
+      if (kb0 + u * 64 < kend) {
 #pragma unroll
-      for (int wm = 0; wm < WM; ++wm) {
-        rs[wm] = __builtin_amdgcn_sdot4(a[wm].x, 0x01010101, rs[wm], false);
-        rs[wm] = __builtin_amdgcn_sdot4(a[wm].y, 0x01010101, rs[wm], false);
-        rs[wm] = __builtin_amdgcn_sdot4(a[wm].z, 0x01010101, rs[wm], false);
-        rs[wm] = __builtin_amdgcn_sdot4(a[wm].w, 0x01010101, rs[wm], false);
+        for (int wm = 0; wm < WM; ++wm)
+#pragma unroll
+          for (int wn = 0; wn < WN; ++wn)
+            acc[wm][wn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u][wm], b[u][wn], acc[wm][wn], 0, 0, 0);
+        if (wzp) {
+#pragma unroll
+          for (int wm = 0; wm < WM; ++wm) rs[wm] = rowsum16(a[u][wm], rs[wm]);
+        }
       }
     }
   }
 
+  if constexpr (SPLITK > 1) {
+    // reduce the K-split partials of the WAVES_M*WAVES_N tiles through LDS
+    __shared__ int red[SPLITK - 1][WAVES_M * WAVES_N][NACC + WM][64];
+    if (kz > 0) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[kz - 1][wt][(i * WN + j) * 4 + r][lane] = acc[i][j][r];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) red[kz - 1][wt][NACC + i][lane] = rs[i];
+    }
+    __syncthreads();
+    if (kz > 0) return;
+#pragma unroll
+    for (int z = 0; z < SPLITK - 1; ++z) {
+#pragma unroll
+      for (int i = 0; i < WM; ++i)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][r] += red[z][wt][(i * WN + j) * 4 + r][lane];
+#pragma unroll
+      for (int i = 0; i < WM; ++i) rs[i] += red[z][wt][NACC + i][lane];
+    }
+  }
+
   int rowsum[WM][4];
-  if constexpr (WZP) {
+  if (wzp) {
 #pragma unroll
     for (int wm = 0; wm < WM; ++wm) {
       int s = rs[wm];
@@ -197,6 +251,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   }
 
   uint8_t* out = (uint8_t*)p.output;
+  const uint8_t* res = (const uint8_t*)p.residual;
+  const bool res_signed = p.in_xor == 0;  // residual shares the activation type
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int n = n0 + wn * 16 + r16;
@@ -211,38 +267,61 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
         const int m = m0 + wm * 16 + 4 * g + r;
         if (m >= M) continue;
         int32_t v = acc[wm][wn][r] + be;
-        if constexpr (WZP) v -= p.w_zp * rowsum[wm][r];
-        v = requant(v, mu, sh) + p.out_zp;
-        out[(long)m * N + n] = (uint8_t)clamp_i32(v, p.act_min, p.act_max);
+        if (wzp) v -= p.w_zp * rowsum[wm][r];
+        v = clamp_i32(requant(v, mu, sh) + p.out_zp, p.act_min, p.act_max);
+        const long o = (long)m * N + n;
+        if (res) {
+          const int32_t q = res_signed ? (int32_t)(int8_t)res[o] : (int32_t)res[o];
+          const int32_t sy = requant_lt1((v + p.add_y_off) * (1 << p.add_left_shift), p.add_y_mult, p.add_y_shift);
+          const int32_t sr = requant_lt1((q + p.add_r_off) * (1 << p.add_left_shift), p.add_r_mult, p.add_r_shift);
+          v = clamp_i32(requant_lt1(sy + sr, p.add_o_mult, p.add_o_shift) + p.add_o_off, p.add_act_min,
+                        p.add_act_max);
+        }
+        out[o] = (uint8_t)v;
       }
     }
   }
 }
 
-template <int WM, int WN, int WAVES_M, int WAVES_N, bool IS1X1, int VEC, bool WZP>
-static int launch_tile(const bh_conv_params& p, int M, int K, int N, hipStream_t s) {
+template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
+static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t s) {
   constexpr int TM = WAVES_M * WM * 16;
   constexpr int TN = WAVES_N * WN * 16;
+  const int ksteps = (K + 63) / 64;
+  const int kchunk = (ksteps + SPLITK - 1) / SPLITK * 64;
+  ConvDivs dv;
+  dv.out_w = FastDiv(p.out_w);
+  dv.out_h = FastDiv(p.out_h);
+  dv.in_c = FastDiv(p.in_c);
+  dv.k_w = FastDiv(p.k_w);
   dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
-  hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, IS1X1, VEC, WZP>), grid, dim3(256), 0, s,
-                     p, M, K, N);
+  hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), grid, dim3(256), 0, s,
+                     p, M, K, N, kchunk, dv);
   return bh_check_launch("conv_mfma_kernel");
 }
 
-template <bool IS1X1, int VEC, bool WZP>
-static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_t s) {
-  if (N <= 16) return launch_tile<2, 1, 4, 1, IS1X1, VEC, WZP>(p, M, K, N, s);
-  if (N <= 32) return launch_tile<2, 2, 4, 1, IS1X1, VEC, WZP>(p, M, K, N, s);
-  return launch_tile<2, 2, 2, 2, IS1X1, VEC, WZP>(p, M, K, N, s);
-}
+static inline long wgs(int M, int N, int tm, int tn) { return (long)((M + tm - 1) / tm) * ((N + tn - 1) / tn); }
 
-template <bool IS1X1, bool WZP>
-static int launch_vec(const bh_conv_params& p, int M, int K, int N, hipStream_t s) {
-  const int c = p.in_c;
-  if (c % 16 == 0) return launch_shape<IS1X1, 16, WZP>(p, M, K, N, s);
-  if (c % 8 == 0) return launch_shape<IS1X1, 8, WZP>(p, M, K, N, s);
-  if (c % 4 == 0) return launch_shape<IS1X1, 4, WZP>(p, M, K, N, s);
-  return launch_shape<IS1X1, 1, WZP>(p, M, K, N, s);
+// Tile selection: the largest tile that still yields >= kTargetWG
+// workgroups, else the smallest; deep-K layers (>= 3 K-steps) split K over
+// the 4 waves of a workgroup.
+constexpr long kTargetWG = 160;
+
+template <bool IS1X1, int VEC>
+static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_t s) {
+  const int ksteps = (K + 63) / 64;
+  if (ksteps >= 3) {
+    if (wgs(M, N, 32, 32) >= kTargetWG) return launch_cfg<2, 2, 1, 1, 4, IS1X1, VEC>(p, M, K, N, s);
+    if (wgs(M, N, 16, 32) >= kTargetWG) return launch_cfg<1, 2, 1, 1, 4, IS1X1, VEC>(p, M, K, N, s);
+    return launch_cfg<1, 1, 1, 1, 4, IS1X1, VEC>(p, M, K, N, s);
+  }
+  if (N <= 16) {
+    if (wgs(M, N, 128, 16) >= kTargetWG) return launch_cfg<2, 1, 4, 1, 1, IS1X1, VEC>(p, M, K, N, s);
+    return launch_cfg<1, 1, 4, 1, 1, IS1X1, VEC>(p, M, K, N, s);
+  }
+  if (N <= 32 && wgs(M, N, 128, 32) >= kTargetWG) return launch_cfg<2, 2, 4, 1, 1, IS1X1, VEC>(p, M, K, N, s);
+  if (wgs(M, N, 64, 64) >= kTargetWG) return launch_cfg<2, 2, 2, 2, 1, IS1X1, VEC>(p, M, K, N, s);
+  return launch_cfg<1, 1, 2, 2, 1, IS1X1, VEC>(p, M, K, N, s);
 }
 
 }  // namespace bh
@@ -289,7 +368,12 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
   const int M = (int)Ml;
   hipStream_t s = (hipStream_t)stream;
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
-  const bool wzp = p.w_zp != 0;
-  if (is1x1) return wzp ? bh::launch_vec<true, true>(p, M, K, N, s) : bh::launch_vec<true, false>(p, M, K, N, s);
-  return wzp ? bh::launch_vec<false, true>(p, M, K, N, s) : bh::launch_vec<false, false>(p, M, K, N, s);
+  const int c = p.in_c;
+  if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);
+  if (is1x1 && c % 8 == 0) return bh::launch_shape<true, 8>(p, M, K, N, s);
+  if (is1x1 && c % 4 == 0) return bh::launch_shape<true, 4>(p, M, K, N, s);
+  if (c % 16 == 0) return bh::launch_shape<false, 16>(p, M, K, N, s);
+  if (c % 8 == 0) return bh::launch_shape<false, 8>(p, M, K, N, s);
+  if (c % 4 == 0) return bh::launch_shape<false, 4>(p, M, K, N, s);
+  return bh::launch_shape<false, 1>(p, M, K, N, s);
 }

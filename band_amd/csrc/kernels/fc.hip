@@ -36,13 +36,13 @@ __device__ __forceinline__ void load_x(const uint8_t* x, int d, int depth, uint3
 }
 
 template <int VEC, bool WZP>
-__global__ __launch_bounds__(256) void fc_kernel(bh_fc_params p) {
+__global__ __launch_bounds__(256) void fc_kernel(bh_fc_params p, FastDiv units) {
   const int wave = threadIdx.x >> 6;
   const int lane = threadIdx.x & 63;
-  const long job = (long)blockIdx.x * 4 + wave;
-  if (job >= (long)p.rows * p.units) return;
-  const int u = (int)(job % p.units);
-  const int r = (int)(job / p.units);
+  const int job = blockIdx.x * 4 + wave;
+  if (job >= p.rows * p.units) return;
+  const int r = units.div(job);
+  const int u = job - r * p.units;
   const uint8_t* x = (const uint8_t*)p.input + (long)r * p.depth;
   const int8_t* w = p.weights + (long)u * p.depth_pad;
   const uint32_t xorw = splat_byte(p.in_xor);
@@ -84,14 +84,19 @@ extern "C" int bh_fc_i8(const bh_fc_params* pp, bh_stream_t stream) {
   const bh_fc_params& p = *pp;
   hipStream_t s = (hipStream_t)stream;
   const long jobs = (long)p.rows * p.units;
+  if (jobs >= INT32_MAX) {
+    bh_set_last_error("bh_fc_i8: too many output elements for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  const bh::FastDiv units(p.units);
   dim3 grid((unsigned)((jobs + 3) / 4));
   const bool vec16 = (p.depth % 16 == 0) && ((uintptr_t)p.input % 16 == 0);
   if (p.w_zp != 0) {
-    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, true>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((bh::fc_kernel<1, true>), grid, dim3(256), 0, s, p);
+    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, true>), grid, dim3(256), 0, s, p, units);
+    else hipLaunchKernelGGL((bh::fc_kernel<1, true>), grid, dim3(256), 0, s, p, units);
   } else {
-    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, false>), grid, dim3(256), 0, s, p);
-    else hipLaunchKernelGGL((bh::fc_kernel<1, false>), grid, dim3(256), 0, s, p);
+    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, false>), grid, dim3(256), 0, s, p, units);
+    else hipLaunchKernelGGL((bh::fc_kernel<1, false>), grid, dim3(256), 0, s, p, units);
   }
   return bh_check_launch("fc_kernel");
 }

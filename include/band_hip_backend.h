@@ -93,12 +93,26 @@ int bhx_list_subgraphs(bhx_executor* e, int* model_ids, int* worker_ids, uint64_
 /* ExecuteSubgraph (synchronous: returns when outputs are in the views) */
 int bhx_execute_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask);
 
+/* --- native worker loop ------------------------------------------------
+ * Runs n_jobs Band jobs back to back on one executor, exactly the per-job
+ * work of Worker::Work (band/worker.cc:222-323) for a single-input /
+ * single-output subgraph: CopyDataFrom(request slot j % n_slots) into the
+ * input view (Engine::TryCopyInputTensors, band/engine.cc:1247-1319),
+ * ExecuteSubgraph (band/engine.cc:843-850), copy the output view out
+ * (TryCopyOutputTensors :1333-1365).  latency_us[j] (optional) receives
+ * end - enqueue of job j.  Stops at the first failing job. */
+int bhx_run_jobs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, const void* const* in_slots,
+                 int n_slots, size_t in_bytes, void* out, size_t out_bytes, int n_jobs, double* latency_us);
+
 /* --- extensions (measurement / tuning; not part of Band's interface) --- */
 int bhx_executor_set_graph(bhx_executor* e, int enabled);
 int bhx_executor_device(bhx_executor* e, int* ordinal);
 /* per-launch HIP-event timing of a prepared subgraph, averaged over iters */
 int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
                          bhx_op_timing* out, int cap, int* n);
+/* device microseconds per pass of a prepared subgraph, `iters` passes issued
+ * back to back on the executor's stream (graph replay when captured) */
+int bhx_time_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters, double* us);
 
 #ifdef __cplusplus
 }

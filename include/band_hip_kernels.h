@@ -103,6 +103,15 @@ typedef struct bh_conv_params {
   const int32_t* bias_eff;        /* [out_c] */
   const int32_t* mult;            /* [out_c] Q31 multipliers */
   const int32_t* shift;           /* [out_c] TFLite exponent (>0 = left) */
+  /* Optional fused residual ADD (TFLite ADD applied to this conv's
+   * requantised 8-bit output y and `residual`, same shape as the output):
+   *   out = ADD(y, residual) with add.cc's left_shift-20 arithmetic.
+   * Enabled when residual != NULL; y itself is then never stored. */
+  const void* residual;
+  int32_t add_y_off, add_r_off, add_o_off;    /* negated zps of y / residual, output zp */
+  int32_t add_left_shift;
+  int32_t add_y_mult, add_y_shift, add_r_mult, add_r_shift, add_o_mult, add_o_shift;
+  int32_t add_act_min, add_act_max;
 } bh_conv_params;
 
 /* DEPTHWISE_CONV_2D.  weights: int8-domain [k_h][k_w][out_c] (TFLite layout
@@ -174,6 +183,51 @@ typedef struct bh_pool_params {
   const void* input;
   void* output;
 } bh_pool_params;
+
+/* Fused MobileNet inverted-residual block (int8 per-channel models):
+ *   [CONV_2D 1x1 expand ->] DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 project [-> ADD x]
+ * exactly as the 3-4 TFLite ops compute it (each intermediate is requantised
+ * to its own 8-bit tensor), but one launch: a workgroup owns a tile of
+ * output pixels, stages the input region (tile + halo) in LDS, computes the
+ * expanded activation for the region into LDS (MFMA), the depthwise output
+ * into LDS (VALU), then the projection (MFMA) + residual epilogue to HBM.
+ * Intermediates never touch HBM. */
+typedef struct bh_irb_params {
+  int batch, in_h, in_w, in_c;        /* x: NHWC int8 */
+  int exp_c;                          /* expanded channels (== in_c when no expand) */
+  int out_h, out_w, out_c;            /* y: NHWC int8 */
+  int stride, pad_h, pad_w;           /* depthwise 3x3 */
+  int has_expand;
+  int tile_h, tile_w;                 /* output pixels per workgroup */
+  /* expand 1x1 (packed like bh_pack_conv_weights: [n_pad][k_pad]) */
+  const int8_t* exp_w; int exp_k_pad;
+  const int32_t* exp_bias_eff; const int32_t* exp_mult; const int32_t* exp_shift;
+  int32_t x_zp;                       /* x zero point */
+  int32_t e_zp, e_act_min, e_act_max; /* expanded tensor quantisation */
+  /* depthwise [3][3][exp_c] */
+  const int8_t* dw_w;
+  const int32_t* dw_bias; const int32_t* dw_mult; const int32_t* dw_shift;
+  int32_t d_zp, d_act_min, d_act_max;
+  /* project 1x1 ([n_pad][k_pad], bias_eff folds d_zp) */
+  const int8_t* proj_w; int proj_k_pad;
+  const int32_t* proj_bias_eff; const int32_t* proj_mult; const int32_t* proj_shift;
+  int32_t p_zp, p_act_min, p_act_max;
+  /* optional residual ADD(p, x) (has_residual: stride 1, in_c == out_c) */
+  int has_residual;
+  int32_t add_p_off, add_x_off, add_o_off, add_left_shift;
+  int32_t add_p_mult, add_p_shift, add_x_mult, add_x_shift, add_o_mult, add_o_shift;
+  int32_t add_act_min, add_act_max;
+  const void* input;
+  void* output;
+  /* diagnostics: when non-NULL, wave 0 of each workgroup writes 8 uint64
+   * s_memrealtime stamps (100 MHz) at phase boundaries to
+   * debug_stamps[8 * workgroup]; NULL in production */
+  void* debug_stamps;
+} bh_irb_params;
+
+/* LDS bytes one workgroup of bh_irb_i8 needs for a tile (0 if unsupported) */
+size_t bh_irb_lds_bytes(const bh_irb_params* p);
+int bh_irb_i8(const bh_irb_params* p, bh_stream_t s);
 
 /* ---- host-side operand packing (pure CPU, no device calls) -------------- */
 

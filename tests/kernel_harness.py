@@ -68,14 +68,29 @@ class ConvCase:
         return orc.conv2d(self.x, self.w, self.bias, **kw)
 
     def gpu(self, lib, stream=None):
+        keep = []
+        p = self.params(lib, keep)
+        fn = lib.bh_dwconv2d_i8 if self.depthwise else lib.bh_conv2d_i8
+        from band_amd import _abi
+        _abi.check(fn(ctypes.byref(p), stream), "bh_dwconv2d_i8" if self.depthwise else "bh_conv2d_i8")
+        out = self._dy.download(self.dtype, (self.b, self.oh, self.ow, self.oc))
+        del keep
+        return out
+
+    def params(self, lib, keep, dx=None, dy=None):
+        """C-ABI params on device copies of the case (buffers appended to
+        `keep`); dx / dy override the activation buffers (timing chains)."""
         from band_amd import _abi
         from band_amd.device import DeviceBuffer
-        dx = DeviceBuffer.from_array(self.x)
         out_shape = (self.b, self.oh, self.ow, self.oc)
-        dy = DeviceBuffer(int(np.prod(out_shape)))
+        if dx is None:
+            dx = DeviceBuffer.from_array(self.x)
+        if dy is None:
+            dy = DeviceBuffer(int(np.prod(out_shape)))
+        self._dy = dy
         dmult = DeviceBuffer.from_array(self.mult.astype(np.int32))
         dshift = DeviceBuffer.from_array(self.shift.astype(np.int32))
-        keep = [dx, dy, dmult, dshift]
+        keep += [dx, dy, dmult, dshift]
         in_zp_d = dom(self.in_zp, self.dtype)
         w_zp_d = dom(self.w_zp, self.dtype) if self.dtype == np.uint8 else 0
         if self.depthwise:
@@ -91,7 +106,6 @@ class ConvCase:
                 w_zp=w_zp_d, out_zp=self.out_zp, act_min=self.amin, act_max=self.amax,
                 input=dx.value, output=dy.value, weights=dw.value, bias=db.value,
                 mult=dmult.value, shift=dshift.value)
-            _abi.check(lib.bh_dwconv2d_i8(ctypes.byref(p), stream), "bh_dwconv2d_i8")
         else:
             K = self.kh * self.kw * self.ic
             kp, npd = ctypes.c_int(), ctypes.c_int()
@@ -113,11 +127,7 @@ class ConvCase:
                 k_pad=kp.value, n_pad=npd.value, in_xor=xor_of(self.dtype), in_zp=in_zp_d, w_zp=w_zp_d,
                 out_zp=self.out_zp, act_min=self.amin, act_max=self.amax, input=dx.value,
                 output=dy.value, weights=dw.value, bias_eff=db.value, mult=dmult.value, shift=dshift.value)
-            _abi.check(lib.bh_conv2d_i8(ctypes.byref(p), stream), "bh_conv2d_i8")
-        from band_amd.device import Stream  # noqa: F401  (null stream sync via blocking d2h)
-        out = dy.download(self.dtype, out_shape)
-        del keep
-        return out
+        return p
 
 
 # The 21 distinct MobileNetV2-1.0-224 conv GEMM shapes:

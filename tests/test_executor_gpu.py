@@ -140,3 +140,49 @@ def test_error_behaviour(gpu_lib, golden_dir):
     spec = ex.InvestigateModelSpec(model)
     assert spec.unsupported_ops[DeviceFlag.kGPU] == {0, 1}
     assert not ex.PrepareSubgraph(model).ok()
+
+
+@pytest.mark.parametrize("arch,dtype,batch", [
+    ("mobilenet_v2", np.int8, 1), ("mobilenet_v2", np.int8, 3), ("mobilenet_v2", np.uint8, 1),
+    ("mobilenet_v1", np.int8, 1), ("mobilenet_v2", np.int8, 8)])
+def test_synthetic_models_bit_exact(gpu_lib, arch, dtype, batch):
+    """The bench models (BASELINE C1/C2, synthetic weights), fused epilogues on."""
+    from band_amd import tflite_synth as S
+    buf = getattr(S, arch)(dtype, seed=7, batch=batch)
+    model = HipModel(11)
+    assert model.FromBuffer(buf).ok()
+    ex = HipModelExecutor(11, 1, DeviceFlag.kGPU)
+    assert ex.PrepareSubgraph(model).ok()
+    key = SubgraphKey(11, 1)
+    om = Model(buf)
+    t = om.tensors[om.inputs[0]]
+    rng = np.random.default_rng(batch)
+    lo, hi = (-128, 128) if dtype == np.int8 else (0, 256)
+    for _ in range(2):
+        x = rng.integers(lo, hi, t.shape).astype(dtype)
+        ex.GetTensorView(key, om.inputs[0]).GetData()[...] = x
+        assert ex.ExecuteSubgraph(key).ok()
+        ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]]
+        np.testing.assert_array_equal(ex.GetTensorView(key, om.outputs[0]).GetData(), ref.reshape(-1, ref.shape[-1]))
+
+
+def test_view_of_fused_tensor_materialises_it(gpu_lib):
+    """Asking for a view of a conv output that an ADD epilogue fused away
+    re-lowers without that fusion; both the tensor and the final output match."""
+    from band_amd import tflite_synth as S
+    buf = S.mobilenet_v2(np.int8, seed=3)
+    om = Model(buf)
+    add_op = next(o for o in om.operators if o.name == "ADD")
+    conv_out = add_op.inputs[0]
+    model = HipModel(12)
+    assert model.FromBuffer(buf).ok()
+    ex = HipModelExecutor(12, 1, DeviceFlag.kGPU)
+    assert ex.PrepareSubgraph(model).ok()
+    key = SubgraphKey(12, 1)
+    v = ex.GetTensorView(key, conv_out)
+    x = np.random.default_rng(0).integers(-128, 128, (1, 224, 224, 3)).astype(np.int8)
+    ex.GetTensorView(key, om.inputs[0]).GetData()[...] = x
+    assert ex.ExecuteSubgraph(key).ok()
+    ref = OracleInterpreter(om).run({om.inputs[0]: x})
+    np.testing.assert_array_equal(v.GetData(), ref[conv_out])
+    np.testing.assert_array_equal(ex.GetTensorView(key, om.outputs[0]).GetData(), ref[om.outputs[0]])

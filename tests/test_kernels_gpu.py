@@ -136,6 +136,10 @@ def test_mul(gpu_lib, dtype):
     dict(shape=(1, 7, 7, 1280), f=(7, 7), s=(1, 1), same=False, dtype=np.int8),
     dict(shape=(2, 13, 11, 6), f=(3, 3), s=(2, 2), same=True, dtype=np.int8),
     dict(shape=(1, 9, 9, 5), f=(2, 2), s=(2, 2), same=True, dtype=np.uint8),
+    # wide-window path (pool_wide_kernel): clipped edge windows, several pixels
+    dict(shape=(2, 9, 9, 40), f=(5, 5), s=(3, 3), same=True, dtype=np.int8),
+    dict(shape=(1, 20, 20, 8), f=(8, 8), s=(4, 4), same=True, dtype=np.uint8),
+    dict(shape=(1, 12, 12, 260), f=(12, 12), s=(1, 1), same=False, dtype=np.int8),
 ])
 def test_pool(gpu_lib, kind, cfg):
     from band_amd import _abi

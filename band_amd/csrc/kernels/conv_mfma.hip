@@ -326,6 +326,8 @@ static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_
 
 }  // namespace bh
 
+int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  // conv_direct.hip
+
 extern "C" int bh_conv_packed_geometry(int out_c, int k, int* k_pad, int* n_pad) {
   if (out_c <= 0 || k <= 0 || !k_pad || !n_pad) return BH_EINVAL;
   *k_pad = (k + 63) / 64 * 64;
@@ -369,6 +371,8 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
   const int c = p.in_c;
+  // RGB-stem-like layers (tiny K, byte-granular gather): direct VALU kernel
+  if (!is1x1 && K <= 64 && c < 8) return bh_conv_direct_launch(p, M, K, s);
   if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);
   if (is1x1 && c % 8 == 0) return bh::launch_shape<true, 8>(p, M, K, N, s);
   if (is1x1 && c % 4 == 0) return bh::launch_shape<true, 4>(p, M, K, N, s);

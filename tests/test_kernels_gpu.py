@@ -44,6 +44,10 @@ def test_conv1x1_uint8_per_tensor(gpu_lib, spatial, ic, oc):
     dict(b=3, ih=8, iw=8, ic=40, oc=24, kh=1, kw=1, stride=(2, 2)),
     dict(b=1, ih=9, iw=9, ic=20, oc=17, kh=1, kw=1, act=0),
     dict(b=1, ih=6, iw=7, ic=8, oc=130, kh=3, kw=3, dtype=np.uint8, act=1),
+    # small-K direct kernel (conv_direct.hip): K 63 / 25 / 18, channel tails
+    dict(b=2, ih=15, iw=12, ic=7, oc=12, kh=3, kw=3, stride=(2, 2)),
+    dict(b=1, ih=10, iw=10, ic=1, oc=8, kh=5, kw=5, dtype=np.uint8),
+    dict(b=1, ih=9, iw=9, ic=2, oc=19, kh=3, kw=3, dil=(2, 2), same=False),
 ])
 def test_conv_general(gpu_lib, args):
     rng = np.random.default_rng(zlib.crc32(repr(sorted(args.items())).encode()))

@@ -72,6 +72,35 @@ class IrbParams(ctypes.Structure):
 
 
 # symbol -> (restype, argtypes)
+CONCAT_MAX_INPUTS = 16
+
+
+class ConcatParams(ctypes.Structure):
+    _fields_ = [("n_inputs", c_int), ("outer", ctypes.c_long),
+                ("row", ctypes.c_long * CONCAT_MAX_INPUTS), ("input", c_void_p * CONCAT_MAX_INPUTS),
+                ("table", c_void_p * CONCAT_MAX_INPUTS), ("output", c_void_p)]
+
+
+class PadParams(ctypes.Structure):
+    _fields_ = [("elem_bytes", c_int), ("in_shape", c_int * 4), ("pad_before", c_int * 4),
+                ("pad_after", c_int * 4), ("value", ctypes.c_uint32), ("input", c_void_p), ("output", c_void_p)]
+
+
+class ResizeNearestParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("batch", "in_h", "in_w", "out_h", "out_w", "row_bytes")] + [
+        (n, c_void_p) for n in ("y_index", "x_index", "input", "output")]
+
+
+class ResizeBilinearParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("batch", "in_h", "in_w", "channels", "out_h", "out_w")] + [
+        (n, c_void_p) for n in ("y_tab", "x_tab", "input", "output")]
+
+
+class SoftmaxParams(ctypes.Structure):
+    _fields_ = [("rows", ctypes.c_long), ("depth", c_int), ("is_signed", c_int), ("table", c_void_p),
+                ("out_scale", ctypes.c_float), ("out_zp", c_int32), ("input", c_void_p), ("output", c_void_p)]
+
+
 KERNEL_SYMBOLS = {
     "bh_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "bh_set_device": (c_int, [c_int]),
@@ -103,6 +132,14 @@ KERNEL_SYMBOLS = {
                                      c_int32, c_int32, c_void_p, c_void_p]),
     "bh_conv_packed_geometry": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
     "bh_conv2d_i8": (c_int, [ctypes.POINTER(ConvParams), c_void_p]),
+    "bh_lut_u8": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
+    "bh_lut_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
+    "bh_quantize_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, ctypes.c_float, c_int32, c_int, c_void_p]),
+    "bh_concat": (c_int, [ctypes.POINTER(ConcatParams), c_void_p]),
+    "bh_pad": (c_int, [ctypes.POINTER(PadParams), c_void_p]),
+    "bh_resize_nearest": (c_int, [ctypes.POINTER(ResizeNearestParams), c_void_p]),
+    "bh_resize_bilinear_i8": (c_int, [ctypes.POINTER(ResizeBilinearParams), c_void_p]),
+    "bh_softmax_i8": (c_int, [ctypes.POINTER(SoftmaxParams), c_void_p]),
     "bh_dwconv2d_i8": (c_int, [ctypes.POINTER(DwConvParams), c_void_p]),
     "bh_fc_i8": (c_int, [ctypes.POINTER(FcParams), c_void_p]),
     "bh_eltwise_i8": (c_int, [ctypes.POINTER(EltwiseParams), c_void_p]),

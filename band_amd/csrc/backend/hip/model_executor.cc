@@ -131,6 +131,59 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
     case kTflSqueeze:
       if (out.type != in.type || out.num_elements() != in.num_elements()) return no("size mismatch");
       return true;
+    case kTflQuantize:
+      if (!IsQ8(out.type) || !HasQ(out)) return no("QUANTIZE output must be 8-bit quantized");
+      if (in.type == DataType::kFloat32) return true;
+      if (!IsQ8(in.type) || !HasQ(in)) return no("QUANTIZE input must be float32 or 8-bit");
+      return true;
+    case kTflDequantize:
+      if (!IsQ8(in.type) || !HasQ(in) || out.type != DataType::kFloat32) return no("only 8-bit -> float32");
+      return true;
+    case kTflRelu:
+    case kTflRelu6:
+    case kTflReluN1To1:
+    case kTflLogistic:
+      if (!IsQ8(in.type) || out.type != in.type || !HasQ(in) || !HasQ(out)) return no("only 8-bit quantized");
+      return true;
+    case kTflSoftmax:
+      if (!IsQ8(in.type) || out.type != in.type || !HasQ(in) || !HasQ(out) || in.shape.empty())
+        return no("only 8-bit quantized in and out");
+      return true;
+    case kTflConcatenation: {
+      if (op.inputs.size() > BH_CONCAT_MAX_INPUTS) return no("too many inputs");
+      if (op.options.valid() && op.options.Int8(1, 0) != 0) return no("fused activation on CONCATENATION");
+      for (int t : op.inputs) {
+        if (t < 0) return no("missing input");
+        const TflTensor& x = T(t);
+        if (x.type != out.type || x.shape.size() != out.shape.size()) return no("type / rank mismatch");
+        if (out.type == DataType::kInt8 && (Scale(x) != Scale(out) || Zp(x) != Zp(out)))
+          return no("int8 inputs must share the output's quantization");
+        if (out.type == DataType::kUInt8 && !HasQ(x)) return no("missing quantization");
+      }
+      const size_t eb = GetDataTypeBytes(out.type);
+      if (eb == 0) return no("unsized type");
+      return true;
+    }
+    case kTflPad:
+    case kTflPadV2: {
+      const size_t eb = GetDataTypeBytes(in.type);
+      if ((eb != 1 && eb != 4) || out.type != in.type || in.shape.size() > 4) return no("1/4-byte types, rank <= 4");
+      if (op.inputs.size() < 2 || op.inputs[1] < 0 || !T(op.inputs[1]).is_const()) return no("paddings must be constant");
+      const TflTensor& pt = T(op.inputs[1]);
+      if (pt.type != DataType::kInt32 && pt.type != DataType::kInt64) return no("paddings must be int32/int64");
+      if (op.builtin == kTflPadV2 && op.inputs.size() > 2 && op.inputs[2] >= 0 && !T(op.inputs[2]).is_const())
+        return no("constant value must be constant");
+      return true;
+    }
+    case kTflResizeNearestNeighbor: {
+      const size_t eb = GetDataTypeBytes(in.type);
+      if (in.shape.size() != 4 || out.shape.size() != 4 || out.type != in.type || eb == 0) return no("4-D only");
+      return true;
+    }
+    case kTflResizeBilinear:
+      if (in.type != DataType::kInt8 || out.type != in.type || in.shape.size() != 4 || out.shape.size() != 4)
+        return no("int8 4-D only (ResizeBilinearInteger)");
+      return true;
     default:
       return no("op not in the HIP kernel set");
   }
@@ -150,11 +203,17 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
     meta_.push_back(std::move(m));
   }
   consumers_.assign(d.tensors.size(), {});
-  for (int i = 0; i < static_cast<int>(d.ops.size()); ++i)
+  producer_.assign(d.tensors.size(), -1);
+  for (int i = 0; i < static_cast<int>(d.ops.size()); ++i) {
     for (int t : d.ops[i].inputs)
       if (t >= 0) consumers_[t].push_back(i);
+    for (int t : d.ops[i].outputs)
+      if (t >= 0) producer_[t] = i;
+  }
   const char* f = std::getenv("BAND_HIP_FUSION");
   if (f && f[0] == '0') allow_fusion_ = false;
+  if (f && std::strcmp(f, "noirb") == 0) allow_irb_ = false;   // diagnostics: one fusion kind at a time
+  if (f && std::strcmp(f, "noadd") == 0) allow_add_ = false;
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
@@ -225,6 +284,215 @@ absl::Status HipModelExecutor::DevicePtr(const HipModel& model, int t, PreparedS
   return absl::OkStatus();
 }
 
+absl::Status HipModelExecutor::UploadConst(const std::string& key, const void* data, size_t bytes,
+                                           PreparedSubgraph* sg, const void** dev) {
+  auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
+  if (!blob) {
+    blob = std::make_shared<DeviceBlob>(ordinal_, bytes);
+    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), data, bytes) != 0) return HipErr(1, "upload table");
+    DeviceRegistry::Get().PutConst(ordinal_, key, blob);
+  }
+  sg->consts.push_back(blob);
+  *dev = blob->ptr();
+  return absl::OkStatus();
+}
+
+// Glue ops.  Every 8-bit unary op becomes a 256-entry
+// table built here with TFLite's formula (quant.cc), so the device does a
+// byte gather; index maps TFLite computes in float are tabulated here too.
+absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in_ptr, void* out_ptr,
+                                         const std::string& ckey, PreparedSubgraph* sg, Launch* L) {
+  const TflModel& d = model.desc();
+  const TflOperator& op = d.ops[oi];
+  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
+  const TflTensor& in = T(op.inputs[0]);
+  const TflTensor& out = T(op.outputs[0]);
+  const bool i8 = in.type == DataType::kInt8;
+  const double in_bytes = static_cast<double>(meta_[op.inputs[0]]->bytes);
+  const double out_bytes = static_cast<double>(meta_[op.outputs[0]]->bytes);
+  L->alg_bytes = in_bytes + out_bytes;
+  switch (op.builtin) {
+    case kTflQuantize:
+    case kTflRelu:
+    case kTflRelu6:
+    case kTflReluN1To1:
+    case kTflLogistic: {
+      L->src = in_ptr;
+      L->dst = out_ptr;
+      L->count = static_cast<long>(out.num_elements());
+      if (op.builtin == kTflQuantize && in.type == DataType::kFloat32) {
+        L->kind = Launch::kQuantF32;
+        L->kernel = "quantize_f32_kernel";
+        L->q_scale = Scale(out);
+        L->q_zp = Zp(out);
+        L->q_signed = out.type == DataType::kInt8 ? 1 : 0;
+        return absl::OkStatus();
+      }
+      uint8_t table[256];
+      if (op.builtin == kTflQuantize) {
+        RequantizeTable(i8, Scale(in), Zp(in), out.type == DataType::kInt8, Scale(out), Zp(out), table);
+      } else if (op.builtin == kTflLogistic) {
+        LogisticTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), table);
+      } else {
+        const float lo = op.builtin == kTflReluN1To1 ? -1.0f : 0.0f;
+        const float hi = op.builtin == kTflRelu6 ? 6.0f : 1.0f;
+        ReluTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), lo, hi, op.builtin == kTflRelu, table);
+      }
+      RETURN_STATUS_IF(UploadConst(ckey + "/lut", table, sizeof(table), sg, &L->table));
+      L->kind = Launch::kLutU8;
+      L->kernel = "lut_u8_kernel";
+      return absl::OkStatus();
+    }
+    case kTflDequantize: {
+      float table[256];
+      DequantizeTable(i8, Scale(in), Zp(in), table);
+      RETURN_STATUS_IF(UploadConst(ckey + "/lut", table, sizeof(table), sg, &L->table));
+      L->kind = Launch::kLutF32;
+      L->kernel = "lut_f32_kernel";
+      L->src = in_ptr;
+      L->dst = out_ptr;
+      L->count = static_cast<long>(out.num_elements());
+      return absl::OkStatus();
+    }
+    case kTflSoftmax: {
+      const float beta = op.options.valid() ? op.options.Float(0, 1.0f) : 1.0f;
+      float table[256];
+      SoftmaxExpTable(Scale(in), beta, table);
+      const void* dt = nullptr;
+      RETURN_STATUS_IF(UploadConst(ckey + "/exp", table, sizeof(table), sg, &dt));
+      bh_softmax_params& p = L->softmax;
+      p = bh_softmax_params{};
+      p.depth = in.shape.back();
+      p.rows = static_cast<long>(in.num_elements() / std::max(p.depth, 1));
+      p.is_signed = i8 ? 1 : 0;
+      p.table = static_cast<const float*>(dt);
+      p.out_scale = Scale(out);
+      p.out_zp = Zp(out);
+      p.input = in_ptr;
+      p.output = out_ptr;
+      L->kind = Launch::kSoftmax;
+      L->kernel = "softmax_kernel";
+      return absl::OkStatus();
+    }
+    case kTflConcatenation: {
+      const int rank = static_cast<int>(out.shape.size());
+      int axis = op.options.valid() ? op.options.Int(0, 0) : 0;
+      if (axis < 0) axis += rank;
+      if (axis < 0 || axis >= rank) return absl::InternalError("CONCATENATION axis out of range");
+      long outer = 1, inner = static_cast<long>(GetDataTypeBytes(out.type));
+      for (int i = 0; i < axis; ++i) outer *= out.shape[i];
+      for (int i = axis + 1; i < rank; ++i) inner *= out.shape[i];
+      bh_concat_params& p = L->concat;
+      p = bh_concat_params{};
+      p.n_inputs = static_cast<int>(op.inputs.size());
+      p.outer = outer;
+      p.output = out_ptr;
+      L->alg_bytes = out_bytes;
+      for (int k = 0; k < p.n_inputs; ++k) {
+        const TflTensor& x = T(op.inputs[k]);
+        void* xp = nullptr;
+        RETURN_STATUS_IF(DevicePtr(model, op.inputs[k], sg, &xp));
+        p.input[k] = xp;
+        p.row[k] = static_cast<long>(x.shape[axis]) * inner;
+        L->alg_bytes += static_cast<double>(meta_.size() > static_cast<size_t>(op.inputs[k]) && meta_[op.inputs[k]]
+                                                ? meta_[op.inputs[k]]->bytes
+                                                : 0);
+        if (out.type == DataType::kUInt8 && (Zp(x) != Zp(out) || Scale(x) != Scale(out))) {
+          uint8_t table[256];
+          ConcatRescaleTable(Scale(x), Zp(x), Scale(out), Zp(out), table);
+          RETURN_STATUS_IF(UploadConst(ckey + "/lut" + std::to_string(k), table, sizeof(table), sg, &p.table[k]));
+        }
+      }
+      L->kind = Launch::kConcat;
+      L->kernel = "concat_kernel";
+      return absl::OkStatus();
+    }
+    case kTflPad:
+    case kTflPadV2: {
+      const TflTensor& pt = T(op.inputs[1]);
+      const int rank = static_cast<int>(in.shape.size());
+      std::vector<int64_t> pads(2 * static_cast<size_t>(rank), 0);
+      for (size_t i = 0; i < pads.size() && i * (pt.type == DataType::kInt64 ? 8 : 4) < pt.data_size; ++i) {
+        if (pt.type == DataType::kInt64) {
+          int64_t v;
+          std::memcpy(&v, pt.data + 8 * i, 8);
+          pads[i] = v;
+        } else {
+          int32_t v;
+          std::memcpy(&v, pt.data + 4 * i, 4);
+          pads[i] = v;
+        }
+      }
+      bh_pad_params& p = L->pad;
+      p = bh_pad_params{};
+      p.elem_bytes = static_cast<int>(GetDataTypeBytes(in.type));
+      Shape4(in.shape, p.in_shape);
+      const int lead = 4 - rank;
+      for (int dd = 0; dd < rank; ++dd) {
+        p.pad_before[lead + dd] = static_cast<int>(pads[2 * dd]);
+        p.pad_after[lead + dd] = static_cast<int>(pads[2 * dd + 1]);
+      }
+      uint32_t value = 0;
+      if (op.builtin == kTflPadV2 && op.inputs.size() > 2 && op.inputs[2] >= 0) {
+        const TflTensor& cv = T(op.inputs[2]);
+        std::memcpy(&value, cv.data, std::min<size_t>(cv.data_size, p.elem_bytes));
+      } else if (IsQ8(in.type)) {
+        value = static_cast<uint32_t>(Zp(out)) & 0xffu;  // quantized PAD pads with the output zero point
+      }
+      p.value = value;
+      p.input = in_ptr;
+      p.output = out_ptr;
+      L->kind = Launch::kPad;
+      L->kernel = "pad_kernel";
+      return absl::OkStatus();
+    }
+    case kTflResizeNearestNeighbor:
+    case kTflResizeBilinear: {
+      const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], c = in.shape[3];
+      const int oh = out.shape[1], ow = out.shape[2];
+      const bool nearest = op.builtin == kTflResizeNearestNeighbor;
+      const bool ac = op.options.valid() && op.options.Bool(nearest ? 0 : 2, false);
+      const bool hp = op.options.valid() && op.options.Bool(nearest ? 1 : 3, false);
+      if (nearest) {
+        std::vector<int32_t> tab(static_cast<size_t>(oh) + ow);
+        for (int y = 0; y < oh; ++y) tab[y] = NearestNeighborIndex(y, ih, oh, ac, hp);
+        for (int x = 0; x < ow; ++x) tab[oh + x] = NearestNeighborIndex(x, iw, ow, ac, hp);
+        const void* dt = nullptr;
+        RETURN_STATUS_IF(UploadConst(ckey + "/idx", tab.data(), tab.size() * 4, sg, &dt));
+        bh_resize_nearest_params& p = L->rnear;
+        p = bh_resize_nearest_params{};
+        p.batch = b; p.in_h = ih; p.in_w = iw; p.out_h = oh; p.out_w = ow;
+        p.row_bytes = c * static_cast<int>(GetDataTypeBytes(in.type));
+        p.y_index = static_cast<const int32_t*>(dt);
+        p.x_index = static_cast<const int32_t*>(dt) + oh;
+        p.input = in_ptr;
+        p.output = out_ptr;
+        L->kind = Launch::kResizeNearest;
+        L->kernel = "resize_nearest_kernel";
+      } else {
+        std::vector<int32_t> ty, tx;
+        BilinearIntegerTable(ih, oh, ac, hp, &ty);
+        BilinearIntegerTable(iw, ow, ac, hp, &tx);
+        ty.insert(ty.end(), tx.begin(), tx.end());
+        const void* dt = nullptr;
+        RETURN_STATUS_IF(UploadConst(ckey + "/tab", ty.data(), ty.size() * 4, sg, &dt));
+        bh_resize_bilinear_params& p = L->rbil;
+        p = bh_resize_bilinear_params{};
+        p.batch = b; p.in_h = ih; p.in_w = iw; p.channels = c; p.out_h = oh; p.out_w = ow;
+        p.y_tab = static_cast<const int32_t*>(dt);
+        p.x_tab = static_cast<const int32_t*>(dt) + 3 * oh;
+        p.input = in_ptr;
+        p.output = out_ptr;
+        L->kind = Launch::kResizeBilinear;
+        L->kernel = "resize_bilinear_kernel";
+      }
+      return absl::OkStatus();
+    }
+    default:
+      return absl::InternalError(std::string("no lowering for ") + TflBuiltinName(op.builtin));
+  }
+}
+
 absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubgraph* sg) {
   sg->launches.clear();
   sg->fused_ops.clear();
@@ -233,7 +501,7 @@ absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubg
     if (sg->fused_ops.count(i)) continue;
     RETURN_STATUS_IF(Lower(model, i, sg));
   }
-  if (allow_fusion_) FuseBlocks(model, sg);
+  if (allow_fusion_ && allow_irb_) FuseBlocks(model, sg);
   return absl::OkStatus();
 }
 
@@ -457,7 +725,7 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
 // conv's 8-bit output, then add.cc's arithmetic), so the result is
 // bit-identical to running the two ops.
 bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, PreparedSubgraph* sg, Launch* L) {
-  if (!allow_fusion_) return false;
+  if (!allow_fusion_ || !allow_add_) return false;
   const TflModel& d = model.desc();
   const int t = d.ops[oi].outputs[0];
   if (consumers_[t].size() != 1) return false;
@@ -472,6 +740,10 @@ bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, Prepare
   const bool conv_is_first = add.inputs[0] == t;
   const int other = conv_is_first ? add.inputs[1] : add.inputs[0];
   if (other == t) return false;
+  // the epilogue reads the other operand while the conv runs, so it must
+  // already exist then: produced by an earlier op (an FPN's ADD of a lateral
+  // conv and an upsampled map produced later must stay unfused)
+  if (other < 0 || producer_[other] > oi) return false;
   const TflTensor& tc = d.tensors[t];
   const TflTensor& tr = d.tensors[other];
   const TflTensor& to = d.tensors[add.outputs[0]];
@@ -721,6 +993,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.kind = Launch::kPool;
     L.kernel = "pool_kernel";
     L.alg_bytes = static_cast<double>(in.num_elements() + out.num_elements());
+  } else if (op.builtin != kTflReshape && op.builtin != kTflSqueeze) {
+    RETURN_STATUS_IF(LowerGlue(model, oi, in_ptr, out_ptr, ckey, sg, &L));
   } else {  // RESHAPE / SQUEEZE: same bytes, new dims
     L.kind = Launch::kCopy;
     L.kernel = "copy";
@@ -930,6 +1204,18 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
     case Launch::kCopy: rc = l.src == l.dst ? 0 : bh_memcpy_d2d_async(l.dst, l.src, l.bytes, stream_); break;
+    case Launch::kLutU8: rc = bh_lut_u8(l.src, l.dst, l.count, l.table, stream_); break;
+    case Launch::kLutF32:
+      rc = bh_lut_f32(l.src, l.dst, l.count, static_cast<const float*>(l.table), stream_);
+      break;
+    case Launch::kQuantF32:
+      rc = bh_quantize_f32(static_cast<const float*>(l.src), l.dst, l.count, l.q_scale, l.q_zp, l.q_signed, stream_);
+      break;
+    case Launch::kConcat: rc = bh_concat(&l.concat, stream_); break;
+    case Launch::kPad: rc = bh_pad(&l.pad, stream_); break;
+    case Launch::kResizeNearest: rc = bh_resize_nearest(&l.rnear, stream_); break;
+    case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
+    case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }

@@ -34,7 +34,10 @@ namespace band {
 namespace hip {
 
 struct Launch {
-  enum Kind { kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb } kind;
+  enum Kind {
+    kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
+    kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax
+  } kind;
   int op_index = -1;
   bh_conv_params conv{};
   bh_dwconv_params dw{};
@@ -42,6 +45,16 @@ struct Launch {
   bh_eltwise_params elt{};
   bh_pool_params pool{};
   bh_irb_params irb{};
+  bh_concat_params concat{};
+  bh_pad_params pad{};
+  bh_resize_nearest_params rnear{};
+  bh_resize_bilinear_params rbil{};
+  bh_softmax_params softmax{};
+  const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
+  long count = 0;               // kLut* / kQuantF32: elements
+  float q_scale = 0.f;          // kQuantF32
+  int32_t q_zp = 0;
+  int q_signed = 0;
   void* dst = nullptr;
   const void* src = nullptr;
   size_t bytes = 0;
@@ -121,13 +134,22 @@ class HipModelExecutor : public interface::IModelExecutor {
   // measured (no GPU stream, or a launch failed).
   double TimeLaunches(const std::vector<const Launch*>& ls, int iters);
   absl::Status DevicePtr(const HipModel& model, int tensor, PreparedSubgraph* sg, void** ptr);
+  // host-built constant (table) resident on this executor's device, shared
+  // across executors by `key`
+  absl::Status UploadConst(const std::string& key, const void* data, size_t bytes, PreparedSubgraph* sg,
+                           const void** dev);
+  absl::Status LowerGlue(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,
+                         PreparedSubgraph* sg, Launch* l);
   absl::Status Enqueue(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
 
   const HipModel* model_ = nullptr;
   std::vector<std::unique_ptr<TensorMeta>> meta_;
   std::vector<std::vector<int>> consumers_;  // tensor -> ops reading it (whole model)
+  std::vector<int> producer_;                // tensor -> op writing it (-1: input / constant)
   bool allow_fusion_ = true;
+  bool allow_irb_ = true;  // BAND_HIP_FUSION=noirb / noadd: diagnostics
+  bool allow_add_ = true;
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;

@@ -1,6 +1,7 @@
 #include "backend/hip/quant.h"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 
 namespace band {
@@ -117,6 +118,114 @@ int ComputePadding(int stride, int dilation, int in, int filter, int out) {
   const int eff = (filter - 1) * dilation + 1;
   const int p = ((out - 1) * stride + eff - in) / 2;
   return p > 0 ? p : 0;
+}
+
+namespace {
+int32_t Srdhm(int32_t a, int32_t b) {
+  const bool overflow = a == b && a == INT32_MIN;
+  const int64_t ab = static_cast<int64_t>(a) * static_cast<int64_t>(b);
+  const int32_t nudge = ab >= 0 ? (1 << 30) : (1 - (1 << 30));
+  const int32_t hi = static_cast<int32_t>((ab + nudge) / (1ll << 31));
+  return overflow ? INT32_MAX : hi;
+}
+int32_t Rdbypot(int32_t x, int e) {
+  const int32_t mask = static_cast<int32_t>((1ll << e) - 1);
+  const int32_t rem = x & mask;
+  const int32_t thr = (mask >> 1) + (x < 0 ? 1 : 0);
+  return (x >> e) + (rem > thr ? 1 : 0);
+}
+int32_t Clamp(int32_t v, int32_t lo, int32_t hi) { return v < lo ? lo : (v > hi ? hi : v); }
+int32_t ByteValue(int b, bool is_signed) { return is_signed ? static_cast<int8_t>(b) : b; }
+}  // namespace
+
+int32_t MultiplyByQuantizedMultiplier(int32_t x, int32_t q, int shift) {
+  const int left = shift > 0 ? shift : 0;
+  const int right = shift > 0 ? 0 : -shift;
+  return Rdbypot(Srdhm(static_cast<int32_t>(static_cast<uint32_t>(x) << left), q), right);
+}
+
+void RequantizeTable(bool in_signed, float in_scale, int32_t in_zp, bool out_signed, float out_scale,
+                     int32_t out_zp, uint8_t table[256]) {
+  int32_t q;
+  int sh;
+  QuantizeMultiplier(static_cast<double>(in_scale) / static_cast<double>(out_scale), &q, &sh);
+  const int32_t lo = out_signed ? -128 : 0, hi = out_signed ? 127 : 255;
+  for (int b = 0; b < 256; ++b)
+    table[b] = static_cast<uint8_t>(
+        Clamp(MultiplyByQuantizedMultiplier(ByteValue(b, in_signed) - in_zp, q, sh) + out_zp, lo, hi));
+}
+
+void ReluTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp, float act_min,
+               float act_max, bool act_max_inf, uint8_t table[256]) {
+  int32_t q;
+  int sh;
+  const double real = in_scale / out_scale;  // float quotient, as ReluPrepare
+  QuantizeMultiplier(real, &q, &sh);
+  const int32_t tmin = is_signed ? -128 : 0, tmax = is_signed ? 127 : 255;
+  const int32_t qmin = std::max(tmin, out_zp + static_cast<int32_t>(std::roundf(act_min / out_scale)));
+  const int32_t qmax =
+      act_max_inf ? tmax : std::min(tmax, out_zp + static_cast<int32_t>(std::roundf(act_max / out_scale)));
+  for (int b = 0; b < 256; ++b)
+    table[b] = static_cast<uint8_t>(
+        Clamp(out_zp + MultiplyByQuantizedMultiplier(ByteValue(b, is_signed) - in_zp, q, sh), qmin, qmax));
+}
+
+void LogisticTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp,
+                   uint8_t table[256]) {
+  const float inverse_scale = 1.0f / out_scale;
+  const int32_t minval = is_signed ? -128 : 0, maxval = is_signed ? 127 : 255;
+  for (int32_t val = minval; val <= maxval; ++val) {
+    const float dequantized = in_scale * static_cast<float>(val - in_zp);
+    const float transformed = 1.0f / (1.0f + std::exp(-dequantized));
+    const float rescaled = std::round(transformed * inverse_scale);
+    const int32_t quantized = static_cast<int32_t>(rescaled + static_cast<float>(out_zp));
+    table[static_cast<uint8_t>(val)] = static_cast<uint8_t>(Clamp(quantized, minval, maxval));
+  }
+}
+
+void DequantizeTable(bool is_signed, float scale, int32_t zp, float table[256]) {
+  for (int b = 0; b < 256; ++b)
+    table[b] = static_cast<float>(static_cast<double>(scale) * static_cast<double>(ByteValue(b, is_signed) - zp));
+}
+
+void ConcatRescaleTable(float in_scale, int32_t in_zp, float out_scale, int32_t out_zp, uint8_t table[256]) {
+  const float inverse_output_scale = 1.f / out_scale;
+  const float s = in_scale * inverse_output_scale;
+  const float bias = -static_cast<float>(in_zp) * s;
+  for (int b = 0; b < 256; ++b) {
+    const int32_t v = static_cast<int32_t>(std::round(static_cast<float>(b) * s + bias)) + out_zp;
+    table[b] = static_cast<uint8_t>(Clamp(v, 0, 255));
+  }
+}
+
+void SoftmaxExpTable(float in_scale, float beta, float table[256]) {
+  const float scale = -in_scale * beta;
+  for (int32_t val = 0; val <= 255; ++val) table[255 - val] = std::exp(scale * static_cast<float>(val));
+}
+
+int NearestNeighborIndex(int v, int in_size, int out_size, bool align_corners, bool half_pixel_centers) {
+  const float scale = (align_corners && out_size > 1)
+                          ? static_cast<float>(in_size - 1) / static_cast<float>(out_size - 1)
+                          : static_cast<float>(in_size) / static_cast<float>(out_size);
+  const float offset = half_pixel_centers ? 0.5f : 0.0f;
+  int32_t o = align_corners ? static_cast<int32_t>(std::round((static_cast<float>(v) + offset) * scale))
+                            : static_cast<int32_t>(std::floor((static_cast<float>(v) + offset) * scale));
+  o = std::min(o, in_size - 1);
+  if (half_pixel_centers) o = std::max(0, o);
+  return o;
+}
+
+void BilinearIntegerTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
+                          std::vector<int32_t>* tab) {
+  int32_t scale_10 = ((1 << 10) * in_size + out_size / 2) / out_size;
+  if (align_corners && out_size > 1) scale_10 = ((1 << 10) * (in_size - 1) + (out_size - 1) / 2) / (out_size - 1);
+  tab->assign(3 * static_cast<size_t>(out_size), 0);
+  for (int v = 0; v < out_size; ++v) {
+    const int32_t scaled = half_pixel_centers ? v * scale_10 + scale_10 / 2 - (1 << 9) : v * scale_10;
+    (*tab)[3 * v] = std::max(scaled / (1 << 10), 0);
+    (*tab)[3 * v + 1] = std::min((scaled + (1 << 10) - 1) / (1 << 10), in_size - 1);
+    (*tab)[3 * v + 2] = scaled;
+  }
 }
 
 }  // namespace hip

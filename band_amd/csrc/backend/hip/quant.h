@@ -44,5 +44,36 @@ void MulMultiplier(float s1, float s2, float so, int32_t* mult, int32_t* shift);
 int ComputeOutSize(bool same, int in, int filter, int stride, int dilation);
 int ComputePadding(int stride, int dilation, int in, int filter, int out);
 
+// ---- glue-op tables: TFLite's formula evaluated for every 8-bit input byte.
+// The device gathers from these (bh_lut_u8 / bh_lut_f32 / bh_softmax_i8), so
+// all float and fixed-point rounding happens here, in the reference's order.
+
+// common.h MultiplyByQuantizedMultiplier (double rounding; no
+// TFLITE_SINGLE_ROUNDING)
+int32_t MultiplyByQuantizedMultiplier(int32_t x, int32_t q, int shift);
+
+// quantize.cc (8-bit -> 8-bit): QuantizeMultiplier(double(s_in)/double(s_out)),
+// reference_ops::Requantize
+void RequantizeTable(bool in_signed, float in_scale, int32_t in_zp, bool out_signed, float out_scale,
+                     int32_t out_zp, uint8_t table[256]);
+// activations.cc ReluPrepare + QuantizedReluX + ReluX; act_max_inf = RELU
+void ReluTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp, float act_min,
+               float act_max, bool act_max_inf, uint8_t table[256]);
+// activations.cc PopulateLookupTable<T> with 1 / (1 + exp(-x))
+void LogisticTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp,
+                   uint8_t table[256]);
+// reference_ops::Dequantize: float(double(scale) * (q - zp))
+void DequantizeTable(bool is_signed, float scale, int32_t zp, float table[256]);
+// concatenation.cc ConcatenationWithScaling (uint8): round(q*s + b) + zp_out
+void ConcatRescaleTable(float in_scale, int32_t in_zp, float out_scale, int32_t out_zp, uint8_t table[256]);
+// optimized_ops::PopulateSoftmaxLookupTable: table[255 - v] = expf(-s_in*beta*v)
+void SoftmaxExpTable(float in_scale, float beta, float table[256]);
+// reference_ops::ResizeNearestNeighbor GetNearestNeighbor
+int NearestNeighborIndex(int v, int in_size, int out_size, bool align_corners, bool half_pixel_centers);
+// reference_ops::ResizeBilinearInteger: per output row / column
+// {lower, upper, 10-bit scaled coordinate}
+void BilinearIntegerTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
+                          std::vector<int32_t>* tab);
+
 }  // namespace hip
 }  // namespace band

@@ -27,7 +27,9 @@ const char* TflBuiltinName(int c) {
     case kTflMaxPool2D: return "MAX_POOL_2D";
     case kTflMul: return "MUL";
     case kTflRelu: return "RELU";
+    case kTflReluN1To1: return "RELU_N1_TO_1";
     case kTflRelu6: return "RELU6";
+    case kTflPadV2: return "PADV2";
     case kTflReshape: return "RESHAPE";
     case kTflResizeBilinear: return "RESIZE_BILINEAR";
     case kTflSoftmax: return "SOFTMAX";

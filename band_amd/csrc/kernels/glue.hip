@@ -1,0 +1,349 @@
+// Glue ops for whole-model residency on gfx950:
+// the TFLite 2.9.2 builtins around the conv stack of detection /
+// segmentation / pose models.  All are byte movers bound by HBM (or, at
+// batch 1, by launch latency), so the design goal is one memory round trip
+// and no per-element division:
+//   * 8-bit unary ops -> one table gather (bh_lut_u8 / bh_lut_f32).  The host
+//     evaluates TFLite's exact formula for all 256 input bytes, so the device
+//     never re-derives float or fixed-point rounding.
+//   * index maps that TFLite computes in float (RESIZE_NEAREST_NEIGHBOR) or in
+//     10-bit fixed point (RESIZE_BILINEAR int8) -> host-built per-row and
+//     per-column tables; the device only gathers and (bilinear) does the
+//     integer 4-tap blend.
+//   * SOFTMAX (8-bit, lookup-table path) -> host-built float exp table; the
+//     per-row sum runs sequentially in TFLite's order, so the float result is
+//     the same.
+#include "common.hpp"
+
+namespace bh {
+
+// ---- table lookups ----------------------------------------------------------
+// Table staged in LDS; 16 input bytes per thread when both pointers are
+// 16-byte aligned, a byte loop for the tail.
+__global__ __launch_bounds__(256) void lut_u8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                     long n, long n16, const uint8_t* __restrict__ table) {
+  __shared__ uint8_t t[256];
+  if (threadIdx.x < 64) *(uint32_t*)(t + 4 * threadIdx.x) = *(const uint32_t*)(table + 4 * threadIdx.x);
+  __syncthreads();
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n16) {
+    v4i v = *(const v4i*)(in + 16 * i);
+    v4i o;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const uint32_t x = (uint32_t)v[w];
+      o[w] = (int)((uint32_t)t[x & 0xff] | ((uint32_t)t[(x >> 8) & 0xff] << 8) |
+                   ((uint32_t)t[(x >> 16) & 0xff] << 16) | ((uint32_t)t[x >> 24] << 24));
+    }
+    *(v4i*)(out + 16 * i) = o;
+  } else {
+    const long j = 16 * n16 + (i - n16);
+    if (j < n) out[j] = t[in[j]];
+  }
+}
+
+__global__ __launch_bounds__(256) void lut_f32_kernel(const uint8_t* __restrict__ in, float* __restrict__ out,
+                                                      long n, const float* __restrict__ table) {
+  __shared__ float t[256];
+  t[threadIdx.x] = table[threadIdx.x];
+  __syncthreads();
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = t[in[i]];
+}
+
+// reference_ops::AffineQuantize: (int32)TfLiteRound(x / scale) + zp, with
+// IEEE division and round-half-away-from-zero
+__global__ __launch_bounds__(256) void quantize_f32_kernel(const float* __restrict__ in, uint8_t* __restrict__ out,
+                                                           long n, float scale, int32_t zp, int32_t lo, int32_t hi) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i < n) out[i] = (uint8_t)clamp_i32((int32_t)roundf(__fdiv_rn(in[i], scale)) + zp, lo, hi);
+}
+
+// ---- concatenation -----------------------------------------------------------
+struct ConcatDivs {
+  FastDiv row[BH_CONCAT_MAX_INPUTS];
+  long off[BH_CONCAT_MAX_INPUTS];  // byte offset of input k inside an output row
+  long out_row;
+  int vec4;                        // every row / offset / pointer dword aligned
+};
+
+// blockIdx.y = input k; its outer x row bytes are copied (dwords when
+// aligned), through its rescale table when one is given
+__global__ __launch_bounds__(256) void concat_kernel(bh_concat_params p, ConcatDivs dv) {
+  const int k = blockIdx.y;
+  const uint8_t* src = (const uint8_t*)p.input[k];
+  const uint8_t* tab = (const uint8_t*)p.table[k];
+  uint8_t* dst = (uint8_t*)p.output + dv.off[k];
+  const long row = p.row[k];
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (dv.vec4 && !tab) {
+    const long units = p.outer * (row / 4);
+    if (i >= units) return;
+    const uint32_t o = dv.row[k].div((uint32_t)(4 * i));  // FastDiv over bytes
+    const long j = 4 * i - (long)o * row;
+    *(uint32_t*)(dst + o * dv.out_row + j) = *(const uint32_t*)(src + 4 * i);
+  } else {
+    if (i >= p.outer * row) return;
+    const uint32_t o = dv.row[k].div((uint32_t)i);
+    const long j = i - (long)o * row;
+    const uint8_t v = src[i];
+    dst[o * dv.out_row + j] = tab ? tab[v] : v;
+  }
+}
+
+// ---- pad --------------------------------------------------------------------
+struct PadDivs {
+  FastDiv c, w, h;
+  int os[4];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void pad_kernel(bh_pad_params p, PadDivs dv, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  uint32_t t = dv.c.div((uint32_t)i);
+  const int c = (int)(i - (long)t * dv.os[3]);
+  uint32_t t2 = dv.w.div(t);
+  const int x = (int)(t - t2 * dv.os[2]);
+  const uint32_t b = dv.h.div(t2);
+  const int y = (int)(t2 - b * dv.os[1]);
+  const int ib = (int)b - p.pad_before[0], iy = y - p.pad_before[1], ix = x - p.pad_before[2],
+            ic = c - p.pad_before[3];
+  T v = (T)p.value;
+  if (ib >= 0 && ib < p.in_shape[0] && iy >= 0 && iy < p.in_shape[1] && ix >= 0 && ix < p.in_shape[2] && ic >= 0 &&
+      ic < p.in_shape[3])
+    v = ((const T*)p.input)[(((long)ib * p.in_shape[1] + iy) * p.in_shape[2] + ix) * p.in_shape[3] + ic];
+  ((T*)p.output)[i] = v;
+}
+
+// ---- resize -----------------------------------------------------------------
+struct ResizeDivs {
+  FastDiv units, ow, oh;
+};
+
+// one thread per (output pixel, 4-byte unit of its row) when rows are dword
+// multiples, else per byte (UNIT = 4 / 1)
+template <int UNIT>
+__global__ __launch_bounds__(256) void resize_nearest_kernel(bh_resize_nearest_params p, ResizeDivs dv, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t pix = dv.units.div((uint32_t)i);
+  const int u = (int)(i - (long)pix * (p.row_bytes / UNIT));
+  const uint32_t t = dv.ow.div(pix);
+  const int x = (int)(pix - t * p.out_w);
+  const uint32_t n = dv.oh.div(t);
+  const int y = (int)(t - n * p.out_h);
+  const long src = (((long)n * p.in_h + p.y_index[y]) * p.in_w + p.x_index[x]) * p.row_bytes + (long)u * UNIT;
+  if constexpr (UNIT == 4) ((uint32_t*)p.output)[i] = *(const uint32_t*)((const uint8_t*)p.input + src);
+  else ((uint8_t*)p.output)[i] = ((const uint8_t*)p.input)[src];
+}
+
+// ResizeBilinearInteger: the four 2^10-fixed-point weights and the int64 sum
+// rounded half away from zero at 2^20
+__global__ __launch_bounds__(256) void resize_bilinear_kernel(bh_resize_bilinear_params p, ResizeDivs dv, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t pix = dv.units.div((uint32_t)i);  // units = channels
+  const int ch = (int)(i - (long)pix * p.channels);
+  const uint32_t t = dv.ow.div(pix);
+  const int x = (int)(pix - t * p.out_w);
+  const uint32_t n = dv.oh.div(t);
+  const int y = (int)(t - n * p.out_h);
+  const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1], iy = p.y_tab[3 * y + 2];
+  const int x0 = p.x_tab[3 * x], x1 = p.x_tab[3 * x + 1], ix = p.x_tab[3 * x + 2];
+  const int8_t* in = (const int8_t*)p.input + (long)n * p.in_h * p.in_w * p.channels + ch;
+  const long r0 = (long)y0 * p.in_w, r1 = (long)y1 * p.in_w;
+  const int64_t v00 = in[(r0 + x0) * p.channels], v10 = in[(r1 + x0) * p.channels];
+  const int64_t v01 = in[(r0 + x1) * p.channels], v11 = in[(r1 + x1) * p.channels];
+  constexpr int32_t one = 1 << 10;
+  const int32_t fy = iy - one * y0, fx = ix - one * x0;
+  const int64_t s = v00 * ((one - fy) * (one - fx)) + v10 * (fy * (one - fx)) + v01 * ((one - fy) * fx) +
+                    v11 * (fy * fx);
+  const int64_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
+  ((int8_t*)p.output)[i] = (int8_t)((s + rnd) / (1 << 20));
+}
+
+// ---- softmax ----------------------------------------------------------------
+// One thread per row; the float operations are issued exactly as the
+// reference's loop runs them (no contraction: explicit _rn intrinsics).
+__global__ __launch_bounds__(256) void softmax_kernel(bh_softmax_params p) {
+  __shared__ float t[256];
+  t[threadIdx.x] = p.table[threadIdx.x];
+  __syncthreads();
+  const long r = (long)blockIdx.x * 256 + threadIdx.x;
+  if (r >= p.rows) return;
+  const uint8_t* x = (const uint8_t*)p.input + r * p.depth;
+  uint8_t* y = (uint8_t*)p.output + r * p.depth;
+  const bool sg = p.is_signed != 0;
+  int32_t mx = sg ? -128 : 0;
+  for (int j = 0; j < p.depth; ++j) mx = max(mx, sg ? (int32_t)(int8_t)x[j] : (int32_t)x[j]);
+  const float* to = t + 255 - mx;
+  float sum = 0.0f;
+  for (int j = 0; j < p.depth; ++j) sum = __fadd_rn(sum, to[sg ? (int32_t)(int8_t)x[j] : (int32_t)x[j]]);
+  const float inv = __fdiv_rn(1.0f, __fmul_rn(sum, p.out_scale));
+  const int32_t lo = sg ? -128 : 0, hi = sg ? 127 : 255;
+  for (int j = 0; j < p.depth; ++j) {
+    const float pr = __fmul_rn(to[sg ? (int32_t)(int8_t)x[j] : (int32_t)x[j]], inv);
+    const int32_t q = sg ? (int32_t)roundf(pr) + p.out_zp : (int32_t)__fadd_rn(pr, 0.5f) + p.out_zp;
+    y[j] = (uint8_t)clamp_i32(q, lo, hi);
+  }
+}
+
+inline unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace bh
+
+extern "C" int bh_lut_u8(const void* in, void* out, long n, const void* table, bh_stream_t s) {
+  if (!in || !out || !table || n < 0 || n >= (1l << 36)) {
+    bh_set_last_error("bh_lut_u8: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (n == 0) return 0;
+  const bool al = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  const long n16 = al ? n / 16 : 0;
+  const long threads = n16 + (n - 16 * n16);
+  hipLaunchKernelGGL(bh::lut_u8_kernel, dim3(bh::blocks(threads)), dim3(256), 0, (hipStream_t)s,
+                     (const uint8_t*)in, (uint8_t*)out, n, n16, (const uint8_t*)table);
+  return bh_check_launch("lut_u8_kernel");
+}
+
+extern "C" int bh_lut_f32(const void* in, void* out, long n, const float* table, bh_stream_t s) {
+  if (!in || !out || !table || n < 0) {
+    bh_set_last_error("bh_lut_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bh::lut_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, (const uint8_t*)in,
+                     (float*)out, n, table);
+  return bh_check_launch("lut_f32_kernel");
+}
+
+extern "C" int bh_quantize_f32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed,
+                               bh_stream_t s) {
+  if (!in || !out || n < 0 || !(scale > 0.f)) {
+    bh_set_last_error("bh_quantize_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bh::quantize_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, in, (uint8_t*)out,
+                     n, scale, zp, out_signed ? -128 : 0, out_signed ? 127 : 255);
+  return bh_check_launch("quantize_f32_kernel");
+}
+
+extern "C" int bh_concat(const bh_concat_params* pp, bh_stream_t s) {
+  if (!pp || pp->n_inputs <= 0 || pp->n_inputs > BH_CONCAT_MAX_INPUTS || pp->outer <= 0 || !pp->output) {
+    bh_set_last_error("bh_concat: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_concat_params& p = *pp;
+  bh::ConcatDivs dv{};
+  long off = 0, maxbytes = 0;
+  bool vec4 = (uintptr_t)p.output % 4 == 0;
+  for (int k = 0; k < p.n_inputs; ++k) {
+    if (!p.input[k] || p.row[k] < 0) {
+      bh_set_last_error("bh_concat: invalid input");
+      return BH_EINVAL;
+    }
+    dv.row[k] = bh::FastDiv((uint32_t)(p.row[k] > 0 ? p.row[k] : 1));
+    dv.off[k] = off;
+    vec4 = vec4 && p.row[k] % 4 == 0 && off % 4 == 0 && (uintptr_t)p.input[k] % 4 == 0;
+    off += p.row[k];
+    maxbytes = p.outer * p.row[k] > maxbytes ? p.outer * p.row[k] : maxbytes;
+  }
+  dv.out_row = off;
+  dv.vec4 = vec4 ? 1 : 0;
+  if (p.outer * off >= INT32_MAX) {
+    bh_set_last_error("bh_concat: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  if (maxbytes == 0) return 0;
+  const dim3 grid(bh::blocks(maxbytes), (unsigned)p.n_inputs);
+  hipLaunchKernelGGL(bh::concat_kernel, grid, dim3(256), 0, (hipStream_t)s, p, dv);
+  return bh_check_launch("concat_kernel");
+}
+
+extern "C" int bh_pad(const bh_pad_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || (pp->elem_bytes != 1 && pp->elem_bytes != 4)) {
+    bh_set_last_error("bh_pad: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_pad_params& p = *pp;
+  bh::PadDivs dv{};
+  long total = 1;
+  for (int d = 0; d < 4; ++d) {
+    if (p.in_shape[d] <= 0 || p.pad_before[d] < 0 || p.pad_after[d] < 0) {
+      bh_set_last_error("bh_pad: bad shape");
+      return BH_EINVAL;
+    }
+    dv.os[d] = p.in_shape[d] + p.pad_before[d] + p.pad_after[d];
+    total *= dv.os[d];
+  }
+  if (total >= INT32_MAX) {
+    bh_set_last_error("bh_pad: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  dv.c = bh::FastDiv(dv.os[3]);
+  dv.w = bh::FastDiv(dv.os[2]);
+  dv.h = bh::FastDiv(dv.os[1]);
+  if (p.elem_bytes == 1)
+    hipLaunchKernelGGL(bh::pad_kernel<uint8_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  else
+    hipLaunchKernelGGL(bh::pad_kernel<uint32_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  return bh_check_launch("pad_kernel");
+}
+
+extern "C" int bh_resize_nearest(const bh_resize_nearest_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->y_index || !pp->x_index || pp->batch <= 0 || pp->out_h <= 0 ||
+      pp->out_w <= 0 || pp->row_bytes <= 0) {
+    bh_set_last_error("bh_resize_nearest: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_resize_nearest_params& p = *pp;
+  const long pixels = (long)p.batch * p.out_h * p.out_w;
+  const bool v4 = p.row_bytes % 4 == 0 && (uintptr_t)p.input % 4 == 0 && (uintptr_t)p.output % 4 == 0;
+  const int units = v4 ? p.row_bytes / 4 : p.row_bytes;
+  const long total = pixels * units;
+  if (pixels * p.row_bytes >= INT32_MAX) {
+    bh_set_last_error("bh_resize_nearest: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  bh::ResizeDivs dv;
+  dv.units = bh::FastDiv(units);
+  dv.ow = bh::FastDiv(p.out_w);
+  dv.oh = bh::FastDiv(p.out_h);
+  if (v4)
+    hipLaunchKernelGGL(bh::resize_nearest_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  else
+    hipLaunchKernelGGL(bh::resize_nearest_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  return bh_check_launch("resize_nearest_kernel");
+}
+
+extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->y_tab || !pp->x_tab || pp->batch <= 0 || pp->channels <= 0 ||
+      pp->out_h <= 0 || pp->out_w <= 0) {
+    bh_set_last_error("bh_resize_bilinear_i8: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_resize_bilinear_params& p = *pp;
+  const long total = (long)p.batch * p.out_h * p.out_w * p.channels;
+  if (total >= INT32_MAX) {
+    bh_set_last_error("bh_resize_bilinear_i8: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  bh::ResizeDivs dv;
+  dv.units = bh::FastDiv(p.channels);
+  dv.ow = bh::FastDiv(p.out_w);
+  dv.oh = bh::FastDiv(p.out_h);
+  hipLaunchKernelGGL(bh::resize_bilinear_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  return bh_check_launch("resize_bilinear_kernel");
+}
+
+extern "C" int bh_softmax_i8(const bh_softmax_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->table || pp->rows < 0 || pp->depth <= 0) {
+    bh_set_last_error("bh_softmax_i8: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (pp->rows == 0) return 0;
+  hipLaunchKernelGGL(bh::softmax_kernel, dim3(bh::blocks(pp->rows)), dim3(256), 0, (hipStream_t)s, *pp);
+  return bh_check_launch("softmax_kernel");
+}

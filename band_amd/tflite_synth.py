@@ -22,11 +22,13 @@ NP_TO_SCHEMA = {np.dtype(np.float32): T_FLOAT32, np.dtype(np.int32): T_INT32,
 ACT = {"NONE": 0, "RELU": 1, "RELU_N1_TO_1": 2, "RELU6": 3}
 OPC = dict(ADD=0, AVERAGE_POOL_2D=1, CONCATENATION=2, CONV_2D=3, DEPTHWISE_CONV_2D=4,
            FULLY_CONNECTED=9, LOGISTIC=14, MAX_POOL_2D=17, MUL=18, RESHAPE=22,
-           RESIZE_BILINEAR=23, SOFTMAX=25, CUSTOM=32, PAD=34, SUB=41, QUANTIZE=114)
+           RESIZE_BILINEAR=23, SOFTMAX=25, CUSTOM=32, PAD=34, SUB=41, QUANTIZE=114,
+           DEQUANTIZE=6, RELU=19, RELU_N1_TO_1=20, RELU6=21, PADV2=60, RESIZE_NEAREST_NEIGHBOR=97)
 # BuiltinOptions union indices
 OPT = dict(Conv2DOptions=1, DepthwiseConv2DOptions=2, Pool2DOptions=5, FullyConnectedOptions=8,
            SoftmaxOptions=9, ConcatenationOptions=10, AddOptions=11, ReshapeOptions=17,
-           ResizeBilinearOptions=15, MulOptions=21, PadOptions=22, SubOptions=28)
+           ResizeBilinearOptions=15, MulOptions=21, PadOptions=22, SubOptions=28,
+           DequantizeOptions=38, PadV2Options=43, ResizeNearestNeighborOptions=74, QuantizeOptions=89)
 
 
 # ---------------------------------------------------------------------------
@@ -385,6 +387,86 @@ class QGraph:
         bt = self._bias(units, s_in, ws, depth)
         y = self.act_tensor([rows, units], s_out, zp)
         self.mb.op("FULLY_CONNECTED", [x, wt, bt], [y], OPT["FullyConnectedOptions"], act_options(act))
+        return y
+
+    # --- glue ops ------------------------------------------------------------
+    def _like(self, x, shape=None, scale=None, zp=None):
+        shp, s, z = self.meta[x]
+        return self.act_tensor(list(shape if shape is not None else shp), s if scale is None else scale,
+                               z if zp is None else zp)
+
+    def quantize(self, x, scale, zp):
+        """QUANTIZE (requantize) to new 8-bit params"""
+        y = self._like(x, scale=scale, zp=zp)
+        self.mb.op("QUANTIZE", [x], [y], OPT["QuantizeOptions"], Table())
+        return y
+
+    def concat(self, xs, axis=3):
+        """CONCATENATION; int8 inputs are requantized to the first input's
+        params first (what the converter does), uint8 ones are rescaled by the
+        op itself (ConcatenationWithScaling)"""
+        shp0, s0, z0 = self.meta[xs[0]]
+        ins = []
+        for x in xs:
+            _, s, z = self.meta[x]
+            if self.dtype == np.int8 and (s != s0 or z != z0):
+                x = self.quantize(x, s0, z0)
+            ins.append(x)
+        shape = list(shp0)
+        shape[axis] = sum(self.meta[x][0][axis] for x in ins)
+        s_out = s0 if self.dtype == np.int8 else float(max(self.meta[x][1] for x in ins))
+        z_out = z0 if self.dtype == np.int8 else self._act_zp()
+        y = self.act_tensor(shape, s_out, z_out)
+        self.mb.op("CONCATENATION", ins, [y], OPT["ConcatenationOptions"], Table().set(0, "i", axis).set(1, "b", 0))
+        return y
+
+    def pad(self, x, pads):
+        """PAD with [[before, after]] per dim (quantized pad = output zero point)"""
+        shp, _, _ = self.meta[x]
+        pt = self.mb.tensor(self._name("paddings"), [len(shp), 2], np.int32, data=np.array(pads, np.int32))
+        y = self._like(x, shape=[shp[d] + pads[d][0] + pads[d][1] for d in range(len(shp))])
+        self.mb.op("PAD", [x, pt], [y], OPT["PadOptions"], Table())
+        return y
+
+    def relu(self, x, kind="RELU"):
+        shp, s, z = self.meta[x]
+        lo = {"RELU": 0.0, "RELU6": 0.0, "RELU_N1_TO_1": -1.0}[kind]
+        hi = {"RELU": None, "RELU6": 6.0, "RELU_N1_TO_1": 1.0}[kind]
+        qmin = -128 if self.dtype == np.int8 else 0
+        span = (hi if hi is not None else s * 200.0) - lo
+        scale = float(span / 255.0)
+        y = self.act_tensor(shp, scale, int(qmin - round(lo / scale)))
+        self.mb.op(kind, [x], [y])
+        return y
+
+    def logistic(self, x):
+        zp = -128 if self.dtype == np.int8 else 0
+        y = self._like(x, scale=1.0 / 256.0, zp=zp)
+        self.mb.op("LOGISTIC", [x], [y])
+        return y
+
+    def softmax(self, x, beta=1.0):
+        zp = -128 if self.dtype == np.int8 else 0
+        y = self._like(x, scale=1.0 / 256.0, zp=zp)
+        self.mb.op("SOFTMAX", [x], [y], OPT["SoftmaxOptions"], Table().set(0, "f", float(beta)))
+        return y
+
+    def resize(self, x, size, bilinear=False, align_corners=False, half_pixel_centers=False):
+        shp, _, _ = self.meta[x]
+        st = self.mb.tensor(self._name("size"), [2], np.int32, data=np.array(size, np.int32))
+        y = self._like(x, shape=[shp[0], size[0], size[1], shp[3]])
+        if bilinear:
+            opt = Table().set(2, "b", int(align_corners)).set(3, "b", int(half_pixel_centers))
+            self.mb.op("RESIZE_BILINEAR", [x, st], [y], OPT["ResizeBilinearOptions"], opt)
+        else:
+            opt = Table().set(0, "b", int(align_corners)).set(1, "b", int(half_pixel_centers))
+            self.mb.op("RESIZE_NEAREST_NEIGHBOR", [x, st], [y], OPT["ResizeNearestNeighborOptions"], opt)
+        return y
+
+    def dequantize(self, x):
+        shp, _, _ = self.meta[x]
+        y = self.mb.tensor(self._name("float"), shp, np.float32)
+        self.mb.op("DEQUANTIZE", [x], [y], OPT["DequantizeOptions"], Table())
         return y
 
     def build(self):

@@ -16,9 +16,17 @@
  *                                            reference_ops::Conv uint8)
  *   bh_dwconv2d_i8    <- DEPTHWISE_CONV_2D  (reference_integer_ops::DepthwiseConvPerChannel)
  *   bh_fc_i8          <- FULLY_CONNECTED    (reference_integer_ops::FullyConnected)
- *   bh_add_i8         <- ADD / SUB          (reference_integer_ops::Add, sub.cc)
- *   bh_mul_i8         <- MUL                (reference_integer_ops::Mul)
+ *   bh_eltwise_i8     <- ADD / SUB / MUL    (reference_integer_ops::Add / Mul, sub.cc)
  *   bh_pool_i8        <- AVERAGE_POOL_2D / MAX_POOL_2D (reference_integer_ops::{Average,Max}Pool)
+ *   bh_irb_i8         <- [CONV_2D 1x1 ->] DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 [-> ADD], fused
+ *   bh_lut_u8         <- QUANTIZE (8-bit -> 8-bit), RELU / RELU6 / RELU_N1_TO_1, LOGISTIC
+ *   bh_lut_f32        <- DEQUANTIZE (8-bit -> float32)
+ *   bh_quantize_f32   <- QUANTIZE (float32 -> 8-bit, reference_ops::AffineQuantize)
+ *   bh_concat         <- CONCATENATION      (reference_ops::Concatenation[WithScaling])
+ *   bh_pad            <- PAD / PADV2        (reference_ops::Pad)
+ *   bh_resize_nearest <- RESIZE_NEAREST_NEIGHBOR (reference_ops::ResizeNearestNeighbor)
+ *   bh_resize_bilinear_i8 <- RESIZE_BILINEAR int8 (reference_ops::ResizeBilinearInteger)
+ *   bh_softmax_i8     <- SOFTMAX 8-bit      (optimized_ops::Softmax, lookup-table path)
  *
  * Quantised tensors live on the device as raw bytes in their TFLite type
  * (int8 or uint8).  Kernels work in the "int8 domain": a uint8 input is
@@ -250,6 +258,73 @@ int bh_dwconv2d_i8(const bh_dwconv_params* p, bh_stream_t s);
 int bh_fc_i8(const bh_fc_params* p, bh_stream_t s);
 int bh_eltwise_i8(const bh_eltwise_params* p, bh_stream_t s);
 int bh_pool_i8(const bh_pool_params* p, bh_stream_t s);
+
+/* ---- glue ops (whole-model residency) ------------- */
+
+/* out[i] = table[in[i]]: every 8-bit unary op whose result depends only on
+ * the input byte.  The host fills the 256-entry device table (indexed by the
+ * raw byte) with TFLite's own formula: QUANTIZE between 8-bit types
+ * (Requantize), RELU / RELU6 / RELU_N1_TO_1 (ReluX), LOGISTIC (the 8-bit
+ * lookup table of activations.cc).  bh_lut_f32: 256 float entries
+ * (DEQUANTIZE: float(double(scale) * (q - zp))). */
+int bh_lut_u8(const void* in, void* out, long n, const void* table, bh_stream_t s);
+int bh_lut_f32(const void* in, void* out, long n, const float* table, bh_stream_t s);
+/* float32 -> 8-bit: clamp((int)roundf(x / scale) + zp) */
+int bh_quantize_f32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed,
+                    bh_stream_t s);
+
+#define BH_CONCAT_MAX_INPUTS 16
+typedef struct {
+  int n_inputs;
+  long outer;                              /* product of the dims before the axis */
+  long row[BH_CONCAT_MAX_INPUTS];          /* bytes per outer index of input k */
+  const void* input[BH_CONCAT_MAX_INPUTS];
+  const void* table[BH_CONCAT_MAX_INPUTS]; /* optional 256-B rescale table (uint8
+                                              ConcatenationWithScaling), NULL = copy */
+  void* output;                            /* row of outer index o: sum_k row[k] bytes */
+} bh_concat_params;
+int bh_concat(const bh_concat_params* p, bh_stream_t s);
+
+typedef struct {
+  int elem_bytes;                 /* 1 or 4 */
+  int in_shape[4];                /* NHWC (lower ranks padded with leading 1s) */
+  int pad_before[4], pad_after[4];
+  uint32_t value;                 /* bit pattern of the pad element */
+  const void* input;
+  void* output;
+} bh_pad_params;
+int bh_pad(const bh_pad_params* p, bh_stream_t s);
+
+typedef struct {
+  int batch, in_h, in_w, out_h, out_w;
+  int row_bytes;                  /* channels * element bytes */
+  const int32_t* y_index;         /* [out_h] source row (host-computed, TFLite float formula) */
+  const int32_t* x_index;         /* [out_w] source column */
+  const void* input;
+  void* output;
+} bh_resize_nearest_params;
+int bh_resize_nearest(const bh_resize_nearest_params* p, bh_stream_t s);
+
+typedef struct {
+  int batch, in_h, in_w, channels, out_h, out_w;
+  const int32_t* y_tab;           /* [out_h][3]: lower row, upper row, 10-bit scaled y */
+  const int32_t* x_tab;           /* [out_w][3] */
+  const void* input;              /* int8 */
+  void* output;
+} bh_resize_bilinear_params;
+int bh_resize_bilinear_i8(const bh_resize_bilinear_params* p, bh_stream_t s);
+
+typedef struct {
+  long rows;
+  int depth;                      /* softmax over the last dim */
+  int is_signed;                  /* int8 (1) or uint8 (0), input and output */
+  const float* table;             /* [256] device: table[255 - v] = expf(-in_scale * beta * v) */
+  float out_scale;
+  int32_t out_zp;
+  const void* input;
+  void* output;
+} bh_softmax_params;
+int bh_softmax_i8(const bh_softmax_params* p, bh_stream_t s);
 
 /* human-readable name of the last error set on this thread */
 const char* bh_last_error(void);

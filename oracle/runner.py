@@ -53,6 +53,22 @@ def lib():
         L.tfl_mul_params.argtypes = [ctypes.c_float, ctypes.c_float, ctypes.c_float, P_I32, P_I32]
         L.tfl_out_size.restype = ctypes.c_int
         L.tfl_padding.restype = ctypes.c_int
+        c_i, c_l, c_f, c_i32, vp = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_int32, ctypes.c_void_p
+        L.tfl_requantize.argtypes = [vp, c_i, c_l, c_i32, c_i32, c_i, c_i, c_i32, vp]
+        L.tfl_quantize_f32.argtypes = [vp, c_l, c_f, c_i32, c_i, vp]
+        L.tfl_dequantize.argtypes = [vp, c_i, c_l, c_f, c_i32, vp]
+        L.tfl_relu_params.argtypes = [c_f, c_f, c_i32, c_i, c_f, c_f, c_i, P_I32, P_I32, P_I32, P_I32]
+        L.tfl_relu_x.argtypes = [vp, c_i, c_l, c_i32, c_i32, c_i32, c_i, c_i32, c_i32, vp]
+        L.tfl_logistic_table.argtypes = [c_f, c_i32, c_f, c_i32, c_i, vp]
+        L.tfl_lookup.argtypes = [vp, c_l, vp, vp]
+        L.tfl_softmax.argtypes = [vp, c_i, c_l, c_i, c_f, c_f, c_f, c_i32, vp]
+        L.tfl_softmax_table.argtypes = [c_f, c_f, vp]
+        L.tfl_concat.argtypes = [c_i, ctypes.POINTER(vp), P_I32, c_l, c_l, P_F32, P_I32, c_f, c_i32, c_i, vp]
+        L.tfl_pad.argtypes = [vp, P_I32, P_I32, ctypes.c_uint8, vp]
+        L.tfl_nearest_index.restype = c_i
+        L.tfl_nearest_index.argtypes = [c_i, c_i, c_i, c_i, c_i]
+        L.tfl_resize_nearest.argtypes = [vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, vp]
+        L.tfl_resize_bilinear_i8.argtypes = [vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, vp]
         _LIB = L
     return _LIB
 
@@ -220,6 +236,127 @@ def add_f32(a, b, amin=-np.inf, amax=np.inf, sub=False):
     return out
 
 
+def _vp(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def requantize(x, *, in_scale, in_zp, out_scale, out_zp, out_dtype):
+    """QUANTIZE between 8-bit types (quantize.cc -> reference_ops::Requantize)."""
+    m, sh = quantize_multiplier(float(np.float64(np.float32(in_scale)) / np.float64(np.float32(out_scale))))
+    x = np.ascontiguousarray(x)
+    out = np.zeros(x.shape, out_dtype)
+    lib().tfl_requantize(_vp(x), _signed(x.dtype), x.size, in_zp, m, sh, _signed(out_dtype), out_zp, _vp(out))
+    return out
+
+
+def quantize_f32(x, *, scale, zp, out_dtype):
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.zeros(x.shape, out_dtype)
+    lib().tfl_quantize_f32(_vp(x), x.size, scale, zp, _signed(out_dtype), _vp(out))
+    return out
+
+
+def dequantize(x, *, scale, zp):
+    x = np.ascontiguousarray(x)
+    out = np.zeros(x.shape, np.float32)
+    lib().tfl_dequantize(_vp(x), _signed(x.dtype), x.size, scale, zp, _vp(out))
+    return out
+
+
+def relu_params(in_scale, out_scale, out_zp, signed, act_min, act_max):
+    """act_max=None: open upper bound (RELU)"""
+    v = [ctypes.c_int32() for _ in range(4)]
+    lib().tfl_relu_params(in_scale, out_scale, out_zp, int(signed), act_min,
+                          0.0 if act_max is None else act_max, int(act_max is None), *[ctypes.byref(t) for t in v])
+    return tuple(t.value for t in v)  # mult, shift, qmin, qmax
+
+
+def relu_x(x, *, in_zp, out_zp, params):
+    m, sh, lo, hi = params
+    x = np.ascontiguousarray(x)
+    out = np.zeros_like(x)
+    lib().tfl_relu_x(_vp(x), _signed(x.dtype), x.size, in_zp, out_zp, m, sh, lo, hi, _vp(out))
+    return out
+
+
+def logistic_table(in_scale, in_zp, out_scale, out_zp, signed):
+    t = np.zeros(256, np.uint8)
+    lib().tfl_logistic_table(in_scale, in_zp, out_scale, out_zp, int(signed), _vp(t))
+    return t
+
+
+def lookup(x, table):
+    x = np.ascontiguousarray(x)
+    out = np.zeros_like(x)
+    lib().tfl_lookup(_vp(x), x.size, _vp(np.ascontiguousarray(table, np.uint8)), _vp(out))
+    return out
+
+
+def softmax(x, *, in_scale, beta, out_scale, out_zp):
+    x = np.ascontiguousarray(x)
+    out = np.zeros_like(x)
+    depth = x.shape[-1]
+    lib().tfl_softmax(_vp(x), _signed(x.dtype), x.size // depth, depth, in_scale, beta, out_scale, out_zp, _vp(out))
+    return out
+
+
+def softmax_table(in_scale, beta):
+    t = np.zeros(256, np.float32)
+    lib().tfl_softmax_table(in_scale, beta, _vp(t))
+    return t
+
+
+def concat(xs, axis, *, scales, zps, out_scale, out_zp):
+    xs = [np.ascontiguousarray(x) for x in xs]
+    rank = xs[0].ndim
+    axis = axis % rank
+    shape = list(xs[0].shape)
+    shape[axis] = sum(x.shape[axis] for x in xs)
+    out = np.zeros(shape, xs[0].dtype)
+    outer = int(np.prod(shape[:axis], dtype=np.int64))
+    inner = int(np.prod(shape[axis + 1:], dtype=np.int64))
+    ptrs = (ctypes.c_void_p * len(xs))(*[x.ctypes.data for x in xs])
+    sizes = np.array([x.shape[axis] for x in xs], np.int32)
+    sc = np.array(scales, np.float32)
+    zp = np.array(zps, np.int32)
+    lib().tfl_concat(len(xs), ptrs, _p(sizes, P_I32), outer, inner, _p(sc, P_F32), _p(zp, P_I32),
+                     out_scale, out_zp, _signed(out.dtype), _vp(out))
+    return out
+
+
+def pad(x, pads, value):
+    """x 4-D; pads [[before, after]] * 4"""
+    x = np.ascontiguousarray(x)
+    p = np.ascontiguousarray(np.asarray(pads, np.int32).reshape(4, 2))
+    shape = [x.shape[d] + p[d, 0] + p[d, 1] for d in range(4)]
+    out = np.zeros(shape, x.dtype)
+    lib().tfl_pad(_vp(x), _p(np.array(x.shape, np.int32), P_I32), _p(p.reshape(-1), P_I32),
+                  ctypes.c_uint8(int(value) & 0xff), _vp(out))
+    return out
+
+
+def nearest_index(v, in_size, out_size, align_corners, half_pixel_centers):
+    return lib().tfl_nearest_index(v, in_size, out_size, int(align_corners), int(half_pixel_centers))
+
+
+def resize_nearest(x, out_hw, align_corners=False, half_pixel_centers=False):
+    x = np.ascontiguousarray(x)
+    b, ih, iw, c = x.shape
+    out = np.zeros((b, out_hw[0], out_hw[1], c), x.dtype)
+    lib().tfl_resize_nearest(_vp(x), b, ih, iw, c, out_hw[0], out_hw[1], int(align_corners),
+                             int(half_pixel_centers), _vp(out))
+    return out
+
+
+def resize_bilinear_i8(x, out_hw, align_corners=False, half_pixel_centers=False):
+    x = np.ascontiguousarray(x, np.int8)
+    b, ih, iw, c = x.shape
+    out = np.zeros((b, out_hw[0], out_hw[1], c), np.int8)
+    lib().tfl_resize_bilinear_i8(_vp(x), b, ih, iw, c, out_hw[0], out_hw[1], int(align_corners),
+                                 int(half_pixel_centers), _vp(out))
+    return out
+
+
 # ---------------------------------------------------------------------------
 # whole-model runner
 # ---------------------------------------------------------------------------
@@ -242,7 +379,10 @@ class OracleInterpreter:
 
     SUPPORTED = {OP["CONV_2D"], OP["DEPTHWISE_CONV_2D"], OP["FULLY_CONNECTED"],
                  OP["ADD"], OP["SUB"], OP["MUL"], OP["AVERAGE_POOL_2D"],
-                 OP["MAX_POOL_2D"], OP["RESHAPE"], OP["SQUEEZE"]}
+                 OP["MAX_POOL_2D"], OP["RESHAPE"], OP["SQUEEZE"], OP["CONCATENATION"], OP["PAD"],
+                 OP["PADV2"], OP["QUANTIZE"], OP["DEQUANTIZE"], OP["RELU"], OP["RELU6"],
+                 OP["RELU_N1_TO_1"], OP["LOGISTIC"], OP["SOFTMAX"], OP["RESIZE_NEAREST_NEIGHBOR"],
+                 OP["RESIZE_BILINEAR"]}
 
     def __init__(self, model):
         self.model = model if isinstance(model, Model) else Model.from_path(model)
@@ -358,4 +498,52 @@ class OracleInterpreter:
                            out_hw=(oh, ow), amin=amin, amax=amax)]
         if code in (OP["RESHAPE"], OP["SQUEEZE"]):
             return [vals[o.inputs[0]].copy()]
+        x = vals[o.inputs[0]]
+        ti, to = T[o.inputs[0]], T[o.outputs[0]]
+        if code == OP["CONCATENATION"]:
+            axis = opt.scalar(0, "i", 0)
+            xs = [vals[i] for i in o.inputs]
+            return [concat(xs, axis, scales=[_q(T[i])[0] for i in o.inputs], zps=[_q(T[i])[1] for i in o.inputs],
+                           out_scale=_q(to)[0], out_zp=_q(to)[1])]
+        if code in (OP["PAD"], OP["PADV2"]):
+            pads = np.asarray(vals[o.inputs[1]], np.int64).reshape(-1, 2)
+            pads = np.concatenate([np.zeros((4 - len(pads), 2), np.int64), pads]) if len(pads) < 4 else pads
+            x4 = x.reshape([1] * (4 - x.ndim) + list(x.shape))
+            if code == OP["PADV2"] and len(o.inputs) > 2 and o.inputs[2] >= 0:
+                value = int(np.asarray(vals[o.inputs[2]]).reshape(-1)[0])
+            else:
+                value = _q(to)[1]
+            return [pad(x4, pads, value)]
+        if code == OP["QUANTIZE"]:
+            s_o, z_o = _q(to)
+            if ti.np_dtype == np.float32:
+                return [quantize_f32(x, scale=s_o, zp=z_o, out_dtype=to.np_dtype)]
+            s_i, z_i = _q(ti)
+            return [requantize(x, in_scale=s_i, in_zp=z_i, out_scale=s_o, out_zp=z_o, out_dtype=to.np_dtype)]
+        if code == OP["DEQUANTIZE"]:
+            s_i, z_i = _q(ti)
+            return [dequantize(x, scale=s_i, zp=z_i)]
+        if code in (OP["RELU"], OP["RELU6"], OP["RELU_N1_TO_1"]):
+            lo, hi = {OP["RELU"]: (0.0, None), OP["RELU6"]: (0.0, 6.0), OP["RELU_N1_TO_1"]: (-1.0, 1.0)}[code]
+            s_i, z_i = _q(ti)
+            s_o, z_o = _q(to)
+            prm = relu_params(s_i, s_o, z_o, to.np_dtype == np.int8, lo, hi)
+            return [relu_x(x, in_zp=z_i, out_zp=z_o, params=prm)]
+        if code == OP["LOGISTIC"]:
+            s_i, z_i = _q(ti)
+            s_o, z_o = _q(to)
+            return [lookup(x, logistic_table(s_i, z_i, s_o, z_o, ti.np_dtype == np.int8))]
+        if code == OP["SOFTMAX"]:
+            beta = opt.scalar(0, "f", 1.0) if opt is not None else 1.0
+            s_o, z_o = _q(to)
+            return [softmax(x, in_scale=_q(ti)[0], beta=beta, out_scale=s_o, out_zp=z_o)]
+        if code in (OP["RESIZE_NEAREST_NEIGHBOR"], OP["RESIZE_BILINEAR"]):
+            oh, ow = to.shape[1], to.shape[2]
+            if code == OP["RESIZE_NEAREST_NEIGHBOR"]:
+                ac, hp = opt.scalar(0, "b", 0) if opt else 0, opt.scalar(1, "b", 0) if opt else 0
+                return [resize_nearest(x, (oh, ow), ac, hp)]
+            ac, hp = opt.scalar(2, "b", 0) if opt else 0, opt.scalar(3, "b", 0) if opt else 0
+            if ti.np_dtype != np.int8:
+                raise NotImplementedError("oracle: RESIZE_BILINEAR restated for int8 only")
+            return [resize_bilinear_i8(x, (oh, ow), ac, hp)]
         raise NotImplementedError("oracle: op %s not restated" % o.name)

@@ -26,9 +26,9 @@ TENSOR_TYPE_NAME = {0: "float32", 1: "float16", 2: "int32", 3: "uint8",
 # BuiltinOperator codes (schema.fbs enum BuiltinOperator)
 OP = dict(ADD=0, AVERAGE_POOL_2D=1, CONCATENATION=2, CONV_2D=3,
           DEPTHWISE_CONV_2D=4, DEQUANTIZE=6, FULLY_CONNECTED=9, LOGISTIC=14,
-          MAX_POOL_2D=17, MUL=18, RELU=19, RELU6=21, RESHAPE=22,
+          MAX_POOL_2D=17, MUL=18, RELU=19, RELU_N1_TO_1=20, RELU6=21, RESHAPE=22,
           RESIZE_BILINEAR=23, SOFTMAX=25, CUSTOM=32, PAD=34, MEAN=40, SUB=41,
-          SQUEEZE=43, TRANSPOSE_CONV=67, RESIZE_NEAREST_NEIGHBOR=97,
+          SQUEEZE=43, PADV2=60, TRANSPOSE_CONV=67, RESIZE_NEAREST_NEIGHBOR=97,
           QUANTIZE=114, HARD_SWISH=117)
 OP_NAME = {v: k for k, v in OP.items()}
 

@@ -352,3 +352,211 @@ void tfl_add_f32(const float* a, const int* sa, const float* b_, const int* sb,
           out[(((long)i0 * so[1] + i1) * so[2] + i2) * so[3] + i3] = v;
         }
 }
+
+/* ======================================================================
+ * Glue ops needed for whole-model residency.
+ * ====================================================================== */
+
+/* quantize.cc (int8/uint8 -> int8/uint8): effective scale
+ * QuantizeMultiplier(double(in_scale) / double(out_scale)), then
+ * reference_ops::Requantize: MBQM(x - in_zp) + out_zp, clamped to the output
+ * type (its same-scale int8<->uint8 XOR fast path gives identical bytes). */
+void tfl_requantize(const uint8_t* in, int in_signed, long n, int32_t in_zp, int32_t mult, int shift,
+                    int out_signed, int32_t out_zp, uint8_t* out) {
+  int32_t lo = out_signed ? -128 : 0, hi = out_signed ? 127 : 255;
+  for (long i = 0; i < n; ++i) out[i] = (uint8_t)clampi(tfl_mbqm(ld(in, i, in_signed) - in_zp, mult, shift) + out_zp, lo, hi);
+}
+
+/* reference_ops::AffineQuantize (float -> int8/uint8):
+ * (int32)TfLiteRound(val / scale) + zp, clamped; float division, roundf. */
+void tfl_quantize_f32(const float* in, long n, float scale, int32_t zp, int out_signed, uint8_t* out) {
+  int32_t lo = out_signed ? -128 : 0, hi = out_signed ? 127 : 255;
+  for (long i = 0; i < n; ++i) out[i] = (uint8_t)clampi((int32_t)roundf(in[i] / scale) + zp, lo, hi);
+}
+
+/* reference_ops::Dequantize: float(double(scale) * (val - zp)) */
+void tfl_dequantize(const uint8_t* in, int in_signed, long n, float scale, int32_t zp, float* out) {
+  for (long i = 0; i < n; ++i) out[i] = (float)((double)scale * (double)(ld(in, i, in_signed) - zp));
+}
+
+/* activations.cc ReluPrepare + QuantizedReluX + reference_ops::ReluX:
+ * multiplier = QuantizeMultiplier(in_scale / out_scale) (a float quotient),
+ * bounds out_zp + roundf(act / out_scale) clipped to the type; act_max_inf
+ * selects the open upper bound (RELU). */
+void tfl_relu_params(float in_scale, float out_scale, int32_t out_zp, int out_signed, float act_min,
+                     float act_max, int act_max_inf, int32_t* mult, int32_t* shift, int32_t* qmin,
+                     int32_t* qmax) {
+  double real = (double)(in_scale / out_scale);
+  int e;
+  tfl_quantize_multiplier(real, mult, &e);
+  *shift = e;
+  int32_t tmin = out_signed ? -128 : 0, tmax = out_signed ? 127 : 255;
+  *qmin = imax(tmin, out_zp + (int32_t)roundf(act_min / out_scale));
+  *qmax = act_max_inf ? tmax : imin(tmax, out_zp + (int32_t)roundf(act_max / out_scale));
+}
+void tfl_relu_x(const uint8_t* in, int is_signed, long n, int32_t in_zp, int32_t out_zp, int32_t mult, int shift,
+                int32_t qmin, int32_t qmax, uint8_t* out) {
+  for (long i = 0; i < n; ++i)
+    out[i] = (uint8_t)clampi(out_zp + tfl_mbqm(ld(in, i, is_signed) - in_zp, mult, shift), qmin, qmax);
+}
+
+/* activations.cc PopulateLookupTable<T> (LOGISTIC, 8-bit, generic-optimized
+ * kernel): dequantize in float, 1/(1+expf(-x)), roundf(y / out_scale as a
+ * product with the float inverse) + zp, clamp; table indexed by the byte. */
+void tfl_logistic_table(float in_scale, int32_t in_zp, float out_scale, int32_t out_zp, int is_signed,
+                        uint8_t* table) {
+  const float inverse_scale = 1.0f / out_scale;
+  int32_t minval = is_signed ? -128 : 0, maxval = is_signed ? 127 : 255;
+  for (int32_t val = minval; val <= maxval; ++val) {
+    const float dequantized = in_scale * (float)(val - in_zp);
+    const float transformed = 1.0f / (1.0f + expf(-dequantized));
+    const float rescaled = roundf(transformed * inverse_scale);
+    const int32_t quantized = (int32_t)(rescaled + (float)out_zp);
+    table[(uint8_t)val] = (uint8_t)clampi(quantized, minval, maxval);
+  }
+}
+void tfl_lookup(const uint8_t* in, long n, const uint8_t* table, uint8_t* out) {
+  for (long i = 0; i < n; ++i) out[i] = table[in[i]];
+}
+
+/* optimized_ops::PopulateSoftmaxLookupTable + optimized_ops::Softmax
+ * (int8/uint8 in and out, generic-optimized kernel):
+ *   table[255 - v] = expf(-in_scale * beta * v), v = 0..255
+ *   per row: max, sum_exp = sum table[255 - max + x] (in order),
+ *   inv = 1 / (sum_exp * out_scale), q = round(table[..] * inv) + out_zp
+ *   (uint8 output on x86: (int32)(p + 0.5f)), clamped. */
+void tfl_softmax(const uint8_t* in, int is_signed, long rows, int depth, float in_scale, float beta,
+                 float out_scale, int32_t out_zp, uint8_t* out) {
+  float table[256];
+  const float scale = -in_scale * beta;
+  for (int32_t val = 0; val <= 255; ++val) table[255 - val] = expf(scale * (float)val);
+  int32_t lo = is_signed ? -128 : 0, hi = is_signed ? 127 : 255;
+  for (long r = 0; r < rows; ++r) {
+    const uint8_t* x = in + r * depth;
+    uint8_t* y = out + r * depth;
+    int32_t max_val = is_signed ? -128 : 0;
+    for (int j = 0; j < depth; ++j) max_val = imax(max_val, ld(x, j, is_signed));
+    float sum_exp = 0.0f;
+    const float* t = &table[255 - max_val];
+    for (int j = 0; j < depth; ++j) sum_exp += t[ld(x, j, is_signed)];
+    const float inv_sum_exp = 1.0f / (sum_exp * out_scale);
+    for (int j = 0; j < depth; ++j) {
+      const float p = t[ld(x, j, is_signed)] * inv_sum_exp;
+      const int32_t q = is_signed ? (int32_t)roundf(p) + out_zp : (int32_t)(p + 0.5f) + out_zp;
+      y[j] = (uint8_t)clampi(q, lo, hi);
+    }
+  }
+}
+
+/* concatenation.cc: int8 = reference_ops::Concatenation (all inputs share
+ * the output's scale / zero point, checked in Prepare: a byte copy); uint8 =
+ * reference_ops::ConcatenationWithScaling:
+ *   same params -> copy, else (int32)round(x * s + b) + out_zp clamped to
+ *   [0,255], s = in_scale * (1/out_scale), b = -in_zp * s (float). */
+void tfl_concat(int n_in, const uint8_t* const* ins, const int* axis_sizes, long outer, long inner,
+                const float* in_scales, const int32_t* in_zps, float out_scale, int32_t out_zp, int is_signed,
+                uint8_t* out) {
+  long out_axis = 0;
+  for (int k = 0; k < n_in; ++k) out_axis += axis_sizes[k];
+  const float inverse_output_scale = 1.0f / out_scale;
+  long off = 0;
+  for (int k = 0; k < n_in; ++k) {
+    const long cp = (long)axis_sizes[k] * inner;
+    const int same = is_signed || (in_zps[k] == out_zp && in_scales[k] == out_scale);
+    const float s = in_scales[k] * inverse_output_scale;
+    const float b = -(float)in_zps[k] * s;
+    for (long o = 0; o < outer; ++o) {
+      const uint8_t* src = ins[k] + o * cp;
+      uint8_t* dst = out + o * out_axis * inner + off;
+      if (same) {
+        memcpy(dst, src, (size_t)cp);
+      } else {
+        for (long j = 0; j < cp; ++j) dst[j] = (uint8_t)clampi((int32_t)roundf((float)src[j] * s + b) + out_zp, 0, 255);
+      }
+    }
+    off += cp;
+  }
+}
+
+/* reference_ops::Pad (4-D, NHWC): pads[2*d], pads[2*d+1] = before / after;
+ * quantized pad value = output zero point (PAD) or the constant (PADV2). */
+void tfl_pad(const uint8_t* in, const int* in_shape, const int* pads, uint8_t value, uint8_t* out) {
+  int os[4];
+  for (int d = 0; d < 4; ++d) os[d] = in_shape[d] + pads[2 * d] + pads[2 * d + 1];
+  long idx = 0;
+  for (int b = 0; b < os[0]; ++b)
+    for (int y = 0; y < os[1]; ++y)
+      for (int x = 0; x < os[2]; ++x)
+        for (int c = 0; c < os[3]; ++c, ++idx) {
+          int ib = b - pads[0], iy = y - pads[2], ix = x - pads[4], ic = c - pads[6];
+          int inside = ib >= 0 && ib < in_shape[0] && iy >= 0 && iy < in_shape[1] && ix >= 0 &&
+                       ix < in_shape[2] && ic >= 0 && ic < in_shape[3];
+          out[idx] = inside ? in[(((long)ib * in_shape[1] + iy) * in_shape[2] + ix) * in_shape[3] + ic] : value;
+        }
+}
+
+/* reference_ops::ResizeNearestNeighbor index map (GetNearestNeighbor) */
+int tfl_nearest_index(int v, int in_size, int out_size, int align_corners, int half_pixel_centers) {
+  const float scale = (align_corners && out_size > 1) ? (float)(in_size - 1) / (float)(out_size - 1)
+                                                      : (float)in_size / (float)out_size;
+  const float offset = half_pixel_centers ? 0.5f : 0.0f;
+  int32_t o = align_corners ? (int32_t)roundf(((float)v + offset) * scale) : (int32_t)floorf(((float)v + offset) * scale);
+  o = imin(o, in_size - 1);
+  if (half_pixel_centers) o = imax(0, o);
+  return o;
+}
+void tfl_resize_nearest(const uint8_t* in, int b, int ih, int iw, int c, int oh, int ow, int align_corners,
+                        int half_pixel_centers, uint8_t* out) {
+  for (int n = 0; n < b; ++n)
+    for (int y = 0; y < oh; ++y) {
+      const int sy = tfl_nearest_index(y, ih, oh, align_corners, half_pixel_centers);
+      for (int x = 0; x < ow; ++x) {
+        const int sx = tfl_nearest_index(x, iw, ow, align_corners, half_pixel_centers);
+        memcpy(out + (((long)n * oh + y) * ow + x) * c, in + (((long)n * ih + sy) * iw + sx) * c, (size_t)c);
+      }
+    }
+}
+
+/* reference_ops::ResizeBilinearInteger (int8): 10-bit fixed-point scales
+ * and ComputeInterpolationValuesInteger; the four-tap sum in int64, rounded
+ * half away from zero at 2^20. */
+static void interp_int(int32_t value, int32_t scale_10, int half_pixel_centers, int32_t input_size,
+                       int32_t* scaled, int32_t* lo, int32_t* hi) {
+  *scaled = half_pixel_centers ? value * scale_10 + scale_10 / 2 - (1 << 9) : value * scale_10;
+  *lo = imax(*scaled / (1 << 10), 0);
+  *hi = imin((*scaled + (1 << 10) - 1) / (1 << 10), input_size - 1);
+}
+void tfl_resize_bilinear_i8(const int8_t* in, int b, int ih, int iw, int c, int oh, int ow, int align_corners,
+                            int half_pixel_centers, int8_t* out) {
+  int32_t hs = ((1 << 10) * ih + oh / 2) / oh;
+  int32_t ws = ((1 << 10) * iw + ow / 2) / ow;
+  if (align_corners && oh > 1) hs = ((1 << 10) * (ih - 1) + (oh - 1) / 2) / (oh - 1);
+  if (align_corners && ow > 1) ws = ((1 << 10) * (iw - 1) + (ow - 1) / 2) / (ow - 1);
+  const int32_t one = 1 << 10;
+  for (int n = 0; n < b; ++n)
+    for (int y = 0; y < oh; ++y) {
+      int32_t iy, y0, y1;
+      interp_int(y, hs, half_pixel_centers, ih, &iy, &y0, &y1);
+      for (int x = 0; x < ow; ++x) {
+        int32_t ix, x0, x1;
+        interp_int(x, ws, half_pixel_centers, iw, &ix, &x0, &x1);
+        for (int ch = 0; ch < c; ++ch) {
+#define AT(yy, xx) ((int64_t)in[(((long)n * ih + (yy)) * iw + (xx)) * c + ch])
+          const int64_t ll = AT(y0, x0) * ((one - (iy - one * y0)) * (one - (ix - one * x0)));
+          const int64_t lu = AT(y1, x0) * ((iy - one * y0) * (one - (ix - one * x0)));
+          const int64_t rl = AT(y0, x1) * ((one - (iy - one * y0)) * (ix - one * x0));
+          const int64_t ru = AT(y1, x1) * ((iy - one * y0) * (ix - one * x0));
+#undef AT
+          const int64_t s = ll + lu + rl + ru;
+          const int64_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
+          out[(((long)n * oh + y) * ow + x) * c + ch] = (int8_t)((s + rnd) / (1 << 20));
+        }
+      }
+    }
+}
+
+/* optimized_ops::PopulateSoftmaxLookupTable alone (the table tfl_softmax uses) */
+void tfl_softmax_table(float in_scale, float beta, float* table) {
+  const float scale = -in_scale * beta;
+  for (int32_t val = 0; val <= 255; ++val) table[255 - val] = expf(scale * (float)val);
+}

@@ -1,0 +1,39 @@
+"""Small synthetic models that put every glue op of the HIP kernel set
+between real conv layers (test fixtures, built with band_amd.tflite_synth)."""
+import numpy as np
+
+from band_amd.tflite_synth import QGraph
+
+
+def glue_zoo(dtype, seed=3):
+    g = QGraph(dtype, seed=seed, name="glue_zoo")
+    x = g.input([1, 12, 10, 8], scale=0.05)
+    a = g.conv(x, 16, k=3, act="NONE")
+    b = g.dwconv(x, act="RELU6")
+    c = g.concat([a, b, g.relu(a, "RELU")])
+    d = g.pad(c, [[0, 0], [1, 2], [2, 1], [0, 0]])
+    e = g.resize(d, (20, 26))
+    f = g.resize(g.conv(e, 8, k=1, act="NONE"), (9, 7), bilinear=(np.dtype(dtype) == np.int8),
+                 half_pixel_centers=True)
+    h = g.logistic(f)
+    k = g.softmax(g.relu(g.quantize(f, 0.1, 3 if np.dtype(dtype) == np.int8 else 130), "RELU_N1_TO_1"), beta=0.7)
+    g.output(h)
+    g.output(k)
+    g.output(g.dequantize(g.relu(e, "RELU6")))
+    return g.build()
+
+
+def fpn(dtype, seed=5):
+    """Feature-pyramid merge: ADD(lateral 1x1 conv, upsampled deeper map) where
+    the lateral conv is produced BEFORE the other ADD operand (the residual
+    epilogue fusion must not fire), plus a residual ADD that may fuse."""
+    g = QGraph(dtype, seed=seed, name="fpn")
+    x = g.input([1, 16, 16, 8], scale=0.05)
+    c1 = g.conv(x, 16, k=3, stride=2, act="RELU6")          # 8x8
+    lat = g.conv(c1, 16, k=1, act="NONE")                    # lateral, consumed only by the ADD
+    c2 = g.conv(c1, 24, k=3, stride=2, act="RELU6")          # 4x4, produced after lat
+    up = g.resize(g.conv(c2, 16, k=1, act="NONE"), (8, 8))
+    p = g.add(lat, up)
+    r = g.add(g.conv(p, 16, k=1, act="NONE"), p)             # residual that can fuse
+    g.output(r)
+    return g.build()

@@ -66,6 +66,9 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_executor_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int)]),
     "bhx_time_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(ctypes.c_double)]),
+    "bhx_run_mixed_jobs": (c_int, [c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, ctypes.c_uint64,
+                                   ctypes.POINTER(c_void_p), c_int, c_int, ctypes.POINTER(ctypes.c_double),
+                                   ctypes.POINTER(c_int)]),
 })
 
 
@@ -430,3 +433,27 @@ class HipModelExecutor:
                 self.handle = None
         except Exception:
             pass
+
+
+def RunMixedJobs(executors, keys, requests, n_jobs, first_model=0):
+    """Native Band-worker loop over a mixed request stream (bhx_run_mixed_jobs).
+    executors / keys / requests: one per model, all keys on the same worker.
+    Returns (latency_us[n_jobs], model_of_job[n_jobs])."""
+    lib = _abi.load()
+    n = len(executors)
+    wids = {k.worker_id for k in keys}
+    if len(wids) != 1 or len(keys) != n or len(requests) != n:
+        raise ValueError("one executor / key / request per model, one worker")
+    arrs = [np.ascontiguousarray(r) for r in requests]
+    ex_arr = (c_void_p * n)(*[e.handle for e in executors])
+    mids = (c_int * n)(*[k.model_id for k in keys])
+    req = (c_void_p * n)(*[a.ctypes.data for a in arrs])
+    lat = np.zeros(max(n_jobs, 1), np.float64)
+    mo = np.zeros(max(n_jobs, 1), np.int32)
+    rc = lib.bhx_run_mixed_jobs(n, ex_arr, mids, keys[0].worker_id, keys[0]._args()[2], req, int(first_model),
+                                int(n_jobs), lat.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                                mo.ctypes.data_as(ctypes.POINTER(c_int)))
+    st = Status.from_rc(rc)
+    if not st.ok():
+        raise _abi.BandHipError("bhx_run_mixed_jobs: " + st.message())
+    return lat[:n_jobs], mo[:n_jobs]

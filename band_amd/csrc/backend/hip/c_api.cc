@@ -269,6 +269,53 @@ int bhx_run_jobs(bhx_executor* e, int mid, int wid, uint64_t mask, const void* c
   return 0;
 }
 
+int bhx_run_mixed_jobs(int n_models, bhx_executor* const* execs, const int* mids, int wid, uint64_t mask,
+                       const void* const* requests, int first_model, int n_jobs, double* latency_us,
+                       int* model_of_job) {
+  if (n_models <= 0 || !execs || !mids || !requests || n_jobs < 0) return Fail("bad arguments");
+  struct Slot {
+    band::interface::IModelExecutor* ex;
+    SubgraphKey key;
+    std::shared_ptr<band::interface::ITensorView> in;
+    std::vector<std::shared_ptr<band::interface::ITensorView>> outs;
+    std::vector<char> sink;  // the job's output ring slot (TryCopyOutputTensors)
+  };
+  std::vector<Slot> slots;
+  for (int m = 0; m < n_models; ++m) {
+    if (!execs[m] || !requests[m]) return Fail("bad arguments");
+    Slot sl{execs[m]->exec.get(), Key(mids[m], wid, mask), nullptr, {}, {}};
+    const auto& ins = sl.ex->GetInputs(sl.key);
+    if (ins.size() != 1) return Fail("bhx_run_mixed_jobs needs single-input subgraphs");
+    sl.in = sl.ex->GetTensorView(sl.key, ins[0]);
+    size_t ob = 0;
+    for (int t : sl.ex->GetOutputs(sl.key)) {
+      sl.outs.push_back(sl.ex->GetTensorView(sl.key, t));
+      if (!sl.outs.back()) return Fail("no output view");
+      ob += sl.outs.back()->GetBytes();
+    }
+    if (!sl.in) return Fail("no input view");
+    sl.sink.resize(ob);
+    slots.push_back(std::move(sl));
+  }
+  for (int j = 0; j < n_jobs; ++j) {
+    const int m = (first_model + j) % n_models;
+    Slot& sl = slots[m];
+    const auto t0 = std::chrono::steady_clock::now();
+    std::memcpy(sl.in->GetData(), requests[m], sl.in->GetBytes());  // TryCopyInputTensors
+    absl::Status s = sl.ex->ExecuteSubgraph(sl.key);                 // Engine::Invoke
+    if (!s.ok()) return Fail(s);
+    size_t off = 0;
+    for (auto& v : sl.outs) {                                         // TryCopyOutputTensors
+      std::memcpy(sl.sink.data() + off, v->GetData(), v->GetBytes());
+      off += v->GetBytes();
+    }
+    if (latency_us)
+      latency_us[j] = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (model_of_job) model_of_job[j] = m;
+  }
+  return 0;
+}
+
 int bhx_executor_set_graph(bhx_executor* e, int enabled) {
   auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;
   if (!h) return Fail("not a HIP executor");

@@ -527,6 +527,108 @@ def mobilenet_v1(dtype=np.int8, seed=0, size=224, batch=1, classes=1001):
     return g.build()
 
 
+# ---------------------------------------------------------------------------
+# BASELINE C3 mix: detection / segmentation / pose heads on MobileNet trunks
+# (synthetic weights, 224x224 inputs - "synthetic 224x224 batches", §8(d))
+# ---------------------------------------------------------------------------
+def _mnv2_trunk(g, x, out_stride=32, tap_expansion_at=None):
+    """MobileNetV2 feature extractor.  out_stride 16 turns the last stride-2
+    stage into stride 1 with dilation 2 (DeepLab).  Returns (features, taps):
+    taps["expansion"] = the 1x1 expansion output of block `tap_expansion_at`
+    (SSD's 'layer_15/expansion_output')."""
+    x = g.conv(x, 32, k=3, stride=2)
+    c_in, os_now, dil, taps, blk = 32, 2, 1, {}, 0
+    for t, c, n, s in MNV2_BLOCKS:
+        for i in range(n):
+            inp, stride = x, (s if i == 0 else 1)
+            if stride == 2 and os_now >= out_stride:
+                stride, dil = 1, dil * 2
+            elif stride == 2:
+                os_now *= 2
+            h = x
+            if t != 1:
+                h = g.conv(h, c_in * t, k=1)
+                if blk == tap_expansion_at:
+                    taps["expansion"] = h
+            h = g.dwconv(h, k=3, stride=stride, dilation=dil)
+            h = g.conv(h, c, k=1, act="NONE")
+            if stride == 1 and c_in == c:
+                h = g.add(h, inp)
+            x, c_in, blk = h, c, blk + 1
+    return x, taps
+
+
+def ssd_mobilenet_v2(dtype=np.int8, seed=1, size=224, batch=1, classes=91):
+    """SSD-MobileNetV2 (TF object-detection API layout): feature maps at
+    layer_15/expansion_output (14x14x576) and the 1280-channel head (7x7),
+    four extra 1x1 -> 3x3 s2 feature layers, 1x1 box / class predictors,
+    RESHAPE + CONCATENATION of all anchors, LOGISTIC class scores.  The
+    TFLite_Detection_PostProcess custom op (CPU NMS) is left out: outputs are
+    box encodings [1,N,4] and class scores [1,N,classes]."""
+    g = QGraph(dtype, seed, "ssd_mobilenet_v2_%s" % np.dtype(dtype).name)
+    x = g.input([batch, size, size, 3])
+    feat, taps = _mnv2_trunk(g, x, tap_expansion_at=13)
+    maps = [taps["expansion"], g.conv(feat, 1280, k=1)]
+    y = maps[-1]
+    for c1, c3 in ((256, 512), (128, 256), (128, 256), (64, 128)):
+        y = g.conv(g.conv(y, c1, k=1), c3, k=3, stride=2)
+        maps.append(y)
+    boxes, scores = [], []
+    for i, m in enumerate(maps):
+        b, h, w, _ = g.meta[m][0]
+        anchors = 3 if i == 0 else 6
+        bx = g.conv(m, anchors * 4, k=1, act="NONE")
+        cl = g.conv(m, anchors * classes, k=1, act="NONE")
+        boxes.append(g.reshape(bx, [batch, h * w * anchors, 4]))
+        scores.append(g.reshape(cl, [batch, h * w * anchors, classes]))
+    g.output(g.concat(boxes, axis=1))
+    g.output(g.logistic(g.concat(scores, axis=1)))
+    return g.build()
+
+
+def deeplab_v3_mobilenet_v2(dtype=np.int8, seed=2, size=224, batch=1, classes=21):
+    """DeepLabV3 with a MobileNetV2 trunk at output stride 16 (dilated last
+    stages) and the mobile ASPP: image pooling (global AVERAGE_POOL_2D, 1x1
+    conv, RESIZE_BILINEAR back) + a 1x1 branch, CONCATENATION, 1x1
+    projection, 1x1 logits, RESIZE_BILINEAR x16 to the input size."""
+    g = QGraph(dtype, seed, "deeplab_v3_mnv2_%s" % np.dtype(dtype).name)
+    x = g.input([batch, size, size, 3])
+    feat, _ = _mnv2_trunk(g, x, out_stride=16)
+    fh = g.meta[feat][0][1]
+    pool = g.conv(g.avgpool(feat, (fh, fh)), 256, k=1, act="RELU")
+    pool = g.resize(pool, (fh, fh), bilinear=True, align_corners=True)
+    aspp0 = g.conv(feat, 256, k=1, act="RELU")
+    y = g.conv(g.concat([pool, aspp0], axis=3), 256, k=1, act="RELU")
+    y = g.conv(y, classes, k=1, act="NONE")
+    g.output(g.resize(y, (size, size), bilinear=True, align_corners=True))
+    return g.build()
+
+
+def posenet_mobilenet_v1(dtype=np.int8, seed=3, size=224, batch=1, keypoints=17):
+    """PoseNet (multi-person, MobileNetV1 trunk at output stride 16): heatmap
+    (LOGISTIC), offset and forward / backward displacement 1x1 heads."""
+    g = QGraph(dtype, seed, "posenet_mnv1_%s" % np.dtype(dtype).name)
+    x = g.input([batch, size, size, 3])
+    x = g.conv(x, 32, k=3, stride=2)
+    os_now, dil = 2, 1
+    for c, s in [(64, 1), (128, 2), (128, 1), (256, 2), (256, 1), (512, 2), (512, 1), (512, 1),
+                 (512, 1), (512, 1), (512, 1), (1024, 2), (1024, 1)]:
+        if s == 2 and os_now >= 16:
+            s, dil = 1, dil * 2
+        elif s == 2:
+            os_now *= 2
+        x = g.dwconv(x, stride=s, dilation=dil)
+        x = g.conv(x, c, k=1)
+    g.output(g.logistic(g.conv(x, keypoints, k=1, act="NONE")))
+    g.output(g.conv(x, 2 * keypoints, k=1, act="NONE"))
+    g.output(g.conv(x, 2 * (keypoints - 1), k=1, act="NONE"))
+    g.output(g.conv(x, 2 * (keypoints - 1), k=1, act="NONE"))
+    return g.build()
+
+
+MIX_C3 = ("mobilenet_v2", "ssd_mobilenet_v2", "deeplab_v3_mobilenet_v2", "posenet_mobilenet_v1")
+
+
 def int8_from_uint8(model_bytes):
     """Convert a uint8 per-tensor TFLite model to int8 per-channel with the
     same float semantics (what TFLite's converter emits for int8): activations

@@ -110,6 +110,15 @@ int bhx_executor_device(bhx_executor* e, int* ordinal);
 /* per-launch HIP-event timing of a prepared subgraph, averaged over iters */
 int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
                          bhx_op_timing* out, int cap, int* n);
+/* A Band GPU worker serving a mixed request stream (BASELINE C3): worker
+ * `wid` holds one prepared executor per model (as Band creates one executor
+ * per (model, worker), band/engine.cc:91-106); job j runs model
+ * (first_model + j) % n_models: copy its request into the input view,
+ * ExecuteSubgraph, copy every output view out.  Per-job latency in us and
+ * the model of each job are written when the arrays are given. */
+int bhx_run_mixed_jobs(int n_models, bhx_executor* const* execs, const int* model_ids, int worker_id,
+                       uint64_t unit_mask, const void* const* requests, int first_model, int n_jobs,
+                       double* latency_us, int* model_of_job);
 /* device microseconds per pass of a prepared subgraph, `iters` passes issued
  * back to back on the executor's stream (graph replay when captured) */
 int bhx_time_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters, double* us);

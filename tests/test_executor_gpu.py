@@ -144,7 +144,9 @@ def test_error_behaviour(gpu_lib, golden_dir):
 
 @pytest.mark.parametrize("arch,dtype,batch", [
     ("mobilenet_v2", np.int8, 1), ("mobilenet_v2", np.int8, 3), ("mobilenet_v2", np.uint8, 1),
-    ("mobilenet_v1", np.int8, 1), ("mobilenet_v2", np.int8, 8)])
+    ("mobilenet_v1", np.int8, 1), ("mobilenet_v2", np.int8, 8),
+    ("ssd_mobilenet_v2", np.int8, 1), ("deeplab_v3_mobilenet_v2", np.int8, 1),
+    ("posenet_mobilenet_v1", np.int8, 1), ("ssd_mobilenet_v2", np.uint8, 1), ("posenet_mobilenet_v1", np.int8, 2)])
 def test_synthetic_models_bit_exact(gpu_lib, arch, dtype, batch):
     """The bench models (BASELINE C1/C2, synthetic weights), fused epilogues on."""
     from band_amd import tflite_synth as S
@@ -162,8 +164,10 @@ def test_synthetic_models_bit_exact(gpu_lib, arch, dtype, batch):
         x = rng.integers(lo, hi, t.shape).astype(dtype)
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = x
         assert ex.ExecuteSubgraph(key).ok()
-        ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]]
-        np.testing.assert_array_equal(ex.GetTensorView(key, om.outputs[0]).GetData(), ref.reshape(-1, ref.shape[-1]))
+        ref = OracleInterpreter(om).run({om.inputs[0]: x})
+        for o in om.outputs:
+            got = ex.GetTensorView(key, o).GetData()
+            np.testing.assert_array_equal(got, ref[o].reshape(got.shape), err_msg="%s output %d" % (arch, o))
 
 
 def test_view_of_fused_tensor_materialises_it(gpu_lib):

@@ -117,3 +117,19 @@ extern "C" int bh_event_sync(bh_event_t ev) { return ck(hipEventSynchronize((hip
 extern "C" int bh_event_elapsed_ms(bh_event_t a, bh_event_t b, float* ms) {
   return ck(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
 }
+
+// One lane spinning on the 100 MHz real-time counter: holds the stream for
+// `us` microseconds so a profiler can enqueue a whole launch sequence (with
+// events between launches) before the GPU reaches it; the events then time
+// back-to-back kernels instead of host submission gaps.  Always terminates.
+__global__ void bh_spin_kernel(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+extern "C" int bh_spin_us(bh_stream_t s, int us) {
+  if (us <= 0) return 0;
+  if (us > 100000) us = 100000;  // 100 ms cap
+  hipLaunchKernelGGL(bh_spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, (unsigned long long)us * 100ull);
+  return bh_check_launch("bh_spin_kernel");
+}

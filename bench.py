@@ -218,7 +218,9 @@ def main():
     execs0, keys0 = workers[0]
     for ex, key in zip(execs0, keys0):
         for r in ex.ProfileSubgraph(key, iters=args.profile_iters):
-            k = by_k.setdefault(r["kernel"], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
+            # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
+            # with its residual epilogue), as rocprofv3 reports them
+            k = by_k.setdefault(r["kernel"].split("+")[0], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
             k["ms"] += r["ms"] / M
             k["bytes"] += r["alg_bytes"] / M
             k["ops"] += r["alg_ops"] / M
@@ -230,6 +232,17 @@ def main():
     ops_per_launch = dom["ops"] / dom["launches"]
     achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
     gpu_ms_total = sum(v["ms"] for v in by_k.values())
+    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
+    # passes (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    # corrections of MI355X_MICROARCH.md), per launch; null when absent
+    traffic, traffic_src = None, None
+    import glob
+    pmc = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic.json")))
+    if pmc:
+        with open(pmc[-1]) as f:
+            tj = json.load(f)
+        if dom_name in tj:
+            traffic, traffic_src = tj[dom_name]["traffic_bytes_per_launch"], os.path.basename(pmc[-1])
     # device-side floor of one job: each model's passes replayed back to back
     # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
     # host launch + sync wakeup
@@ -270,7 +283,7 @@ def main():
             "device_us_per_model": device_us,
             "roofline": {
                 "kernel": dom_name, "bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
-                "frac": achieved_gbs / 8000.0, "traffic": None,
+                "frac": achieved_gbs / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
                 "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
                 "launches_per_inference": dom["launches"],
                 "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,

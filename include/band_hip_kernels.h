@@ -83,6 +83,9 @@ int bh_event_destroy(bh_event_t ev);
 int bh_event_record(bh_event_t ev, bh_stream_t s);
 int bh_event_sync(bh_event_t ev);
 int bh_event_elapsed_ms(bh_event_t start, bh_event_t end, float* ms);
+/* hold the stream for `us` microseconds (<= 100 ms): lets a profiler enqueue
+ * a launch sequence before the GPU starts it, so events time execution */
+int bh_spin_us(bh_stream_t s, int us);
 
 /* ---- op parameter blocks ------------------------------------------------ */
 

@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Reproduces the profiles/ evidence for one round on an MI355X box:
+#   1. bench.py (default workload), writing the fused-block tuning decisions
+#      to a tune file;
+#   2. the same bench command under rocprofv3 --kernel-trace --stats
+#      (--no-graph: rocprofv3 crashes inside hipGraphLaunch with kernel
+#      tracing), replaying the same tuning decisions -> per-kernel durations;
+#   3. two PMC passes (FETCH_SIZE, WRITE_SIZE; never combined with
+#      sys/runtime traces) -> HBM traffic per launch (tools/pmc_traffic.py).
+# usage: tools/profile_bench.sh <tag> [extra bench args]   (outputs in gpurun_out/<tag>_*)
+set -euo pipefail
+TAG=${1:?tag}
+shift
+R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}
+cd "$R"
+export TMPDIR=/tmp
+O=$R/gpurun_out
+mkdir -p "$O"
+export BAND_HIP_TUNE_FILE=$O/${TAG}_tune.txt
+rm -f "$BAND_HIP_TUNE_FILE"
+ARGS="--steps 2000 --warmup 200 --workers-per-gpu 1 $*"
+timeout -k 10 300 python3 bench.py $ARGS > "$O/${TAG}_bench.json"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${TAG}_trace" -o run -- \
+  python3 bench.py $ARGS --no-graph --no-cpu-baseline > "$O/${TAG}_bench_profiled.json" 2> "$O/${TAG}_trace.err"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcf" -o run -- \
+  python3 bench.py --steps 200 --warmup 20 --workers-per-gpu 1 --no-graph --no-cpu-baseline --profile-iters 2 $* \
+  > /dev/null 2> "$O/${TAG}_pmcf.err"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcw" -o run -- \
+  python3 bench.py --steps 200 --warmup 20 --workers-per-gpu 1 --no-graph --no-cpu-baseline --profile-iters 2 $* \
+  > /dev/null 2> "$O/${TAG}_pmcw.err"
+python3 tools/pmc_traffic.py "$O/${TAG}_pmcf" "$O/${TAG}_pmcw" "$O/${TAG}_pmc_traffic.json" > "$O/${TAG}_pmc_traffic.txt"
+cp "$O/${TAG}_trace/run_kernel_stats.csv" "$O/${TAG}_kernel_stats.csv"
+echo "profile $TAG done"

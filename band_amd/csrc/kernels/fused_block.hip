@@ -32,7 +32,7 @@ struct IrbGeom {
   int ce_p, ds;         // K-padded expanded channels, LDS row stride of dw output
   int T, MT1, MT3;      // tile pixels, 16-row tiles of region / tile
   int np3;              // padded output channels (phase-3 accumulator row)
-  size_t x_off, e_off, d_off, w_off, bytes;
+  size_t x_off, e_off, d_off, a_off, w_off, bytes;
   // w region: dw filter [9][ce16] bytes, then int32 dw bias/mult/shift [ce],
   // then int32 project bias_eff/mult/shift [out_c]
   int ce16;
@@ -55,12 +55,12 @@ __host__ __device__ inline IrbGeom irb_geom(const bh_irb_params& p) {
   g.x_off = 0;
   const size_t xb = p.has_expand ? (size_t)g.MT1 * 16 * g.xs : 0;
   g.e_off = xb;
-  // the expanded buffer is reused for the int32 phase-3 accumulators
-  size_t eb = (size_t)g.R * g.es;
-  const size_t ab = (size_t)g.MT3 * 16 * g.np3 * 4;
-  if (ab > eb) eb = ab;
+  // int32 phase-3 accumulators get their own region, zeroed during phase 0
+  // (no extra barrier)
+  const size_t eb = (size_t)g.R * g.es;
   g.d_off = (g.e_off + eb + 15) / 16 * 16;
-  g.w_off = (g.d_off + (size_t)g.MT3 * 16 * g.ds + 15) / 16 * 16;
+  g.a_off = (g.d_off + (size_t)g.MT3 * 16 * g.ds + 15) / 16 * 16;
+  g.w_off = (g.a_off + (size_t)g.MT3 * 16 * g.np3 * 4 + 15) / 16 * 16;
   g.ce16 = (p.exp_c + 15) / 16 * 16;
   g.bytes = g.w_off + 9 * (size_t)g.ce16 + 12 * (size_t)g.ce16 + 12 * (size_t)p.out_c;
   return g;
@@ -72,6 +72,7 @@ struct IrbDivs {
   FastDiv upr;     // 8-byte (expand) / 4-byte (no expand) units per region row
   FastDiv rw;      // region width
   FastDiv groups;  // exp_c / 4
+  FastDiv expc;    // exp_c (one-channel depthwise items)
   FastDiv tile_w;
   FastDiv out_c;
   FastDiv mt1;     // 16-row tiles of the region
@@ -205,6 +206,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
         if (u0 + j * NT < units) *(uint32_t*)(el + dst[j]) = v[j];
     }
   }
+  int* accl = (int*)(smem + G.a_off);
+  for (int i = tid; i < G.MT3 * 16 * G.np3; i += NT) accl[i] = 0;
   __syncthreads();
   IRB_STAMP(1)
 
@@ -246,10 +249,12 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
   IRB_STAMP(2)
 
   // ---- phase 2: depthwise 3x3 (VALU) -> LDS -----------------------------
-  {
-    // Only the T tile rows are produced: the MFMA padding rows of dl feed
-    // accumulator rows phase 4 never reads, and the K tail of the project
-    // operand meets zero-packed weights, so neither needs initialising.
+  // Only the T tile rows are produced: the MFMA padding rows of dl feed
+  // accumulator rows phase 4 never reads, and the K tail of the project
+  // operand meets zero-packed weights, so neither needs initialising.  Four
+  // channels per item when that still covers every thread, else one (small
+  // tiles: a 4x shorter per-thread chain).
+  if (G.T * (p.exp_c / 4) >= NT) {
     const int groups = p.exp_c / 4;
     for (int it = tid; it < G.T * groups; it += NT) {
       const int pi = dv.groups.div(it);
@@ -287,15 +292,39 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
       }
       *(uint32_t*)(dl + pi * G.ds + c0) = packed;
     }
+  } else {
+    for (int it = tid; it < G.T * p.exp_c; it += NT) {
+      const int pi = dv.expc.div(it);
+      const int c = it - pi * p.exp_c;
+      const int ty = dv.tile_w.div(pi);
+      const int tx = pi - ty * p.tile_w;
+      const int oy = oy0 + ty, ox = ox0 + tx;
+      int32_t v = 0;
+      if (oy < p.out_h && ox < p.out_w) {
+        int32_t acc = 0;
+#pragma unroll
+        for (int fy = 0; fy < 3; ++fy) {
+          const int iy = oy * p.stride - p.pad_h + fy;
+          if (iy < 0 || iy >= p.in_h) continue;
+#pragma unroll
+          for (int fx = 0; fx < 3; ++fx) {
+            const int ix = ox * p.stride - p.pad_w + fx;
+            if (ix < 0 || ix >= p.in_w) continue;
+            const int er = (ty * p.stride + fy) * G.RW + tx * p.stride + fx;
+            acc += ((int32_t)(int8_t)el[er * G.es + c] - p.e_zp) * (int32_t)(int8_t)wl[(fy * 3 + fx) * G.ce16 + c];
+          }
+        }
+        v = clamp_i32(requant(acc + dwt[c], dwt[G.ce16 + c], dwt[2 * G.ce16 + c]) + p.d_zp, p.d_act_min,
+                      p.d_act_max);
+      }
+      dl[pi * G.ds + c] = (unsigned char)v;
+    }
   }
   __syncthreads();
   IRB_STAMP(3)
+  IRB_STAMP(4)
 
   // ---- phase 3: project 1x1 (MFMA), split-K, LDS-atomic accumulation -----
-  int* accl = (int*)el;  // the expanded tensor is dead now
-  for (int i = tid; i < G.MT3 * 16 * G.np3; i += NT) accl[i] = 0;
-  __syncthreads();
-  IRB_STAMP(4)
   {
     for (int item = wave; item < G.MT3 * NT3 * ksplit; item += NW) {
       const int tile = dv.ksplit.div(item);
@@ -400,6 +429,7 @@ static int launch_irb(const bh_irb_params& p, size_t lds, hipStream_t s) {
   dv.upr = FastDiv(p.has_expand ? G.cin_p / 8 : p.in_c / 4);
   dv.rw = FastDiv(G.RW);
   dv.groups = FastDiv(p.exp_c / 4);
+  dv.expc = FastDiv(p.exp_c);
   dv.tile_w = FastDiv(p.tile_w);
   dv.out_c = FastDiv(p.out_c);
   dv.mt1 = FastDiv(G.MT1);

@@ -115,18 +115,39 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
   const int KS1 = G.cin_p / 64;  // <= 4 (host-checked)
   const int NT3 = G.np3 / 16;
   const int KS3 = G.ce_p / 64;
-  // Staged copies issue all loads of an iteration before any store: a loop
-  // that stores right after each load pays one memory round trip per
-  // iteration.
+  // Expand filter fragments + tables of this wave's first phase-1 item: issued
+  // first, so their latency hides behind the prologue.
+  const int n_items1 = p.has_expand ? G.MT1 * NT1 : 0;
+  v4i b1[4];
+  int32_t be1 = 0, mu1 = 0, sh1 = 0;
+  auto load_b1 = [&](int item, v4i* b, int32_t& be, int32_t& mu, int32_t& sh) {
+    const int col = dv.mt1.div(item) * 16 + r16;
+    const int8_t* wrow = p.exp_w + (long)col * p.exp_k_pad + g * 16;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+      if (ks < KS1) b[ks] = *(const v4i*)(wrow + ks * 64);
+    be = p.exp_bias_eff[col];
+    mu = p.exp_mult[col];
+    sh = p.exp_shift[col];
+  };
+  if (wave < n_items1) load_b1(wave, b1, be1, mu1, sh1);
+
+  // ---- phase 0: depthwise filter + int32 tables + input region -> LDS -------
+  // One loop, each iteration issuing ALL its loads (tables, filter, a batch of
+  // region units) before any store, so the prologue costs one memory round
+  // trip per iteration (usually one).
   {
-    // dw filter (same [9][exp_c] layout, exp_c % 16 == 0) and the int32
-    // tables: three independent 16-byte ranges, all loads of an iteration
-    // issued before its stores
-    const int n16 = 9 * p.exp_c / 16;
+    const int n16 = 9 * p.exp_c / 16;  // dw filter [9][exp_c], exp_c % 16 == 0
     const int c16 = p.exp_c / 4;
-    const int p16 = p.out_c / 4;  // out_c % 4 == 0 (host-checked)
+    const int p16 = p.out_c / 4;       // out_c % 4 == 0 (host-checked)
     const int span = max(n16, max(c16, p16));
-    for (int u = tid; u < span; u += NT) {
+    // region: 8-byte units (expand input; pad pixels = x_zp, K tail = 0) or
+    // 4-byte units (no expand: the region is the depthwise input)
+    const int upr = p.has_expand ? G.cin_p / 8 : p.in_c / 4;
+    const int units = p.has_expand ? G.MT1 * 16 * upr : G.R * upr;
+    const uint32_t zpw = splat_byte(p.x_zp);
+    for (int it = 0; it * NT < span || it * 4 * NT < units; ++it) {
+      const int u = it * NT + tid;
       v4i w = {0, 0, 0, 0}, t0 = w, t1 = w, t2 = w, q0 = w, q1 = w, q2 = w;
       if (u < n16) w = *(const v4i*)(p.dw_w + u * 16);
       if (u < c16) {
@@ -139,6 +160,35 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
         q1 = *(const v4i*)(p.proj_mult + u * 4);
         q2 = *(const v4i*)(p.proj_shift + u * 4);
       }
+      v2i v[4];
+      int dst[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ru = it * 4 * NT + j * NT + tid;
+        dst[j] = -1;
+        v[j] = (v2i){0, 0};
+        if (ru >= units) continue;
+        const int r = dv.upr.div(ru);
+        if (p.has_expand) {
+          const int k = (ru - r * upr) * 8;
+          dst[j] = r * G.xs + k;
+          if (r < G.R && k < p.in_c) {
+            const int ry = dv.rw.div(r);
+            const int iy = ry0 + ry, ix = rx0 + (r - ry * G.RW);
+            if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
+              v[j] = *(const v2i*)(x + ((long)iy * p.in_w + ix) * p.in_c + k);
+            else
+              v[j] = (v2i){(int)zpw, (int)zpw};
+          }
+        } else {
+          const int k = (ru - r * upr) * 4;
+          dst[j] = r * G.es + k;
+          const int ry = dv.rw.div(r);
+          const int iy = ry0 + ry, ix = rx0 + (r - ry * G.RW);
+          if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
+            v[j].x = *(const int*)(x + ((long)iy * p.in_w + ix) * p.in_c + k);
+        }
+      }
       if (u < n16) *(v4i*)(wl + u * 16) = w;
       if (u < c16) {
         *(v4i*)(dwt + u * 4) = t0;
@@ -150,60 +200,12 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
         *(v4i*)(pjt + p.out_c + u * 4) = q1;
         *(v4i*)(pjt + 2 * p.out_c + u * 4) = q2;
       }
-    }
-  }
-
-  // ---- phase 0: input region -> LDS -------------------------------------
-  if (p.has_expand) {
-    const int upr = G.cin_p / 8;  // 8-byte units per row; pad pixels = x_zp, K tail = 0
-    const int units = G.MT1 * 16 * upr;
-    const uint32_t zpw = splat_byte(p.x_zp);
-    for (int u0 = tid; u0 < units; u0 += 4 * NT) {
-      v2i v[4];
-      int dst[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int u = u0 + j * NT;
-        const int r = dv.upr.div(u);
-        const int k = (u - r * upr) * 8;
-        dst[j] = r * G.xs + k;
-        v[j] = (v2i){0, 0};
-        if (u < units && r < G.R && k < p.in_c) {
-          const int ry = dv.rw.div(r);
-          const int iy = ry0 + ry;
-          const int ix = rx0 + (r - ry * G.RW);
-          if (iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
-            v[j] = *(const v2i*)(x + ((long)iy * p.in_w + ix) * p.in_c + k);
-          else
-            v[j] = (v2i){(int)zpw, (int)zpw};
-        }
+        if (dst[j] < 0) continue;
+        if (p.has_expand) *(v2i*)(xl + dst[j]) = v[j];
+        else *(int*)(el + dst[j]) = v[j].x;
       }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (u0 + j * NT < units) *(v2i*)(xl + dst[j]) = v[j];
-    }
-  } else {
-    const int upr = p.in_c / 4;  // no expand: the region itself is the depthwise input
-    const int units = G.R * upr;
-    for (int u0 = tid; u0 < units; u0 += 4 * NT) {
-      uint32_t v[4];
-      int dst[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int u = u0 + j * NT;
-        const int r = dv.upr.div(u);
-        const int k = (u - r * upr) * 4;
-        const int ry = dv.rw.div(r);
-        const int iy = ry0 + ry;
-        const int ix = rx0 + (r - ry * G.RW);
-        dst[j] = r * G.es + k;
-        v[j] = 0;
-        if (u < units && iy >= 0 && iy < p.in_h && ix >= 0 && ix < p.in_w)
-          v[j] = *(const uint32_t*)(x + ((long)iy * p.in_w + ix) * p.in_c + k);
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        if (u0 + j * NT < units) *(uint32_t*)(el + dst[j]) = v[j];
     }
   }
   int* accl = (int*)(smem + G.a_off);
@@ -213,23 +215,16 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
 
   // ---- phase 1: expand 1x1 (MFMA) -> LDS --------------------------------
   if (p.has_expand) {
-    int cur_nt = -1;
-    v4i b1[4];
-    int32_t be1 = 0, mu1 = 0, sh1 = 0;
-    for (int item = wave; item < G.MT1 * NT1; item += NW) {
+    // software pipeline: the next item's filter fragments and tables are in
+    // flight while this item multiplies and requantises
+    for (int item = wave; item < n_items1; item += NW) {
       const int nt = dv.mt1.div(item);
       const int mt = item - nt * G.MT1;
       const int col = nt * 16 + r16;
-      if (nt != cur_nt) {
-        const int8_t* wrow = p.exp_w + (long)col * p.exp_k_pad + g * 16;
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-          if (ks < KS1) b1[ks] = *(const v4i*)(wrow + ks * 64);
-        be1 = p.exp_bias_eff[col];
-        mu1 = p.exp_mult[col];
-        sh1 = p.exp_shift[col];
-        cur_nt = nt;
-      }
+      v4i bn[4];
+      int32_t ben = 0, mun = 0, shn = 0;
+      const bool next = item + NW < n_items1;
+      if (next) load_b1(item + NW, bn, ben, mun, shn);
       v4i acc = (v4i){0, 0, 0, 0};
       const unsigned char* arow = xl + (mt * 16 + r16) * G.xs + g * 16;
 #pragma unroll
@@ -243,10 +238,19 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
           el[row * G.es + col] = (unsigned char)v;
         }
       }
+      if (next) {
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks) b1[ks] = bn[ks];
+        be1 = ben;
+        mu1 = mun;
+        sh1 = shn;
+      }
     }
     __syncthreads();
   }
   IRB_STAMP(2)
+
+  const int n_items3 = G.MT3 * NT3 * ksplit;
 
   // ---- phase 2: depthwise 3x3 (VALU) -> LDS -----------------------------
   // Only the T tile rows are produced: the MFMA padding rows of dl feed
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
 
   // ---- phase 3: project 1x1 (MFMA), split-K, LDS-atomic accumulation -----
   {
-    for (int item = wave; item < G.MT3 * NT3 * ksplit; item += NW) {
+    for (int item = wave; item < n_items3; item += NW) {
       const int tile = dv.ksplit.div(item);
       const int kz = item - tile * ksplit;
       const int nt = dv.mt3.div(tile);
@@ -462,7 +466,7 @@ extern "C" int bh_irb_i8(const bh_irb_params* pp, bh_stream_t stream) {
     bh_set_last_error("bh_irb_i8: invalid or unsupported parameters");
     return BH_EINVAL;
   }
-  // 16 waves when one workgroup fills the CU's LDS, else 8 (two fit)
-  return lds > 80 * 1024 ? bh::launch_irb<16>(*pp, lds, (hipStream_t)stream)
-                         : bh::launch_irb<8>(*pp, lds, (hipStream_t)stream);
+  // 16 waves: at batch 1 a block has fewer workgroups than CUs, so each
+  // workgroup owns a CU anyway and more waves shorten every phase's item chain
+  return bh::launch_irb<16>(*pp, lds, (hipStream_t)stream);
 }

@@ -98,7 +98,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
   const int8_t* x = (const int8_t*)p.input + (long)n * p.in_h * p.in_w * p.in_c;
   unsigned long long* stamps =
       p.debug_stamps ? (unsigned long long*)p.debug_stamps +
-                           8 * (((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x)
+                           16 * (((long)blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x)
                      : nullptr;
 #define IRB_STAMP(k) \
   if (stamps && tid == 0) stamps[k] = __builtin_amdgcn_s_memrealtime();

@@ -232,7 +232,7 @@ typedef struct bh_irb_params {
   void* output;
   /* diagnostics: when non-NULL, wave 0 of each workgroup writes 8 uint64
    * s_memrealtime stamps (100 MHz) at phase boundaries to
-   * debug_stamps[8 * workgroup]; NULL in production */
+   * debug_stamps[16 * workgroup] (slots 0-7 used); NULL in production */
   void* debug_stamps;
 } bh_irb_params;
 

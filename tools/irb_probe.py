@@ -37,7 +37,7 @@ def main():
                 continue
             oh, ow = c.out_shape[1], c.out_shape[2]
             nwg = ((oh + tile - 1) // tile) * ((ow + tile - 1) // tile)
-            stamps = DeviceBuffer(nwg * 8 * 8)
+            stamps = DeviceBuffer(nwg * 16 * 8)
             # timing without stamps
             for _ in range(3):
                 lib.bh_irb_i8(ctypes.byref(q), s)
@@ -52,13 +52,21 @@ def main():
             q.debug_stamps = stamps.value
             lib.bh_irb_i8(ctypes.byref(q), s)
             lib.bh_stream_sync(s)
-            st_ = stamps.download(np.uint64, (nwg, 8)).astype(np.float64)
+            st16 = stamps.download(np.uint64, (nwg, 16)).astype(np.float64)
+            st_ = st16[:, :8]
             d = np.diff(st_[:, :7], axis=1) * 0.01  # 100 MHz ticks -> us
             span = (st_[:, 6].max() - st_[:, 0].min()) * 0.01
             clk = np.median(st_[:, 7] / np.maximum((st_[:, 6] - st_[:, 0]) * 0.01, 1e-3)) / 1e3  # GHz
             print("blk %3d %3d->%4d->%3d s%d tile %d wg %4d lds %6d  kernel %6.2f us  wg-span %6.2f clk %.2fGHz " % (
                 h, cin, cin * t, cout, st, tile, nwg, lds, ms.value * 1e3 / n, span, clk) +
                 " ".join("%s %.2f/%.2f" % (nm, d[:, i].mean(), d[:, i].max()) for i, nm in enumerate(names)))
+            # wave-0 cycle stamps (s_memtime): phase-1 start 11, item0 weights ready 8,
+            # MFMA done 9, requant+stores done 10; phase-2 start 12, taps done 13,
+            # requant+store done 14; end 15
+            c = st16[0]
+            if c[11] > 0:
+                print("    cycles: p1 start->w %d, w->mfma %d, mfma->req+st %d | p2 start->taps %d, taps->req+st %d | p1 start->end %d" % (
+                    c[8] - c[11], c[9] - c[8], c[10] - c[9], c[13] - c[12], c[14] - c[13], c[15] - c[11]))
             sys.stdout.flush()
 
 

@@ -31,6 +31,8 @@ def main():
         buf = S.mobilenet_v2(np.int8, seed=0, batch=a.batch)
     elif a.model == "mobilenet_v1_int8":
         buf = S.mobilenet_v1(np.int8, seed=0, batch=a.batch)
+    elif hasattr(S, a.model):  # e.g. ssd_mobilenet_v2, deeplab_v3_mobilenet_v2, posenet_mobilenet_v1
+        buf = getattr(S, a.model)(np.int8, batch=a.batch)
     else:
         buf = open(a.model, "rb").read()
     desc = read(buf)

@@ -22,7 +22,7 @@ class ConvParams(ctypes.Structure):
         (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift", "residual")] + [
         (n, c_int32) for n in ("add_y_off", "add_r_off", "add_o_off", "add_left_shift", "add_y_mult",
                                "add_y_shift", "add_r_mult", "add_r_shift", "add_o_mult", "add_o_shift",
-                               "add_act_min", "add_act_max")]
+                               "add_act_min", "add_act_max")] + [("out_table", c_void_p)]
 
 
 class DwConvParams(ctypes.Structure):
@@ -30,13 +30,13 @@ class DwConvParams(ctypes.Structure):
         "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "depth_multiplier",
         "k_h", "k_w", "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "in_xor")] + [
         (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
-        (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift")]
+        (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift", "out_table")]
 
 
 class FcParams(ctypes.Structure):
     _fields_ = [(n, c_int) for n in ("rows", "depth", "depth_pad", "units", "in_xor")] + [
         (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
-        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift")]
+        (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift", "out_table")]
 
 
 class EltwiseParams(ctypes.Structure):

@@ -502,6 +502,7 @@ absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubg
     RETURN_STATUS_IF(Lower(model, i, sg));
   }
   if (allow_fusion_ && allow_irb_) FuseBlocks(model, sg);
+  if (allow_fusion_) FuseGlue(model, sg);
   return absl::OkStatus();
 }
 
@@ -738,6 +739,7 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
     Launch F;
     F.kind = Launch::kIrb;
     F.op_index = E ? E->op_index : D.op_index;
+    F.out_tensor = P.out_tensor;
     F.irb = q;
     F.kernel = "irb_kernel";
     // algorithmic bytes: block input + block output + all filters/tables
@@ -752,6 +754,108 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
     if (E) sg->fused_tensors.insert(d.ops[E->op_index].outputs[0]);
     i = j + 1;  // consumed [E] D P
   }
+  sg->launches.swap(out);
+}
+
+namespace {
+void** OutSlot(Launch& l) {
+  switch (l.kind) {
+    case Launch::kConv: return &l.conv.output;
+    case Launch::kDwConv: return &l.dw.output;
+    case Launch::kFc: return &l.fc.output;
+    case Launch::kEltwise: return &l.elt.out;
+    case Launch::kPool: return &l.pool.output;
+    case Launch::kIrb: return &l.irb.output;
+    case Launch::kLutU8: return &l.dst;
+    default: return nullptr;
+  }
+}
+const void** TableSlot(Launch& l) {
+  switch (l.kind) {
+    case Launch::kConv: return l.conv.residual ? nullptr : &l.conv.out_table;  // + ADD epilogue: keep apart
+    case Launch::kDwConv: return &l.dw.out_table;
+    case Launch::kFc: return &l.fc.out_table;
+    default: return nullptr;
+  }
+}
+}  // namespace
+
+void HipModelExecutor::FuseGlue(const HipModel& model, PreparedSubgraph* sg) {
+  const TflModel& d = model.desc();
+  auto in_outputs = [&](int t) {
+    return std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end() ||
+           std::find(d.outputs.begin(), d.outputs.end(), t) != d.outputs.end();
+  };
+  // t reaches op `to` through RESHAPE / SQUEEZE aliases only, every tensor on
+  // the way read by nothing else and needed by nobody outside; collects them
+  auto private_chain = [&](int t, int to, std::vector<int>* chain) {
+    while (t >= 0) {
+      if (consumers_[t].size() != 1 || in_outputs(t) || sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
+      chain->push_back(t);
+      const int c = consumers_[t][0];
+      if (c == to) return true;
+      const TflOperator& op = d.ops[c];
+      if ((op.builtin != kTflReshape && op.builtin != kTflSqueeze) ||
+          !std::binary_search(sg->ops.begin(), sg->ops.end(), c))
+        return false;
+      t = op.outputs[0];
+    }
+    return false;
+  };
+  auto producer_of = [&](size_t i, const void* ptr) -> int {
+    for (size_t j = i; j-- > 0;) {
+      void** o = OutSlot(sg->launches[j]);
+      if (o && *o == ptr) return static_cast<int>(j);
+    }
+    return -1;
+  };
+  std::vector<bool> dead(sg->launches.size(), false);
+  // (1) byte tables into the producer's epilogue
+  for (size_t i = 0; i < sg->launches.size(); ++i) {
+    Launch& L = sg->launches[i];
+    if (L.kind != Launch::kLutU8) continue;
+    const int j = producer_of(i, L.src);
+    if (j < 0 || dead[j]) continue;
+    Launch& P = sg->launches[j];
+    const void** ts = TableSlot(P);
+    std::vector<int> chain;
+    if (!ts || *ts || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
+    *ts = L.table;
+    *OutSlot(P) = L.dst;
+    P.out_tensor = L.out_tensor;
+    P.alg_bytes += 0;  // same bytes: the table gather happens on the stored value
+    for (int t : chain) sg->fused_tensors.insert(t);
+    sg->fused_ops.insert(L.op_index);
+    dead[i] = true;
+  }
+  // (2) CONCATENATION whose inputs are contiguous slices of the output
+  for (size_t i = 0; i < sg->launches.size(); ++i) {
+    Launch& C = sg->launches[i];
+    if (C.kind != Launch::kConcat || C.concat.outer != 1) continue;
+    bool ok = true;
+    std::vector<int> prod(C.concat.n_inputs, -1);
+    std::vector<int> chain;
+    for (int k = 0; k < C.concat.n_inputs && ok; ++k) {
+      if (C.concat.table[k]) ok = false;
+      const int j = ok ? producer_of(i, C.concat.input[k]) : -1;
+      ok = ok && j >= 0 && !dead[j] && OutSlot(sg->launches[j]) &&
+           private_chain(sg->launches[j].out_tensor, C.op_index, &chain);
+      if (ok) prod[k] = j;
+      for (int kk = 0; kk < k && ok; ++kk) ok = prod[kk] != j;  // one producer per slice
+    }
+    if (!ok) continue;
+    long off = 0;
+    for (int k = 0; k < C.concat.n_inputs; ++k) {
+      *OutSlot(sg->launches[prod[k]]) = static_cast<char*>(C.concat.output) + off;
+      off += C.concat.row[k];
+    }
+    for (int t : chain) sg->fused_tensors.insert(t);
+    sg->fused_ops.insert(C.op_index);
+    dead[i] = true;
+  }
+  std::vector<Launch> out;
+  for (size_t i = 0; i < sg->launches.size(); ++i)
+    if (!dead[i]) out.push_back(sg->launches[i]);
   sg->launches.swap(out);
 }
 
@@ -808,6 +912,7 @@ bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, Prepare
   L->alg_bytes += static_cast<double>(tr.num_elements());  // residual read; y never stored
   L->kernel = std::strcmp(L->kernel, "conv_direct_kernel") == 0 ? "conv_direct_kernel+add" : "conv_mfma_kernel+add";
   sg->fused_ops.insert(j);
+  L->out_tensor = add.outputs[0];
   sg->fused_tensors.insert(t);
   return true;
 }
@@ -830,6 +935,7 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
   const std::string ckey = "m" + Hex(model.serial()) + "/op" + std::to_string(oi);
   Launch L;
   L.op_index = oi;
+  L.out_tensor = op.outputs[0];
 
   if (op.builtin == kTflConv2D || op.builtin == kTflDepthwiseConv2D) {
     const bool dw = op.builtin == kTflDepthwiseConv2D;
@@ -1053,6 +1159,7 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
       Launch F;
       F.kind = Launch::kFc;
       F.op_index = oi;
+      F.out_tensor = L.out_tensor;
       bh_fc_params& f = F.fc;
       f = bh_fc_params{};
       f.rows = static_cast<int>(M); f.depth = c.in_c; f.depth_pad = c.k_pad; f.units = c.out_c;

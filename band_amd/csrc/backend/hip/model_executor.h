@@ -39,6 +39,7 @@ struct Launch {
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax
   } kind;
   int op_index = -1;
+  int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
   bh_conv_params conv{};
   bh_dwconv_params dw{};
   bh_fc_params fc{};
@@ -130,6 +131,9 @@ class HipModelExecutor : public interface::IModelExecutor {
   absl::Status BuildLaunches(const HipModel& model, PreparedSubgraph* sg);
   bool TryFuseResidualAdd(const HipModel& model, int conv_op, PreparedSubgraph* sg, Launch* l);
   void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
+  // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
+  // CONCATENATION with outer size 1 elided (producers write their slices)
+  void FuseGlue(const HipModel& model, PreparedSubgraph* sg);
   // Mean device time (us) of one pass over `ls`, or < 0 when it cannot be
   // measured (no GPU stream, or a launch failed).
   double TimeLaunches(const std::vector<const Launch*>& ls, int iters);

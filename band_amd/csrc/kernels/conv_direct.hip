@@ -79,7 +79,8 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(bh_conv_params p, int 
       const int32_t sr = requant_lt1((q + p.add_r_off) * (1 << p.add_left_shift), p.add_r_mult, p.add_r_shift);
       v = clamp_i32(requant_lt1(sy + sr, p.add_o_mult, p.add_o_shift) + p.add_o_off, p.add_act_min, p.add_act_max);
     }
-    packed[c >> 2] |= ((uint32_t)v & 0xffu) << (8 * (c & 3));
+    const uint32_t byte = p.out_table ? ((const uint8_t*)p.out_table)[(uint8_t)v] : ((uint32_t)v & 0xffu);
+    packed[c >> 2] |= byte << (8 * (c & 3));
   }
   uint8_t* out = (uint8_t*)p.output + obase + c0;
   if (c0 + 8 <= p.out_c && (p.out_c % 8) == 0) {

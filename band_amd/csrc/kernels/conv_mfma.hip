@@ -253,6 +253,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   uint8_t* out = (uint8_t*)p.output;
   const uint8_t* res = (const uint8_t*)p.residual;
   const bool res_signed = p.in_xor == 0;  // residual shares the activation type
+  const uint8_t* tab = (const uint8_t*)p.out_table;
 #pragma unroll
   for (int wn = 0; wn < WN; ++wn) {
     const int n = n0 + wn * 16 + r16;
@@ -277,7 +278,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
           v = clamp_i32(requant_lt1(sy + sr, p.add_o_mult, p.add_o_shift) + p.add_o_off, p.add_act_min,
                         p.add_act_max);
         }
-        out[o] = (uint8_t)v;
+        out[o] = tab ? tab[(uint8_t)v] : (uint8_t)v;
       }
     }
   }

@@ -101,7 +101,8 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int 
     for (int b = 0; b < 4; ++b) {
       int32_t r = requant(acc[d * 4 + b] + bb[b], mm[b], ss[b]) + p.out_zp;
       r = clamp_i32(r, p.act_min, p.act_max);
-      o |= ((uint32_t)r & 0xffu) << (8 * b);
+      const uint32_t byte = p.out_table ? ((const uint8_t*)p.out_table)[(uint8_t)r] : ((uint32_t)r & 0xffu);
+      o |= byte << (8 * b);
     }
     packed[d] = o;
   }
@@ -136,8 +137,9 @@ __global__ __launch_bounds__(256) void dwconv_generic_kernel(bh_dwconv_params p,
     }
   }
   int32_t r = requant(acc + p.bias[c], p.mult[c], p.shift[c]) + p.out_zp;
+  const uint8_t byte = (uint8_t)clamp_i32(r, p.act_min, p.act_max);
   ((uint8_t*)p.output)[(((long)n * p.out_h + oy) * p.out_w + ox) * p.out_c + c] =
-      (uint8_t)clamp_i32(r, p.act_min, p.act_max);
+      p.out_table ? ((const uint8_t*)p.out_table)[byte] : byte;
 }
 
 static DwDivs dw_divs(const bh_dwconv_params& p, int groups) {

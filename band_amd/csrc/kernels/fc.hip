@@ -69,7 +69,8 @@ __global__ __launch_bounds__(256) void fc_kernel(bh_fc_params p, FastDiv units) 
     int32_t v = acc + p.bias_eff[u];
     if constexpr (WZP) v -= p.w_zp * xs;
     v = requant(v, p.mult[u], p.shift[u]) + p.out_zp;
-    ((uint8_t*)p.output)[(long)r * p.units + u] = (uint8_t)clamp_i32(v, p.act_min, p.act_max);
+    const uint8_t byte = (uint8_t)clamp_i32(v, p.act_min, p.act_max);
+    ((uint8_t*)p.output)[(long)r * p.units + u] = p.out_table ? ((const uint8_t*)p.out_table)[byte] : byte;
   }
 }
 

@@ -123,6 +123,10 @@ typedef struct bh_conv_params {
   int32_t add_left_shift;
   int32_t add_y_mult, add_y_shift, add_r_mult, add_r_shift, add_o_mult, add_o_shift;
   int32_t add_act_min, add_act_max;
+  /* optional 256-entry byte table applied to every stored output byte: a
+   * following 8-bit unary op (QUANTIZE / RELU family / LOGISTIC) folded into
+   * this epilogue (NULL = none) */
+  const void* out_table;
 } bh_conv_params;
 
 /* DEPTHWISE_CONV_2D.  weights: int8-domain [k_h][k_w][out_c] (TFLite layout
@@ -143,6 +147,10 @@ typedef struct bh_dwconv_params {
   const int32_t* bias;            /* [out_c] raw int32 bias (zeros if absent) */
   const int32_t* mult;
   const int32_t* shift;
+  /* optional 256-entry byte table applied to every stored output byte: a
+   * following 8-bit unary op (QUANTIZE / RELU family / LOGISTIC) folded into
+   * this epilogue (NULL = none) */
+  const void* out_table;
 } bh_dwconv_params;
 
 /* FULLY_CONNECTED.  input [rows][depth] bytes, weights int8-domain
@@ -159,6 +167,10 @@ typedef struct bh_fc_params {
   const int32_t* bias_eff;
   const int32_t* mult;            /* [units] */
   const int32_t* shift;
+  /* optional 256-entry byte table applied to every stored output byte: a
+   * following 8-bit unary op (QUANTIZE / RELU family / LOGISTIC) folded into
+   * this epilogue (NULL = none) */
+  const void* out_table;
 } bh_fc_params;
 
 /* ADD / SUB / MUL with TFLite 4-D broadcasting.  Shapes are extended to 4-D

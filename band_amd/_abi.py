@@ -101,6 +101,11 @@ class SoftmaxParams(ctypes.Structure):
                 ("out_scale", ctypes.c_float), ("out_zp", c_int32), ("input", c_void_p), ("output", c_void_p)]
 
 
+class ZeroInsertParams(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("batch", "in_h", "in_w", "channels", "stride_h", "stride_w", "out_h",
+                                     "out_w")] + [("fill", ctypes.c_uint32), ("input", c_void_p), ("output", c_void_p)]
+
+
 KERNEL_SYMBOLS = {
     "bh_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "bh_set_device": (c_int, [c_int]),
@@ -141,6 +146,7 @@ KERNEL_SYMBOLS = {
     "bh_resize_nearest": (c_int, [ctypes.POINTER(ResizeNearestParams), c_void_p]),
     "bh_resize_bilinear_i8": (c_int, [ctypes.POINTER(ResizeBilinearParams), c_void_p]),
     "bh_softmax_i8": (c_int, [ctypes.POINTER(SoftmaxParams), c_void_p]),
+    "bh_zero_insert": (c_int, [ctypes.POINTER(ZeroInsertParams), c_void_p]),
     "bh_dwconv2d_i8": (c_int, [ctypes.POINTER(DwConvParams), c_void_p]),
     "bh_fc_i8": (c_int, [ctypes.POINTER(FcParams), c_void_p]),
     "bh_eltwise_i8": (c_int, [ctypes.POINTER(EltwiseParams), c_void_p]),

@@ -180,6 +180,24 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
       if (in.shape.size() != 4 || out.shape.size() != 4 || out.type != in.type || eb == 0) return no("4-D only");
       return true;
     }
+    case kTflTransposeConv: {
+      // inputs: output_shape (const int32 [4]), weights OHWI, input, [bias]
+      if (op.inputs.size() < 3 || op.inputs[1] < 0 || op.inputs[2] < 0) return no("missing operands");
+      const TflTensor& os = T(op.inputs[0]);
+      const TflTensor& w = T(op.inputs[1]);
+      const TflTensor& x = T(op.inputs[2]);
+      if (!os.is_const() || !w.is_const()) return no("output shape and filter must be constant");
+      if (x.type != DataType::kInt8 || w.type != DataType::kInt8 || out.type != DataType::kInt8)
+        return no("int8 only (reference_integer_ops::TransposeConv)");
+      if (!HasQ(x) || !HasQ(w) || !HasQ(out)) return no("missing quantization");
+      if (x.shape.size() != 4 || w.shape.size() != 4 || out.shape.size() != 4 || w.shape[3] != x.shape[3])
+        return no("4-D, filter [oc][kh][kw][ic]");
+      if (op.inputs.size() > 3 && op.inputs[3] >= 0) {
+        const TflTensor& b = T(op.inputs[3]);
+        if (!b.is_const() || b.type != DataType::kInt32) return no("bias must be constant int32");
+      }
+      return true;
+    }
     case kTflResizeBilinear:
       if (in.type != DataType::kInt8 || out.type != in.type || in.shape.size() != 4 || out.shape.size() != 4)
         return no("int8 4-D only (ResizeBilinearInteger)");
@@ -294,6 +312,101 @@ absl::Status HipModelExecutor::UploadConst(const std::string& key, const void* d
   }
   sg->consts.push_back(blob);
   *dev = blob->ptr();
+  return absl::OkStatus();
+}
+
+// TRANSPOSE_CONV (int8; reference_integer_ops::TransposeConv scatters
+// (x - zp) * w into an int32 scratch).  MI355X form: a transpose conv is a
+// stride-1 CONV_2D over the zero-inserted input U (U[y*s][x*s] = x, the input
+// zero point elsewhere, so inserted positions contribute exactly 0) with
+// spatially flipped filters and top/left padding k-1-pad; integer sums are
+// order-free, so the result is bit-identical.  Two launches: zero insertion
+// into a per-subgraph scratch buffer, then the MFMA conv.
+absl::Status HipModelExecutor::LowerTransposeConv(const HipModel& model, int oi, void* out_ptr,
+                                                  const std::string& ckey, PreparedSubgraph* sg, Launch* L) {
+  const TflModel& d = model.desc();
+  const TflOperator& op = d.ops[oi];
+  const TflTensor& w = d.tensors[op.inputs[1]];
+  const TflTensor& x = d.tensors[op.inputs[2]];
+  const TflTensor& out = d.tensors[op.outputs[0]];
+  void* x_ptr = nullptr;
+  RETURN_STATUS_IF(DevicePtr(model, op.inputs[2], sg, &x_ptr));
+  const int32_t* bias = nullptr;
+  if (op.inputs.size() > 3 && op.inputs[3] >= 0) bias = reinterpret_cast<const int32_t*>(d.tensors[op.inputs[3]].data);
+  const FbTable& o = op.options;
+  const bool same = !o.valid() || o.Int8(0, 0) == 0;
+  const int sw = o.valid() ? o.Int(1, 1) : 1, sh = o.valid() ? o.Int(2, 1) : 1;
+  const int b = x.shape[0], ih = x.shape[1], iw = x.shape[2], ic = x.shape[3];
+  const int oc = w.shape[0], kh = w.shape[1], kw = w.shape[2];
+  const int oh = out.shape[1], ow = out.shape[2];
+  if (out.shape[0] != b || out.shape[3] != oc) return absl::InternalError("TRANSPOSE_CONV shape mismatch");
+  // transpose_conv.cc: padding computed as for a conv whose input is the output
+  const int ph = ComputePadding(sh, 1, oh, kh, ComputeOutSize(same, oh, kh, sh, 1));
+  const int pw = ComputePadding(sw, 1, ow, kw, ComputeOutSize(same, ow, kw, sw, 1));
+  const int uh = (ih - 1) * sh + 1, uw = (iw - 1) * sw + 1;
+  // zero-inserted input in a scratch buffer owned by this subgraph
+  auto scratch = std::make_shared<DeviceBlob>(ordinal_, static_cast<size_t>(b) * uh * uw * ic);
+  if (!scratch->ok()) return absl::InternalError("HBM scratch allocation failed");
+  sg->consts.push_back(scratch);
+  Launch Z;
+  Z.kind = Launch::kZeroInsert;
+  Z.op_index = oi;
+  Z.kernel = "zero_insert_kernel";
+  Z.zi = bh_zero_insert_params{};
+  Z.zi.batch = b; Z.zi.in_h = ih; Z.zi.in_w = iw; Z.zi.channels = ic;
+  Z.zi.stride_h = sh; Z.zi.stride_w = sw; Z.zi.out_h = uh; Z.zi.out_w = uw;
+  Z.zi.fill = static_cast<uint32_t>(Zp(x)) & 0xffu;
+  Z.zi.input = x_ptr;
+  Z.zi.output = scratch->ptr();
+  Z.alg_bytes = static_cast<double>(x.num_elements()) + static_cast<double>(b) * uh * uw * ic;
+  sg->launches.push_back(Z);
+  // flipped, packed filters + folded bias (int8 filters: zero point 0)
+  const int K = kh * kw * ic;
+  int kp = 0, np = 0;
+  bh_conv_packed_geometry(oc, K, &kp, &np);
+  const size_t wbytes = static_cast<size_t>(kp) * np;
+  const size_t tbytes = 12ull * oc;
+  std::vector<int32_t> mult, shift;
+  ConvMultipliers(Scale(x), w.scale, oc, Scale(out), false, &mult, &shift);
+  auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
+  if (!blob) {
+    std::vector<int8_t> flipped(static_cast<size_t>(oc) * K);
+    for (int co = 0; co < oc; ++co)
+      for (int fy = 0; fy < kh; ++fy)
+        for (int fx = 0; fx < kw; ++fx)
+          for (int ci = 0; ci < ic; ++ci)
+            flipped[((static_cast<size_t>(co) * kh + fy) * kw + fx) * ic + ci] = static_cast<int8_t>(
+                w.data[((static_cast<size_t>(co) * kh + (kh - 1 - fy)) * kw + (kw - 1 - fx)) * ic + ci]);
+    std::vector<int8_t> packed(wbytes);
+    std::vector<int32_t> tables(3ull * oc);
+    if (bh_pack_conv_weights(flipped.data(), 1, oc, K, kp, np, bias, Zp(x), 0, packed.data(), tables.data()) != 0)
+      return absl::InternalError("weight packing failed");
+    std::copy(mult.begin(), mult.end(), tables.begin() + oc);
+    std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
+    blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
+    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
+        bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+      return HipErr(1, "upload transpose-conv operands");
+    DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
+  }
+  sg->consts.push_back(blob);
+  const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
+  bh_conv_params& p = L->conv;
+  p = bh_conv_params{};
+  p.batch = b; p.in_h = uh; p.in_w = uw; p.in_c = ic;
+  p.out_h = oh; p.out_w = ow; p.out_c = oc; p.k_h = kh; p.k_w = kw;
+  p.stride_h = 1; p.stride_w = 1; p.dil_h = 1; p.dil_w = 1;
+  p.pad_h = kh - 1 - ph; p.pad_w = kw - 1 - pw;
+  p.k_pad = kp; p.n_pad = np; p.in_xor = 0;
+  p.in_zp = Zp(x); p.w_zp = 0; p.out_zp = Zp(out); p.act_min = -128; p.act_max = 127;
+  p.input = scratch->ptr(); p.output = out_ptr;
+  p.weights = static_cast<const int8_t*>(blob->ptr());
+  p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+  L->kind = Launch::kConv;
+  L->kernel = (kh * kw * ic <= 64 && ic < 8) ? "conv_direct_kernel" : "conv_mfma_kernel";
+  const double M = static_cast<double>(b) * oh * ow;
+  L->alg_ops = 2.0 * M * oc * K;
+  L->alg_bytes = static_cast<double>(b) * uh * uw * ic + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
   return absl::OkStatus();
 }
 
@@ -1138,6 +1251,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.kind = Launch::kPool;
     L.kernel = "pool_kernel";
     L.alg_bytes = static_cast<double>(in.num_elements() + out.num_elements());
+  } else if (op.builtin == kTflTransposeConv) {
+    RETURN_STATUS_IF(LowerTransposeConv(model, oi, out_ptr, ckey, sg, &L));
   } else if (op.builtin != kTflReshape && op.builtin != kTflSqueeze) {
     RETURN_STATUS_IF(LowerGlue(model, oi, in_ptr, out_ptr, ckey, sg, &L));
   } else {  // RESHAPE / SQUEEZE: same bytes, new dims
@@ -1362,6 +1477,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kResizeNearest: rc = bh_resize_nearest(&l.rnear, stream_); break;
     case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
     case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
+    case Launch::kZeroInsert: rc = bh_zero_insert(&l.zi, stream_); break;
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }

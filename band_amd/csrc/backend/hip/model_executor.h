@@ -36,7 +36,7 @@ namespace hip {
 struct Launch {
   enum Kind {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
-    kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax
+    kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
@@ -51,6 +51,7 @@ struct Launch {
   bh_resize_nearest_params rnear{};
   bh_resize_bilinear_params rbil{};
   bh_softmax_params softmax{};
+  bh_zero_insert_params zi{};
   const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
   long count = 0;               // kLut* / kQuantF32: elements
   float q_scale = 0.f;          // kQuantF32
@@ -142,6 +143,8 @@ class HipModelExecutor : public interface::IModelExecutor {
   // across executors by `key`
   absl::Status UploadConst(const std::string& key, const void* data, size_t bytes, PreparedSubgraph* sg,
                            const void** dev);
+  absl::Status LowerTransposeConv(const HipModel& model, int op_index, void* out_ptr, const std::string& ckey,
+                                  PreparedSubgraph* sg, Launch* l);
   absl::Status LowerGlue(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,
                          PreparedSubgraph* sg, Launch* l);
   absl::Status Enqueue(PreparedSubgraph* sg);

@@ -189,6 +189,35 @@ __global__ __launch_bounds__(256) void softmax_kernel(bh_softmax_params p) {
   }
 }
 
+// ---- zero insertion (TRANSPOSE_CONV as a stride-1 conv) -------------------
+struct ZiDivs {
+  FastDiv units, ow, oh, sh, sw;
+};
+
+// one thread per (U pixel, UNIT bytes of its channels)
+template <int UNIT>
+__global__ __launch_bounds__(256) void zero_insert_kernel(bh_zero_insert_params p, ZiDivs dv, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t pix = dv.units.div((uint32_t)i);
+  const int u = (int)(i - (long)pix * dv.units.d);
+  const uint32_t t = dv.ow.div(pix);
+  const int x = (int)(pix - t * p.out_w);
+  const uint32_t n = dv.oh.div(t);
+  const int y = (int)(t - n * p.out_h);
+  const uint32_t iy = dv.sh.div((uint32_t)y), ix = dv.sw.div((uint32_t)x);
+  const bool hit = (int)iy * p.stride_h == y && (int)ix * p.stride_w == x;
+  if constexpr (UNIT == 4) {
+    uint32_t v = p.fill * 0x01010101u;
+    if (hit) v = ((const uint32_t*)p.input)[(((long)n * p.in_h + iy) * p.in_w + ix) * dv.units.d + u];
+    ((uint32_t*)p.output)[i] = v;
+  } else {
+    uint8_t v = (uint8_t)p.fill;
+    if (hit) v = ((const uint8_t*)p.input)[(((long)n * p.in_h + iy) * p.in_w + ix) * p.channels + u];
+    ((uint8_t*)p.output)[i] = v;
+  }
+}
+
 inline unsigned blocks(long n) { return (unsigned)((n + 255) / 256); }
 
 }  // namespace bh
@@ -346,4 +375,32 @@ extern "C" int bh_softmax_i8(const bh_softmax_params* pp, bh_stream_t s) {
   if (pp->rows == 0) return 0;
   hipLaunchKernelGGL(bh::softmax_kernel, dim3(bh::blocks(pp->rows)), dim3(256), 0, (hipStream_t)s, *pp);
   return bh_check_launch("softmax_kernel");
+}
+
+extern "C" int bh_zero_insert(const bh_zero_insert_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || pp->batch <= 0 || pp->channels <= 0 || pp->stride_h <= 0 ||
+      pp->stride_w <= 0 || pp->out_h != (pp->in_h - 1) * pp->stride_h + 1 ||
+      pp->out_w != (pp->in_w - 1) * pp->stride_w + 1) {
+    bh_set_last_error("bh_zero_insert: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_zero_insert_params& p = *pp;
+  const long pixels = (long)p.batch * p.out_h * p.out_w;
+  if (pixels * p.channels >= INT32_MAX) {
+    bh_set_last_error("bh_zero_insert: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  const bool v4 = p.channels % 4 == 0 && (uintptr_t)p.input % 4 == 0 && (uintptr_t)p.output % 4 == 0;
+  bh::ZiDivs dv;
+  dv.units = bh::FastDiv(v4 ? p.channels / 4 : p.channels);
+  dv.ow = bh::FastDiv(p.out_w);
+  dv.oh = bh::FastDiv(p.out_h);
+  dv.sh = bh::FastDiv(p.stride_h);
+  dv.sw = bh::FastDiv(p.stride_w);
+  const long total = pixels * dv.units.d;
+  if (v4)
+    hipLaunchKernelGGL(bh::zero_insert_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  else
+    hipLaunchKernelGGL(bh::zero_insert_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  return bh_check_launch("zero_insert_kernel");
 }

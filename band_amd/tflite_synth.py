@@ -23,12 +23,14 @@ ACT = {"NONE": 0, "RELU": 1, "RELU_N1_TO_1": 2, "RELU6": 3}
 OPC = dict(ADD=0, AVERAGE_POOL_2D=1, CONCATENATION=2, CONV_2D=3, DEPTHWISE_CONV_2D=4,
            FULLY_CONNECTED=9, LOGISTIC=14, MAX_POOL_2D=17, MUL=18, RESHAPE=22,
            RESIZE_BILINEAR=23, SOFTMAX=25, CUSTOM=32, PAD=34, SUB=41, QUANTIZE=114,
-           DEQUANTIZE=6, RELU=19, RELU_N1_TO_1=20, RELU6=21, PADV2=60, RESIZE_NEAREST_NEIGHBOR=97)
+           DEQUANTIZE=6, RELU=19, RELU_N1_TO_1=20, RELU6=21, PADV2=60, RESIZE_NEAREST_NEIGHBOR=97,
+           TRANSPOSE_CONV=67)
 # BuiltinOptions union indices
 OPT = dict(Conv2DOptions=1, DepthwiseConv2DOptions=2, Pool2DOptions=5, FullyConnectedOptions=8,
            SoftmaxOptions=9, ConcatenationOptions=10, AddOptions=11, ReshapeOptions=17,
            ResizeBilinearOptions=15, MulOptions=21, PadOptions=22, SubOptions=28,
-           DequantizeOptions=38, PadV2Options=43, ResizeNearestNeighborOptions=74, QuantizeOptions=89)
+           DequantizeOptions=38, PadV2Options=43, TransposeConvOptions=49, ResizeNearestNeighborOptions=74,
+           QuantizeOptions=89)
 
 
 # ---------------------------------------------------------------------------
@@ -461,6 +463,25 @@ class QGraph:
         else:
             opt = Table().set(0, "b", int(align_corners)).set(1, "b", int(half_pixel_centers))
             self.mb.op("RESIZE_NEAREST_NEIGHBOR", [x, st], [y], OPT["ResizeNearestNeighborOptions"], opt)
+        return y
+
+    def transpose_conv(self, x, out_c, k=3, stride=2, padding="SAME", bias=True):
+        """TRANSPOSE_CONV (int8 per-channel): output = input * stride (SAME)
+        or (input - 1) * stride + k (VALID)"""
+        shp, s_in, _ = self.meta[x]
+        b, h, w, c = shp
+        oh = h * stride if padding == "SAME" else (h - 1) * stride + k
+        ow = w * stride if padding == "SAME" else (w - 1) * stride + k
+        s_out, zp = float(s_in) * 1.5, self._act_zp()
+        K = max(1, k * k * c // (stride * stride))
+        wt, ws = self._weights([out_c, k, k, c], out_c, 0, s_in, s_out, K)
+        shape_t = self.mb.tensor(self._name("out_shape"), [4], np.int32, data=np.array([b, oh, ow, out_c], np.int32))
+        ins = [shape_t, wt, x]
+        if bias:
+            ins.append(self._bias(out_c, s_in, ws, K))
+        y = self.act_tensor([b, oh, ow, out_c], s_out, zp)
+        opt = Table().set(0, "b", 0 if padding == "SAME" else 1).set(1, "i", stride).set(2, "i", stride)
+        self.mb.op("TRANSPOSE_CONV", ins, [y], OPT["TransposeConvOptions"], opt)
         return y
 
     def dequantize(self, x):

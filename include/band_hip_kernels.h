@@ -27,6 +27,7 @@
  *   bh_resize_nearest <- RESIZE_NEAREST_NEIGHBOR (reference_ops::ResizeNearestNeighbor)
  *   bh_resize_bilinear_i8 <- RESIZE_BILINEAR int8 (reference_ops::ResizeBilinearInteger)
  *   bh_softmax_i8     <- SOFTMAX 8-bit      (optimized_ops::Softmax, lookup-table path)
+ *   bh_zero_insert + bh_conv2d_i8 <- TRANSPOSE_CONV int8 (reference_integer_ops::TransposeConv)
  *
  * Quantised tensors live on the device as raw bytes in their TFLite type
  * (int8 or uint8).  Kernels work in the "int8 domain": a uint8 input is
@@ -340,6 +341,18 @@ typedef struct {
   void* output;
 } bh_softmax_params;
 int bh_softmax_i8(const bh_softmax_params* p, bh_stream_t s);
+
+/* TRANSPOSE_CONV support: U[y*sh][x*sw][:] = in[y][x][:], every other
+ * position of U (out_h x out_w = (in-1)*stride+1) holds `fill` (the input
+ * zero point, so it contributes 0).  A transpose conv is then a stride-1
+ * CONV_2D over U with spatially flipped filters and padding k-1-pad. */
+typedef struct {
+  int batch, in_h, in_w, channels, stride_h, stride_w, out_h, out_w;
+  uint32_t fill;                  /* byte */
+  const void* input;
+  void* output;
+} bh_zero_insert_params;
+int bh_zero_insert(const bh_zero_insert_params* p, bh_stream_t s);
 
 /* human-readable name of the last error set on this thread */
 const char* bh_last_error(void);

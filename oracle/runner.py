@@ -63,6 +63,8 @@ def lib():
         L.tfl_lookup.argtypes = [vp, c_l, vp, vp]
         L.tfl_softmax.argtypes = [vp, c_i, c_l, c_i, c_f, c_f, c_f, c_i32, vp]
         L.tfl_softmax_table.argtypes = [c_f, c_f, vp]
+        L.tfl_transpose_conv_i8.argtypes = [vp, c_i, c_i, c_i, c_i, vp, c_i, c_i, c_i, vp, vp, c_i, c_i, c_i, c_i,
+                                            c_i, c_i, c_i32, c_i32, vp, vp]
         L.tfl_concat.argtypes = [c_i, ctypes.POINTER(vp), P_I32, c_l, c_l, P_F32, P_I32, c_f, c_i32, c_i, vp]
         L.tfl_pad.argtypes = [vp, P_I32, P_I32, ctypes.c_uint8, vp]
         L.tfl_nearest_index.restype = c_i
@@ -300,6 +302,21 @@ def softmax(x, *, in_scale, beta, out_scale, out_zp):
     return out
 
 
+def transpose_conv_i8(x, w, bias, *, in_zp, out_zp, mult, shift, stride, pad, out_hw):
+    x = np.ascontiguousarray(x, np.int8)
+    w = np.ascontiguousarray(w, np.int8)
+    b, ih, iw, ic = x.shape
+    oc, kh, kw, _ = w.shape
+    out = np.zeros((b, out_hw[0], out_hw[1], oc), np.int8)
+    bias = None if bias is None else np.ascontiguousarray(bias, np.int32)
+    m = np.ascontiguousarray(mult, np.int32)
+    s = np.ascontiguousarray(shift, np.int32)
+    lib().tfl_transpose_conv_i8(_vp(x), b, ih, iw, ic, _vp(w), oc, kh, kw, None if bias is None else _vp(bias),
+                                _vp(out), out_hw[0], out_hw[1], stride[0], stride[1], pad[0], pad[1], -in_zp,
+                                out_zp, _vp(m), _vp(s))
+    return out
+
+
 def softmax_table(in_scale, beta):
     t = np.zeros(256, np.float32)
     lib().tfl_softmax_table(in_scale, beta, _vp(t))
@@ -382,7 +399,7 @@ class OracleInterpreter:
                  OP["MAX_POOL_2D"], OP["RESHAPE"], OP["SQUEEZE"], OP["CONCATENATION"], OP["PAD"],
                  OP["PADV2"], OP["QUANTIZE"], OP["DEQUANTIZE"], OP["RELU"], OP["RELU6"],
                  OP["RELU_N1_TO_1"], OP["LOGISTIC"], OP["SOFTMAX"], OP["RESIZE_NEAREST_NEIGHBOR"],
-                 OP["RESIZE_BILINEAR"]}
+                 OP["RESIZE_BILINEAR"], OP["TRANSPOSE_CONV"]}
 
     def __init__(self, model):
         self.model = model if isinstance(model, Model) else Model.from_path(model)
@@ -498,6 +515,23 @@ class OracleInterpreter:
                            out_hw=(oh, ow), amin=amin, amax=amax)]
         if code in (OP["RESHAPE"], OP["SQUEEZE"]):
             return [vals[o.inputs[0]].copy()]
+        if code == OP["TRANSPOSE_CONV"]:
+            # inputs: output_shape, weights (OHWI), input, [bias]
+            w, x = vals[o.inputs[1]], vals[o.inputs[2]]
+            tw, tx, to = T[o.inputs[1]], T[o.inputs[2]], T[o.outputs[0]]
+            bias = vals.get(o.inputs[3]) if len(o.inputs) > 3 and o.inputs[3] >= 0 else None
+            if tx.np_dtype != np.int8:
+                raise NotImplementedError("oracle: TRANSPOSE_CONV restated for int8 only")
+            same = opt.scalar(0, "b", 0) == 0
+            sw, sh = opt.scalar(1, "i", 1), opt.scalar(2, "i", 1)
+            oh, ow = to.shape[1], to.shape[2]
+            kh, kw = w.shape[1], w.shape[2]
+            # transpose_conv.cc: padding as for a conv whose input is the output
+            ph = padding(sh, 1, oh, kh, out_size(same, oh, kh, sh, 1))
+            pw = padding(sw, 1, ow, kw, out_size(same, ow, kw, sw, 1))
+            mult, shift = conv_multipliers(_q(tx)[0], tw.scale, w.shape[0], _q(to)[0], False)
+            return [transpose_conv_i8(x, w, bias, in_zp=_q(tx)[1], out_zp=_q(to)[1], mult=mult, shift=shift,
+                                      stride=(sh, sw), pad=(ph, pw), out_hw=(oh, ow))]
         x = vals[o.inputs[0]]
         ti, to = T[o.inputs[0]], T[o.outputs[0]]
         if code == OP["CONCATENATION"]:

@@ -560,3 +560,38 @@ void tfl_softmax_table(float in_scale, float beta, float* table) {
   const float scale = -in_scale * beta;
   for (int32_t val = 0; val <= 255; ++val) table[255 - val] = expf(scale * (float)val);
 }
+
+/* reference_integer_ops::TransposeConv (int8 per-channel), TFLite 2.9.2:
+ * zeroed int32 scratch, scatter of (x + input_offset) * w over every
+ * (input pixel, filter tap, out channel) that lands inside the output, then
+ * bias + MultiplyByQuantizedMultiplier per channel + zp, clamped to int8.
+ * Filter OHWI [oc][kh][kw][ic]; padding from padding.h computed with the
+ * output as the conv input (transpose_conv.cc). */
+void tfl_transpose_conv_i8(const int8_t* in, int b, int ih, int iw, int ic, const int8_t* w, int oc, int kh,
+                           int kw, const int32_t* bias, int8_t* out, int oh, int ow, int sh, int sw, int ph,
+                           int pw, int32_t input_offset, int32_t out_zp, const int32_t* mult, const int32_t* shift) {
+  long n = (long)b * oh * ow * oc;
+  int32_t* acc = (int32_t*)calloc((size_t)n, sizeof(int32_t));
+  for (int bb = 0; bb < b; ++bb)
+    for (int y = 0; y < ih; ++y)
+      for (int x = 0; x < iw; ++x)
+        for (int ci = 0; ci < ic; ++ci) {
+          const int oy0 = y * sh - ph, ox0 = x * sw - pw;
+          const int32_t v = (int32_t)in[(((long)bb * ih + y) * iw + x) * ic + ci] + input_offset;
+          for (int fy = 0; fy < kh; ++fy)
+            for (int fx = 0; fx < kw; ++fx)
+              for (int co = 0; co < oc; ++co) {
+                const int oy = oy0 + fy, ox = ox0 + fx;
+                if (oy >= 0 && oy < oh && ox >= 0 && ox < ow)
+                  acc[(((long)bb * oh + oy) * ow + ox) * oc + co] +=
+                      v * (int32_t)w[(((long)co * kh + fy) * kw + fx) * ic + ci];
+              }
+        }
+  for (long i = 0; i < n; ++i) {
+    const int co = (int)(i % oc);
+    int32_t a = acc[i] + (bias ? bias[co] : 0);
+    a = tfl_mbqm(a, mult[co], shift[co]) + out_zp;
+    out[i] = (int8_t)clampi(a, -128, 127);
+  }
+  free(acc);
+}

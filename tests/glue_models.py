@@ -37,3 +37,18 @@ def fpn(dtype, seed=5):
     r = g.add(g.conv(p, 16, k=1, act="NONE"), p)             # residual that can fuse
     g.output(r)
     return g.build()
+
+
+def tconv_zoo(seed=7):
+    """TRANSPOSE_CONV variants (int8): stride 2 / 1 / 3, SAME / VALID, with and
+    without bias, odd spatial sizes and channel counts"""
+    g = QGraph(np.int8, seed=seed, name="tconv_zoo")
+    x = g.input([1, 5, 7, 12], scale=0.05)
+    a = g.transpose_conv(x, 16, k=3, stride=2, padding="SAME")
+    b = g.transpose_conv(a, 8, k=2, stride=2, padding="VALID", bias=False)
+    c = g.transpose_conv(x, 5, k=3, stride=1, padding="SAME")
+    d = g.transpose_conv(x, 6, k=4, stride=3, padding="VALID")
+    g.output(b)
+    g.output(c)
+    g.output(d)
+    return g.build()

@@ -200,9 +200,9 @@ def _run_model(buf, mid, feed_seed=0, all_tensors=True):
         tt = om.tensors[t]
         feed[t] = rand_q(rng, tt.shape, tt.np_dtype)
         ex.GetTensorView(key, t).GetData()[...] = feed[t]
+    ref = OracleInterpreter(om).run(feed)
     for _ in range(2):  # eager, then captured graph
         assert ex.ExecuteSubgraph(key).ok()
-        ref = OracleInterpreter(om).run(feed)
         for t in inter:
             np.testing.assert_array_equal(views[t].GetData(), ref[t].reshape(views[t].GetDims()),
                                           err_msg="tensor %d (%s)" % (t, om.tensors[t].name))
@@ -233,3 +233,37 @@ def test_retinaface_whole_model(gpu_lib, golden_dir, all_tensors):
     with open(os.path.join(golden_dir, "retinaface_mbv2_quant_160.tflite"), "rb") as f:
         buf = f.read()
     _run_model(buf, 45 + int(all_tensors), all_tensors=all_tensors)
+
+
+def test_zero_insert(gpu_lib):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(9)
+    for shape, (sh, sw), fill in (((2, 5, 7, 8), (2, 2), -3), ((1, 4, 3, 5), (3, 2), 17)):
+        x = rand_q(rng, shape, np.int8)
+        b, ih, iw, c = shape
+        uh, uw = (ih - 1) * sh + 1, (iw - 1) * sw + 1
+        ref = np.full((b, uh, uw, c), fill, np.int8)
+        ref[:, ::sh, ::sw, :] = x
+        dx, dy = _dev(x), DeviceBuffer(ref.nbytes)
+        p = _abi.ZeroInsertParams(batch=b, in_h=ih, in_w=iw, channels=c, stride_h=sh, stride_w=sw, out_h=uh,
+                                  out_w=uw, fill=fill & 0xff, input=dx.value, output=dy.value)
+        _check(gpu_lib.bh_zero_insert(ctypes.byref(p), None), "zero_insert")
+        np.testing.assert_array_equal(dy.download(np.int8, ref.shape), ref)
+
+
+@pytest.mark.parametrize("all_tensors", [True, False])
+def test_transpose_conv_models(gpu_lib, all_tensors):
+    """TRANSPOSE_CONV as zero insertion + stride-1 MFMA conv with flipped
+    filters, against the oracle's restatement of TFLite's scatter kernel"""
+    from tests.glue_models import tconv_zoo
+    _run_model(tconv_zoo(), 50 + int(all_tensors), all_tensors=all_tensors)
+
+
+@pytest.mark.parametrize("all_tensors", [True, False])
+def test_icn_whole_model(gpu_lib, golden_dir, all_tensors):
+    """The reference's int8 ICN (47 CONV_2D, 22 ADD, 4 TRANSPOSE_CONV,
+    DEPTHWISE, QUANTIZE, CONCATENATION) runs whole on the GPU"""
+    with open(os.path.join(golden_dir, "ICN_quant.tflite"), "rb") as f:
+        buf = f.read()
+    _run_model(buf, 52 + int(all_tensors), all_tensors=all_tensors)

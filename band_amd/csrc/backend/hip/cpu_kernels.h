@@ -1,0 +1,78 @@
+// Host execution of the lowered launch program for kCPU workers.
+//
+// Band runs a model on a CPU worker when the configuration has one (C1:
+// MobileNetV1 on 1 CPU worker) and places the ops the GPU cannot run on it
+// when the model analyzer splits a model (band/model_analyzer.cc:484-606).
+// A kCPU HipModelExecutor lowers its subgraph exactly as a kGPU one does
+// (same packed operands, folded biases, requantisation tables and epilogue
+// fusions, all in host memory) and runs every launch here, with the
+// TFLite 2.9.2 integer arithmetic the HIP kernels implement.  This is the CPU
+// *device* of the backend, not a fallback of the GPU path: a kGPU executor
+// never calls into this file.
+#pragma once
+
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+#include "band_hip_kernels.h"
+
+namespace band {
+namespace hip {
+
+// A fixed pool of worker threads (the executor's num_threads; the calling
+// thread is one of them) running ParallelFor over index ranges.
+class CpuPool {
+ public:
+  explicit CpuPool(int num_threads);
+  ~CpuPool();
+  CpuPool(const CpuPool&) = delete;
+  CpuPool& operator=(const CpuPool&) = delete;
+  int size() const { return static_cast<int>(threads_.size()) + 1; }
+  // fn(begin, end) over [0, n) split into contiguous chunks
+  void ParallelFor(long n, const std::function<void(long, long)>& fn);
+
+ private:
+  void Loop(int id);
+  std::vector<std::thread> threads_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(long, long)>* job_ = nullptr;
+  long n_ = 0;
+  int generation_ = 0;
+  int pending_ = 0;
+  bool stop_ = false;
+};
+
+// the launch kinds of model_executor.h with their host implementations
+void CpuConv(const bh_conv_params& p, CpuPool& pool);
+void CpuDwConv(const bh_dwconv_params& p, CpuPool& pool);
+void CpuFc(const bh_fc_params& p, CpuPool& pool);
+void CpuEltwise(const bh_eltwise_params& p, CpuPool& pool);
+void CpuPool2D(const bh_pool_params& p, CpuPool& pool);
+void CpuLutU8(const void* in, void* out, long n, const uint8_t* table);
+void CpuLutF32(const void* in, float* out, long n, const float* table);
+void CpuQuantizeF32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed);
+void CpuConcat(const bh_concat_params& p);
+void CpuPad(const bh_pad_params& p);
+void CpuResizeNearest(const bh_resize_nearest_params& p);
+void CpuResizeBilinear(const bh_resize_bilinear_params& p);
+void CpuSoftmax(const bh_softmax_params& p);
+void CpuZeroInsert(const bh_zero_insert_params& p);
+
+// float32 elementwise ADD / SUB / MUL with 4-D broadcast and a fused
+// activation clamp (kernels/add.cc float path); CPU-only
+struct CpuEltwiseF32 {
+  int kind;  // 0 add, 1 sub, 2 mul
+  int shape_a[4], shape_b[4], shape_o[4];
+  float act_min, act_max;
+  const float* a;
+  const float* b;
+  float* out;
+};
+void CpuEltwiseFloat(const CpuEltwiseF32& p);
+
+}  // namespace hip
+}  // namespace band

@@ -1,18 +1,36 @@
 #include "backend/hip/device.h"
 
+#include <cstdlib>
 #include <cstring>
 
 namespace band {
 namespace hip {
 
 DeviceBlob::DeviceBlob(int ordinal, size_t bytes) : bytes_(bytes), ordinal_(ordinal) {
+  if (ordinal < 0) {
+    const size_t n = ((bytes ? bytes : 16) + 63) / 64 * 64;
+    ptr_ = std::aligned_alloc(64, n);
+    if (ptr_) std::memset(ptr_, 0, n);
+    return;
+  }
   if (bh_set_device(ordinal) == 0 && bh_malloc(&ptr_, bytes ? bytes : 16) != 0) ptr_ = nullptr;
 }
 DeviceBlob::~DeviceBlob() {
-  if (ptr_) {
-    bh_set_device(ordinal_);
-    bh_free(ptr_);
+  if (!ptr_) return;
+  if (ordinal_ < 0) {
+    std::free(ptr_);
+    return;
   }
+  bh_set_device(ordinal_);
+  bh_free(ptr_);
+}
+bool DeviceBlob::Upload(size_t offset, const void* src, size_t bytes) {
+  if (!ptr_ || offset + bytes > (bytes_ ? bytes_ : 16)) return false;
+  if (ordinal_ < 0) {
+    std::memcpy(static_cast<char*>(ptr_) + offset, src, bytes);
+    return true;
+  }
+  return bh_set_device(ordinal_) == 0 && bh_memcpy_h2d(static_cast<char*>(ptr_) + offset, src, bytes) == 0;
 }
 
 PinnedBuffer::PinnedBuffer(size_t bytes, bool pinned) : bytes_(bytes), pinned_(pinned) {

@@ -23,7 +23,8 @@
 namespace band {
 namespace hip {
 
-// RAII device allocation.
+// RAII device allocation; ordinal < 0 is host memory (the operands and
+// arena of a kCPU executor, see cpu_kernels.h).
 class DeviceBlob {
  public:
   DeviceBlob(int ordinal, size_t bytes);
@@ -34,6 +35,9 @@ class DeviceBlob {
   size_t bytes() const { return bytes_; }
   int ordinal() const { return ordinal_; }
   bool ok() const { return ptr_ != nullptr; }
+  bool host() const { return ordinal_ < 0; }
+  // copies host bytes into the blob at `offset` (H2D for device blobs)
+  bool Upload(size_t offset, const void* src, size_t bytes);
 
  private:
   void* ptr_ = nullptr;

@@ -1,6 +1,7 @@
 #include "backend/hip/model_executor.h"
 
 #include <algorithm>
+#include <limits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -59,6 +60,9 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   if (device_flag_ == DeviceFlag::kGPU && DeviceRegistry::Get().GpuAvailable()) {
     ordinal_ = DeviceRegistry::Get().OrdinalForWorker(worker_id_);
     stream_ = DeviceRegistry::Get().StreamForWorker(worker_id_);
+  } else if (device_flag_ == DeviceFlag::kCPU) {
+    // host execution of the lowered program (cpu_kernels.h)
+    cpu_pool_ = std::make_unique<CpuPool>(num_threads_ > 0 ? num_threads_ : 1);
   }
   const char* g = std::getenv("BAND_HIP_GRAPH");
   if (g && g[0] == '0') use_graph_ = false;
@@ -207,6 +211,28 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
   }
 }
 
+bool HipModelExecutor::CpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
+  if (GpuSupports(m, op, nullptr)) return true;
+  auto T = [&](int i) -> const TflTensor& { return m.tensors[i]; };
+  if ((op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) && op.inputs.size() == 2 &&
+      op.inputs[0] >= 0 && op.inputs[1] >= 0 && !op.outputs.empty()) {
+    const TflTensor& a = T(op.inputs[0]);
+    const TflTensor& b = T(op.inputs[1]);
+    const TflTensor& o = T(op.outputs[0]);
+    if (a.type == DataType::kFloat32 && b.type == DataType::kFloat32 && o.type == DataType::kFloat32 &&
+        a.shape.size() <= 4 && b.shape.size() <= 4 && o.shape.size() <= 4) {
+      int sa[4], sb[4], so[4];
+      Shape4(a.shape, sa);
+      Shape4(b.shape, sb);
+      Shape4(o.shape, so);
+      bool ok = true;
+      for (int d = 0; d < 4; ++d) ok &= (sa[d] == so[d] || sa[d] == 1) && (sb[d] == so[d] || sb[d] == 1);
+      if (ok) return true;
+    }
+  }
+  return GpuSupports(m, op, why);
+}
+
 absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (!meta_.empty()) return absl::OkStatus();
   const TflModel& d = model.desc();
@@ -274,6 +300,8 @@ absl::StatusOr<ModelSpec> HipModelExecutor::InvestigateModelSpec(interface::IMod
     for (int i = 0; i < num_ops; ++i)
       if (!GpuSupports(d, d.ops[i], nullptr)) unsupported[flag].insert(i);
   }
+  for (int i = 0; i < num_ops; ++i)
+    if (!CpuSupports(d, d.ops[i], nullptr)) unsupported[DeviceFlag::kCPU].insert(i);
   ModelSpec spec(num_ops, static_cast<int>(d.tensors.size()), tensor_types,
                  std::set<int>(d.inputs.begin(), d.inputs.end()),
                  std::set<int>(d.outputs.begin(), d.outputs.end()), op_in, op_out, unsupported, unavailable);
@@ -293,7 +321,7 @@ absl::Status HipModelExecutor::DevicePtr(const HipModel& model, int t, PreparedS
   auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
   if (!blob) {
     blob = std::make_shared<DeviceBlob>(ordinal_, tt.data_size);
-    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), tt.data, tt.data_size) != 0)
+    if (!blob->ok() || !blob->Upload(0, tt.data, tt.data_size))
       return HipErr(1, "upload constant");
     DeviceRegistry::Get().PutConst(ordinal_, key, blob);
   }
@@ -307,7 +335,7 @@ absl::Status HipModelExecutor::UploadConst(const std::string& key, const void* d
   auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
   if (!blob) {
     blob = std::make_shared<DeviceBlob>(ordinal_, bytes);
-    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), data, bytes) != 0) return HipErr(1, "upload table");
+    if (!blob->ok() || !blob->Upload(0, data, bytes)) return HipErr(1, "upload table");
     DeviceRegistry::Get().PutConst(ordinal_, key, blob);
   }
   sg->consts.push_back(blob);
@@ -384,8 +412,8 @@ absl::Status HipModelExecutor::LowerTransposeConv(const HipModel& model, int oi,
     std::copy(mult.begin(), mult.end(), tables.begin() + oc);
     std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
     blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-    if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
-        bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+    if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
+        !blob->Upload(wbytes, tables.data(), tbytes))
       return HipErr(1, "upload transpose-conv operands");
     DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
   }
@@ -614,7 +642,8 @@ absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubg
     if (sg->fused_ops.count(i)) continue;
     RETURN_STATUS_IF(Lower(model, i, sg));
   }
-  if (allow_fusion_ && allow_irb_) FuseBlocks(model, sg);
+  // fused blocks are GPU kernels picked by on-device timing
+  if (allow_fusion_ && allow_irb_ && device_flag_ == DeviceFlag::kGPU) FuseBlocks(model, sg);
   if (allow_fusion_) FuseGlue(model, sg);
   return absl::OkStatus();
 }
@@ -1034,9 +1063,10 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
   const TflModel& d = model.desc();
   const TflOperator& op = d.ops[oi];
   std::string why;
-  if (!GpuSupports(d, op, &why))
+  const bool cpu = device_flag_ == DeviceFlag::kCPU;
+  if (!(cpu ? CpuSupports(d, op, &why) : GpuSupports(d, op, &why)))
     return absl::InternalError("HIP backend cannot run op " + std::to_string(oi) + " (" +
-                               TflBuiltinName(op.builtin) + "): " + why);
+                               TflBuiltinName(op.builtin) + ") on " + ToString(device_flag_) + ": " + why);
   auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
   const TflTensor& in = T(op.inputs[0]);
   const TflTensor& out = T(op.outputs[0]);
@@ -1091,8 +1121,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
         std::copy(mult.begin(), mult.end(), tables.begin() + oc);
         std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
         blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-        if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
-            bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+        if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
+            !blob->Upload(wbytes, tables.data(), tbytes))
           return HipErr(1, "upload conv operands");
         DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
       }
@@ -1129,8 +1159,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
         std::copy(mult.begin(), mult.end(), tables.begin() + oc);
         std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
         blob = std::make_shared<DeviceBlob>(ordinal_, wpad + tbytes);
-        if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), wd.data(), wpad) != 0 ||
-            bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wpad, tables.data(), tbytes) != 0)
+        if (!blob->ok() || !blob->Upload(0, wd.data(), wpad) ||
+            !blob->Upload(wpad, tables.data(), tbytes))
           return HipErr(1, "upload depthwise operands");
         DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
       }
@@ -1182,8 +1212,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
         tables[2 * units + u] = shift;
       }
       blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-      if (!blob->ok() || bh_memcpy_h2d(blob->ptr(), packed.data(), wbytes) != 0 ||
-          bh_memcpy_h2d(static_cast<char*>(blob->ptr()) + wbytes, tables.data(), tbytes) != 0)
+      if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
+          !blob->Upload(wbytes, tables.data(), tbytes))
         return HipErr(1, "upload fc operands");
       DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
     }
@@ -1201,6 +1231,25 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.alg_ops = 2.0 * rows * units * depth;
     L.alg_bytes = static_cast<double>(rows) * depth + static_cast<double>(rows) * units +
                   static_cast<double>(units) * depth + 12.0 * units;
+  } else if ((op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) &&
+             in.type == DataType::kFloat32) {
+    // float graph on the CPU worker (add.cc float path, fused activation)
+    const TflTensor& b = T(op.inputs[1]);
+    void* b_ptr = nullptr;
+    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
+    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
+    CpuEltwiseF32& p = L.eltf;
+    p.kind = op.builtin == kTflAdd ? 0 : (op.builtin == kTflSub ? 1 : 2);
+    Shape4(in.shape, p.shape_a);
+    Shape4(b.shape, p.shape_b);
+    Shape4(out.shape, p.shape_o);
+    p.act_min = act == 1 || act == 3 ? 0.f : (act == 2 ? -1.f : -std::numeric_limits<float>::infinity());
+    p.act_max = act == 3 ? 6.f : (act == 2 ? 1.f : std::numeric_limits<float>::infinity());
+    p.a = static_cast<const float*>(in_ptr);
+    p.b = static_cast<const float*>(b_ptr);
+    p.out = static_cast<float*>(out_ptr);
+    L.kind = Launch::kEltwiseF32;
+    L.kernel = "eltwise_f32_host";
   } else if (op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) {
     const TflTensor& b = T(op.inputs[1]);
     void* b_ptr = nullptr;
@@ -1338,15 +1387,18 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
 
   // host-pinned boundary mirrors (Band memcpy's job I/O through these)
   const bool pinned = device_flag_ == DeviceFlag::kGPU;
+  const bool cpu = device_flag_ == DeviceFlag::kCPU;
   for (int t : sg->inputs) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
   for (int t : sg->outputs)
     if (!sg->host.count(t)) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
   for (auto& kv : sg->host)
     if (!kv.second->ok()) return absl::InternalError("pinned host allocation failed");
 
-  if (device_flag_ == DeviceFlag::kGPU) {
-    if (ordinal_ < 0 || !stream_) return absl::InternalError("Failed to create HIP executor: no gfx950 device");
-    if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
+  if (device_flag_ == DeviceFlag::kGPU || cpu) {
+    if (!cpu) {
+      if (ordinal_ < 0 || !stream_) return absl::InternalError("Failed to create HIP executor: no gfx950 device");
+      if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
+    }
     // RESHAPE / SQUEEZE outputs alias their input's slot (same bytes, and
     // every tensor is immutable once produced), so they cost no launch.
     std::map<int, int> alias;
@@ -1367,9 +1419,9 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
     }
     for (const auto& kv : alias) sg->offset[kv.first] = sg->offset.at(kv.second);
     sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
-    if (!sg->arena->ok()) return absl::InternalError("HBM arena allocation failed");
+    if (!sg->arena->ok()) return absl::InternalError("arena allocation failed");
     RETURN_STATUS_IF(BuildLaunches(*hm, sg.get()));
-  } else if (device_flag_ != DeviceFlag::kCPU) {
+  } else {
     return absl::InternalError(std::string("Unsupported device type ") + ToString(device_flag_));
   }
   SubgraphKey key(model->GetId(), worker_id_, unit_indices);
@@ -1433,14 +1485,14 @@ std::shared_ptr<interface::ITensorView> HipModelExecutor::GetTensorView(const Su
   const TflTensor& t = model_->desc().tensors[index];
   if (t.is_const())
     return std::make_shared<HipTensorView>(m, const_cast<char*>(reinterpret_cast<const char*>(t.data)));
-  if (device_flag_ == DeviceFlag::kGPU && sg->offset.count(index)) {
+  if ((device_flag_ == DeviceFlag::kGPU || device_flag_ == DeviceFlag::kCPU) && sg->offset.count(index)) {
     // an intermediate of this subgraph: mirror it and copy it back on every run
     auto buf = std::make_unique<PinnedBuffer>(m->bytes);
     if (!buf->ok()) return nullptr;
     char* data = buf->data();
     sg->host[index] = std::move(buf);
     sg->extra_d2h.insert(index);
-    bh_set_device(ordinal_);
+    if (ordinal_ >= 0) bh_set_device(ordinal_);
     if (sg->graph) {
       bh_graph_destroy(sg->graph);
       sg->graph = nullptr;
@@ -1478,6 +1530,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
     case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
     case Launch::kZeroInsert: rc = bh_zero_insert(&l.zi, stream_); break;
+    case Launch::kEltwiseF32: return absl::InternalError("float eltwise is a CPU-worker op");
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }
@@ -1500,11 +1553,49 @@ absl::Status HipModelExecutor::Enqueue(PreparedSubgraph* sg) {
   return absl::OkStatus();
 }
 
+// kCPU worker: the same launch program over host memory (cpu_kernels.h)
+absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
+  char* arena = static_cast<char*>(sg->arena->ptr());
+  for (int t : sg->inputs) std::memcpy(arena + sg->offset.at(t), sg->host.at(t)->data(), meta_[t]->bytes);
+  CpuPool& pool = *cpu_pool_;
+  for (const Launch& l : sg->launches) {
+    switch (l.kind) {
+      case Launch::kConv: CpuConv(l.conv, pool); break;
+      case Launch::kDwConv: CpuDwConv(l.dw, pool); break;
+      case Launch::kFc: CpuFc(l.fc, pool); break;
+      case Launch::kEltwise: CpuEltwise(l.elt, pool); break;
+      case Launch::kPool: CpuPool2D(l.pool, pool); break;
+      case Launch::kCopy:
+        if (l.src != l.dst) std::memmove(l.dst, l.src, l.bytes);
+        break;
+      case Launch::kLutU8: CpuLutU8(l.src, l.dst, l.count, static_cast<const uint8_t*>(l.table)); break;
+      case Launch::kLutF32:
+        CpuLutF32(l.src, static_cast<float*>(l.dst), l.count, static_cast<const float*>(l.table));
+        break;
+      case Launch::kQuantF32:
+        CpuQuantizeF32(static_cast<const float*>(l.src), l.dst, l.count, l.q_scale, l.q_zp, l.q_signed);
+        break;
+      case Launch::kConcat: CpuConcat(l.concat); break;
+      case Launch::kPad: CpuPad(l.pad); break;
+      case Launch::kResizeNearest: CpuResizeNearest(l.rnear); break;
+      case Launch::kResizeBilinear: CpuResizeBilinear(l.rbil); break;
+      case Launch::kSoftmax: CpuSoftmax(l.softmax); break;
+      case Launch::kZeroInsert: CpuZeroInsert(l.zi); break;
+      case Launch::kEltwiseF32: CpuEltwiseFloat(l.eltf); break;
+      default: return absl::InternalError(std::string("no host implementation of ") + l.kernel);
+    }
+  }
+  for (int t : sg->outputs) std::memcpy(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes);
+  for (int t : sg->extra_d2h) std::memcpy(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes);
+  ++sg->runs;
+  return absl::OkStatus();
+}
+
 absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   PreparedSubgraph* sg = Find(key);
   if (!sg) return absl::InternalError("Cannot find subgraph");
-  if (device_flag_ != DeviceFlag::kGPU)
-    return absl::InternalError("HIP backend: CPU workers host model metadata only; jobs must run on kGPU workers");
+  if (device_flag_ == DeviceFlag::kCPU) return ExecuteOnHost(sg);
+  if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("Unsupported device type");
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) {

@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "backend/hip/cpu_kernels.h"
 #include "backend/hip/device.h"
 #include "backend/hip/model.h"
 #include "backend/hip/tensor.h"
@@ -36,7 +37,8 @@ namespace hip {
 struct Launch {
   enum Kind {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
-    kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert
+    kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
+    kEltwiseF32  // CPU-only (float graphs, e.g. the reference's add.tflite)
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
@@ -52,6 +54,7 @@ struct Launch {
   bh_resize_bilinear_params rbil{};
   bh_softmax_params softmax{};
   bh_zero_insert_params zi{};
+  CpuEltwiseF32 eltf{};
   const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
   long count = 0;               // kLut* / kQuantF32: elements
   float q_scale = 0.f;          // kQuantF32
@@ -124,6 +127,8 @@ class HipModelExecutor : public interface::IModelExecutor {
 
   // Whether the GPU kernel set covers `op` of `model` (drives unsupported_ops[kGPU]).
   static bool GpuSupports(const TflModel& model, const TflOperator& op, std::string* why);
+  // The kCPU worker's set: the GPU set plus host-only ops (float graphs).
+  static bool CpuSupports(const TflModel& model, const TflOperator& op, std::string* why);
 
  private:
   PreparedSubgraph* Find(const SubgraphKey& key) const;
@@ -148,6 +153,7 @@ class HipModelExecutor : public interface::IModelExecutor {
   absl::Status LowerGlue(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,
                          PreparedSubgraph* sg, Launch* l);
   absl::Status Enqueue(PreparedSubgraph* sg);
+  absl::Status ExecuteOnHost(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
 
   const HipModel* model_ = nullptr;
@@ -161,6 +167,7 @@ class HipModelExecutor : public interface::IModelExecutor {
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;
   bh_stream_t stream_ = nullptr;
+  std::unique_ptr<CpuPool> cpu_pool_;  // kCPU executors
   bool use_graph_ = true;
   static const std::vector<int> kEmpty;
 };

@@ -19,6 +19,12 @@ template <> size_t EnumLength<BackendType>() { return 1; }
 template <> size_t EnumLength<DataType>() { return static_cast<size_t>(DataType::kFloat64) + 1; }
 template <> size_t EnumLength<DeviceFlag>() { return static_cast<size_t>(DeviceFlag::kNPU) + 1; }
 template <> size_t EnumLength<QuantizationType>() { return 2; }
+template <> size_t EnumLength<SchedulerType>() {
+  return static_cast<size_t>(SchedulerType::kHeterogeneousEarliestFinishTimeReserved) + 1;
+}
+template <> size_t EnumLength<SubgraphPreparationType>() { return 4; }
+template <> size_t EnumLength<JobStatus>() { return static_cast<size_t>(JobStatus::kInvokeFailure) + 1; }
+template <> size_t EnumLength<CPUMaskFlag>() { return 4; }
 
 template <> const char* ToString(BackendType) { return "tfl"; }
 template <> const char* ToString(DataType t) {
@@ -34,6 +40,45 @@ template <> const char* ToString(DeviceFlag t) {
 }
 template <> const char* ToString(QuantizationType t) {
   return t == QuantizationType::kAffineQuantization ? "AffineQuantization" : "NoQuantization";
+}
+
+template <> const char* ToString(SchedulerType t) {
+  static const char* names[] = {"fixed_worker",
+                                "round_robin",
+                                "shortest_expected_latency",
+                                "fixed_worker_global_queue",
+                                "heterogeneous_earliest_finish_time",
+                                "least_slack_time_first",
+                                "heterogeneous_earliest_finish_time_reserved"};
+  size_t i = static_cast<size_t>(t);
+  return i < 7 ? names[i] : "Unknown scheduler type";
+}
+template <> const char* ToString(SubgraphPreparationType t) {
+  static const char* names[] = {"no_fallback_subgraph", "fallback_per_worker", "unit_subgraph",
+                                "merge_unit_subgraph"};
+  size_t i = static_cast<size_t>(t);
+  return i < 4 ? names[i] : "Unknown subgraph preparation type";
+}
+template <> const char* ToString(JobStatus t) {
+  static const char* names[] = {"EnqueueFailed",     "Queued",           "Success",      "SLOViolation",
+                                "InputCopyFailure", "OutputCopyFailure", "InvokeFailure"};
+  size_t i = static_cast<size_t>(t);
+  return i < 7 ? names[i] : "Unknown job status";
+}
+template <> const char* ToString(CPUMaskFlag t) {
+  static const char* names[] = {"ALL", "LITTLE", "BIG", "PRIMARY"};
+  size_t i = static_cast<size_t>(t);
+  return i < 4 ? names[i] : "Unknown CPU mask";
+}
+
+std::string IndexSetToString(const std::set<int>& indices) {
+  std::string s;
+  for (int i : indices) s += (s.empty() ? "" : ",") + std::to_string(i);
+  return s;
+}
+
+std::size_t JobIdBitMaskHash::operator()(const std::pair<int, BitMask>& p) const {
+  return std::hash<int>()(p.first) ^ std::hash<unsigned long long>()(p.second.to_ullong());
 }
 
 SubgraphKey::SubgraphKey() {}
@@ -56,14 +101,10 @@ std::set<int> SubgraphKey::GetUnitIndicesSet() const {
     if (unit_indices.test(i)) s.insert(static_cast<int>(i));
   return s;
 }
-std::string SubgraphKey::GetUnitIndicesString() const {
-  std::string s;
-  for (int u : GetUnitIndicesSet()) s += std::to_string(u) + ",";
-  return s;
-}
+std::string SubgraphKey::GetUnitIndicesString() const { return IndexSetToString(GetUnitIndicesSet()); }
 std::string SubgraphKey::ToString() const {
   return "Model id " + std::to_string(model_id) + " Worker id " + std::to_string(worker_id) +
-         " Units " + GetUnitIndicesString();
+         " Unit indices (" + GetUnitIndicesString() + ")";
 }
 bool SubgraphKey::IsValid() const { return model_id != -1 && worker_id != -1; }
 

@@ -10,6 +10,7 @@
 #include <bitset>
 #include <cstddef>
 #include <cstdint>
+#include <list>
 #include <set>
 #include <string>
 #include <vector>
@@ -26,6 +27,18 @@ size_t EnumLength();
 template <typename EnumType>
 const char* ToString(EnumType t);
 
+// String -> enum by scanning ToString over the enum's range; an unknown
+// string falls back to the first value, as the reference does
+// (band/common.h:61-71: e.g. "fixed_device" -> kFixedWorker).
+template <typename EnumType>
+EnumType FromString(const std::string& str) {
+  for (size_t i = 0; i < EnumLength<EnumType>(); i++) {
+    EnumType t = static_cast<EnumType>(i);
+    if (str == ToString(t)) return t;
+  }
+  return static_cast<EnumType>(0);
+}
+
 enum class BackendType : size_t { kTfLite = 0 };
 
 enum class CPUMaskFlag : size_t { kAll = 0, kLittle, kBig, kPrimary };
@@ -41,14 +54,36 @@ enum class DeviceFlag : size_t { kCPU = 0, kGPU, kDSP, kNPU };
 
 enum class QuantizationType : size_t { kNoQuantization = 0, kAffineQuantization };
 
+// Harness enums (band/common.h:75-200); numbering matches the C API's
+// BandSchedulerType / BandWorkerType / BandSubgraphPreparationType.
+enum class SchedulerType : size_t {
+  kFixedWorker = 0, kRoundRobin, kShortestExpectedLatency, kFixedWorkerGlobalQueue,
+  kHeterogeneousEarliestFinishTime, kLeastSlackTimeFirst, kHeterogeneousEarliestFinishTimeReserved,
+};
+enum class WorkerType : size_t { kDeviceQueue = 1 << 0, kGlobalQueue = 1 << 1 };
+enum class SubgraphPreparationType : size_t {
+  kNoFallbackSubgraph = 0, kFallbackPerWorker, kUnitSubgraph, kMergeUnitSubgraph,
+};
+enum class JobStatus : size_t {
+  kEnqueueFailed = 0, kQueued, kSuccess, kSLOViolation, kInputCopyFailure, kOutputCopyFailure, kInvokeFailure,
+};
+
 template <> size_t EnumLength<BackendType>();
 template <> size_t EnumLength<DataType>();
 template <> size_t EnumLength<DeviceFlag>();
 template <> size_t EnumLength<QuantizationType>();
+template <> size_t EnumLength<SchedulerType>();
+template <> size_t EnumLength<SubgraphPreparationType>();
+template <> size_t EnumLength<JobStatus>();
+template <> size_t EnumLength<CPUMaskFlag>();
 template <> const char* ToString(BackendType t);
 template <> const char* ToString(DataType t);
 template <> const char* ToString(DeviceFlag t);
 template <> const char* ToString(QuantizationType t);
+template <> const char* ToString(SchedulerType t);
+template <> const char* ToString(SubgraphPreparationType t);
+template <> const char* ToString(JobStatus t);
+template <> const char* ToString(CPUMaskFlag t);
 
 struct AffineQuantizationParams {
   std::vector<float> scale;
@@ -91,6 +126,41 @@ class SubgraphKey {
 
 struct SubgraphHash {
   std::size_t operator()(const SubgraphKey& p) const;
+};
+
+// "1,2,3" (band/common.cc:428-437)
+std::string IndexSetToString(const std::set<int>& indices);
+
+// One request (or the remaining part of a split request) moving through
+// planner -> worker (band/common.h:333-378).  Times are NowMicros().
+struct Job {
+  Job() : model_id(-1) {}
+  explicit Job(ModelId model_id) : model_id(model_id) {}
+  Job(ModelId model_id, int64_t slo) : model_id(model_id), slo_us(slo) {}
+
+  ModelId model_id;
+  int input_handle = -1;
+  int output_handle = -1;
+  JobId job_id = -1;
+  std::string model_fname;
+  bool require_callback = true;
+  int64_t enqueue_time = 0;
+  int64_t invoke_time = 0;
+  int64_t end_time = 0;
+  int64_t profiled_execution_time = 0;
+  int64_t expected_execution_time = 0;
+  int64_t expected_latency = 0;
+  int64_t slo_us = 0;
+  WorkerId target_worker_id = -1;
+  JobStatus status = JobStatus::kQueued;
+  SubgraphKey subgraph_key;
+  std::vector<Job> following_jobs;
+  BitMask resolved_unit_subgraphs;
+  std::list<SubgraphKey> previous_subgraph_keys;
+};
+
+struct JobIdBitMaskHash {
+  std::size_t operator()(const std::pair<int, BitMask>& p) const;
 };
 
 }  // namespace band

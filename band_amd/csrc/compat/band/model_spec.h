@@ -29,6 +29,16 @@ class ModelSpec {
   // every non-constant output of `op_indices`
   std::set<int> GetOutputTensors(const std::set<int>& op_indices) const;
 
+  // Unit subgraphs (band/model_spec.cc:53-118): the model_analyzer's
+  // partition of the ops; unit i depends on unit j < i when i consumes a
+  // tensor j produces.
+  absl::Status SetUnitSubgraphs(std::vector<std::set<int>> ops);
+  size_t GetNumUnitSubgraphs() const { return unit_subgraph_ops.size(); }
+  const std::set<int>& GetUnitSubgraphOps(size_t index) const { return unit_subgraph_ops[index]; }
+  const BitMask& GetUnitSubgraphDependency(size_t index) const { return unit_subgraph_dependencies[index]; }
+  // dependencies of a set of units on units outside the set
+  BitMask GetUnitSubgraphDependency(const BitMask& unit_subgraphs) const;
+
   const int num_ops;
   const int num_tensors;
   const std::vector<DataType> tensor_types;
@@ -39,5 +49,9 @@ class ModelSpec {
   const std::map<DeviceFlag, std::set<int>> unsupported_ops;
   const std::set<DeviceFlag> unavailable_devices;
   std::string path;
+
+ private:
+  std::vector<std::set<int>> unit_subgraph_ops;
+  std::vector<BitMask> unit_subgraph_dependencies;
 };
 }  // namespace band

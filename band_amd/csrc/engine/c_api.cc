@@ -1,0 +1,382 @@
+// Band C API over the native harness (band/c/c_api.cc restated; see
+// include/band_c_api.h for the contract).
+#include "band_c_api.h"
+
+#include <cstdarg>
+#include <cstring>
+#include <list>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "engine/engine.h"
+#include "engine/logger.h"
+
+struct BandConfigBuilder {
+  band::RuntimeConfig config;
+  bool cfg_online = true;
+  // the builder starts with no scheduler; Build() requires one
+  // (band/config_builder.cc:34-40)
+};
+
+struct BandConfig {
+  band::RuntimeConfig impl;
+};
+
+struct BandModel {
+  BandModel() : impl(std::make_shared<band::Model>()) {}
+  std::shared_ptr<band::Model> impl;
+};
+
+struct BandTensor {
+  explicit BandTensor(band::Tensor* t) : impl(t) {}
+  std::unique_ptr<band::Tensor> impl;
+};
+
+struct BandEngine {
+  explicit BandEngine(std::unique_ptr<band::Engine> e) : impl(std::move(e)) {}
+  std::list<std::shared_ptr<band::Model>> models;
+  std::unique_ptr<band::Engine> impl;
+};
+
+namespace {
+using band::LogSeverity;
+
+// only an internal error is an error for C callers (band/c/c_api.cc:33-47)
+BandStatus ToBandStatus(const absl::Status& s) {
+  return s.code() == absl::StatusCode::kInternal ? kBandErr : kBandOk;
+}
+
+band::Tensors ToVec(BandTensor** tensors, int n) {
+  band::Tensors v;
+  for (int i = 0; tensors && i < n; ++i) v.push_back(tensors[i] ? tensors[i]->impl.get() : nullptr);
+  return v;
+}
+
+band::RequestOption ToOption(const BandRequestOption& o) {
+  band::RequestOption r;
+  r.target_worker = o.target_worker;
+  r.require_callback = o.require_callback;
+  r.slo_us = o.slo_us;
+  r.slo_scale = o.slo_scale;
+  return r;
+}
+
+// validity rules of band/config_builder.cc:12-80
+absl::Status Validate(const band::RuntimeConfig& c) {
+  const auto& p = c.profile_config;
+  if (p.num_warmups <= 0) return absl::InvalidArgumentError("[ProfileConfigBuilder] num_warmups_ > 0");
+  if (p.num_runs <= 0) return absl::InvalidArgumentError("[ProfileConfigBuilder] num_runs_ > 0");
+  if (p.smoothing_factor < 0.f || p.smoothing_factor > 1.f)
+    return absl::InvalidArgumentError("[ProfileConfigBuilder] smoothing_factor_ in [0, 1]");
+  if (!p.online && p.profile_data_path.empty())
+    return absl::InvalidArgumentError("[ProfileConfigBuilder] profile_data_path_ != \"\"");
+  if (c.planner_config.schedule_window_size <= 0)
+    return absl::InvalidArgumentError("[PlannerConfigBuilder] schedule_window_size_ > 0");
+  if (c.planner_config.schedulers.empty())
+    return absl::InvalidArgumentError("[PlannerConfigBuilder] schedulers_.size() > 0");
+  const auto& w = c.worker_config;
+  for (auto f : w.workers)
+    if (static_cast<size_t>(f) >= band::EnumLength<band::DeviceFlag>())
+      return absl::InvalidArgumentError("[WorkerConfigBuilder] invalid device");
+  if (w.cpu_masks.size() != w.workers.size())
+    return absl::InvalidArgumentError("[WorkerConfigBuilder] cpu_masks_.size() == workers_.size()");
+  if (w.num_threads.size() != w.workers.size())
+    return absl::InvalidArgumentError("[WorkerConfigBuilder] num_threads_.size() == workers_.size()");
+  for (int t : w.num_threads)
+    if (t < 0) return absl::InvalidArgumentError("[WorkerConfigBuilder] num_threads_[i] >= 0");
+  if (w.availability_check_interval_ms <= 0)
+    return absl::InvalidArgumentError("[WorkerConfigBuilder] availability_check_interval_ms_ > 0");
+  if (c.subgraph_config.minimum_subgraph_size <= 0)
+    return absl::InvalidArgumentError("[RuntimeConfigBuilder] minimum_subgraph_size_ > 0");
+  return absl::OkStatus();
+}
+}  // namespace
+
+extern "C" {
+
+void BandSetLogSeverity(BandLogSeverity severity) {
+  band::Logger::Get().SetVerbosity(static_cast<LogSeverity>(severity));
+}
+
+BandCallbackHandle BandSetLogReporter(void (*reporter)(BandLogSeverity, const char*)) {
+  return band::Logger::Get().SetReporter(
+      [reporter](LogSeverity s, const char* m) { reporter(static_cast<BandLogSeverity>(s), m); });
+}
+
+void BandUnsetLogReporter(BandCallbackHandle handle) {
+  if (!band::Logger::Get().RemoveReporter(handle))
+    BAND_LOG(LogSeverity::kWarning, "Failed to remove reporter with handle %d", handle);
+}
+
+BandConfigBuilder* BandConfigBuilderCreate(void) { return new BandConfigBuilder; }
+
+void BandAddConfig(BandConfigBuilder* b, int field, int count, ...) {
+  if (!b) {
+    BAND_LOG(LogSeverity::kError, "BandConfigBuilder is null");
+    return;
+  }
+  band::RuntimeConfig& c = b->config;
+  va_list vl;
+  va_start(vl, count);
+  switch (field) {
+    case BAND_PROFILE_ONLINE: c.profile_config.online = va_arg(vl, int) != 0; break;
+    case BAND_PROFILE_NUM_WARMUPS: c.profile_config.num_warmups = va_arg(vl, int); break;
+    case BAND_PROFILE_NUM_RUNS: c.profile_config.num_runs = va_arg(vl, int); break;
+    case BAND_PROFILE_SMOOTHING_FACTOR: c.profile_config.smoothing_factor = static_cast<float>(va_arg(vl, double)); break;
+    case BAND_PROFILE_DATA_PATH: c.profile_config.profile_data_path = va_arg(vl, const char*); break;
+    case BAND_PLANNER_SCHEDULE_WINDOW_SIZE: c.planner_config.schedule_window_size = va_arg(vl, int); break;
+    case BAND_PLANNER_SCHEDULERS: {
+      std::vector<band::SchedulerType> s;
+      for (int i = 0; i < count; ++i) s.push_back(static_cast<band::SchedulerType>(va_arg(vl, int)));
+      if (!s.empty()) c.planner_config.schedulers = s;
+    } break;
+    case BAND_PLANNER_CPU_MASK: c.planner_config.cpu_mask = static_cast<band::CPUMaskFlag>(va_arg(vl, int)); break;
+    case BAND_PLANNER_LOG_PATH: c.planner_config.log_path = va_arg(vl, const char*); break;
+    case BAND_WORKER_WORKERS: {
+      std::vector<band::DeviceFlag> w;
+      for (int i = 0; i < count; ++i) w.push_back(static_cast<band::DeviceFlag>(va_arg(vl, int)));
+      if (!w.empty()) c.worker_config.workers = w;
+    } break;
+    case BAND_WORKER_CPU_MASKS: {
+      std::vector<band::CPUMaskFlag> m;
+      for (int i = 0; i < count; ++i) m.push_back(static_cast<band::CPUMaskFlag>(va_arg(vl, int)));
+      if (!m.empty()) c.worker_config.cpu_masks = m;
+    } break;
+    case BAND_WORKER_NUM_THREADS: {
+      std::vector<int> t;
+      for (int i = 0; i < count; ++i) t.push_back(va_arg(vl, int));
+      if (!t.empty()) c.worker_config.num_threads = t;
+    } break;
+    case BAND_WORKER_ALLOW_WORKSTEAL: c.worker_config.allow_worksteal = va_arg(vl, int) != 0; break;
+    case BAND_WORKER_AVAILABILITY_CHECK_INTERVAL_MS:
+      c.worker_config.availability_check_interval_ms = va_arg(vl, int);
+      break;
+    case BAND_MINIMUM_SUBGRAPH_SIZE: c.subgraph_config.minimum_subgraph_size = va_arg(vl, int); break;
+    case BAND_SUBGRAPH_PREPARATION_TYPE:
+      c.subgraph_config.subgraph_preparation_type = static_cast<band::SubgraphPreparationType>(va_arg(vl, int));
+      break;
+    case BAND_CPU_MASK: c.cpu_mask = static_cast<band::CPUMaskFlag>(va_arg(vl, int)); break;
+    case BAND_RESOURCE_MONITOR_DEVICE_PATH:
+      (void)va_arg(vl, int);
+      (void)va_arg(vl, const char*);
+      break;  // no resource monitor on this platform
+    case BAND_RESOURCE_MONITOR_INTERVAL_MS: (void)va_arg(vl, int); break;
+    case BAND_RESOURCE_MONITOR_LOG_PATH: (void)va_arg(vl, const char*); break;
+    default: BAND_LOG(LogSeverity::kWarning, "unknown config field %d", field);
+  }
+  va_end(vl);
+}
+
+void BandConfigBuilderDelete(BandConfigBuilder* b) { delete b; }
+
+BandConfig* BandConfigCreate(BandConfigBuilder* b) {
+  if (!b) return nullptr;
+  absl::Status s = Validate(b->config);
+  if (!s.ok()) {
+    BAND_LOG(LogSeverity::kError, "invalid config: %s", s.message().c_str());
+    return nullptr;
+  }
+  return new BandConfig{b->config};
+}
+
+void BandConfigDelete(BandConfig* config) { delete config; }
+
+BandModel* BandModelCreate(void) { return new BandModel; }
+void BandModelDelete(BandModel* model) { delete model; }
+
+BandStatus BandModelAddFromBuffer(BandModel* model, BandBackendType backend_type, const void* data, size_t size) {
+  if (!model) return kBandErr;
+  return ToBandStatus(
+      model->impl->FromBuffer(static_cast<band::BackendType>(backend_type), static_cast<const char*>(data), size));
+}
+
+BandStatus BandModelAddFromFile(BandModel* model, BandBackendType backend_type, const char* path) {
+  if (!model || !path) return kBandErr;
+  return ToBandStatus(model->impl->FromPath(static_cast<band::BackendType>(backend_type), path));
+}
+
+void BandTensorDelete(BandTensor* t) { delete t; }
+BandDataType BandTensorGetType(BandTensor* t) {
+  return t ? static_cast<BandDataType>(t->impl->GetType()) : kBandNumDataType;
+}
+void* BandTensorGetData(BandTensor* t) { return t ? t->impl->GetData() : nullptr; }
+size_t BandTensorGetNumDims(BandTensor* t) { return t ? t->impl->GetNumDims() : 0; }
+const int* BandTensorGetDims(BandTensor* t) { return t ? t->impl->GetDims() : nullptr; }
+size_t BandTensorGetBytes(BandTensor* t) { return t ? t->impl->GetBytes() : 0; }
+const char* BandTensorGetName(BandTensor* t) { return t ? t->impl->GetName() : nullptr; }
+BandQuantizationType BandTensorGetQuantizationType(BandTensor* t) {
+  return t ? static_cast<BandQuantizationType>(t->impl->GetQuantization().GetType()) : kBandNumQuantizationType;
+}
+void* BandTensorGetQuantizationParams(BandTensor* t) { return t ? t->impl->GetQuantization().GetParams() : nullptr; }
+
+BandRequestOption BandRequestOptionGetDefault(void) { return {-1, true, -1, -1.f}; }
+
+// band::RuntimeConfigBuilder::GetDefaultConfig (band/config_builder.cc:181-204),
+// minus its Android paths
+BandEngine* BandEngineCreateWithDefaultConfig(void) {
+  BandConfig config;
+  auto& c = config.impl;
+  c.planner_config.schedulers = {band::SchedulerType::kHeterogeneousEarliestFinishTime};
+  c.planner_config.schedule_window_size = 10;
+  c.subgraph_config.minimum_subgraph_size = 7;
+  c.subgraph_config.subgraph_preparation_type = band::SubgraphPreparationType::kMergeUnitSubgraph;
+  c.worker_config.workers = {band::DeviceFlag::kCPU, band::DeviceFlag::kGPU, band::DeviceFlag::kDSP,
+                             band::DeviceFlag::kNPU};
+  c.worker_config.num_threads = {1, 1, 1, 1};
+  c.worker_config.cpu_masks.assign(4, band::CPUMaskFlag::kBig);
+  c.worker_config.allow_worksteal = true;
+  return BandEngineCreate(&config);
+}
+
+BandEngine* BandEngineCreate(BandConfig* config) {
+  if (!config) return nullptr;
+  auto engine = band::Engine::Create(config->impl);
+  return engine ? new BandEngine(std::move(engine)) : nullptr;
+}
+
+void BandEngineDelete(BandEngine* engine) { delete engine; }
+
+BandStatus BandEngineRegisterModel(BandEngine* engine, BandModel* model) {
+  if (!engine || !model) return kBandErr;
+  absl::Status s = engine->impl->RegisterModel(model->impl.get());
+  if (s.ok()) engine->models.push_back(model->impl);
+  else BAND_LOG(LogSeverity::kError, "RegisterModel: %s", s.message().c_str());
+  return ToBandStatus(s);
+}
+
+int BandEngineGetNumInputTensors(BandEngine* engine, BandModel* model) {
+  if (!engine || !model) return -1;
+  return static_cast<int>(engine->impl->GetInputTensorIndices(model->impl->GetId()).size());
+}
+
+int BandEngineGetNumOutputTensors(BandEngine* engine, BandModel* model) {
+  if (!engine || !model) return -1;
+  return static_cast<int>(engine->impl->GetOutputTensorIndices(model->impl->GetId()).size());
+}
+
+int BandEngineGetNumWorkers(BandEngine* engine) { return engine ? static_cast<int>(engine->impl->GetNumWorkers()) : -1; }
+
+BandDeviceFlag BandEngineGetWorkerDevice(BandEngine* engine, int worker_id) {
+  if (!engine || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return kBandNumDeviceFlag;
+  return static_cast<BandDeviceFlag>(engine->impl->GetWorkerDevice(worker_id));
+}
+
+BandTensor* BandEngineCreateInputTensor(BandEngine* engine, BandModel* model, size_t index) {
+  if (!engine || !model) return nullptr;
+  auto idx = engine->impl->GetInputTensorIndices(model->impl->GetId());
+  if (index >= idx.size()) return nullptr;
+  band::Tensor* t = engine->impl->CreateTensor(model->impl->GetId(), idx[index]);
+  return t ? new BandTensor(t) : nullptr;
+}
+
+BandTensor* BandEngineCreateOutputTensor(BandEngine* engine, BandModel* model, size_t index) {
+  if (!engine || !model) return nullptr;
+  auto idx = engine->impl->GetOutputTensorIndices(model->impl->GetId());
+  if (index >= idx.size()) return nullptr;
+  band::Tensor* t = engine->impl->CreateTensor(model->impl->GetId(), idx[index]);
+  return t ? new BandTensor(t) : nullptr;
+}
+
+BandStatus BandEngineRequestSync(BandEngine* engine, BandModel* model, BandTensor** inputs, BandTensor** outputs) {
+  return BandEngineRequestSyncOptions(engine, model, BandRequestOptionGetDefault(), inputs, outputs);
+}
+
+BandRequestHandle BandEngineRequestAsync(BandEngine* engine, BandModel* model, BandTensor** inputs) {
+  return BandEngineRequestAsyncOptions(engine, model, BandRequestOptionGetDefault(), inputs);
+}
+
+BandStatus BandEngineRequestSyncOptions(BandEngine* engine, BandModel* model, BandRequestOption options,
+                                        BandTensor** inputs, BandTensor** outputs) {
+  if (!engine || !model) return kBandErr;
+  return ToBandStatus(engine->impl->RequestSync(model->impl->GetId(), ToOption(options),
+                                                ToVec(inputs, BandEngineGetNumInputTensors(engine, model)),
+                                                ToVec(outputs, BandEngineGetNumOutputTensors(engine, model))));
+}
+
+BandRequestHandle BandEngineRequestAsyncOptions(BandEngine* engine, BandModel* model, BandRequestOption options,
+                                                BandTensor** inputs) {
+  if (!engine || !model) return -1;
+  auto id = engine->impl->RequestAsync(model->impl->GetId(), ToOption(options),
+                                       ToVec(inputs, BandEngineGetNumInputTensors(engine, model)));
+  if (!id.ok()) {
+    BAND_LOG(LogSeverity::kError, "RequestAsync: %s", id.status().message().c_str());
+    return -1;
+  }
+  return id.value();
+}
+
+BandStatus BandEngineWait(BandEngine* engine, BandRequestHandle handle, BandTensor** outputs, size_t num_outputs) {
+  if (!engine) return kBandErr;
+  return ToBandStatus(engine->impl->Wait(handle, ToVec(outputs, static_cast<int>(num_outputs))));
+}
+
+BandCallbackHandle BandEngineSetOnEndRequest(BandEngine* engine, void (*cb)(void*, BandRequestHandle, BandStatus),
+                                             void* user_data) {
+  if (!engine || !cb) return -1;
+  return engine->impl->SetOnEndRequest(
+      [cb, user_data](int job_id, absl::Status s) { cb(user_data, job_id, ToBandStatus(s)); });
+}
+
+BandStatus BandEngineUnsetOnEndRequest(BandEngine* engine, BandCallbackHandle handle) {
+  if (!engine) return kBandErr;
+  return ToBandStatus(engine->impl->UnsetOnEndRequest(handle));
+}
+
+BandStatus BandxEngineGetJobRecord(BandEngine* engine, BandRequestHandle handle, BandxJobRecord* r) {
+  if (!engine || !r) return kBandErr;
+  band::Job j = engine->impl->GetFinishedJob(handle);
+  if (j.job_id == -1) return kBandErr;
+  r->job_id = j.job_id;
+  r->model_id = j.model_id;
+  r->worker_id = j.subgraph_key.GetWorkerId();
+  r->status = static_cast<int>(j.status);
+  r->enqueue_time_us = j.enqueue_time;
+  r->invoke_time_us = j.invoke_time;
+  r->end_time_us = j.end_time;
+  r->expected_latency_us = j.expected_latency;
+  r->slo_us = j.slo_us;
+  r->unit_indices = j.subgraph_key.GetUnitIndices().to_ullong();
+  return kBandOk;
+}
+
+int BandxModelGetId(BandModel* model) { return model ? model->impl->GetId() : -1; }
+
+size_t BandxEngineGetProfileJson(BandEngine* engine, char* buf, size_t cap) {
+  if (!engine) return 0;
+  const std::string s = engine->impl->ProfileToJson();
+  if (buf && cap) {
+    const size_t n = std::min(cap - 1, s.size());
+    std::memcpy(buf, s.data(), n);
+    buf[n] = 0;
+  }
+  return s.size();
+}
+
+BandStatus BandxEngineDumpProfile(BandEngine* engine) {
+  return engine ? ToBandStatus(engine->impl->DumpProfile()) : kBandErr;
+}
+
+int BandxEngineGetSubgraphs(BandEngine* engine, BandModel* model, int* worker_ids, uint64_t* masks, int cap) {
+  if (!engine || !model) return -1;
+  auto keys = engine->impl->GetSubgraphKeys(model->impl->GetId());
+  for (int i = 0; i < static_cast<int>(keys.size()) && i < cap; ++i) {
+    if (worker_ids) worker_ids[i] = keys[i].GetWorkerId();
+    if (masks) masks[i] = keys[i].GetUnitIndices().to_ullong();
+  }
+  return static_cast<int>(keys.size());
+}
+
+int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandModel* model, int worker_id, uint64_t unit_mask) {
+  if (!engine || !model) return -1;
+  std::set<int> units;
+  for (int i = 0; i < 64; ++i)
+    if (unit_mask >> i & 1) units.insert(i);
+  return engine->impl->GetExpected(band::SubgraphKey(model->impl->GetId(), worker_id, units));
+}
+
+void BandxEngineWaitAll(BandEngine* engine) {
+  if (engine) engine->impl->WaitAll();
+}
+
+}  // extern "C"

@@ -1,0 +1,54 @@
+// Runtime configuration of the harness (band/config.h:10-89): profiling,
+// planner, workers and subgraph preparation.  Defaults are the reference's.
+#pragma once
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "band/common.h"
+
+namespace band {
+
+struct ProfileConfig {
+  bool online = true;
+  int num_warmups = 1;
+  int num_runs = 1;
+  std::string profile_data_path;
+  float smoothing_factor = 0.1f;
+};
+
+struct PlannerConfig {
+  int schedule_window_size = std::numeric_limits<int>::max();
+  std::vector<SchedulerType> schedulers;
+  CPUMaskFlag cpu_mask = CPUMaskFlag::kAll;
+  std::string log_path;
+};
+
+struct WorkerConfig {
+  // one worker per device flag unless configured (band/config.h:46-56)
+  WorkerConfig() {
+    for (size_t i = 0; i < EnumLength<DeviceFlag>(); i++) workers.push_back(static_cast<DeviceFlag>(i));
+    cpu_masks.assign(workers.size(), CPUMaskFlag::kAll);
+    num_threads.assign(workers.size(), 1);
+  }
+  std::vector<DeviceFlag> workers;
+  std::vector<CPUMaskFlag> cpu_masks;
+  std::vector<int> num_threads;
+  bool allow_worksteal = false;
+  int availability_check_interval_ms = 30000;
+};
+
+struct SubgraphConfig {
+  int minimum_subgraph_size = 7;
+  SubgraphPreparationType subgraph_preparation_type = SubgraphPreparationType::kMergeUnitSubgraph;
+};
+
+struct RuntimeConfig {
+  CPUMaskFlag cpu_mask = CPUMaskFlag::kAll;
+  SubgraphConfig subgraph_config;
+  ProfileConfig profile_config;
+  PlannerConfig planner_config;
+  WorkerConfig worker_config;
+};
+
+}  // namespace band

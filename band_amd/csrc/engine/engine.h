@@ -1,0 +1,150 @@
+// Engine (band/engine.h/.cc): the host harness that owns workers, the
+// planner, the latency estimator, one model executor per (model, worker)
+// and the per-model request ring buffers, and implements the request API
+// (RequestSync / RequestAsync / Wait) on top of them.
+//
+// Deviations from the reference, each to make GPU-only configurations work
+// (SURVEY.md s7 hard part 3):
+//  * the request ring buffers are shaped from the tensor views of the
+//    first worker hosting the model (a CPU worker when there is one, as in
+//    the reference) instead of requiring a CPU worker (band/engine.cc:243-252);
+//  * workers_waiting_ is keyed by worker id (the reference keys it by
+//    config index, band/engine.cc:707);
+//  * the model analyzer resolves op support by device flag (see
+//    model_analyzer.cc).
+#pragma once
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <vector>
+
+#include "absl/status/statusor.h"
+#include "band/interface/model_executor.h"
+#include "engine/config.h"
+#include "engine/engine_interface.h"
+#include "engine/latency_estimator.h"
+#include "engine/model.h"
+#include "engine/model_analyzer.h"
+#include "engine/planner.h"
+#include "engine/tensor.h"
+#include "engine/worker.h"
+
+namespace band {
+
+using Tensors = std::vector<interface::ITensor*>;
+
+// per-request options (band/common.h:271-290); slo_scale multiplies the
+// model's worst profiled latency, slo_us overrides it
+struct RequestOption {
+  int target_worker = -1;
+  bool require_callback = true;
+  int slo_us = -1;
+  float slo_scale = -1.f;
+  static RequestOption GetDefaultOption() { return RequestOption(); }
+};
+
+class Engine : public IEngine {
+ public:
+  static std::unique_ptr<Engine> Create(const RuntimeConfig& config, absl::Status* status = nullptr);
+  ~Engine() override;
+
+  absl::Status RegisterModel(Model* model);
+  absl::Status UnregisterModel(Model* model);
+  // a host tensor shaped like `tensor_index` of the model (caller owns)
+  Tensor* CreateTensor(ModelId model_id, int tensor_index);
+  std::vector<int> GetInputTensorIndices(ModelId model_id) const;
+  std::vector<int> GetOutputTensorIndices(ModelId model_id) const;
+
+  absl::Status RequestSync(ModelId model_id, RequestOption options = RequestOption::GetDefaultOption(),
+                           Tensors inputs = {}, Tensors outputs = {});
+  absl::Status RequestSync(std::vector<ModelId> model_ids, std::vector<RequestOption> options,
+                           std::vector<Tensors> inputs = {}, std::vector<Tensors> outputs = {});
+  absl::StatusOr<JobId> RequestAsync(ModelId model_id, RequestOption options = RequestOption::GetDefaultOption(),
+                                     Tensors inputs = {});
+  absl::StatusOr<std::vector<JobId>> RequestAsync(std::vector<ModelId> model_ids, std::vector<RequestOption> options,
+                                                  std::vector<Tensors> inputs = {});
+  absl::Status Wait(JobId job_id, Tensors outputs = {});
+  absl::Status Wait(std::vector<JobId> job_ids, std::vector<Tensors> outputs = {});
+  void WaitAll();
+  absl::Status GetOutputTensors(JobId job_id, Tensors outputs);
+  CallbackId SetOnEndRequest(std::function<void(int, absl::Status)> on_end_request);
+  absl::Status UnsetOnEndRequest(CallbackId callback_id);
+
+  // harness extensions (job tracer / benchmark / profile persistence)
+  Job GetFinishedJob(JobId job_id) { return planner_->GetFinishedJob(job_id); }
+  std::vector<Job> GetFinishedJobs() { return planner_->GetFinishedJobs(); }
+  absl::Status DumpProfile() { return latency_estimator_->DumpProfile(); }
+  std::string ProfileToJson() const { return latency_estimator_->ProfileToJson(); }
+  interface::IModelExecutor* GetModelExecutor(const SubgraphKey& key);
+  std::vector<SubgraphKey> GetSubgraphKeys(ModelId model_id) const;
+  WorkerId GetDeviceWorkerId(DeviceFlag flag) const;
+
+  // IEngine
+  void UpdateWorkersWaiting() const override;
+  WorkerWaitingTime GetWorkerWaitingTime() const override { return workers_waiting_; }
+  std::set<WorkerId> GetIdleWorkers() const override;
+  size_t GetNumWorkers() const override { return workers_.size(); }
+  DeviceFlag GetWorkerDevice(WorkerId id) const override;
+  Worker* GetWorker(WorkerId id) override;
+  const Worker* GetWorker(WorkerId id) const override;
+  SubgraphKey GetLargestSubgraphKey(ModelId model_id, WorkerId worker_id) const override;
+  const ModelSpec* GetModelSpec(ModelId model_id) const override;
+  WorkerId GetModelWorker(ModelId model_id) const override;
+  bool IsBegin(const SubgraphKey& key) const override;
+  bool IsEnd(const SubgraphKey& key) const override;
+  bool HasSubgraph(const SubgraphKey& key) const override;
+  void ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) const override;
+  absl::Status Invoke(const SubgraphKey& key) override;
+  std::pair<std::vector<SubgraphKey>, int64_t> GetSubgraphWithShortestLatency(
+      const Job& job, const WorkerWaitingTime& worker_waiting) const override;
+  std::pair<SubgraphKey, int64_t> GetShortestSubgraphKey(const std::vector<SubgraphKey>& keys, int64_t start_time,
+                                                         const WorkerWaitingTime& worker_waiting) const override;
+  absl::Status TryCopyInputTensors(const Job& job) override;
+  absl::Status TryCopyOutputTensors(const Job& job) override;
+  void UpdateLatency(const SubgraphKey& key, int64_t latency) override { latency_estimator_->UpdateLatency(key, latency); }
+  int64_t GetProfiled(const SubgraphKey& key) const override { return latency_estimator_->GetProfiled(key); }
+  int64_t GetExpected(const SubgraphKey& key) const override { return latency_estimator_->GetExpected(key); }
+  int64_t GetWorst(ModelId model_id) const override { return latency_estimator_->GetWorst(model_id); }
+  void Trigger() override { planner_->Trigger(); }
+  JobId EnqueueRequest(Job job, bool push_front = false) override { return planner_->EnqueueRequest(job, push_front); }
+  std::vector<JobId> EnqueueBatch(std::vector<Job> jobs, bool push_front = false) override {
+    return planner_->EnqueueBatch(std::move(jobs), push_front);
+  }
+  void PrepareReenqueue(Job& job) override { planner_->PrepareReenqueue(job); }
+  void EnqueueFinishedJob(Job& job) override { planner_->EnqueueFinishedJob(job); }
+  bool EnqueueToWorker(const ScheduleAction& action) override { return planner_->EnqueueToWorker({action}); }
+  bool EnqueueToWorkerBatch(const std::vector<ScheduleAction>& actions) override {
+    return planner_->EnqueueToWorker(actions);
+  }
+
+  // shortest finish time over the unit-subgraph DAG from `start_unit_idx`
+  // (band/engine.cc:966-1058) and the fallback-per-worker recursion
+  // (band/engine.cc:856-964)
+  std::pair<std::vector<SubgraphKey>, int64_t> GetShortestLatencyWithUnitSubgraph(
+      ModelId model_id, int start_unit_idx, const WorkerWaitingTime& worker_waiting) const;
+  std::pair<SubgraphKey, int64_t> GetShortestLatency(ModelId model_id, BitMask resolved_unit_subgraphs,
+                                                     int64_t start_time,
+                                                     const WorkerWaitingTime& worker_waiting) const;
+  std::vector<SubgraphKey> GetSubgraphCandidates(ModelId model_id, BitMask resolved_unit_subgraphs) const;
+
+ private:
+  Engine() = default;
+  absl::Status Init(const RuntimeConfig& config);
+  const interface::IModelExecutor* GetModelExecutor(const SubgraphKey& key) const;
+
+  SubgraphConfig subgraph_config_;
+  std::vector<std::unique_ptr<Worker>> workers_;
+  mutable WorkerWaitingTime workers_waiting_;
+  std::unique_ptr<LatencyEstimator> latency_estimator_;
+  std::unique_ptr<Planner> planner_;
+  std::map<std::pair<ModelId, WorkerId>, std::unique_ptr<interface::IModelExecutor>> model_executors_;
+  std::map<ModelId, ModelSpec> model_specs_;
+  // model -> first unit -> last unit -> keys covering exactly [first, last]
+  std::map<ModelId, std::map<int, std::map<int, std::vector<SubgraphKey>>>> unit_subgraphs_to_subgraph_keys_;
+  std::map<ModelId, std::unique_ptr<TensorRingBuffer>> model_input_buffer_;
+  std::map<ModelId, std::unique_ptr<TensorRingBuffer>> model_output_buffer_;
+  mutable std::map<std::pair<ModelId, unsigned long long>, std::pair<SubgraphKey, int64_t>> cache_;
+};
+
+}  // namespace band

@@ -1,0 +1,140 @@
+#include "engine/tensor.h"
+
+#include <cstdlib>
+#include <cstring>
+
+namespace band {
+
+namespace {
+// TfLiteFloatArray / TfLiteIntArray / TfLiteAffineQuantization layout
+struct FArr {
+  int size;
+  float data[1];
+};
+struct IArr {
+  int size;
+  int data[1];
+};
+struct Affine {
+  FArr* scale;
+  IArr* zero_point;
+  int32_t quantized_dimension;
+};
+
+Affine* CloneAffine(const Affine* src) {
+  if (!src) return nullptr;
+  auto* a = static_cast<Affine*>(std::calloc(1, sizeof(Affine)));
+  a->quantized_dimension = src->quantized_dimension;
+  if (src->scale) {
+    const int n = src->scale->size;
+    a->scale = static_cast<FArr*>(std::calloc(1, sizeof(int) + sizeof(float) * (n > 0 ? n : 1)));
+    a->scale->size = n;
+    std::memcpy(a->scale->data, src->scale->data, sizeof(float) * n);
+  }
+  if (src->zero_point) {
+    const int n = src->zero_point->size;
+    a->zero_point = static_cast<IArr*>(std::calloc(1, sizeof(int) + sizeof(int) * (n > 0 ? n : 1)));
+    a->zero_point->size = n;
+    std::memcpy(a->zero_point->data, src->zero_point->data, sizeof(int) * n);
+  }
+  return a;
+}
+}  // namespace
+
+Tensor::Tensor(const interface::ITensor* view, bool copy_data)
+    : type_(view->GetType()),
+      dims_(view->GetDims(), view->GetDims() + view->GetNumDims()),
+      data_(view->GetBytes()),
+      name_(view->GetName() ? view->GetName() : "") {
+  Quantization q = view->GetQuantization();
+  if (q.GetType() == QuantizationType::kAffineQuantization && q.GetParams()) {
+    qtype_ = QuantizationType::kAffineQuantization;
+    qparams_ = CloneAffine(static_cast<const Affine*>(q.GetParams()));
+  }
+  if (copy_data && !data_.empty()) std::memcpy(data_.data(), view->GetData(), data_.size());
+}
+
+Tensor::~Tensor() { FreeQuant(); }
+
+void Tensor::FreeQuant() {
+  if (!qparams_) return;
+  auto* a = static_cast<Affine*>(qparams_);
+  std::free(a->scale);
+  std::free(a->zero_point);
+  std::free(a);
+  qparams_ = nullptr;
+}
+
+void Tensor::SetDims(const std::vector<int>& dims) {
+  dims_ = dims;
+  size_t n = GetDataTypeBytes(type_);
+  for (int d : dims_) n *= static_cast<size_t>(d);
+  data_.resize(n);
+}
+
+Quantization Tensor::GetQuantization() const { return Quantization(qtype_, qparams_); }
+
+absl::Status Tensor::SetQuantization(Quantization q) {
+  FreeQuant();
+  qtype_ = q.GetType();
+  if (qtype_ == QuantizationType::kAffineQuantization && q.GetParams())
+    qparams_ = CloneAffine(static_cast<const Affine*>(q.GetParams()));
+  return absl::OkStatus();
+}
+
+TensorRingBuffer::TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors,
+                                   std::vector<int> tensor_indices, int size)
+    : size_(size > 0 ? size : 1), num_tensors_(tensors.size()), slots_(size_) {
+  for (auto& slot : slots_)
+    for (const auto& t : tensors) slot.emplace_back(new Tensor(t.get()));
+  for (size_t i = 0; i < tensor_indices.size(); ++i) tensor_to_buffer_[tensor_indices[i]] = static_cast<int>(i);
+}
+
+int TensorRingBuffer::Alloc() {
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  return head_++;
+}
+
+bool TensorRingBuffer::IsHandleValid(int handle) const {
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  return handle >= 0 && head_ - size_ <= handle && handle < head_;
+}
+
+absl::Status TensorRingBuffer::GetTensorFromHandle(interface::ITensor* dst, int tensor_index, int handle) const {
+  auto it = tensor_to_buffer_.find(tensor_index);
+  if (it == tensor_to_buffer_.end())
+    return absl::InternalError("GetTensorFromHandle: Invalid tensor index: " + std::to_string(tensor_index));
+  if (!IsHandleValid(handle))
+    return absl::InternalError("GetTensorFromHandle: Invalid memory handle: " + std::to_string(handle));
+  return dst->CopyDataFrom(slots_[Slot(handle)][it->second].get());
+}
+
+absl::Status TensorRingBuffer::PutTensorToHandle(const interface::ITensor* src, int tensor_index, int handle) {
+  auto it = tensor_to_buffer_.find(tensor_index);
+  if (it == tensor_to_buffer_.end())
+    return absl::InternalError("PutTensorToHandle: Invalid tensor index: " + std::to_string(tensor_index));
+  if (!IsHandleValid(handle))
+    return absl::InternalError("PutTensorToHandle: Invalid memory handle: " + std::to_string(handle));
+  return slots_[Slot(handle)][it->second]->CopyDataFrom(src);
+}
+
+absl::Status TensorRingBuffer::GetTensorsFromHandle(std::vector<interface::ITensor*>& dst, int handle) const {
+  if (!IsHandleValid(handle))
+    return absl::InternalError("GetTensorsFromHandle: Invalid memory handle: " + std::to_string(handle));
+  if (dst.size() != num_tensors_) return absl::InternalError("Invalid tensor length");
+  for (size_t i = 0; i < num_tensors_; ++i)
+    if (!dst[i] || !dst[i]->CopyDataFrom(slots_[Slot(handle)][i].get()).ok())
+      return absl::InternalError("Failed to copy tensors.");
+  return absl::OkStatus();
+}
+
+absl::Status TensorRingBuffer::PutTensorsToHandle(const std::vector<interface::ITensor*>& src, int handle) {
+  if (!IsHandleValid(handle))
+    return absl::InternalError("PutTensorsToHandle: Invalid memory handle: " + std::to_string(handle));
+  if (src.size() != num_tensors_) return absl::InternalError("Invalid tensor length");
+  for (size_t i = 0; i < num_tensors_; ++i)
+    if (!slots_[Slot(handle)][i]->CopyDataFrom(src[i]).ok()) return absl::InternalError("Failed to copy tensors.");
+  return absl::OkStatus();
+}
+
+}  // namespace band

@@ -1,0 +1,73 @@
+// band::Tensor - a host tensor owning its bytes, created from a backend
+// tensor view (band/tensor.h/.cc); the element type of the request ring
+// buffers and of the C API's BandTensor.  Affine quantization parameters are
+// deep-copied in the TfLiteAffineQuantization layout the views hand out.
+#pragma once
+#include <memory>
+#include <mutex>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "band/interface/tensor.h"
+
+namespace band {
+
+class Tensor : public interface::ITensor {
+ public:
+  explicit Tensor(const interface::ITensor* view, bool copy_data = false);
+  ~Tensor() override;
+  Tensor(const Tensor&) = delete;
+  Tensor& operator=(const Tensor&) = delete;
+
+  DataType GetType() const override { return type_; }
+  void SetType(DataType type) override { type_ = type; }
+  const char* GetData() const override { return data_.data(); }
+  char* GetData() override { return data_.data(); }
+  const int* GetDims() const override { return dims_.data(); }
+  size_t GetNumDims() const override { return dims_.size(); }
+  void SetDims(const std::vector<int>& dims) override;
+  size_t GetBytes() const override { return data_.size(); }
+  const char* GetName() const override { return name_.c_str(); }
+  Quantization GetQuantization() const override;
+  absl::Status SetQuantization(Quantization quantization) override;
+
+ private:
+  void FreeQuant();
+  DataType type_;
+  std::vector<int> dims_;
+  std::vector<char> data_;
+  std::string name_;
+  QuantizationType qtype_ = QuantizationType::kNoQuantization;
+  void* qparams_ = nullptr;  // TfLiteAffineQuantization layout, owned
+};
+
+// Per-model ring of request I/O slots (band/tensor_ring_buffer.h/.cc): a
+// handle is a monotonically increasing slot number; slot = handle % size.
+// Only the handle bookkeeping is under the lock - the memcpy of a slot runs
+// outside it, so copies of different requests of one model proceed in
+// parallel (the reference copies under the ring's mutex).
+class TensorRingBuffer {
+ public:
+  TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
+                   int size = 128);
+  int Alloc();
+  bool IsTensorIndexValid(int tensor_index) const { return tensor_to_buffer_.count(tensor_index) != 0; }
+  bool IsHandleValid(int handle) const;
+  int GetTensorsLength() const { return static_cast<int>(num_tensors_); }
+  absl::Status GetTensorFromHandle(interface::ITensor* dst, int tensor_index, int handle) const;
+  absl::Status PutTensorToHandle(const interface::ITensor* src, int tensor_index, int handle);
+  absl::Status GetTensorsFromHandle(std::vector<interface::ITensor*>& dst, int handle) const;
+  absl::Status PutTensorsToHandle(const std::vector<interface::ITensor*>& src, int handle);
+
+ private:
+  int Slot(int handle) const { return handle % size_; }
+  const int size_;
+  size_t num_tensors_;
+  std::vector<std::vector<std::unique_ptr<Tensor>>> slots_;
+  std::map<int, int> tensor_to_buffer_;
+  mutable std::mutex head_mtx_;
+  int head_ = 0;
+};
+
+}  // namespace band

@@ -1,0 +1,172 @@
+#include "engine/worker.h"
+
+#include <algorithm>
+#include <cstdio>
+
+#include "engine/logger.h"
+
+#include "engine/time.h"
+
+namespace band {
+
+Worker::Worker(IEngine* engine, WorkerId worker_id, DeviceFlag device_flag)
+    : engine_(engine), worker_id_(worker_id), device_flag_(device_flag) {}
+
+Worker::~Worker() {
+  if (started_ && !kill_worker_) End();
+}
+
+absl::Status Worker::Init(const WorkerConfig& config) {
+  availability_check_interval_ms_ = config.availability_check_interval_ms;
+  // per-worker settings are indexed by worker id (band/worker.cc:35-45)
+  const size_t i = static_cast<size_t>(worker_id_);
+  const CPUMaskFlag mask = i < config.cpu_masks.size() ? config.cpu_masks[i] : CPUMaskFlag::kAll;
+  cpu_set_ = BandCPUMaskGetSet(mask);
+  num_threads_ = i < config.num_threads.size() ? config.num_threads[i] : 1;
+  return absl::OkStatus();
+}
+
+void Worker::Start() {
+  std::call_once(start_once_, [this] {
+    started_ = true;
+    thread_ = std::thread([this] { Work(); });
+  });
+}
+
+void Worker::End() {
+  {
+    std::lock_guard<std::mutex> lock(device_mtx_);
+    kill_worker_ = true;
+  }
+  request_cv_.notify_all();
+  if (thread_.joinable()) thread_.join();
+}
+
+void Worker::Pause() {
+  std::lock_guard<std::mutex> lock(device_mtx_);
+  is_paused_ = true;
+}
+
+void Worker::Resume() {
+  {
+    std::lock_guard<std::mutex> lock(device_mtx_);
+    is_paused_ = false;
+  }
+  request_cv_.notify_one();
+}
+
+void Worker::Wait() {
+  std::unique_lock<std::mutex> lock(device_mtx_);
+  wait_cv_.wait(lock, [this] { return !HasJob(); });
+}
+
+bool Worker::IsValid(const Job& job) {
+  return job.model_id >= 0 && job.subgraph_key.IsValid() && job.enqueue_time > 0 && job.invoke_time == 0 &&
+         job.end_time == 0;
+}
+
+// The per-job hot loop (band/worker.cc:222-323).  Differences from the
+// reference: an invoke error finishes the job as kInvokeFailure instead of
+// entering HandleDeviceError (which double-locks its mutex there,
+// band/worker_device_queue.cc), and the job stays at the queue head until
+// it is done so GetWaitingTime() keeps counting it.
+void Worker::Work() {
+  while (true) {
+    std::unique_lock<std::mutex> lock(device_mtx_);
+    if (!HasJob()) wait_cv_.notify_all();
+    request_cv_.wait(lock, [this] { return kill_worker_ || (HasJob() && !is_paused_); });
+    if (kill_worker_) break;
+    Job* job = GetCurrentJob();
+    lock.unlock();
+
+    if (!job || !IsValid(*job)) {
+      BAND_LOG(LogSeverity::kError, "worker %d spotted an invalid job (model %d)", worker_id_,
+                   job ? job->model_id : -1);
+      lock.lock();
+      if (job) {
+        job->status = JobStatus::kInvokeFailure;
+        Job failed = *job;
+        EndEnqueue();
+        lock.unlock();
+        engine_->EnqueueFinishedJob(failed);
+        engine_->Trigger();
+      }
+      continue;
+    }
+
+    const SubgraphKey key = job->subgraph_key;
+    if (engine_->TryCopyInputTensors(*job).ok()) {
+      lock.lock();
+      job->invoke_time = time::NowMicros();
+      lock.unlock();
+      const absl::Status status = engine_->Invoke(key);
+      job->end_time = time::NowMicros();
+      if (status.ok()) {
+        engine_->UpdateLatency(key, job->end_time - job->invoke_time);
+        if (!job->following_jobs.empty()) engine_->EnqueueBatch(job->following_jobs, true);
+        const absl::Status out = engine_->TryCopyOutputTensors(*job);
+        job->status = out.ok() ? JobStatus::kSuccess : JobStatus::kOutputCopyFailure;
+        if (!out.ok()) BAND_LOG(LogSeverity::kWarning, "%s", out.message().c_str());
+      } else {
+        BAND_LOG(LogSeverity::kError, "worker %d failed to invoke job %d: %s", worker_id_, job->job_id,
+                     status.message().c_str());
+        job->status = JobStatus::kInvokeFailure;
+      }
+    } else {
+      BAND_LOG(LogSeverity::kError, "worker %d failed to copy input of job %d", worker_id_, job->job_id);
+      job->status = JobStatus::kInputCopyFailure;
+    }
+    engine_->EnqueueFinishedJob(*job);
+    lock.lock();
+    EndEnqueue();
+    lock.unlock();
+    engine_->Trigger();
+  }
+}
+
+bool DeviceQueueWorker::EnqueueJob(Job& job) {
+  if (!IsEnqueueReady()) return false;
+  requests_.push_back(job);
+  request_cv_.notify_one();
+  return true;
+}
+
+// sum of the expected latencies of the queued jobs, minus the elapsed part
+// of the running one (band/worker_device_queue.cc:41-66)
+int64_t DeviceQueueWorker::GetWaitingTime() {
+  std::lock_guard<std::mutex> lock(device_mtx_);
+  if (!IsAvailable()) return kLargeWaitingTime;
+  int64_t total = 0;
+  for (auto it = requests_.begin(); it != requests_.end(); ++it) {
+    const int64_t expected = engine_->GetExpected(it->subgraph_key);
+    total += expected;
+    if (it == requests_.begin() && it->invoke_time > 0) {
+      const int64_t elapsed = time::NowMicros() - it->invoke_time;
+      if (elapsed > 0) total -= std::min(elapsed, expected);
+    }
+  }
+  return total;
+}
+
+bool GlobalQueueWorker::EnqueueJob(Job& job) {
+  if (!IsEnqueueReady()) return false;
+  current_job_ = job;
+  is_busy_ = true;
+  request_cv_.notify_one();
+  return true;
+}
+
+// expected remaining time of the running job (band/worker_global_queue.cc:130-160)
+int64_t GlobalQueueWorker::GetWaitingTime() {
+  std::unique_lock<std::mutex> lock(device_mtx_);
+  if (!IsAvailable()) return kLargeWaitingTime;
+  if (!is_busy_) return 0;
+  const int64_t invoke_time = current_job_.invoke_time;
+  const SubgraphKey key = current_job_.subgraph_key;
+  lock.unlock();
+  const int64_t expected = engine_->GetExpected(key);
+  if (invoke_time == 0) return expected;
+  return std::max<int64_t>(expected - (time::NowMicros() - invoke_time), 0);
+}
+
+}  // namespace band

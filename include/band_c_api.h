@@ -1,0 +1,222 @@
+/*
+ * Band engine C API, served by libband_hip.so.
+ *
+ * Same entry points, types and enum values as the reference's public C API
+ * (band/c/c_api.h:47-190, band/c/c_api_type.h:27-196), so a client built
+ * against Band's C header links against this library unchanged.  The
+ * engine behind it is the native harness in band_amd/csrc/engine (planner,
+ * workers, schedulers, latency estimator, model analyzer) with the HIP
+ * backend registered under kBandTfLite.
+ *
+ * Differences a client can observe:
+ *   - BandEngineRequestAsync* return -1 on failure (the reference aborts
+ *     in StatusOr::value(), band/c/c_api.cc:512-521);
+ *   - Bandx* functions at the end are extensions (job records, profile
+ *     persistence, the benchmark driver); the reference has no equivalent
+ *     C entry points.
+ * Status mapping follows the reference: only an internal error is kBandErr;
+ * an SLO violation (DeadlineExceeded) is reported as kBandOk
+ * (band/c/c_api.cc:33-47).
+ */
+#ifndef BAND_HIP_C_API_H_
+#define BAND_HIP_C_API_H_
+
+#include <stdarg.h>
+#include <stdbool.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define BAND_CAPI_EXPORT __attribute__((visibility("default")))
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum BandLogSeverity { kBandInternal = 0, kBandInfo, kBandWarning, kBandError, kBandLogNumSeverities } BandLogSeverity;
+typedef enum BandBackendType { kBandTfLite = 0, kBandNumBackendType } BandBackendType;
+typedef enum BandStatus { kBandOk = 0, kBandErr, kBandDelegateErr } BandStatus;
+typedef enum BandWorkerType { kBandDeviceQueue = 1 << 0, kBandGlobalQueue = 1 << 1 } BandWorkerType;
+typedef enum BandSchedulerType {
+  kBandFixedWorker = 0,
+  kBandRoundRobin,
+  kBandShortestExpectedLatency,
+  kBandFixedWorkerGlobalQueue,
+  kBandHeterogeneousEarliestFinishTime,
+  kBandLeastSlackTimeFirst,
+  kBandHeterogeneousEarliestFinishTimeReserved,
+  kBandNumSchedulerType
+} BandSchedulerType;
+typedef enum BandCPUMaskFlag { kBandAll = 0, kBandLittle, kBandBig, kBandPrimary, kBandNumCpuMask } BandCPUMaskFlag;
+typedef enum BandSubgraphPreparationType {
+  kBandNoFallbackSubgraph = 0,
+  kBandFallbackPerWorker,
+  kBandUnitSubgraph,
+  kBandMergeUnitSubgraph,
+  kBandNumSubgraphPreparationType
+} BandSubgraphPreparationType;
+typedef enum {
+  kBandNoType = 0,
+  kBandFloat32,
+  kBandInt32,
+  kBandUInt8,
+  kBandInt64,
+  kBandString,
+  kBandBool,
+  kBandInt16,
+  kBandComplex64,
+  kBandInt8,
+  kBandFloat16,
+  kBandFloat64,
+  kBandNumDataType,
+} BandDataType;
+typedef enum BandQuantizationType { kBandNoQuantization = 0, kBandAffineQuantization, kBandNumQuantizationType } BandQuantizationType;
+typedef enum BandDeviceFlag { kBandCPU = 0, kBandGPU, kBandDSP, kBandNPU, kBandNumDeviceFlag } BandDeviceFlag;
+typedef enum BandConfigField {
+  BAND_PROFILE_ONLINE = 0,
+  BAND_PROFILE_NUM_WARMUPS,
+  BAND_PROFILE_NUM_RUNS,
+  BAND_PROFILE_SMOOTHING_FACTOR,
+  BAND_PROFILE_DATA_PATH,
+  BAND_PLANNER_SCHEDULE_WINDOW_SIZE,
+  BAND_PLANNER_SCHEDULERS,
+  BAND_PLANNER_CPU_MASK,
+  BAND_PLANNER_LOG_PATH,
+  BAND_WORKER_WORKERS,
+  BAND_WORKER_CPU_MASKS,
+  BAND_WORKER_NUM_THREADS,
+  BAND_WORKER_ALLOW_WORKSTEAL,
+  BAND_WORKER_AVAILABILITY_CHECK_INTERVAL_MS,
+  BAND_MINIMUM_SUBGRAPH_SIZE,
+  BAND_SUBGRAPH_PREPARATION_TYPE,
+  BAND_CPU_MASK,
+  BAND_RESOURCE_MONITOR_DEVICE_PATH,
+  BAND_RESOURCE_MONITOR_INTERVAL_MS,
+  BAND_RESOURCE_MONITOR_LOG_PATH,
+} BandConfigField;
+
+typedef struct BandRequestOption {
+  int target_worker;
+  bool require_callback;
+  int slo_us;
+  float slo_scale;
+} BandRequestOption;
+
+typedef struct BandConfigBuilder BandConfigBuilder;
+typedef struct BandConfig BandConfig;
+typedef struct BandModel BandModel;
+typedef struct BandTensor BandTensor;
+typedef struct BandEngine BandEngine;
+typedef int BandRequestHandle;
+typedef int BandCallbackHandle;
+
+/* logging */
+BAND_CAPI_EXPORT void BandSetLogSeverity(BandLogSeverity severity);
+BAND_CAPI_EXPORT BandCallbackHandle BandSetLogReporter(void (*reporter)(BandLogSeverity severity, const char* msg));
+BAND_CAPI_EXPORT void BandUnsetLogReporter(BandCallbackHandle handle);
+
+/* config builder: BandAddConfig(b, field, count, values...) as in
+ * band/c/c_api.cc:86-196 */
+BAND_CAPI_EXPORT BandConfigBuilder* BandConfigBuilderCreate(void);
+BAND_CAPI_EXPORT void BandAddConfig(BandConfigBuilder* b, int field, int count, ...);
+BAND_CAPI_EXPORT void BandConfigBuilderDelete(BandConfigBuilder* b);
+BAND_CAPI_EXPORT BandConfig* BandConfigCreate(BandConfigBuilder* b);
+BAND_CAPI_EXPORT void BandConfigDelete(BandConfig* config);
+
+/* model */
+BAND_CAPI_EXPORT BandModel* BandModelCreate(void);
+BAND_CAPI_EXPORT void BandModelDelete(BandModel* model);
+BAND_CAPI_EXPORT BandStatus BandModelAddFromBuffer(BandModel* model, BandBackendType backend_type,
+                                                   const void* model_data, size_t model_size);
+BAND_CAPI_EXPORT BandStatus BandModelAddFromFile(BandModel* model, BandBackendType backend_type,
+                                                 const char* model_path);
+
+/* tensor */
+BAND_CAPI_EXPORT void BandTensorDelete(BandTensor* tensor);
+BAND_CAPI_EXPORT BandDataType BandTensorGetType(BandTensor* tensor);
+BAND_CAPI_EXPORT void* BandTensorGetData(BandTensor* tensor);
+BAND_CAPI_EXPORT size_t BandTensorGetNumDims(BandTensor* tensor);
+BAND_CAPI_EXPORT const int* BandTensorGetDims(BandTensor* tensor);
+BAND_CAPI_EXPORT size_t BandTensorGetBytes(BandTensor* tensor);
+BAND_CAPI_EXPORT const char* BandTensorGetName(BandTensor* tensor);
+BAND_CAPI_EXPORT BandQuantizationType BandTensorGetQuantizationType(BandTensor* tensor);
+BAND_CAPI_EXPORT void* BandTensorGetQuantizationParams(BandTensor* tensor);
+
+/* request option */
+BAND_CAPI_EXPORT BandRequestOption BandRequestOptionGetDefault(void);
+
+/* engine */
+BAND_CAPI_EXPORT BandEngine* BandEngineCreateWithDefaultConfig(void);
+BAND_CAPI_EXPORT BandEngine* BandEngineCreate(BandConfig* config);
+BAND_CAPI_EXPORT void BandEngineDelete(BandEngine* engine);
+BAND_CAPI_EXPORT BandStatus BandEngineRegisterModel(BandEngine* engine, BandModel* model);
+BAND_CAPI_EXPORT int BandEngineGetNumInputTensors(BandEngine* engine, BandModel* model);
+BAND_CAPI_EXPORT int BandEngineGetNumOutputTensors(BandEngine* engine, BandModel* model);
+BAND_CAPI_EXPORT int BandEngineGetNumWorkers(BandEngine* engine);
+BAND_CAPI_EXPORT BandDeviceFlag BandEngineGetWorkerDevice(BandEngine* engine, int worker_id);
+BAND_CAPI_EXPORT BandTensor* BandEngineCreateInputTensor(BandEngine* engine, BandModel* model, size_t index);
+BAND_CAPI_EXPORT BandTensor* BandEngineCreateOutputTensor(BandEngine* engine, BandModel* model, size_t index);
+BAND_CAPI_EXPORT BandStatus BandEngineRequestSync(BandEngine* engine, BandModel* model, BandTensor** input_tensors,
+                                                  BandTensor** output_tensors);
+BAND_CAPI_EXPORT BandRequestHandle BandEngineRequestAsync(BandEngine* engine, BandModel* model,
+                                                          BandTensor** input_tensors);
+BAND_CAPI_EXPORT BandStatus BandEngineRequestSyncOptions(BandEngine* engine, BandModel* model,
+                                                         BandRequestOption options, BandTensor** input_tensors,
+                                                         BandTensor** output_tensors);
+BAND_CAPI_EXPORT BandRequestHandle BandEngineRequestAsyncOptions(BandEngine* engine, BandModel* model,
+                                                                 BandRequestOption options,
+                                                                 BandTensor** input_tensors);
+BAND_CAPI_EXPORT BandStatus BandEngineWait(BandEngine* engine, BandRequestHandle handle, BandTensor** output_tensors,
+                                           size_t num_outputs);
+BAND_CAPI_EXPORT BandCallbackHandle BandEngineSetOnEndRequest(BandEngine* engine,
+                                                              void (*on_end_invoke)(void* user_data,
+                                                                                    BandRequestHandle job_id,
+                                                                                    BandStatus status),
+                                                              void* user_data);
+BAND_CAPI_EXPORT BandStatus BandEngineUnsetOnEndRequest(BandEngine* engine, BandCallbackHandle callback_handle);
+
+/* ---- extensions (no reference counterpart) ---- */
+
+/* the planner's record of a finished job (band/common.h:333-378 fields);
+ * returns kBandErr when the job is unknown or not finished */
+typedef struct BandxJobRecord {
+  int job_id;
+  int model_id;
+  int worker_id;
+  int status; /* band::JobStatus: 0 EnqueueFailed .. 6 InvokeFailure */
+  int64_t enqueue_time_us;
+  int64_t invoke_time_us;
+  int64_t end_time_us;
+  int64_t expected_latency_us;
+  int64_t slo_us;
+  uint64_t unit_indices; /* bit mask of the last subgraph's unit indices */
+} BandxJobRecord;
+BAND_CAPI_EXPORT BandStatus BandxEngineGetJobRecord(BandEngine* engine, BandRequestHandle handle,
+                                                    BandxJobRecord* record);
+/* the model id behind a BandModel (job records carry it) */
+BAND_CAPI_EXPORT int BandxModelGetId(BandModel* model);
+/* latency profile database as JSON text (reference layout, see
+ * latency_estimator.h); returns the full length, writes at most cap bytes */
+BAND_CAPI_EXPORT size_t BandxEngineGetProfileJson(BandEngine* engine, char* buf, size_t cap);
+BAND_CAPI_EXPORT BandStatus BandxEngineDumpProfile(BandEngine* engine);
+/* subgraph keys prepared for a model: up to cap (worker_id, unit mask)
+ * pairs; returns the total count */
+BAND_CAPI_EXPORT int BandxEngineGetSubgraphs(BandEngine* engine, BandModel* model, int* worker_ids,
+                                             uint64_t* unit_masks, int cap);
+/* expected latency (us) the estimator holds for one subgraph */
+BAND_CAPI_EXPORT int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandModel* model, int worker_id,
+                                                       uint64_t unit_mask);
+/* blocks until every submitted job finished */
+BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
+
+/* The benchmark tool (band/tool/benchmark.cc) driven by a JSON config in the
+ * reference's format (band/test/data/benchmark_config.json: "models",
+ * "schedulers", "workers", "execution_mode" periodic|stream|workload, ...).
+ * Writes a JSON result (per-model request counts, latency mean/p50/p99,
+ * SLO satisfaction, throughput) into out (at most cap bytes); returns the
+ * full length of the result, or 0 on error (message in the result). */
+BAND_CAPI_EXPORT size_t BandxBenchmarkRun(const char* config_json, char* out, size_t cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BAND_HIP_C_API_H_ */

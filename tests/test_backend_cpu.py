@@ -27,6 +27,13 @@ def _declared_symbols():
     return syms
 
 
+def _declared_c_api():
+    """Band engine C API (include/band_c_api.h): the exported functions"""
+    src = open(os.path.join(ROOT, "include", "band_c_api.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return set(re.findall(r"BAND_CAPI_EXPORT\s+[\w\s\*]*?\b(Bandx?[A-Z]\w*)\s*\(", src))
+
+
 def test_library_exports_every_declared_symbol():
     lib = _abi.load()
     syms = _declared_symbols()
@@ -39,6 +46,21 @@ def test_python_mirror_binds_every_symbol():
     import band_amd.backend  # noqa: F401  (registers bhx_* prototypes)
     bound = set(_abi.KERNEL_SYMBOLS) | set(_abi.BACKEND_SYMBOLS)
     assert _declared_symbols() <= bound | {"bh_set_last_error"}
+
+
+def test_library_exports_band_c_api():
+    """the drop-in C API: every function of include/band_c_api.h (the
+    reference's band/c/c_api.h names plus Bandx extensions) is exported and
+    bound by band_amd.engine (logging / variadic config calls are called
+    without prototypes)"""
+    import band_amd.engine  # noqa: F401
+    lib = _abi.load()
+    syms = _declared_c_api()
+    assert len(syms) >= 45
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    unbound = syms - set(_abi.BACKEND_SYMBOLS) - {"BandAddConfig", "BandSetLogReporter", "BandUnsetLogReporter"}
+    assert not unbound, unbound
 
 
 def _model(golden_dir, name, mid=0):
@@ -142,12 +164,45 @@ def test_tensor_view_semantics(golden_dir):
     assert w.GetDims() == [32, 3, 3, 3]
 
 
-def test_cpu_executor_refuses_execution(golden_dir):
+def test_cpu_executor_unknown_key(golden_dir):
     m = _model(golden_dir, "mobilenet_v2_1.0_224_quant.tflite")
     ex = HipModelExecutor(0, 0, DeviceFlag.kCPU)
     assert ex.PrepareSubgraph(m).ok()
-    assert not ex.ExecuteSubgraph(SubgraphKey(0, 0)).ok()
     assert ex.ExecuteSubgraph(SubgraphKey(0, 7)).message() == "Cannot find subgraph"
+
+
+def test_cpu_worker_add_kat(golden_dir):
+    """tfl_minimal_test.cc:76-86 on a kCPU worker: add.tflite {1,3} -> {3,9}"""
+    m = _model(golden_dir, "add.tflite")
+    ex = HipModelExecutor(0, 0, DeviceFlag.kCPU)
+    assert ex.PrepareSubgraph(m).ok()
+    key = SubgraphKey(0, 0)
+    x = ex.GetTensorView(key, ex.GetInputs(key)[0])
+    x.GetData().reshape(-1)[:2] = [1, 3]
+    assert ex.ExecuteSubgraph(key).ok()
+    y = ex.GetTensorView(key, ex.GetOutputs(key)[0]).GetData().reshape(-1)
+    assert list(y[:2]) == [3, 9]
+
+
+def test_cpu_worker_mnv2_cat_282_bit_exact(golden_dir):
+    """the kCPU worker runs the same lowered program as the GPU (host
+    kernels); bit-exact with the oracle and argmax 282 on cat.jpg"""
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model
+    from tests.test_oracle import load_cat
+    path = os.path.join(golden_dir, "mobilenet_v2_1.0_224_quant.tflite")
+    m = _model(golden_dir, "mobilenet_v2_1.0_224_quant.tflite")
+    ex = HipModelExecutor(0, 0, DeviceFlag.kCPU, num_threads=4)
+    assert ex.PrepareSubgraph(m).ok()
+    key = SubgraphKey(0, 0)
+    x = load_cat(golden_dir)
+    ex.GetTensorView(key, ex.GetInputs(key)[0]).GetData()[...] = x
+    assert ex.ExecuteSubgraph(key).ok()
+    out = ex.GetTensorView(key, ex.GetOutputs(key)[0]).GetData().reshape(-1).copy()
+    assert int(np.argmax(out)) == 282
+    om = Model.from_path(path)
+    ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]].reshape(-1)
+    np.testing.assert_array_equal(out, ref)
 
 
 def test_prepare_wrong_model_id(golden_dir):

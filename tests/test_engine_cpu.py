@@ -1,0 +1,188 @@
+"""The native Band harness end to end on CPU workers (no GPU needed).
+
+Mirrors the reference's engine-level tests: band/test/c/c_api_test.cc
+(sync / async / callback / fixed worker on add.tflite), tfl_minimal_test.cc
+(MobileNetV2-quant + cat.jpg -> 282 through the engine) and the planner /
+latency-estimator behaviour (band/test/planner_test.cc,
+latency_estimator_test.cc), driven through the C API (include/band_c_api.h).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from band_amd import DeviceFlag
+from band_amd.engine import (ConfigBuilder, ConfigField, Engine, JobStatus, Model, RequestOptionGetDefault,
+                             SchedulerType, SubgraphPreparationType, make_config, BenchmarkRun, kBandOk)
+
+
+def _add_engine(golden_dir, scheduler, workers=(DeviceFlag.kCPU, DeviceFlag.kCPU)):
+    e = Engine(make_config([scheduler], list(workers), num_threads=[3, 4][:len(workers)] + [1] * (len(workers) - 2)))
+    m = Model()
+    assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+    assert e.RegisterModel(m)
+    return e, m
+
+
+def _check_add(t):
+    assert list(t.data().reshape(-1)[:2]) == [3.0, 9.0]
+    assert t.dims() == [1, 8, 8, 3]
+
+
+def test_engine_simple_sync_invoke(golden_dir):
+    e, m = _add_engine(golden_dir, SchedulerType.kRoundRobin)
+    assert e.GetNumInputTensors(m) == 1 and e.GetNumOutputTensors(m) == 1
+    i, o = e.CreateInputTensor(m, 0), e.CreateOutputTensor(m, 0)
+    i.data().reshape(-1)[:2] = [1, 3]
+    assert e.RequestSync(m, [i], [o]) == kBandOk
+    _check_add(o)
+
+
+def test_engine_simple_async_invoke_with_callback(golden_dir):
+    e, m = _add_engine(golden_dir, SchedulerType.kRoundRobin)
+    done = []
+    cb = e.SetOnEndRequest(lambda job, status: done.append((job, status)))
+    i, o = e.CreateInputTensor(m, 0), e.CreateOutputTensor(m, 0)
+    i.data().reshape(-1)[:2] = [1, 3]
+    h = e.RequestAsync(m, [i])
+    assert h >= 0
+    assert e.Wait(h, [o]) == kBandOk
+    _check_add(o)
+    assert (h, 0) in done
+    assert e.UnsetOnEndRequest(cb) == kBandOk
+    assert e.UnsetOnEndRequest(cb) != kBandOk  # unknown handle
+
+
+def test_engine_fixed_worker_target(golden_dir):
+    e, m = _add_engine(golden_dir, SchedulerType.kFixedWorker)
+    i, o = e.CreateInputTensor(m, 0), e.CreateOutputTensor(m, 0)
+    i.data().reshape(-1)[:2] = [1, 3]
+    for w in (0, 1):
+        opt = RequestOptionGetDefault()
+        opt.target_worker = w
+        assert e.RequestSync(m, [i], [o], option=opt) == kBandOk
+        _check_add(o)
+    h = e.RequestAsync(m, [i], option=opt)
+    e.Wait(h, [o])
+    assert e.GetJobRecord(h).worker_id == 1
+    bad = RequestOptionGetDefault()
+    bad.target_worker = 7
+    assert e.RequestAsync(m, [i], option=bad) == -1  # invalid worker
+
+
+def test_default_option_values():
+    o = RequestOptionGetDefault()
+    assert (o.target_worker, o.require_callback, o.slo_us, o.slo_scale) == (-1, True, -1, -1.0)
+
+
+def test_config_builder_validation():
+    b = ConfigBuilder()
+    with pytest.raises(Exception):
+        b.build()  # no scheduler
+    b.add(ConfigField.BAND_PLANNER_SCHEDULERS, SchedulerType.kRoundRobin)
+    b.add(ConfigField.BAND_PROFILE_NUM_RUNS, 0)
+    with pytest.raises(Exception):
+        b.build()
+    b.add(ConfigField.BAND_PROFILE_NUM_RUNS, 1)
+    b.build()
+
+
+@pytest.mark.parametrize("sched", [SchedulerType.kFixedWorker, SchedulerType.kRoundRobin,
+                                   SchedulerType.kShortestExpectedLatency,
+                                   SchedulerType.kHeterogeneousEarliestFinishTime,
+                                   SchedulerType.kHeterogeneousEarliestFinishTimeReserved,
+                                   SchedulerType.kLeastSlackTimeFirst, SchedulerType.kFixedWorkerGlobalQueue])
+def test_every_scheduler_runs_mnv2_bit_exact(golden_dir, sched):
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    from tests.test_oracle import load_cat
+    path = os.path.join(golden_dir, "mobilenet_v2_1.0_224_quant.tflite")
+    e = Engine(make_config([sched], [DeviceFlag.kCPU, DeviceFlag.kCPU], num_threads=[2, 2]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    x = load_cat(golden_dir)
+    ins = [e.CreateInputTensor(m, 0) for _ in range(6)]
+    outs = [e.CreateOutputTensor(m, 0) for _ in range(6)]
+    rng = np.random.default_rng(1)
+    xs = [x] + [rng.integers(0, 256, x.shape).astype(np.uint8) for _ in range(5)]
+    hs = []
+    for t, v in zip(ins, xs):
+        t.data()[...] = v
+        hs.append(e.RequestAsync(m, [t]))
+    om = OModel.from_path(path)
+    workers = set()
+    for h, o, v in zip(hs, outs, xs):
+        assert e.Wait(h, [o]) == kBandOk
+        ref = OracleInterpreter(om).run({om.inputs[0]: v})[om.outputs[0]]
+        np.testing.assert_array_equal(o.data().reshape(-1), ref.reshape(-1))
+        r = e.GetJobRecord(h)
+        assert r.status == JobStatus.kSuccess
+        assert r.enqueue_time_us <= r.invoke_time_us <= r.end_time_us
+        workers.add(r.worker_id)
+    assert int(np.argmax(outs[0].data())) == 282
+    if sched == SchedulerType.kRoundRobin:
+        assert workers == {0, 1}  # jobs spread over both workers
+
+
+def test_profile_json_and_offline_reload(golden_dir, tmp_path):
+    prof = str(tmp_path / "profile.json")
+    e = Engine(make_config([SchedulerType.kShortestExpectedLatency], [DeviceFlag.kCPU], profile_path=prof))
+    m = Model()
+    assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+    assert e.RegisterModel(m)
+    js = e.GetProfileJson()
+    path_key = os.path.join(golden_dir, "add.tflite")
+    assert "hash" in js and path_key in js
+    lat = js[path_key]["0"][0]
+    assert lat > 0
+    assert e.DumpProfile()
+    e.close()
+    # offline: the estimator loads the dumped file instead of measuring
+    e2 = Engine(make_config([SchedulerType.kShortestExpectedLatency], [DeviceFlag.kCPU], online=False,
+                            profile_path=prof))
+    m2 = Model()
+    assert m2.FromPath(path_key)
+    assert e2.RegisterModel(m2)
+    assert e2.GetExpectedLatency(m2, 0, 1) == lat
+
+
+def test_planner_log_written(golden_dir, tmp_path):
+    log = str(tmp_path / "log.json")
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], log_path=log))
+    m = Model()
+    assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+    assert e.RegisterModel(m)
+    i, o = e.CreateInputTensor(m, 0), e.CreateOutputTensor(m, 0)
+    for _ in range(3):
+        assert e.RequestSync(m, [i], [o]) == kBandOk
+    e.close()
+    recs = [json.loads(l) for l in open(log)]
+    assert len(recs) == 3 and all(r["status"] == "Success" for r in recs)
+
+
+def test_benchmark_tool_stream(golden_dir):
+    cfg = {
+        "models": [{"graph": os.path.join(golden_dir, "add.tflite"), "batch_size": 2}],
+        "execution_mode": "stream", "running_time_ms": 300, "schedulers": ["round_robin"],
+        "workers": [{"device": "CPU", "num_threads": 1}, {"device": "CPU", "num_threads": 1}],
+    }
+    r = BenchmarkRun(cfg)
+    assert r["completed"] > 0 and r["failed"] == 0
+    assert r["latency_us"]["p99"] >= r["latency_us"]["p50"] > 0
+    assert len(r["jobs_per_worker"]) == 2
+
+
+def test_benchmark_tool_periodic_and_workload(golden_dir):
+    g = os.path.join(golden_dir, "add.tflite")
+    base = {"schedulers": ["heterogeneous_earliest_finish_time"], "running_time_ms": 300,
+            "workers": [{"device": "CPU"}]}
+    r = BenchmarkRun(dict(base, execution_mode="periodic",
+                          models=[{"graph": g, "period_ms": 10, "slo_us": 100000}]))
+    assert 10 <= r["completed"] <= 40
+    assert r["models"][0]["slo_satisfactory_rate"] == 100.0
+    r = BenchmarkRun(dict(base, execution_mode="workload", seed=3, models=[{"graph": g, "request_rate": 200}]))
+    assert r["completed"] > 20
+    with pytest.raises(Exception):
+        BenchmarkRun(dict(base, execution_mode="bogus", models=[{"graph": g}]))

@@ -11,6 +11,8 @@
 #include <cstddef>
 #include <cstdint>
 #include <list>
+#include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <vector>
@@ -157,6 +159,12 @@ struct Job {
   std::vector<Job> following_jobs;
   BitMask resolved_unit_subgraphs;
   std::list<SubgraphKey> previous_subgraph_keys;
+  // Harness addition: bytes of the tensors earlier subgraphs of this job
+  // produced, captured right after they ran.  The reference re-reads the
+  // previous executor's live views when the next subgraph starts
+  // (band/engine.cc:1262-1285), by which time that worker may already have
+  // run the same subgraph for another request and overwritten them.
+  std::shared_ptr<std::map<int, std::vector<char>>> intermediates;
 };
 
 struct JobIdBitMaskHash {

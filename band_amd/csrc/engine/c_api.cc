@@ -2,8 +2,12 @@
 // include/band_c_api.h for the contract).
 #include "band_c_api.h"
 
+#include <condition_variable>
 #include <cstdarg>
 #include <cstring>
+#include <deque>
+#include <mutex>
+#include <thread>
 #include <list>
 #include <memory>
 #include <string>
@@ -11,6 +15,7 @@
 
 #include "engine/engine.h"
 #include "engine/logger.h"
+#include "engine/time.h"
 
 struct BandConfigBuilder {
   band::RuntimeConfig config;
@@ -373,6 +378,75 @@ int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandModel* model, int 
   for (int i = 0; i < 64; ++i)
     if (unit_mask >> i & 1) units.insert(i);
   return engine->impl->GetExpected(band::SubgraphKey(model->impl->GetId(), worker_id, units));
+}
+
+BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
+                                    int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
+                                    double* wall_s) {
+  if (!engine || !models || n_models <= 0 || n_jobs < 0 || max_inflight <= 0) return kBandErr;
+  band::Engine& e = *engine->impl;
+  // per model: one input tensor (copied into the request ring at submit)
+  // and one output tensor (the waiter copies results out of the ring)
+  std::vector<std::vector<std::unique_ptr<band::Tensor>>> own_in(n_models), outs(n_models);
+  std::vector<band::Tensors> in_ptrs(n_models), out_ptrs(n_models);
+  for (int m = 0; m < n_models; ++m) {
+    const band::ModelId id = models[m]->impl->GetId();
+    const auto in_idx = e.GetInputTensorIndices(id);
+    if (inputs && inputs[m] && in_idx.size() == 1) {
+      in_ptrs[m].push_back(inputs[m]->impl.get());
+    } else {
+      for (int t : in_idx) {
+        own_in[m].emplace_back(e.CreateTensor(id, t));
+        if (!own_in[m].back()) return kBandErr;
+        std::memset(own_in[m].back()->GetData(), 0, own_in[m].back()->GetBytes());
+        in_ptrs[m].push_back(own_in[m].back().get());
+      }
+    }
+    for (int t : e.GetOutputTensorIndices(id)) {
+      outs[m].emplace_back(e.CreateTensor(id, t));
+      if (!outs[m].back()) return kBandErr;
+      out_ptrs[m].push_back(outs[m].back().get());
+    }
+  }
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<std::pair<int, band::JobId>> pending;  // (job index, handle)
+  int inflight = 0;
+  bool failed = false;
+  const int64_t t0 = band::time::NowMicros();
+  std::thread waiter([&] {
+    for (int done = 0; done < n_jobs; ++done) {
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return !pending.empty(); });
+      auto item = pending.front();
+      pending.pop_front();
+      l.unlock();
+      const int m = item.first % n_models;
+      absl::Status s = item.second >= 0 ? e.Wait(item.second, out_ptrs[m]) : absl::InternalError("submit");
+      band::Job j = item.second >= 0 ? e.GetFinishedJob(item.second) : band::Job();
+      l.lock();
+      if (!s.ok() || j.job_id != item.second || j.status != band::JobStatus::kSuccess) failed = true;
+      if (latency_us) latency_us[item.first] = static_cast<double>(j.end_time - j.enqueue_time);
+      if (worker_ids) worker_ids[item.first] = j.subgraph_key.GetWorkerId();
+      --inflight;
+      cv.notify_all();
+    }
+  });
+  for (int j = 0; j < n_jobs; ++j) {
+    {
+      std::unique_lock<std::mutex> l(mu);
+      cv.wait(l, [&] { return inflight < max_inflight; });
+      ++inflight;
+    }
+    const int m = j % n_models;
+    auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
+    std::lock_guard<std::mutex> l(mu);
+    pending.emplace_back(j, id.ok() ? id.value() : -1);
+    cv.notify_all();
+  }
+  waiter.join();
+  if (wall_s) *wall_s = (band::time::NowMicros() - t0) * 1e-6;
+  return failed ? kBandErr : kBandOk;
 }
 
 void BandxEngineWaitAll(BandEngine* engine) {

@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <cassert>
 #include <cstdio>
+#include <cstring>
 
 #include "engine/logger.h"
 #include <limits>
@@ -544,6 +545,20 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
   interface::IModelExecutor* exec = GetModelExecutor(key);
   if (!exec) return absl::InternalError("no executor for " + key.ToString());
   std::set<int> unresolved(exec->GetInputs(key).begin(), exec->GetInputs(key).end());
+  if (job.intermediates) {
+    for (auto it = unresolved.begin(); it != unresolved.end();) {
+      auto hit = job.intermediates->find(*it);
+      if (hit == job.intermediates->end()) {
+        ++it;
+        continue;
+      }
+      auto dst = exec->GetTensorView(key, *it);
+      if (!dst || dst->GetBytes() != hit->second.size())
+        return absl::InternalError("intermediate tensor " + std::to_string(*it) + " does not fit its view");
+      std::memcpy(dst->GetData(), hit->second.data(), hit->second.size());
+      it = unresolved.erase(it);
+    }
+  }
   for (const SubgraphKey& prev : job.previous_subgraph_keys) {
     interface::IModelExecutor* pexec = GetModelExecutor(prev);
     if (!pexec) continue;
@@ -571,6 +586,26 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
     it = unresolved.erase(it);
   }
   if (!unresolved.empty()) return absl::InternalError("Some tensors fail to be resolved.");
+  return absl::OkStatus();
+}
+
+// captures what this subgraph produced for the rest of the job, on the
+// worker thread right after ExecuteSubgraph, before that worker can run
+// another request (see Job::intermediates)
+absl::Status Engine::SaveIntermediates(Job& job) {
+  if (job.following_jobs.empty()) return absl::OkStatus();
+  const SubgraphKey& key = job.subgraph_key;
+  interface::IModelExecutor* exec = GetModelExecutor(key);
+  if (!exec) return absl::InternalError("no executor for " + key.ToString());
+  auto snap = std::make_shared<std::map<int, std::vector<char>>>();
+  if (job.intermediates) *snap = *job.intermediates;
+  for (int t : exec->GetOutputs(key)) {
+    auto v = exec->GetTensorView(key, t);
+    if (!v) return absl::InternalError("no view of output tensor " + std::to_string(t));
+    const char* d = v->GetData();
+    (*snap)[t].assign(d, d + v->GetBytes());
+  }
+  for (Job& f : job.following_jobs) f.intermediates = snap;
   return absl::OkStatus();
 }
 

@@ -102,6 +102,7 @@ class Engine : public IEngine {
                                                          const WorkerWaitingTime& worker_waiting) const override;
   absl::Status TryCopyInputTensors(const Job& job) override;
   absl::Status TryCopyOutputTensors(const Job& job) override;
+  absl::Status SaveIntermediates(Job& job) override;
   void UpdateLatency(const SubgraphKey& key, int64_t latency) override { latency_estimator_->UpdateLatency(key, latency); }
   int64_t GetProfiled(const SubgraphKey& key) const override { return latency_estimator_->GetProfiled(key); }
   int64_t GetExpected(const SubgraphKey& key) const override { return latency_estimator_->GetExpected(key); }

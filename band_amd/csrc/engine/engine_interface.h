@@ -54,6 +54,8 @@ class IEngine {
   // job data movement (worker thread)
   virtual absl::Status TryCopyInputTensors(const Job& job) = 0;
   virtual absl::Status TryCopyOutputTensors(const Job& job) = 0;
+  // snapshot a non-final subgraph's outputs into the job's following jobs
+  virtual absl::Status SaveIntermediates(Job& job) { return absl::OkStatus(); }
 
   // latency estimator
   virtual void UpdateLatency(const SubgraphKey& key, int64_t latency) = 0;

@@ -50,11 +50,14 @@ bool FixedWorkerGlobalQueueScheduler::Schedule(JobQueue& requests) {
 }
 
 bool RoundRobinScheduler::Schedule(JobQueue& requests) {
-  // Note: like the reference, this reads the cached waiting times without
-  // refreshing them, so every worker counts as idle and each pass hands at
-  // most one job to every worker (round_robin_scheduler.cc:8).
   bool ok = true;
-  for (WorkerId w : engine_.GetIdleWorkers()) {
+  engine_.UpdateWorkersWaiting();
+  const std::set<WorkerId> idle = engine_.GetIdleWorkers();
+  if (idle.empty() || requests.empty()) return ok;
+  // idle workers in rotation order, starting at next_
+  std::vector<WorkerId> order(idle.lower_bound(next_), idle.end());
+  order.insert(order.end(), idle.begin(), idle.lower_bound(next_));
+  for (WorkerId w : order) {
     if (requests.empty()) break;
     auto it = std::find_if(requests.begin(), requests.end(), [&](const Job& j) {
       return engine_.GetLargestSubgraphKey(j.model_id, w).IsValid();
@@ -64,6 +67,7 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
     requests.erase(it);
     const SubgraphKey key = engine_.GetLargestSubgraphKey(job.model_id, w);
     ok &= engine_.EnqueueToWorker({job, key});
+    next_ = w + 1;
   }
   return ok;
 }

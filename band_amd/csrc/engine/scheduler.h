@@ -44,13 +44,21 @@ class FixedWorkerGlobalQueueScheduler : public IScheduler {
 };
 
 // one job per idle worker, first job in queue order that the worker can run
-// (round_robin_scheduler.cc:7-30)
+// (round_robin_scheduler.cc:7-30).  Deviation: the reference never refreshes
+// the waiting times, so every worker looks idle forever and requests that
+// arrive one at a time all land on the lowest worker id (SURVEY.md s7 hard
+// part 3).  Here the waiting times are refreshed and the scan starts after
+// the worker served last, so arrivals rotate over the idle workers; a job
+// with no idle worker waits in the planner until a worker frees up.
 class RoundRobinScheduler : public IScheduler {
  public:
   using IScheduler::IScheduler;
   bool Schedule(JobQueue& requests) override;
   bool NeedFallbackSubgraphs() override { return false; }
   WorkerType GetWorkerType() override { return WorkerType::kDeviceQueue; }
+
+ private:
+  WorkerId next_ = 0;  // scan starts here
 };
 
 // repeatedly place the job whose best plan finishes last ("largest shortest

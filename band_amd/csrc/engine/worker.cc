@@ -103,7 +103,11 @@ void Worker::Work() {
       job->end_time = time::NowMicros();
       if (status.ok()) {
         engine_->UpdateLatency(key, job->end_time - job->invoke_time);
-        if (!job->following_jobs.empty()) engine_->EnqueueBatch(job->following_jobs, true);
+        if (!job->following_jobs.empty()) {
+          const absl::Status snap = engine_->SaveIntermediates(*job);
+          if (!snap.ok()) BAND_LOG(LogSeverity::kError, "%s", snap.message().c_str());
+          engine_->EnqueueBatch(job->following_jobs, true);
+        }
         const absl::Status out = engine_->TryCopyOutputTensors(*job);
         job->status = out.ok() ? JobStatus::kSuccess : JobStatus::kOutputCopyFailure;
         if (!out.ok()) BAND_LOG(LogSeverity::kWarning, "%s", out.message().c_str());

@@ -133,6 +133,8 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineGetExpectedLatency": (c_int64, [c_void_p, c_void_p, c_int, c_uint64]),
     "BandxEngineWaitAll": (None, [c_void_p]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
+    "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
+                                         POINTER(c_double), POINTER(c_int), POINTER(c_double)]),
 })
 
 
@@ -369,6 +371,24 @@ class Engine:
 
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))
+
+    def RunClosedLoop(self, models, n_jobs, max_inflight, inputs=None):
+        """Native closed-loop driver (BandxEngineRunClosedLoop): n_jobs requests
+        round-robin over `models`, <= max_inflight outstanding.  Returns
+        (latency_us array, worker id array, wall seconds)."""
+        ms = (c_void_p * len(models))(*[m.handle.value for m in models])
+        ins = None
+        if inputs is not None:
+            ins = (c_void_p * len(models))(*[t.handle.value if t is not None else None for t in inputs])
+        lat = np.zeros(max(n_jobs, 1), np.float64)
+        wid = np.zeros(max(n_jobs, 1), np.int32)
+        wall = c_double(0)
+        rc = self.lib.BandxEngineRunClosedLoop(self.handle, ms, ins, len(models), int(n_jobs), int(max_inflight),
+                                               lat.ctypes.data_as(POINTER(c_double)),
+                                               wid.ctypes.data_as(POINTER(c_int)), ctypes.byref(wall))
+        if rc != kBandOk:
+            raise _abi.BandHipError("BandxEngineRunClosedLoop: a job failed")
+        return lat[:n_jobs], wid[:n_jobs], wall.value
 
     def close(self):
         if getattr(self, "handle", None):

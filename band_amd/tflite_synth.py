@@ -262,6 +262,7 @@ class QGraph:
         self.mb = ModelBuilder(name)
         self.n = 0
         self.meta = {}  # tensor -> (shape, scale, zp)
+        self.fshape = {}  # float32 tensor -> shape
 
     def _name(self, kind):
         self.n += 1
@@ -488,6 +489,20 @@ class QGraph:
         shp, _, _ = self.meta[x]
         y = self.mb.tensor(self._name("float"), shp, np.float32)
         self.mb.op("DEQUANTIZE", [x], [y], OPT["DequantizeOptions"], Table())
+        self.fshape[y] = list(shp)
+        return y
+
+    def float_add(self, a, b, act="NONE"):
+        """float32 ADD (a CPU-worker op: the GPU set is 8-bit only)"""
+        y = self.mb.tensor(self._name("float"), self.fshape[a], np.float32)
+        self.mb.op("ADD", [a, b], [y], OPT["AddOptions"], act_options(act))
+        self.fshape[y] = list(self.fshape[a])
+        return y
+
+    def quantize_float(self, xf, scale, zp=None):
+        """QUANTIZE float32 -> 8-bit"""
+        y = self.act_tensor(self.fshape[xf], scale, self._act_zp() if zp is None else zp)
+        self.mb.op("QUANTIZE", [xf], [y], OPT["QuantizeOptions"], Table())
         return y
 
     def build(self):

@@ -4,20 +4,22 @@
 Workload (default, N=1): BASELINE config C3 - the 4-DNN int8 mix
 (MobileNetV2, SSD-MobileNetV2, DeepLabV3-MobileNetV2, PoseNet-MobileNetV1;
 224x224, synthetic seeded weights with TFLite-converter-shaped quantisation)
-served round-robin by the Band GPU workers of one MI355X.  `--model
-mobilenet_v2_int8` etc. run the single-model configs (C2).  A "step" is one
-Band job: the per-job work of `Worker::Work` (band/worker.cc:222-323) - copy
-the request into the executor's input view (Engine::TryCopyInputTensors,
-band/engine.cc:1247-1319), `IModelExecutor::ExecuteSubgraph`
-(band/engine.cc:843-850), copy the output views out (TryCopyOutputTensors
-:1333-1365).  Job latency = end - enqueue (band/common.h:351-353).  Each Band
-GPU worker holds one executor per model (band/engine.cc:91-106) on its own
-HIP stream, like AddWorkers({kGPU, kGPU, ...}).
+served by the native Band engine (band_amd/csrc/engine) with round_robin over
+`--workers-per-gpu` Band GPU workers of one MI355X (AddWorkers({kGPU, ...})).
+`--model mobilenet_v2_int8` etc. run single-model configs (C2).
 
-N>1: one process per GPU (torchrun), jobs shard across GPUs with no
-data-path collective (weak scaling); a gloo process group only provides the
-barrier and the max-over-ranks timing.  The GPU is driven exclusively
-through libband_hip.so; torch never touches the device here.
+A "step" is one Band job, end to end through the harness: RequestAsync
+(user tensor -> request ring, band/engine.cc:455-529) -> planner thread ->
+scheduler -> worker queue (band/planner.cc:268-365) -> Worker::Work: input
+copy into the executor's view, IModelExecutor::ExecuteSubgraph on the GPU,
+output copy (band/worker.cc:222-323) -> Wait.  A native closed-loop driver
+(BandxEngineRunClosedLoop) keeps 2 x workers requests in flight.  Job
+latency = end - enqueue of the planner's job record (band/common.h:351-353).
+
+N>1: one process per GPU (torchrun), each with its own engine over its GPU;
+jobs shard across GPUs with no data-path collective (weak scaling); a gloo
+process group only provides the barrier and the max-over-ranks timing.  The
+GPU is driven exclusively through libband_hip.so; torch never touches it.
 
 Prints ONE JSON line on rank 0.
 """
@@ -26,7 +28,6 @@ import json
 import os
 import platform
 import tempfile
-import threading
 import time
 
 import numpy as np
@@ -35,8 +36,8 @@ import numpy as np
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=4000, help="jobs per rank in the timed region")
-    p.add_argument("--warmup", type=int, default=400)
+    p.add_argument("--steps", type=int, default=20000, help="jobs per rank in the timed region")
+    p.add_argument("--warmup", type=int, default=2000)
     p.add_argument("--workers-per-gpu", type=int, default=8)
     p.add_argument("--hw-queues", type=int, default=4,
                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4; <= 32)")
@@ -47,6 +48,10 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
     p.add_argument("--profile-iters", type=int, default=20)
+    p.add_argument("--scheduler", default="round_robin",
+                   choices=["round_robin", "fixed_worker", "shortest_expected_latency",
+                            "heterogeneous_earliest_finish_time"])
+    p.add_argument("--inflight", type=int, default=0, help="outstanding requests (default 2 x workers)")
     return p.parse_args()
 
 
@@ -102,18 +107,6 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def run_worker(execs, keys, requests, n_jobs, first, lat, results, idx):
-    """One Band GPU worker thread: closed-loop jobs over the mixed stream
-    (C++ loop bhx_run_mixed_jobs; the GIL is released for the whole batch)."""
-    from band_amd import RunMixedJobs
-    try:
-        us, _ = RunMixedJobs(execs, keys, requests, n_jobs, first_model=first)
-        lat.extend((us * 1e-6).tolist())
-        results[idx] = True
-    except Exception as e:  # noqa: BLE001
-        results[idx] = str(e)
-
-
 def cpu_baseline(models, seconds):
     """Oracle (scalar C port of TFLite's reference kernels) on the host, the
     same round-robin request stream over the models."""
@@ -149,73 +142,72 @@ def main():
     D = Dist()
     import band_amd
     from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
+    from band_amd.engine import Engine, Model, SchedulerType, make_config
 
     models = model_list(args.model)
     M = len(models)
     W = max(1, args.workers_per_gpu)
-    hip_models = []
-    for mid, (name, buf) in enumerate(models):
-        tmp = tempfile.NamedTemporaryFile(prefix="band_bench_", suffix=".tflite", delete=False)
+    paths = []
+    for name, buf in models:
+        tmp = tempfile.NamedTemporaryFile(prefix="band_bench_%s_" % name, suffix=".tflite", delete=False)
         tmp.write(buf)
         tmp.close()
-        hm = HipModel(mid)  # one IModel per model, shared by every worker's executor, as in Band
-        st = hm.FromPath(tmp.name)
-        os.unlink(tmp.name)
-        assert st.ok(), st
-        hip_models.append(hm)
-    workers = []  # per worker: ([executor per model], [key per model])
+        paths.append(tmp.name)
+    if args.no_graph:
+        os.environ["BAND_HIP_GRAPH"] = "0"
+
+    # this rank's Band engine: W GPU workers, all on the local MI355X
+    # (worker id -> device ordinal; each worker owns one HIP stream)
     for w in range(W):
-        wid = 1 + w  # worker 0 is Band's CPU worker
-        band_amd.SetWorkerDevice(wid, D.local_rank)
-        execs, keys = [], []
-        for mid, hm in enumerate(hip_models):
-            ex = HipModelExecutor(mid, wid, DeviceFlag.kGPU)
-            if args.no_graph:
-                ex.SetUseGraph(False)
-            spec = ex.InvestigateModelSpec(hm)
-            assert not spec.unsupported_ops[DeviceFlag.kGPU], spec.unsupported_ops
-            st = ex.PrepareSubgraph(hm)
-            assert st.ok(), st
-            execs.append(ex)
-            keys.append(SubgraphKey(mid, wid))
-        workers.append((execs, keys))
-
-    # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
+        band_amd.SetWorkerDevice(w, D.local_rank)
+    sched = {"round_robin": SchedulerType.kRoundRobin, "fixed_worker": SchedulerType.kFixedWorker,
+             "shortest_expected_latency": SchedulerType.kShortestExpectedLatency,
+             "heterogeneous_earliest_finish_time": SchedulerType.kHeterogeneousEarliestFinishTime}[args.scheduler]
+    engine = Engine(make_config([sched], [DeviceFlag.kGPU] * W, num_warmups=3, num_runs=5))
+    band_models, inputs = [], []
     rng = np.random.default_rng(5489 + D.rank)
-    requests = []
-    for ex, key in zip(*workers[0]):
-        arr = ex.GetTensorView(key, ex.GetInputs(key)[0]).GetData()
+    for path in paths:
+        m = Model()
+        assert m.FromPath(path), path
+        assert engine.RegisterModel(m), path
+        band_models.append(m)
+        # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
+        t = engine.CreateInputTensor(m, 0)
+        arr = t.data()
         lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
-        requests.append(rng.integers(lo, hi, arr.shape).astype(arr.dtype))
+        arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
+        inputs.append(t)
+    inflight = args.inflight or 2 * W
 
-    def run(n_total):
-        lats = [[] for _ in range(W)]
-        res = [None] * W
-        share = [n_total // W + (1 if i < n_total % W else 0) for i in range(W)]
-        ths = [threading.Thread(target=run_worker, args=(execs, keys, requests, share[i], i % M, lats[i], res, i))
-               for i, (execs, keys) in enumerate(workers)]
-        for t in ths:
-            t.start()
-        for t in ths:
-            t.join()
-        bad = [r for r in res if r is not True]
-        if bad:
-            raise RuntimeError("job failed: %s" % bad)
-        return [x for l in lats for x in l]
-
-    run(max(args.warmup, 2 * W * M))
+    engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
     D.barrier()
     t0 = time.perf_counter()
-    lat = run(args.steps)
+    lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, args.steps, inflight, inputs)
     t1 = time.perf_counter()
     D.barrier()
     elapsed = D.max(t1 - t0)
-    all_lat = [x for part in D.gather(lat) for x in part]
+    all_lat = [x for part in D.gather((lat_us * 1e-6).tolist()) for x in part]
+    jobs_per_worker = np.bincount(worker_ids, minlength=W).tolist()
+
+    # profiling executors (outside the engine, same backend code) for the
+    # per-kernel roofline and the device-side floor of a job
+    prof_wid = 1000
+    band_amd.SetWorkerDevice(prof_wid, D.local_rank)
+    execs0, keys0 = [], []
+    for mid, path in enumerate(paths):
+        hm = HipModel(100 + mid)
+        assert hm.FromPath(path).ok()
+        ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
+        if args.no_graph:
+            ex.SetUseGraph(False)
+        assert ex.PrepareSubgraph(hm).ok()
+        execs0.append(ex)
+        keys0.append(SubgraphKey(100 + mid, prof_wid))
+        ex._model_ref = hm
 
     # roofline of the dominant kernel: per-launch HIP events on the worker's
     # stream, over one inference of each model (the mix is uniform)
     by_k = {}
-    execs0, keys0 = workers[0]
     for ex, key in zip(execs0, keys0):
         for r in ex.ProfileSubgraph(key, iters=args.profile_iters):
             # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
@@ -267,12 +259,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "int8" if "int8" in args.model else "uint8",
+            "dtype": "uint8" if args.model.endswith("uint8") else "int8",
             "data": "synthetic (seeded int8 inputs and weights; no checkpoint)",
-            "config": {"workload": ("C3: 4-DNN int8 mix (%s), 224x224 batch-1 jobs round-robin over %d Band GPU "
-                                    "worker(s) per MI355X" % (", ".join(nm for nm, _ in models), W))
-                       if M > 1 else ("C2: %s 224x224 batch-1 jobs, %d Band GPU worker(s) per MI355X, fixed_worker"
-                                      % (args.model, W)),
+            "config": {"workload": ("C3: 4-DNN int8 mix (%s), 224x224 batch-1 jobs through the Band engine, "
+                                    "%s over %d Band GPU worker(s) per MI355X" %
+                                    (", ".join(nm for nm, _ in models), args.scheduler, W))
+                       if M > 1 else ("C2: %s 224x224 batch-1 jobs through the Band engine, %s over %d Band GPU "
+                                      "worker(s) per MI355X" % (args.model, args.scheduler, W)),
+                       "harness": "native Band engine (planner + workers + %s), %d requests in flight"
+                                  % (args.scheduler, inflight),
+                       "jobs_per_worker_rank0": jobs_per_worker,
                        "model": args.model, "global_batch": n * W, "seq_len": None,
                        "parallelism": "job-sharded x%d (no collective)" % n, "hipgraph": not args.no_graph,
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
@@ -293,6 +289,9 @@ def main():
             "host": platform.node(),
         }
         print(json.dumps(line), flush=True)
+    engine.close()
+    for path in paths:
+        os.unlink(path)
     D.close()
 
 

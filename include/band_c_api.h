@@ -208,6 +208,17 @@ BAND_CAPI_EXPORT int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandM
 /* blocks until every submitted job finished */
 BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
 
+/* Closed-loop request driver: submits exactly n_jobs requests, round-robin
+ * over the n_models models (model j % n_models), with at most max_inflight
+ * outstanding, and waits for all of them.  Inputs are the engine-created
+ * tensors of each model (caller fills them first, or NULL for zeros).
+ * latency_us[j] = end - enqueue of job j (band/common.h:351-353);
+ * worker_ids[j] = worker that ran its last subgraph (may be NULL);
+ * *wall_s = submission of the first job to completion of the last. */
+BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs,
+                                                     int n_models, int n_jobs, int max_inflight, double* latency_us,
+                                                     int* worker_ids, double* wall_s);
+
 /* The benchmark tool (band/tool/benchmark.cc) driven by a JSON config in the
  * reference's format (band/test/data/benchmark_config.json: "models",
  * "schedulers", "workers", "execution_mode" periodic|stream|workload, ...).

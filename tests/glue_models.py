@@ -52,3 +52,23 @@ def tconv_zoo(seed=7):
     g.output(c)
     g.output(d)
     return g.build()
+
+
+def split_zoo(dtype=np.int8, seed=11):
+    """A model the model analyzer must split: two GPU runs of >= 7 ops around
+    a float32 ADD only the CPU worker runs (DEQUANTIZE -> ADD(x, x) ->
+    QUANTIZE), plus a side output from the first run."""
+    g = QGraph(dtype, seed=seed, name="split_zoo")
+    x = g.input([1, 16, 16, 8], scale=0.05)
+    a = g.conv(x, 16, k=3, act="RELU6")
+    for _ in range(3):
+        a = g.add(g.conv(g.dwconv(a), 16, k=1, act="NONE"), a)
+    f = g.dequantize(a)
+    f = g.float_add(f, f)
+    q = g.quantize_float(f, 0.1)
+    b = g.conv(q, 24, k=3, stride=2, act="RELU6")
+    for _ in range(3):
+        b = g.add(g.conv(g.dwconv(b), 24, k=1, act="NONE"), b)
+    g.output(g.fully_connected(g.reshape(g.avgpool(b, (8, 8)), [1, 24]), 10))
+    g.output(g.logistic(a))
+    return g.build()

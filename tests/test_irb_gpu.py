@@ -26,6 +26,8 @@ def test_irb_mnv2_blocks(gpu_lib, h, cin, t, cout, s):
     dict(b=1, h=11, w=10, cin=16, ce=64, cout=40, stride=2),
     dict(b=3, h=5, w=5, cin=8, ce=48, cout=8, stride=1, residual=False),
     dict(b=1, h=6, w=7, cin=32, ce=32, cout=16, stride=1, has_expand=False),
+    dict(b=1, h=8, w=8, cin=16, ce=16, cout=16, stride=1, has_expand=False),  # no expand + residual
+    dict(b=2, h=7, w=9, cin=32, ce=32, cout=32, stride=1, has_expand=False),
 ])
 def test_irb_general(gpu_lib, args):
     rng = np.random.default_rng(len(args) * 7 + args["cin"] + args["cout"])

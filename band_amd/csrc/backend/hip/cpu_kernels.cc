@@ -486,5 +486,86 @@ void CpuEltwiseFloat(const CpuEltwiseF32& p) {
   }
 }
 
+// DecodeCenterSizeBoxes + MultiClassFastNMS (max_classes_per_detection 1)
+// + NonMaxSuppressionSingleClassHelper, in the reference's arithmetic order
+void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool) {
+  const int n = p.num_boxes;
+  struct Box {
+    float ymin, xmin, ymax, xmax;
+  };
+  std::vector<Box> boxes(static_cast<size_t>(n));
+  std::vector<float> max_score(static_cast<size_t>(n));
+  std::vector<int> best(static_cast<size_t>(n));
+  const int label_offset = p.num_classes_with_background - p.num_classes;
+  pool.ParallelFor(n, [&](long b, long e) {
+    for (long i = b; i < e; ++i) {
+      const float* be = p.box_encodings + 4 * i;
+      const float* an = p.anchors + 4 * i;
+      const float yc = static_cast<float>(static_cast<double>(be[0]) / static_cast<double>(p.scale_y) *
+                                              static_cast<double>(an[2]) +
+                                          static_cast<double>(an[0]));
+      const float xc = static_cast<float>(static_cast<double>(be[1]) / static_cast<double>(p.scale_x) *
+                                              static_cast<double>(an[3]) +
+                                          static_cast<double>(an[1]));
+      const float hh = static_cast<float>(0.5 * std::exp(static_cast<double>(be[2]) / static_cast<double>(p.scale_h)) *
+                                          static_cast<double>(an[2]));
+      const float hw = static_cast<float>(0.5 * std::exp(static_cast<double>(be[3]) / static_cast<double>(p.scale_w)) *
+                                          static_cast<double>(an[3]));
+      boxes[i] = {yc - hh, xc - hw, yc + hh, xc + hw};
+      const float* sc = p.class_scores + i * p.num_classes_with_background + label_offset;
+      int arg = 0;
+      float mx = sc[0];
+      for (int c = 1; c < p.num_classes; ++c)
+        if (sc[c] > mx) {
+          mx = sc[c];
+          arg = c;
+        }
+      max_score[i] = mx;
+      best[i] = arg;
+    }
+  });
+  std::vector<int> keep;
+  for (int i = 0; i < n; ++i)
+    if (max_score[i] >= p.score_threshold) keep.push_back(i);
+  std::stable_sort(keep.begin(), keep.end(), [&](int a, int b) { return max_score[a] > max_score[b]; });
+  const int out_size = std::min(static_cast<int>(keep.size()), p.max_detections);
+  std::vector<uint8_t> active(keep.size(), 1);
+  std::vector<int> selected;
+  auto area = [&](const Box& b) { return (b.ymax - b.ymin) * (b.xmax - b.xmin); };
+  for (size_t i = 0; i < keep.size() && static_cast<int>(selected.size()) < out_size; ++i) {
+    if (!active[i]) continue;
+    selected.push_back(keep[i]);
+    active[i] = 0;
+    const Box& bi = boxes[keep[i]];
+    const float ai = area(bi);
+    for (size_t j = i + 1; j < keep.size(); ++j) {
+      if (!active[j]) continue;
+      const Box& bj = boxes[keep[j]];
+      const float aj = area(bj);
+      float iou = 0.0f;
+      if (ai > 0.0f && aj > 0.0f) {
+        const float iy0 = std::max(bi.ymin, bj.ymin), ix0 = std::max(bi.xmin, bj.xmin);
+        const float iy1 = std::min(bi.ymax, bj.ymax), ix1 = std::min(bi.xmax, bj.xmax);
+        const float inter = std::max(iy1 - iy0, 0.0f) * std::max(ix1 - ix0, 0.0f);
+        iou = inter / (ai + aj - inter);
+      }
+      if (iou > p.iou_threshold) active[j] = 0;
+    }
+  }
+  std::memset(p.out_boxes, 0, sizeof(float) * 4 * p.max_detections);
+  std::memset(p.out_classes, 0, sizeof(float) * p.max_detections);
+  std::memset(p.out_scores, 0, sizeof(float) * p.max_detections);
+  for (size_t k = 0; k < selected.size(); ++k) {
+    const Box& b = boxes[selected[k]];
+    p.out_boxes[4 * k] = b.ymin;
+    p.out_boxes[4 * k + 1] = b.xmin;
+    p.out_boxes[4 * k + 2] = b.ymax;
+    p.out_boxes[4 * k + 3] = b.xmax;
+    p.out_classes[k] = static_cast<float>(best[selected[k]]);
+    p.out_scores[k] = max_score[selected[k]];
+  }
+  p.out_num[0] = static_cast<float>(selected.size());
+}
+
 }  // namespace hip
 }  // namespace band

@@ -74,5 +74,21 @@ struct CpuEltwiseF32 {
 };
 void CpuEltwiseFloat(const CpuEltwiseF32& p);
 
+// TFLite_Detection_PostProcess (CUSTOM, detection_postprocess.cc): float
+// inputs, fast class-agnostic NMS, one class per detection; CPU-only
+struct CpuDetectionParams {
+  int num_boxes, num_classes, num_classes_with_background, max_detections;
+  float score_threshold, iou_threshold;
+  float scale_y, scale_x, scale_h, scale_w;
+  const float* box_encodings;  // [num_boxes, 4] (y, x, h, w)
+  const float* class_scores;   // [num_boxes, num_classes_with_background]
+  const float* anchors;        // [num_boxes, 4] (y, x, h, w)
+  float* out_boxes;            // [max_detections, 4] (ymin, xmin, ymax, xmax)
+  float* out_classes;          // [max_detections]
+  float* out_scores;           // [max_detections]
+  float* out_num;              // [1]
+};
+void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool);
+
 }  // namespace hip
 }  // namespace band

@@ -211,8 +211,48 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
   }
 }
 
+namespace {
+// TFLite_Detection_PostProcess in the form the host kernel implements
+bool DetectionSupported(const TflModel& m, const TflOperator& op, CpuDetectionParams* p) {
+  if (op.builtin != kTflCustom || op.custom_code != "TFLite_Detection_PostProcess") return false;
+  if (op.inputs.size() != 3 || op.outputs.size() != 4) return false;
+  for (int t : op.inputs)
+    if (t < 0) return false;
+  const TflTensor& be = m.tensors[op.inputs[0]];
+  const TflTensor& cs = m.tensors[op.inputs[1]];
+  const TflTensor& an = m.tensors[op.inputs[2]];
+  if (be.type != DataType::kFloat32 || cs.type != DataType::kFloat32 || an.type != DataType::kFloat32 ||
+      !an.is_const())
+    return false;
+  FlexMap f;
+  if (!f.Parse(op.custom_options, op.custom_options_size)) return false;
+  if (f.Number("use_regular_nms", 0) != 0 || f.Number("max_classes_per_detection", 1) != 1) return false;
+  const int n = an.shape.empty() ? 0 : an.shape[0];
+  if (n <= 0 || be.num_elements() != static_cast<size_t>(n) * 4 || cs.num_elements() % n) return false;
+  CpuDetectionParams d{};
+  d.num_boxes = n;
+  d.num_classes = static_cast<int>(f.Number("num_classes", 0));
+  d.num_classes_with_background = static_cast<int>(cs.num_elements() / n);
+  d.max_detections = static_cast<int>(f.Number("max_detections", 0));
+  // options are read with AsFloat (float), detection_postprocess.cc Init()
+  d.score_threshold = static_cast<float>(f.Number("nms_score_threshold", 0));
+  d.iou_threshold = static_cast<float>(f.Number("nms_iou_threshold", 0));
+  d.scale_y = static_cast<float>(f.Number("y_scale", 0));
+  d.scale_x = static_cast<float>(f.Number("x_scale", 0));
+  d.scale_h = static_cast<float>(f.Number("h_scale", 0));
+  d.scale_w = static_cast<float>(f.Number("w_scale", 0));
+  if (d.num_classes <= 0 || d.num_classes > d.num_classes_with_background || d.max_detections <= 0) return false;
+  for (int k = 0; k < 4; ++k)
+    if (m.tensors[op.outputs[k]].type != DataType::kFloat32) return false;
+  if (m.tensors[op.outputs[0]].num_elements() != static_cast<size_t>(d.max_detections) * 4) return false;
+  if (p) *p = d;
+  return true;
+}
+}  // namespace
+
 bool HipModelExecutor::CpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   if (GpuSupports(m, op, nullptr)) return true;
+  if (DetectionSupported(m, op, nullptr)) return true;
   auto T = [&](int i) -> const TflTensor& { return m.tensors[i]; };
   if ((op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) && op.inputs.size() == 2 &&
       op.inputs[0] >= 0 && op.inputs[1] >= 0 && !op.outputs.empty()) {
@@ -1300,6 +1340,25 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.kind = Launch::kPool;
     L.kernel = "pool_kernel";
     L.alg_bytes = static_cast<double>(in.num_elements() + out.num_elements());
+  } else if (op.builtin == kTflCustom) {
+    // TFLite_Detection_PostProcess (CPU worker only: CpuSupports)
+    CpuDetectionParams& p = L.det;
+    if (!DetectionSupported(d, op, &p)) return absl::InternalError("unsupported custom op " + op.custom_code);
+    void* scores = nullptr;
+    void* anchors = nullptr;
+    void* outs[4];
+    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &scores));
+    RETURN_STATUS_IF(DevicePtr(model, op.inputs[2], sg, &anchors));
+    for (int k = 0; k < 4; ++k) RETURN_STATUS_IF(DevicePtr(model, op.outputs[k], sg, &outs[k]));
+    p.box_encodings = static_cast<const float*>(in_ptr);
+    p.class_scores = static_cast<const float*>(scores);
+    p.anchors = static_cast<const float*>(anchors);
+    p.out_boxes = static_cast<float*>(outs[0]);
+    p.out_classes = static_cast<float*>(outs[1]);
+    p.out_scores = static_cast<float*>(outs[2]);
+    p.out_num = static_cast<float*>(outs[3]);
+    L.kind = Launch::kDetectionPost;
+    L.kernel = "detection_postprocess_host";
   } else if (op.builtin == kTflTransposeConv) {
     RETURN_STATUS_IF(LowerTransposeConv(model, oi, out_ptr, ckey, sg, &L));
   } else if (op.builtin != kTflReshape && op.builtin != kTflSqueeze) {
@@ -1530,7 +1589,8 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
     case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
     case Launch::kZeroInsert: rc = bh_zero_insert(&l.zi, stream_); break;
-    case Launch::kEltwiseF32: return absl::InternalError("float eltwise is a CPU-worker op");
+    case Launch::kEltwiseF32:
+    case Launch::kDetectionPost: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }
@@ -1582,6 +1642,7 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
       case Launch::kSoftmax: CpuSoftmax(l.softmax); break;
       case Launch::kZeroInsert: CpuZeroInsert(l.zi); break;
       case Launch::kEltwiseF32: CpuEltwiseFloat(l.eltf); break;
+      case Launch::kDetectionPost: CpuDetectionPostprocess(l.det, pool); break;
       default: return absl::InternalError(std::string("no host implementation of ") + l.kernel);
     }
   }

@@ -38,7 +38,8 @@ struct Launch {
   enum Kind {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
-    kEltwiseF32  // CPU-only (float graphs, e.g. the reference's add.tflite)
+    kEltwiseF32,     // CPU-only (float graphs, e.g. the reference's add.tflite)
+    kDetectionPost   // CPU-only TFLite_Detection_PostProcess
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
@@ -55,6 +56,7 @@ struct Launch {
   bh_softmax_params softmax{};
   bh_zero_insert_params zi{};
   CpuEltwiseF32 eltf{};
+  CpuDetectionParams det{};
   const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
   long count = 0;               // kLut* / kQuantF32: elements
   float q_scale = 0.f;          // kQuantF32

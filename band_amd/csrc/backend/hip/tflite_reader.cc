@@ -267,9 +267,93 @@ bool TflModel::Parse(const uint8_t* buf, size_t size, std::string* error) {
       if (i < 0 || i >= nt) return fail("operator output index out of range");
     op.options_type = o.UInt8(3, 0);
     op.options = o.Table(4);
+    o.VecBytes(5, &op.custom_options, &op.custom_options_size);
     ops.push_back(std::move(op));
   }
   return true;
+}
+
+namespace {
+uint64_t ReadU(const uint8_t* p, int w) {
+  uint64_t v = 0;
+  for (int i = 0; i < w; ++i) v |= static_cast<uint64_t>(p[i]) << (8 * i);
+  return v;
+}
+int64_t ReadI(const uint8_t* p, int w) {
+  const uint64_t u = ReadU(p, w);
+  if (w >= 8) return static_cast<int64_t>(u);
+  const uint64_t sign = 1ull << (8 * w - 1);
+  return static_cast<int64_t>((u ^ sign) - sign);
+}
+}  // namespace
+
+// FlexBuffers: the root (offset, packed type, byte width) sits at the end;
+// a map's elements are preceded by [keys vector offset, keys width, size]
+// and followed by one packed type byte per element (type << 2 | width).
+bool FlexMap::Parse(const uint8_t* buf, size_t size) {
+  items_.clear();
+  if (!buf || size < 3) return false;
+  const int rw = buf[size - 1];
+  const uint8_t rtype = buf[size - 2];
+  if ((rtype >> 2) != 9 || (rw != 1 && rw != 2 && rw != 4 && rw != 8) || size < static_cast<size_t>(2 + rw))
+    return false;
+  const size_t root = size - 2 - rw;
+  const uint64_t off = ReadU(buf + root, rw);
+  if (off > root) return false;
+  const size_t m = root - off;
+  const int w = 1 << (rtype & 3);
+  if (m < static_cast<size_t>(3 * w)) return false;
+  const uint64_t n = ReadU(buf + m - w, w);
+  const int kw = static_cast<int>(ReadU(buf + m - 2 * w, w));
+  const uint64_t koff = ReadU(buf + m - 3 * w, w);
+  if (koff > m - 3 * w || (kw != 1 && kw != 2 && kw != 4 && kw != 8) || m + n * (w + 1) > size) return false;
+  const size_t keys = m - 3 * w - koff;
+  for (uint64_t i = 0; i < n; ++i) {
+    const size_t kp = keys + i * kw;
+    if (kp + kw > size) return false;
+    const uint64_t so = ReadU(buf + kp, kw);
+    if (so > kp) return false;
+    const size_t ks = kp - so;
+    size_t ke = ks;
+    while (ke < size && buf[ke]) ++ke;
+    if (ke >= size) return false;
+    const std::string key(reinterpret_cast<const char*>(buf + ks), ke - ks);
+    const uint8_t t = buf[m + n * w + i] >> 2;
+    const uint8_t* v = buf + m + i * w;
+    double value;
+    switch (t) {
+      case 1: value = static_cast<double>(ReadI(v, w)); break;       // INT
+      case 2: case 26: value = static_cast<double>(ReadU(v, w)); break;  // UINT / BOOL
+      case 3: {                                                        // FLOAT
+        if (w == 8) {
+          double d;
+          std::memcpy(&d, v, 8);
+          value = d;
+        } else if (w == 4) {
+          float f;
+          std::memcpy(&f, v, 4);
+          value = f;
+        } else {
+          return false;
+        }
+      } break;
+      default: continue;  // not a scalar this backend reads
+    }
+    items_.emplace_back(key, value);
+  }
+  return true;
+}
+
+bool FlexMap::Has(const std::string& key) const {
+  for (const auto& kv : items_)
+    if (kv.first == key) return true;
+  return false;
+}
+
+double FlexMap::Number(const std::string& key, double dflt) const {
+  for (const auto& kv : items_)
+    if (kv.first == key) return kv.second;
+  return dflt;
 }
 
 }  // namespace hip

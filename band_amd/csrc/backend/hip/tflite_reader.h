@@ -87,6 +87,20 @@ struct TflOperator {
   std::vector<int> inputs, outputs;
   int options_type = 0;
   FbTable options;  // builtin_options table (slot meanings per op, schema.fbs)
+  const uint8_t* custom_options = nullptr;  // FlexBuffers bytes (CUSTOM ops)
+  size_t custom_options_size = 0;
+};
+
+// Scalars of a FlexBuffers map (TFLite custom options, e.g.
+// TFLite_Detection_PostProcess's, detection_postprocess.cc Init()).
+class FlexMap {
+ public:
+  bool Parse(const uint8_t* buf, size_t size);
+  bool Has(const std::string& key) const;
+  double Number(const std::string& key, double dflt) const;
+
+ private:
+  std::vector<std::pair<std::string, double>> items_;
 };
 
 struct TflModel {

@@ -34,6 +34,57 @@ OPT = dict(Conv2DOptions=1, DepthwiseConv2DOptions=2, Pool2DOptions=5, FullyConn
 
 
 # ---------------------------------------------------------------------------
+# FlexBuffers map (the encoding of TFLite custom options)
+# ---------------------------------------------------------------------------
+FBT_INT, FBT_FLOAT, FBT_MAP, FBT_BOOL = 1, 3, 9, 26
+
+
+def flexbuffer_map(values):
+    """A FlexBuffers map of scalars: sorted keys, 8-byte elements.  Layout:
+    key strings, the typed key vector, [keys offset, keys width, size],
+    elements, one packed type byte per element, then the root (offset, type,
+    width)."""
+    buf = bytearray()
+
+    def align(n):
+        while len(buf) % n:
+            buf.append(0)
+
+    keys = sorted(values)
+    key_pos = []
+    for k in keys:
+        key_pos.append(len(buf))
+        buf += k.encode() + b"\0"
+    align(8)
+    buf += struct.pack("<Q", len(keys))
+    keys_start = len(buf)
+    for kp in key_pos:
+        buf += struct.pack("<Q", len(buf) - kp)
+    align(8)
+    buf += struct.pack("<Q", len(buf) - keys_start)  # keys vector, relative
+    buf += struct.pack("<Q", 8)                      # keys element width
+    buf += struct.pack("<Q", len(keys))
+    map_start = len(buf)
+    types = []
+    for k in keys:
+        v = values[k]
+        if isinstance(v, bool):
+            buf += struct.pack("<Q", int(v))
+            types.append(FBT_BOOL << 2 | 3)
+        elif isinstance(v, (int, np.integer)):
+            buf += struct.pack("<q", int(v))
+            types.append(FBT_INT << 2 | 3)
+        else:
+            buf += struct.pack("<d", float(v))
+            types.append(FBT_FLOAT << 2 | 3)
+    buf += bytes(types)
+    align(8)
+    buf += struct.pack("<Q", len(buf) - map_start)
+    buf += bytes([FBT_MAP << 2 | 3, 8])
+    return bytes(buf)
+
+
+# ---------------------------------------------------------------------------
 # minimal flatbuffer serializer
 # ---------------------------------------------------------------------------
 class Table:
@@ -183,12 +234,12 @@ class ModelBuilder:
                                  buffer=buf, scale=scale, zero_point=zero_point, qdim=qdim))
         return len(self.tensors) - 1
 
-    def op(self, builtin, inputs, outputs, options_type=0, options=None, custom=None):
+    def op(self, builtin, inputs, outputs, options_type=0, options=None, custom=None, custom_options=None):
         key = (OPC[builtin] if isinstance(builtin, str) else builtin, custom)
         if key not in self.opcodes:
             self.opcodes.append(key)
         self.ops.append(dict(opcode=self.opcodes.index(key), inputs=list(inputs), outputs=list(outputs),
-                             options_type=options_type, options=options))
+                             options_type=options_type, options=options, custom_options=custom_options))
         return len(self.ops) - 1
 
     def build(self):
@@ -209,6 +260,8 @@ class ModelBuilder:
             ot = Table().set(0, "I", o["opcode"]).set(1, "o", Vec("i", o["inputs"])).set(2, "o", Vec("i", o["outputs"]))
             if o["options_type"]:
                 ot.set(3, "B", o["options_type"]).set(4, "o", o["options"])
+            if o.get("custom_options") is not None:
+                ot.set(5, "o", Vec("B", o["custom_options"]))  # custom_options_format FLEXBUFFERS (0)
             ops.append(ot)
         sg = (Table().set(0, "o", VecT(tens)).set(1, "o", Vec("i", self.inputs))
               .set(2, "o", Vec("i", self.outputs)).set(3, "o", VecT(ops)).set(4, "o", Str("main")))
@@ -315,13 +368,26 @@ class QGraph:
         bs = (np.float32(in_scale) * (ws if len(ws) > 1 else np.repeat(ws, out_c))).astype(np.float32)
         return self.mb.tensor(self._name("bias"), [out_c], np.int32, scale=bs, zero_point=[0] * out_c, data=b)
 
-    def conv(self, x, out_c, k=1, stride=1, act="RELU6", padding="SAME", dilation=1):
+    def conv(self, x, out_c, k=1, stride=1, act="RELU6", padding="SAME", dilation=1, out_scale=None,
+             bias_offset_lsb=0):
+        """CONV_2D; `out_scale` overrides the output scale and
+        `bias_offset_lsb` shifts every output channel by that many output
+        LSBs (a detection head's class prior)"""
         shp, s_in, _ = self.meta[x]
         b, h, w, c = shp
         s_out, zp = self._out_q(act, s_in)
+        if out_scale is not None:
+            s_out = float(out_scale)
         K = k * k * c
         wt, ws = self._weights([out_c, k, k, c], out_c, 0, s_in, s_out, K)
         bt = self._bias(out_c, s_in, ws, K)
+        if bias_offset_lsb:
+            bias = self.mb.tensors[bt]
+            bufi = bias["buffer"]
+            vals = np.frombuffer(self.mb.buffers[bufi], np.int32).copy()
+            wsc = ws if len(ws) > 1 else np.repeat(ws, out_c)
+            vals += np.round(bias_offset_lsb * s_out / (s_in * wsc.astype(np.float64))).astype(np.int32)
+            self.mb.buffers[bufi] = vals.tobytes()
         eff = (k - 1) * dilation + 1
         oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
         ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
@@ -499,6 +565,27 @@ class QGraph:
         self.fshape[y] = list(self.fshape[a])
         return y
 
+    def detection_postprocess(self, boxes_f, scores_f, anchors, num_classes, max_detections=25,
+                              score_threshold=0.4, iou_threshold=0.5, scales=(10.0, 10.0, 5.0, 5.0)):
+        """TFLite_Detection_PostProcess (CUSTOM; fast NMS, one class per
+        detection): float box encodings [1,N,4], float class scores
+        [1,N,C(+1)], constant anchors [N,4] (y, x, h, w) -> boxes, classes,
+        scores, num_detections"""
+        n = anchors.shape[0]
+        a = self.mb.tensor(self._name("anchors"), [n, 4], np.float32, data=anchors.astype(np.float32))
+        outs = [self.mb.tensor(self._name("detection_boxes"), [1, max_detections, 4], np.float32),
+                self.mb.tensor(self._name("detection_classes"), [1, max_detections], np.float32),
+                self.mb.tensor(self._name("detection_scores"), [1, max_detections], np.float32),
+                self.mb.tensor(self._name("num_detections"), [1], np.float32)]
+        opts = flexbuffer_map(dict(max_detections=int(max_detections), max_classes_per_detection=1,
+                                   detections_per_class=100, use_regular_nms=False,
+                                   nms_score_threshold=float(score_threshold), nms_iou_threshold=float(iou_threshold),
+                                   num_classes=int(num_classes), y_scale=float(scales[0]), x_scale=float(scales[1]),
+                                   h_scale=float(scales[2]), w_scale=float(scales[3])))
+        self.mb.op("CUSTOM", [boxes_f, scores_f, a], outs, custom="TFLite_Detection_PostProcess",
+                   custom_options=opts)
+        return outs
+
     def quantize_float(self, xf, scale, zp=None):
         """QUANTIZE float32 -> 8-bit"""
         y = self.act_tensor(self.fshape[xf], scale, self._act_zp() if zp is None else zp)
@@ -619,6 +706,119 @@ def ssd_mobilenet_v2(dtype=np.int8, seed=1, size=224, batch=1, classes=91):
         scores.append(g.reshape(cl, [batch, h * w * anchors, classes]))
     g.output(g.concat(boxes, axis=1))
     g.output(g.logistic(g.concat(scores, axis=1)))
+    return g.build()
+
+
+def _round_filters(c, width):
+    """EfficientNet channel rounding to a multiple of 8"""
+    new = max(8, int(c * width + 4) // 8 * 8)
+    if new < 0.9 * c * width:
+        new += 8
+    return new
+
+
+# EfficientNet-B0 stages: (expand, kernel, stride, channels, repeats)
+EFFNET_STAGES = [(1, 3, 1, 16, 1), (6, 3, 2, 24, 2), (6, 5, 2, 40, 2), (6, 3, 2, 80, 3), (6, 5, 1, 112, 3),
+                 (6, 5, 2, 192, 4), (6, 3, 1, 320, 1)]
+
+
+def efficientdet_anchors(size, levels=(3, 4, 5, 6, 7), anchor_scale=4.0):
+    """normalised (ycenter, xcenter, h, w) per feature-map cell x 9 anchors,
+    in the order the heads' RESHAPE lays them out"""
+    out = []
+    for lvl in levels:
+        stride = 2 ** lvl
+        n = -(-size // stride)
+        for y in range(n):
+            for x in range(n):
+                for sc in (1.0, 2 ** (1 / 3), 2 ** (2 / 3)):
+                    for rh, rw in ((1.0, 1.0), (1.4, 0.7), (0.7, 1.4)):
+                        base = anchor_scale * stride * sc
+                        out.append(((y + 0.5) * stride / size, (x + 0.5) * stride / size,
+                                    base * rh / size, base * rw / size))
+    return np.array(out, np.float32)
+
+
+def efficientdet_lite2(dtype=np.int8, seed=4, size=448, batch=1, classes=90, fpn_channels=112, fpn_repeats=5,
+                       head_repeats=3, max_detections=25, postprocess=True):
+    """EfficientDet-Lite2 (BASELINE C4): EfficientNet-Lite2 backbone (width
+    1.1, depth 1.2, ReLU6, no squeeze-excite), BiFPN P3-P7 with 112
+    channels x 5 cells (sum fusion, separable convs, nearest upsampling,
+    3x3/s2 max-pool downsampling), separable-conv class / box heads with 9
+    anchors per cell, LOGISTIC scores, and TFLite_Detection_PostProcess
+    (CUSTOM) on DEQUANTIZEd boxes / scores - the op the GPU worker cannot
+    run, so the model analyzer splits the model there."""
+    g = QGraph(dtype, seed, "efficientdet_lite2_%s" % np.dtype(dtype).name)
+    x = g.input([batch, size, size, 3])
+    y = g.conv(x, 32, k=3, stride=2)
+    taps = []
+    n_stages = len(EFFNET_STAGES)
+    for si, (t, k, s_, c, r) in enumerate(EFFNET_STAGES):
+        c = _round_filters(c, 1.1)
+        reps = r if si in (0, n_stages - 1) else int(np.ceil(r * 1.2))
+        for i in range(reps):
+            stride = s_ if i == 0 else 1
+            cin = g.meta[y][0][3]
+            h = g.conv(y, cin * t, k=1) if t != 1 else y
+            h = g.dwconv(h, k=k, stride=stride)
+            h = g.conv(h, c, k=1, act="NONE")
+            y = g.add(h, y) if stride == 1 and cin == c else h
+        if si in (2, 4, 6):  # strides 8, 16, 32
+            taps.append(y)
+    F = fpn_channels
+    p3, p4, p5 = (g.conv(t_, F, k=1, act="NONE") for t_ in taps)
+    p6 = g.maxpool(g.conv(taps[2], F, k=1, act="NONE"), (3, 3), 2)
+    p7 = g.maxpool(p6, (3, 3), 2)
+    feats = [p3, p4, p5, p6, p7]
+
+    def size_of(t):
+        return tuple(g.meta[t][0][1:3])
+
+    def sep(t, act="NONE"):
+        return g.conv(g.dwconv(t, k=3, act="NONE"), F, k=1, act=act)
+
+    def fuse(*ts):
+        acc = ts[0]
+        for i, t in enumerate(ts[1:]):
+            acc = g.add(acc, t, act="RELU6" if i == len(ts) - 2 else "NONE")
+        return sep(acc)
+
+    for _ in range(fpn_repeats):
+        td = [None] * 5
+        td[4] = feats[4]
+        for l in (3, 2, 1):
+            td[l] = fuse(feats[l], g.resize(td[l + 1], size_of(feats[l])))
+        out = [None] * 5
+        out[0] = fuse(feats[0], g.resize(td[1], size_of(feats[0])))
+        for l in (1, 2, 3):
+            out[l] = fuse(feats[l], td[l], g.maxpool(out[l - 1], (3, 3), 2))
+        out[4] = fuse(feats[4], g.maxpool(out[3], (3, 3), 2))
+        feats = out
+
+    boxes, scores = [], []
+    for f in feats:
+        b_, h, w, _ = g.meta[f][0]
+        cl, bx = f, f
+        for _ in range(head_repeats):
+            cl = sep(cl, act="RELU6")
+            bx = sep(bx, act="RELU6")
+        # class prior: logits around -5.4, scale 4.6 / 60 (a few hundred anchors pass 0.4)
+        cl = g.conv(g.dwconv(cl, k=3, act="NONE"), 9 * classes, k=1, act="NONE", out_scale=4.6 / 60,
+                    bias_offset_lsb=-70)
+        bx = g.conv(g.dwconv(bx, k=3, act="NONE"), 9 * 4, k=1, act="NONE")
+        scores.append(g.reshape(cl, [batch, h * w * 9, classes]))
+        boxes.append(g.reshape(bx, [batch, h * w * 9, 4]))
+    box_enc = g.concat(boxes, axis=1)
+    cls = g.logistic(g.concat(scores, axis=1))
+    if not postprocess:
+        g.output(box_enc)
+        g.output(cls)
+        return g.build()
+    anchors = efficientdet_anchors(size)
+    outs = g.detection_postprocess(g.dequantize(box_enc), g.dequantize(cls), anchors, classes,
+                                   max_detections=max_detections)
+    for o in outs:
+        g.output(o)
     return g.build()
 
 

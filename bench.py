@@ -43,7 +43,11 @@ def parse():
                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4; <= 32)")
     p.add_argument("--model", default="mix_c3",
                    choices=["mix_c3", "mobilenet_v2_int8", "mobilenet_v2_uint8", "mobilenet_v1_int8",
-                            "ssd_mobilenet_v2_int8", "deeplab_v3_mobilenet_v2_int8", "posenet_mobilenet_v1_int8"])
+                            "ssd_mobilenet_v2_int8", "deeplab_v3_mobilenet_v2_int8", "posenet_mobilenet_v1_int8",
+                            "efficientdet_lite2_int8"])
+    p.add_argument("--cpu-workers", type=int, default=-1,
+                   help="Band CPU workers (worker ids first); default: 1 when the model has CPU-only ops")
+    p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
@@ -66,6 +70,8 @@ def model_list(name):
         return [(name, S.mobilenet_v2(np.uint8, seed=0))]
     if name == "mobilenet_v1_int8":
         return [(name, S.mobilenet_v1(np.int8, seed=0))]
+    if name == "efficientdet_lite2_int8":
+        return [(name, S.efficientdet_lite2(np.int8, size=448))]
     base = name[:-len("_int8")]
     return [(name, getattr(S, base)(np.int8))]
 
@@ -156,14 +162,21 @@ def main():
     if args.no_graph:
         os.environ["BAND_HIP_GRAPH"] = "0"
 
-    # this rank's Band engine: W GPU workers, all on the local MI355X
-    # (worker id -> device ordinal; each worker owns one HIP stream)
-    for w in range(W):
+    # this rank's Band engine: [CPU workers] + W GPU workers, all GPU
+    # workers on the local MI355X (worker id -> device ordinal; each worker
+    # owns one HIP stream)
+    n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if args.model == "efficientdet_lite2_int8" else 0)
+    workers = [DeviceFlag.kCPU] * n_cpu + [DeviceFlag.kGPU] * W
+    for w in range(n_cpu, n_cpu + W):
         band_amd.SetWorkerDevice(w, D.local_rank)
     sched = {"round_robin": SchedulerType.kRoundRobin, "fixed_worker": SchedulerType.kFixedWorker,
              "shortest_expected_latency": SchedulerType.kShortestExpectedLatency,
              "heterogeneous_earliest_finish_time": SchedulerType.kHeterogeneousEarliestFinishTime}[args.scheduler]
-    engine = Engine(make_config([sched], [DeviceFlag.kGPU] * W, num_warmups=3, num_runs=5))
+    if n_cpu and args.scheduler in ("round_robin", "fixed_worker"):
+        sched = SchedulerType.kHeterogeneousEarliestFinishTime  # a split model needs fallback subgraphs
+        args.scheduler = "heterogeneous_earliest_finish_time"
+    engine = Engine(make_config([sched], workers, num_threads=[args.cpu_threads] * n_cpu + [1] * W,
+                                num_warmups=3, num_runs=5))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + D.rank)
     for path in paths:
@@ -187,7 +200,7 @@ def main():
     D.barrier()
     elapsed = D.max(t1 - t0)
     all_lat = [x for part in D.gather((lat_us * 1e-6).tolist()) for x in part]
-    jobs_per_worker = np.bincount(worker_ids, minlength=W).tolist()
+    jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
 
     # profiling executors (outside the engine, same backend code) for the
     # per-kernel roofline and the device-side floor of a job
@@ -200,7 +213,10 @@ def main():
         ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
         if args.no_graph:
             ex.SetUseGraph(False)
-        assert ex.PrepareSubgraph(hm).ok()
+        spec = ex.InvestigateModelSpec(hm)
+        gpu_ops = [i for i in range(spec.num_ops) if i not in spec.unsupported_ops[DeviceFlag.kGPU]]
+        # a split model: profile its GPU part (ops before the first CPU-only op)
+        assert ex.PrepareSubgraph(hm, gpu_ops if len(gpu_ops) < spec.num_ops else ()).ok()
         execs0.append(ex)
         keys0.append(SubgraphKey(100 + mid, prof_wid))
         ex._model_ref = hm
@@ -264,8 +280,12 @@ def main():
             "config": {"workload": ("C3: 4-DNN int8 mix (%s), 224x224 batch-1 jobs through the Band engine, "
                                     "%s over %d Band GPU worker(s) per MI355X" %
                                     (", ".join(nm for nm, _ in models), args.scheduler, W))
-                       if M > 1 else ("C2: %s 224x224 batch-1 jobs through the Band engine, %s over %d Band GPU "
-                                      "worker(s) per MI355X" % (args.model, args.scheduler, W)),
+                       if M > 1 else (("C4: EfficientDet-Lite2 int8 448x448 batch-1 jobs through the Band engine, "
+                                       "model_analyzer split (network on GPU workers, TFLite_Detection_PostProcess "
+                                       "on %d CPU worker(s)), %s over %d Band GPU worker(s) per MI355X"
+                                       % (n_cpu, args.scheduler, W)) if args.model == "efficientdet_lite2_int8" else
+                                      ("C2: %s 224x224 batch-1 jobs through the Band engine, %s over %d Band GPU "
+                                       "worker(s) per MI355X" % (args.model, args.scheduler, W))),
                        "harness": "native Band engine (planner + workers + %s), %d requests in flight"
                                   % (args.scheduler, inflight),
                        "jobs_per_worker_rank0": jobs_per_worker,

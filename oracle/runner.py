@@ -399,7 +399,7 @@ class OracleInterpreter:
                  OP["MAX_POOL_2D"], OP["RESHAPE"], OP["SQUEEZE"], OP["CONCATENATION"], OP["PAD"],
                  OP["PADV2"], OP["QUANTIZE"], OP["DEQUANTIZE"], OP["RELU"], OP["RELU6"],
                  OP["RELU_N1_TO_1"], OP["LOGISTIC"], OP["SOFTMAX"], OP["RESIZE_NEAREST_NEIGHBOR"],
-                 OP["RESIZE_BILINEAR"], OP["TRANSPOSE_CONV"]}
+                 OP["RESIZE_BILINEAR"], OP["TRANSPOSE_CONV"], OP["CUSTOM"]}
 
     def __init__(self, model):
         self.model = model if isinstance(model, Model) else Model.from_path(model)
@@ -580,4 +580,8 @@ class OracleInterpreter:
             if ti.np_dtype != np.int8:
                 raise NotImplementedError("oracle: RESIZE_BILINEAR restated for int8 only")
             return [resize_bilinear_i8(x, (oh, ow), ac, hp)]
+        if code == OP["CUSTOM"] and o.custom == "TFLite_Detection_PostProcess":
+            from .detection_postprocess import detection_postprocess, read_flexbuffer_map
+            return list(detection_postprocess(vals[o.inputs[0]], vals[o.inputs[1]], vals[o.inputs[2]],
+                                              read_flexbuffer_map(o.custom_options)))
         raise NotImplementedError("oracle: op %s not restated" % o.name)

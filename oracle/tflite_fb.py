@@ -141,6 +141,8 @@ class Operator:
         self.outputs = [] if outs is None else [int(x) for x in outs]
         self.options_type = o.scalar(3, "B", 0)
         self.options = o.table(4)
+        co = o.vector(5, "u1")
+        self.custom_options = bytes(co) if co is not None else b""
 
     @property
     def name(self):

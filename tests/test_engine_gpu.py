@@ -122,3 +122,24 @@ def test_benchmark_tool_gpu_stream(gpu_lib, golden_dir):
     r = BenchmarkRun(cfg)
     assert r["failed"] == 0 and r["completed"] > 100
     assert min(r["jobs_per_worker"]) > 0
+
+
+def test_c4_efficientdet_split_heft(gpu_lib, tmp_path):
+    """C4's mechanism: EfficientDet-Lite2 with TFLite_Detection_PostProcess;
+    HEFT over [CPU, GPU, GPU] runs the network on a GPU worker and the
+    postprocess on the CPU worker; outputs bit-exact vs the oracle."""
+    path = _write(tmp_path, "edet.tflite", tflite_synth.efficientdet_lite2(size=256))
+    e = Engine(make_config([SchedulerType.kHeterogeneousEarliestFinishTime],
+                           [DeviceFlag.kCPU, DeviceFlag.kGPU, DeviceFlag.kGPU], num_threads=[8, 1, 1],
+                           subgraph_type=SubgraphPreparationType.kMergeUnitSubgraph))
+    m = _model(path)
+    assert e.RegisterModel(m)
+    subs = e.GetSubgraphs(m)
+    gpu = [k for k in subs if k[0] in (1, 2)]
+    cpu = [k for k in subs if k[0] == 0]
+    assert gpu and cpu
+    last_unit = max(k[1].bit_length() for k in subs) - 1
+    assert all(not (k[1] >> last_unit) & 1 for k in gpu)  # the postprocess unit never on a GPU
+    rng = np.random.default_rng(4)
+    xs = [rng.integers(-128, 128, (1, 256, 256, 3)).astype(np.int8) for _ in range(3)]
+    _run_and_check(e, m, path, xs)

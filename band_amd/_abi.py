@@ -106,6 +106,32 @@ class ZeroInsertParams(ctypes.Structure):
                                      "out_w")] + [("fill", ctypes.c_uint32), ("input", c_void_p), ("output", c_void_p)]
 
 
+class ConvF32Params(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "k_h", "k_w", "stride_h", "stride_w",
+        "dil_h", "dil_w", "pad_h", "pad_w", "depthwise", "depth_multiplier")] + [
+        ("act_min", ctypes.c_float), ("act_max", ctypes.c_float)] + [
+        (n, c_void_p) for n in ("input", "output", "weights", "bias")]
+
+
+class FcF32Params(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("rows", "depth", "units")] + [
+        ("act_min", ctypes.c_float), ("act_max", ctypes.c_float)] + [
+        (n, c_void_p) for n in ("input", "output", "weights", "bias")]
+
+
+class EltwiseF32Params(ctypes.Structure):
+    _fields_ = [("kind", c_int), ("shape_a", c_int * 4), ("shape_b", c_int * 4), ("shape_o", c_int * 4),
+                ("act_min", ctypes.c_float), ("act_max", ctypes.c_float)] + [(n, c_void_p) for n in ("a", "b", "out")]
+
+
+class PoolF32Params(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in (
+        "kind", "batch", "in_h", "in_w", "channels", "out_h", "out_w", "f_h", "f_w", "stride_h", "stride_w",
+        "pad_h", "pad_w")] + [("act_min", ctypes.c_float), ("act_max", ctypes.c_float)] + [
+        (n, c_void_p) for n in ("input", "output")]
+
+
 KERNEL_SYMBOLS = {
     "bh_device_count": (c_int, [ctypes.POINTER(c_int)]),
     "bh_set_device": (c_int, [c_int]),
@@ -147,6 +173,12 @@ KERNEL_SYMBOLS = {
     "bh_resize_bilinear_i8": (c_int, [ctypes.POINTER(ResizeBilinearParams), c_void_p]),
     "bh_softmax_i8": (c_int, [ctypes.POINTER(SoftmaxParams), c_void_p]),
     "bh_zero_insert": (c_int, [ctypes.POINTER(ZeroInsertParams), c_void_p]),
+    "bh_conv2d_f32": (c_int, [ctypes.POINTER(ConvF32Params), c_void_p]),
+    "bh_fc_f32": (c_int, [ctypes.POINTER(FcF32Params), c_void_p]),
+    "bh_eltwise_f32": (c_int, [ctypes.POINTER(EltwiseF32Params), c_void_p]),
+    "bh_pool_f32": (c_int, [ctypes.POINTER(PoolF32Params), c_void_p]),
+    "bh_unary_f32": (c_int, [c_int, c_void_p, c_void_p, ctypes.c_long, ctypes.c_float, ctypes.c_float, c_void_p]),
+    "bh_softmax_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_int, ctypes.c_float, c_void_p]),
     "bh_dwconv2d_i8": (c_int, [ctypes.POINTER(DwConvParams), c_void_p]),
     "bh_fc_i8": (c_int, [ctypes.POINTER(FcParams), c_void_p]),
     "bh_eltwise_i8": (c_int, [ctypes.POINTER(EltwiseParams), c_void_p]),

@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <limits>
 
 namespace band {
 namespace hip {
@@ -468,7 +469,61 @@ void CpuZeroInsert(const bh_zero_insert_params& p) {
                     static_cast<size_t>(p.channels));
 }
 
-void CpuEltwiseFloat(const CpuEltwiseF32& p) {
+namespace {
+inline float ClampF(float v, float lo, float hi) { return std::min(std::max(v, lo), hi); }
+}  // namespace
+
+void CpuConvF32(const bh_conv_f32_params& p, CpuPool& pool) {
+  const long pixels = static_cast<long>(p.batch) * p.out_h * p.out_w;
+  pool.ParallelFor(pixels, [&](long m0, long m1) {
+    std::vector<float> acc(static_cast<size_t>(p.out_c));
+    for (long m = m0; m < m1; ++m) {
+      const int ox = static_cast<int>(m % p.out_w);
+      const long t = m / p.out_w;
+      const int oy = static_cast<int>(t % p.out_h);
+      const int n = static_cast<int>(t / p.out_h);
+      std::fill(acc.begin(), acc.end(), 0.f);
+      for (int fy = 0; fy < p.k_h; ++fy) {
+        const int y = oy * p.stride_h - p.pad_h + fy * p.dil_h;
+        if (y < 0 || y >= p.in_h) continue;
+        for (int fx = 0; fx < p.k_w; ++fx) {
+          const int x = ox * p.stride_w - p.pad_w + fx * p.dil_w;
+          if (x < 0 || x >= p.in_w) continue;
+          const float* src = p.input + ((static_cast<long>(n) * p.in_h + y) * p.in_w + x) * p.in_c;
+          if (p.depthwise) {
+            const float* w = p.weights + static_cast<long>(fy * p.k_w + fx) * p.out_c;
+            for (int c = 0; c < p.out_c; ++c) acc[c] += src[c / p.depth_multiplier] * w[c];
+          } else {
+            const float* w = p.weights + static_cast<long>((fy * p.k_w + fx) * p.in_c) * p.out_c;
+            for (int ci = 0; ci < p.in_c; ++ci) {
+              const float xv = src[ci];
+              const float* wr = w + static_cast<long>(ci) * p.out_c;
+              for (int c = 0; c < p.out_c; ++c) acc[c] += xv * wr[c];
+            }
+          }
+        }
+      }
+      float* o = p.output + m * p.out_c;
+      for (int c = 0; c < p.out_c; ++c) o[c] = ClampF(acc[c] + (p.bias ? p.bias[c] : 0.f), p.act_min, p.act_max);
+    }
+  });
+}
+
+void CpuFcF32(const bh_fc_f32_params& p, CpuPool& pool) {
+  pool.ParallelFor(static_cast<long>(p.rows) * p.units, [&](long b, long e) {
+    for (long i = b; i < e; ++i) {
+      const long r = i / p.units;
+      const int u = static_cast<int>(i % p.units);
+      const float* x = p.input + r * p.depth;
+      const float* w = p.weights + static_cast<long>(u) * p.depth;
+      float acc = 0.f;
+      for (int k = 0; k < p.depth; ++k) acc += x[k] * w[k];
+      p.output[i] = ClampF(acc + (p.bias ? p.bias[u] : 0.f), p.act_min, p.act_max);
+    }
+  });
+}
+
+void CpuEltwiseF32(const bh_eltwise_f32_params& p) {
   const int* so = p.shape_o;
   const long n = static_cast<long>(so[0]) * so[1] * so[2] * so[3];
   auto index = [](const int* s, long i0, long i1, long i2, long i3) {
@@ -481,8 +536,48 @@ void CpuEltwiseFloat(const CpuEltwiseF32& p) {
     const long i1 = t2 % so[1], i0 = t2 / so[1];
     const float a = p.a[index(p.shape_a, i0, i1, i2, i3)];
     const float b = p.b[index(p.shape_b, i0, i1, i2, i3)];
-    const float v = p.kind == 0 ? a + b : (p.kind == 1 ? a - b : a * b);
-    p.out[i] = std::min(std::max(v, p.act_min), p.act_max);
+    const float v = p.kind == BH_ELTF_ADD ? a + b : (p.kind == BH_ELTF_SUB ? a - b : a * b);
+    p.out[i] = ClampF(v, p.act_min, p.act_max);
+  }
+}
+
+void CpuPoolF32(const bh_pool_f32_params& p) {
+  long i = 0;
+  for (int n = 0; n < p.batch; ++n)
+    for (int oy = 0; oy < p.out_h; ++oy)
+      for (int ox = 0; ox < p.out_w; ++ox) {
+        const int y0 = oy * p.stride_h - p.pad_h, x0 = ox * p.stride_w - p.pad_w;
+        const int fy0 = std::max(0, -y0), fy1 = std::min(p.f_h, p.in_h - y0);
+        const int fx0 = std::max(0, -x0), fx1 = std::min(p.f_w, p.in_w - x0);
+        for (int c = 0; c < p.channels; ++c, ++i) {
+          float acc = p.kind == BH_POOL_AVG ? 0.f : -std::numeric_limits<float>::infinity();
+          int cnt = 0;
+          for (int fy = fy0; fy < fy1; ++fy)
+            for (int fx = fx0; fx < fx1; ++fx) {
+              const float v = p.input[((static_cast<long>(n) * p.in_h + y0 + fy) * p.in_w + x0 + fx) * p.channels + c];
+              acc = p.kind == BH_POOL_AVG ? acc + v : std::max(acc, v);
+              ++cnt;
+            }
+          if (p.kind == BH_POOL_AVG) acc = acc / static_cast<float>(cnt);
+          p.output[i] = ClampF(acc, p.act_min, p.act_max);
+        }
+      }
+}
+
+void CpuUnaryF32(int kind, const float* in, float* out, long n, float lo, float hi) {
+  for (long i = 0; i < n; ++i)
+    out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + std::exp(-in[i])) : ClampF(in[i], lo, hi);
+}
+
+void CpuSoftmaxF32(const float* in, float* out, long rows, int depth, float beta) {
+  for (long r = 0; r < rows; ++r) {
+    const float* x = in + r * depth;
+    float* y = out + r * depth;
+    float mx = -std::numeric_limits<float>::infinity();
+    for (int k = 0; k < depth; ++k) mx = std::max(mx, x[k]);
+    float sum = 0.f;
+    for (int k = 0; k < depth; ++k) sum += std::exp((x[k] - mx) * beta);
+    for (int k = 0; k < depth; ++k) y[k] = std::exp((x[k] - mx) * beta) / sum;
   }
 }
 

@@ -62,17 +62,13 @@ void CpuResizeBilinear(const bh_resize_bilinear_params& p);
 void CpuSoftmax(const bh_softmax_params& p);
 void CpuZeroInsert(const bh_zero_insert_params& p);
 
-// float32 elementwise ADD / SUB / MUL with 4-D broadcast and a fused
-// activation clamp (kernels/add.cc float path); CPU-only
-struct CpuEltwiseF32 {
-  int kind;  // 0 add, 1 sub, 2 mul
-  int shape_a[4], shape_b[4], shape_o[4];
-  float act_min, act_max;
-  const float* a;
-  const float* b;
-  float* out;
-};
-void CpuEltwiseFloat(const CpuEltwiseF32& p);
+// float32 graphs (the bh_*_f32 kernels' host forms)
+void CpuConvF32(const bh_conv_f32_params& p, CpuPool& pool);
+void CpuFcF32(const bh_fc_f32_params& p, CpuPool& pool);
+void CpuEltwiseF32(const bh_eltwise_f32_params& p);
+void CpuPoolF32(const bh_pool_f32_params& p);
+void CpuUnaryF32(int kind, const float* in, float* out, long n, float lo, float hi);
+void CpuSoftmaxF32(const float* in, float* out, long rows, int depth, float beta);
 
 // TFLite_Detection_PostProcess (CUSTOM, detection_postprocess.cc): float
 // inputs, fast class-agnostic NMS, one class per detection; CPU-only

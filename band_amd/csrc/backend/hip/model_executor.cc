@@ -78,6 +78,139 @@ HipModelExecutor::~HipModelExecutor() {
   subgraphs_.clear();
 }
 
+namespace {
+// TFLite fp16 post-training quantization keeps constants in float16 behind
+// DEQUANTIZE ops; such a tensor is a constant of the float graph
+const TflOperator* ProducerOf(const TflModel& m, int t) {
+  for (const TflOperator& op : m.ops)
+    for (int o : op.outputs)
+      if (o == t) return &op;
+  return nullptr;
+}
+bool FoldableF16(const TflModel& m, int t) {
+  if (t < 0 || m.tensors[t].type != DataType::kFloat32) return false;
+  const TflOperator* p = ProducerOf(m, t);
+  return p && p->builtin == kTflDequantize && !p->inputs.empty() && p->inputs[0] >= 0 &&
+         m.tensors[p->inputs[0]].is_const() && m.tensors[p->inputs[0]].type == DataType::kFloat16;
+}
+bool ConstFloat(const TflModel& m, int t) {
+  return t >= 0 && ((m.tensors[t].is_const() && m.tensors[t].type == DataType::kFloat32) || FoldableF16(m, t));
+}
+float HalfToFloat(uint16_t h) {
+  const uint32_t sign = (h & 0x8000u) << 16;
+  uint32_t exp = (h >> 10) & 0x1fu, man = h & 0x3ffu, bits;
+  if (exp == 0) {
+    if (man == 0) {
+      bits = sign;
+    } else {  // subnormal: renormalise
+      exp = 127 - 15 + 1;
+      while (!(man & 0x400u)) {
+        man <<= 1;
+        --exp;
+      }
+      bits = sign | (exp << 23) | ((man & 0x3ffu) << 13);
+    }
+  } else if (exp == 31) {
+    bits = sign | 0x7f800000u | (man << 13);
+  } else {
+    bits = sign | ((exp + 127 - 15) << 23) | (man << 13);
+  }
+  float f;
+  std::memcpy(&f, &bits, 4);
+  return f;
+}
+// float values of a ConstFloat tensor
+std::vector<float> FloatData(const TflModel& m, int t) {
+  const TflTensor* src = &m.tensors[t];
+  if (!src->is_const()) src = &m.tensors[ProducerOf(m, t)->inputs[0]];
+  const size_t n = src->num_elements();
+  std::vector<float> v(n);
+  if (src->type == DataType::kFloat32) {
+    std::memcpy(v.data(), src->data, 4 * n);
+  } else {
+    for (size_t i = 0; i < n; ++i) {
+      uint16_t h;
+      std::memcpy(&h, src->data + 2 * i, 2);
+      v[i] = HalfToFloat(h);
+    }
+  }
+  return v;
+}
+// fused activation bounds of a float op (kernels/kernel_util.h
+// CalculateActivationRange)
+void FloatActRange(int act, float* lo, float* hi) {
+  const float inf = std::numeric_limits<float>::infinity();
+  *lo = act == 1 || act == 3 ? 0.f : (act == 2 ? -1.f : -inf);
+  *hi = act == 3 ? 6.f : (act == 2 ? 1.f : inf);
+}
+bool IsFloatOp(const TflModel& m, const TflOperator& op) {
+  if (op.inputs.empty() || op.inputs[0] < 0) return false;
+  const DataType t = m.tensors[op.inputs[0]].type;
+  switch (op.builtin) {
+    case kTflConv2D: case kTflDepthwiseConv2D: case kTflFullyConnected: case kTflAdd: case kTflSub: case kTflMul:
+    case kTflAveragePool2D: case kTflMaxPool2D: case kTflRelu: case kTflRelu6: case kTflReluN1To1:
+    case kTflLogistic: case kTflSoftmax:
+      return t == DataType::kFloat32;
+    case kTflDequantize:
+      return t == DataType::kFloat16;
+    default:
+      return false;
+  }
+}
+// the float32 op set (fp16-weight models)
+bool FloatSupports(const TflModel& m, const TflOperator& op, std::string* why) {
+  auto no = [&](const char* w) {
+    if (why) *why = w;
+    return false;
+  };
+  const TflTensor& in = m.tensors[op.inputs[0]];
+  const TflTensor& out = m.tensors[op.outputs[0]];
+  if (op.builtin == kTflDequantize)
+    return in.is_const() && out.type == DataType::kFloat32 ? true : no("float16 DEQUANTIZE of a constant only");
+  if (out.type != DataType::kFloat32) return no("float32 output expected");
+  switch (op.builtin) {
+    case kTflConv2D:
+    case kTflDepthwiseConv2D:
+    case kTflFullyConnected: {
+      if (op.inputs.size() < 2 || !ConstFloat(m, op.inputs[1])) return no("filter must be a float constant");
+      if (op.inputs.size() > 2 && op.inputs[2] >= 0 && !ConstFloat(m, op.inputs[2]))
+        return no("bias must be a float constant");
+      const TflTensor& w = m.tensors[op.inputs[1]];
+      if (op.builtin == kTflFullyConnected)
+        return w.shape.size() == 2 && w.shape[1] > 0 && in.num_elements() % w.shape[1] == 0 ? true
+                                                                                          : no("FC weights");
+      if (in.shape.size() != 4 || w.shape.size() != 4 || out.shape.size() != 4) return no("conv needs 4-D");
+      if (op.builtin == kTflConv2D && w.shape[3] != in.shape[3]) return no("grouped conv unsupported");
+      if (op.builtin == kTflDepthwiseConv2D && (in.shape[3] == 0 || w.shape[3] % in.shape[3] != 0))
+        return no("bad depth multiplier");
+      return true;
+    }
+    case kTflAdd:
+    case kTflSub:
+    case kTflMul: {
+      if (op.inputs.size() != 2 || op.inputs[1] < 0) return no("binary op needs 2 inputs");
+      const TflTensor& b = m.tensors[op.inputs[1]];
+      if (b.type != DataType::kFloat32 || in.shape.size() > 4 || b.shape.size() > 4 || out.shape.size() > 4)
+        return no("float32, rank <= 4");
+      int sa[4], sb[4], so[4];
+      Shape4(in.shape, sa);
+      Shape4(b.shape, sb);
+      Shape4(out.shape, so);
+      for (int d = 0; d < 4; ++d)
+        if ((sa[d] != so[d] && sa[d] != 1) || (sb[d] != so[d] && sb[d] != 1)) return no("bad broadcast");
+      return true;
+    }
+    case kTflAveragePool2D:
+    case kTflMaxPool2D:
+      return in.shape.size() == 4 ? true : no("4-D only");
+    case kTflSoftmax:
+      return !in.shape.empty() ? true : no("rank >= 1");
+    default:
+      return true;  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC
+  }
+}
+}  // namespace
+
 bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   auto no = [&](const char* w) {
     if (why) *why = w;
@@ -87,6 +220,7 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
   if (op.inputs.empty() || op.outputs.empty() || op.inputs[0] < 0) return no("no operands");
   const TflTensor& in = T(op.inputs[0]);
   const TflTensor& out = T(op.outputs[0]);
+  if (IsFloatOp(m, op)) return FloatSupports(m, op, why);
   switch (op.builtin) {
     case kTflConv2D:
     case kTflDepthwiseConv2D:
@@ -253,23 +387,6 @@ bool DetectionSupported(const TflModel& m, const TflOperator& op, CpuDetectionPa
 bool HipModelExecutor::CpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   if (GpuSupports(m, op, nullptr)) return true;
   if (DetectionSupported(m, op, nullptr)) return true;
-  auto T = [&](int i) -> const TflTensor& { return m.tensors[i]; };
-  if ((op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) && op.inputs.size() == 2 &&
-      op.inputs[0] >= 0 && op.inputs[1] >= 0 && !op.outputs.empty()) {
-    const TflTensor& a = T(op.inputs[0]);
-    const TflTensor& b = T(op.inputs[1]);
-    const TflTensor& o = T(op.outputs[0]);
-    if (a.type == DataType::kFloat32 && b.type == DataType::kFloat32 && o.type == DataType::kFloat32 &&
-        a.shape.size() <= 4 && b.shape.size() <= 4 && o.shape.size() <= 4) {
-      int sa[4], sb[4], so[4];
-      Shape4(a.shape, sa);
-      Shape4(b.shape, sb);
-      Shape4(o.shape, so);
-      bool ok = true;
-      for (int d = 0; d < 4; ++d) ok &= (sa[d] == so[d] || sa[d] == 1) && (sb[d] == so[d] || sb[d] == 1);
-      if (ok) return true;
-    }
-  }
   return GpuSupports(m, op, why);
 }
 
@@ -1099,6 +1216,186 @@ bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, Prepare
   return true;
 }
 
+// float32 graphs (fp16-weight models): constants (fp16 behind DEQUANTIZE,
+// or float32) are folded on the host into the layouts the bh_*_f32 kernels
+// read; a DEQUANTIZE whose consumers all fold it emits nothing.
+absl::Status HipModelExecutor::LowerFloat(const HipModel& model, int oi, void* in_ptr, void* out_ptr,
+                                          const std::string& ckey, PreparedSubgraph* sg, Launch* L, bool* emit) {
+  const TflModel& d = model.desc();
+  const TflOperator& op = d.ops[oi];
+  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
+  const TflTensor& in = T(op.inputs[0]);
+  const TflTensor& out = T(op.outputs[0]);
+  const double io_bytes = 4.0 * (static_cast<double>(in.num_elements()) + out.num_elements());
+  L->alg_bytes = io_bytes;
+  auto upload = [&](const std::string& key, const std::vector<float>& v, const void** dev) {
+    return UploadConst(key, v.data(), v.size() * sizeof(float), sg, dev);
+  };
+  switch (op.builtin) {
+    case kTflDequantize: {
+      const int t = op.outputs[0];
+      bool all_fold = true;
+      for (int c : consumers_[t]) {
+        const TflOperator& co = d.ops[c];
+        const bool folds = (co.builtin == kTflConv2D || co.builtin == kTflDepthwiseConv2D ||
+                            co.builtin == kTflFullyConnected) &&
+                           co.inputs[0] != t;
+        all_fold = all_fold && folds;
+      }
+      std::set<int> subgraph_outputs(sg->outputs.begin(), sg->outputs.end());
+      if (all_fold && !subgraph_outputs.count(t) && !sg->no_fuse.count(t)) {
+        *emit = false;
+        return absl::OkStatus();
+      }
+      const void* dev = nullptr;
+      RETURN_STATUS_IF(upload(ckey + "/f32", FloatData(d, t), &dev));
+      L->kind = Launch::kCopy;
+      L->kernel = "copy";
+      L->src = dev;
+      L->dst = out_ptr;
+      L->bytes = 4 * out.num_elements();
+      L->alg_bytes = 2.0 * L->bytes;
+      return absl::OkStatus();
+    }
+    case kTflConv2D:
+    case kTflDepthwiseConv2D: {
+      const bool dw = op.builtin == kTflDepthwiseConv2D;
+      const TflTensor& w = T(op.inputs[1]);
+      const FbTable& o = op.options;
+      const bool same = o.Int8(0, 0) == 0;
+      const int sw = o.Int(1, 1), sh = o.Int(2, 1);
+      const int act = dw ? o.Int8(4, 0) : o.Int8(3, 0);
+      const int dlw = dw ? o.Int(5, 1) : o.Int(4, 1);
+      const int dlh = dw ? o.Int(6, 1) : o.Int(5, 1);
+      const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], ic = in.shape[3];
+      const int oc = dw ? w.shape[3] : w.shape[0];
+      const int kh = w.shape[1], kw = w.shape[2];
+      const int oh = ComputeOutSize(same, ih, kh, sh, dlh), ow = ComputeOutSize(same, iw, kw, sw, dlw);
+      if (out.shape != std::vector<int>{b, oh, ow, oc}) return absl::InternalError("conv output shape mismatch");
+      std::vector<float> wf = FloatData(d, op.inputs[1]);
+      std::vector<float> laid(wf.size());
+      if (dw) {
+        laid = wf;  // [1][kh][kw][oc] is already [kh*kw][oc]
+      } else {
+        const int K = kh * kw * ic;  // OHWI -> [K][oc]
+        for (int c = 0; c < oc; ++c)
+          for (int k = 0; k < K; ++k) laid[static_cast<size_t>(k) * oc + c] = wf[static_cast<size_t>(c) * K + k];
+      }
+      bh_conv_f32_params& p = L->convf;
+      p = bh_conv_f32_params{};
+      const void* wdev = nullptr;
+      RETURN_STATUS_IF(upload(ckey + "/w", laid, &wdev));
+      p.weights = static_cast<const float*>(wdev);
+      if (op.inputs.size() > 2 && op.inputs[2] >= 0) {
+        const void* bdev = nullptr;
+        RETURN_STATUS_IF(upload(ckey + "/b", FloatData(d, op.inputs[2]), &bdev));
+        p.bias = static_cast<const float*>(bdev);
+      }
+      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic; p.out_h = oh; p.out_w = ow; p.out_c = oc;
+      p.k_h = kh; p.k_w = kw; p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw;
+      p.pad_h = ComputePadding(sh, dlh, ih, kh, oh);
+      p.pad_w = ComputePadding(sw, dlw, iw, kw, ow);
+      p.depthwise = dw ? 1 : 0;
+      p.depth_multiplier = dw ? oc / ic : 1;
+      FloatActRange(act, &p.act_min, &p.act_max);
+      p.input = static_cast<const float*>(in_ptr);
+      p.output = static_cast<float*>(out_ptr);
+      L->kind = Launch::kConvF32;
+      L->kernel = dw ? "dwconv_f32_kernel" : "conv_f32_kernel";
+      L->alg_ops = 2.0 * b * oh * ow * oc * kh * kw * (dw ? 1 : ic);
+      L->alg_bytes = io_bytes + 4.0 * laid.size() + 4.0 * oc;
+      return absl::OkStatus();
+    }
+    case kTflFullyConnected: {
+      const TflTensor& w = T(op.inputs[1]);
+      const int units = w.shape[0], depth = w.shape[1];
+      bh_fc_f32_params& p = L->fcf;
+      p = bh_fc_f32_params{};
+      const void* wdev = nullptr;
+      RETURN_STATUS_IF(upload(ckey + "/w", FloatData(d, op.inputs[1]), &wdev));
+      p.weights = static_cast<const float*>(wdev);
+      if (op.inputs.size() > 2 && op.inputs[2] >= 0) {
+        const void* bdev = nullptr;
+        RETURN_STATUS_IF(upload(ckey + "/b", FloatData(d, op.inputs[2]), &bdev));
+        p.bias = static_cast<const float*>(bdev);
+      }
+      p.rows = static_cast<int>(in.num_elements() / depth);
+      p.depth = depth;
+      p.units = units;
+      FloatActRange(op.options.valid() ? op.options.Int8(0, 0) : 0, &p.act_min, &p.act_max);
+      p.input = static_cast<const float*>(in_ptr);
+      p.output = static_cast<float*>(out_ptr);
+      L->kind = Launch::kFcF32;
+      L->kernel = "fc_f32_kernel";
+      L->alg_ops = 2.0 * p.rows * units * depth;
+      L->alg_bytes = io_bytes + 4.0 * units * depth;
+      return absl::OkStatus();
+    }
+    case kTflAdd:
+    case kTflSub:
+    case kTflMul: {
+      const TflTensor& bt = T(op.inputs[1]);
+      void* b_ptr = nullptr;
+      RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
+      bh_eltwise_f32_params& p = L->eltf;
+      p = bh_eltwise_f32_params{};
+      p.kind = op.builtin == kTflAdd ? BH_ELTF_ADD : (op.builtin == kTflSub ? BH_ELTF_SUB : BH_ELTF_MUL);
+      Shape4(in.shape, p.shape_a);
+      Shape4(bt.shape, p.shape_b);
+      Shape4(out.shape, p.shape_o);
+      FloatActRange(op.options.valid() ? op.options.Int8(0, 0) : 0, &p.act_min, &p.act_max);
+      p.a = static_cast<const float*>(in_ptr);
+      p.b = static_cast<const float*>(b_ptr);
+      p.out = static_cast<float*>(out_ptr);
+      L->kind = Launch::kEltwiseF32;
+      L->kernel = "eltwise_f32_kernel";
+      L->alg_bytes += 4.0 * bt.num_elements();
+      return absl::OkStatus();
+    }
+    case kTflAveragePool2D:
+    case kTflMaxPool2D: {
+      const FbTable& o = op.options;
+      const bool same = o.Int8(0, 0) == 0;
+      const int sw = o.Int(1, 1), sh = o.Int(2, 1), fw = o.Int(3, 1), fh = o.Int(4, 1);
+      bh_pool_f32_params& p = L->poolf;
+      p = bh_pool_f32_params{};
+      p.kind = op.builtin == kTflAveragePool2D ? BH_POOL_AVG : BH_POOL_MAX;
+      p.batch = in.shape[0]; p.in_h = in.shape[1]; p.in_w = in.shape[2]; p.channels = in.shape[3];
+      p.out_h = ComputeOutSize(same, p.in_h, fh, sh, 1);
+      p.out_w = ComputeOutSize(same, p.in_w, fw, sw, 1);
+      p.f_h = fh; p.f_w = fw; p.stride_h = sh; p.stride_w = sw;
+      p.pad_h = ComputePadding(sh, 1, p.in_h, fh, p.out_h);
+      p.pad_w = ComputePadding(sw, 1, p.in_w, fw, p.out_w);
+      FloatActRange(o.Int8(5, 0), &p.act_min, &p.act_max);
+      p.input = static_cast<const float*>(in_ptr);
+      p.output = static_cast<float*>(out_ptr);
+      L->kind = Launch::kPoolF32;
+      L->kernel = "pool_f32_kernel";
+      return absl::OkStatus();
+    }
+    case kTflSoftmax:
+      L->kind = Launch::kSoftmaxF32;
+      L->kernel = "softmax_f32_kernel";
+      L->beta = op.options.valid() ? op.options.Float(0, 1.0f) : 1.0f;
+      L->depth = in.shape.back();
+      L->count = static_cast<long>(in.num_elements() / std::max(L->depth, 1));
+      L->src = in_ptr;
+      L->dst = out_ptr;
+      return absl::OkStatus();
+    default: {  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC
+      L->kind = Launch::kUnaryF32;
+      L->kernel = "unary_f32_kernel";
+      L->unary_kind = op.builtin == kTflLogistic ? BH_UNARY_LOGISTIC : BH_UNARY_CLAMP;
+      L->lo = op.builtin == kTflReluN1To1 ? -1.f : 0.f;
+      L->hi = op.builtin == kTflRelu6 ? 6.f : (op.builtin == kTflReluN1To1 ? 1.f : std::numeric_limits<float>::infinity());
+      L->count = static_cast<long>(in.num_elements());
+      L->src = in_ptr;
+      L->dst = out_ptr;
+      return absl::OkStatus();
+    }
+  }
+}
+
 absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubgraph* sg) {
   const TflModel& d = model.desc();
   const TflOperator& op = d.ops[oi];
@@ -1120,6 +1417,12 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
   L.op_index = oi;
   L.out_tensor = op.outputs[0];
 
+  if (IsFloatOp(d, op)) {
+    bool emit = true;
+    RETURN_STATUS_IF(LowerFloat(model, oi, in_ptr, out_ptr, ckey, sg, &L, &emit));
+    if (emit) sg->launches.push_back(L);
+    return absl::OkStatus();
+  }
   if (op.builtin == kTflConv2D || op.builtin == kTflDepthwiseConv2D) {
     const bool dw = op.builtin == kTflDepthwiseConv2D;
     const TflTensor& w = T(op.inputs[1]);
@@ -1271,25 +1574,6 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.alg_ops = 2.0 * rows * units * depth;
     L.alg_bytes = static_cast<double>(rows) * depth + static_cast<double>(rows) * units +
                   static_cast<double>(units) * depth + 12.0 * units;
-  } else if ((op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) &&
-             in.type == DataType::kFloat32) {
-    // float graph on the CPU worker (add.cc float path, fused activation)
-    const TflTensor& b = T(op.inputs[1]);
-    void* b_ptr = nullptr;
-    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
-    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
-    CpuEltwiseF32& p = L.eltf;
-    p.kind = op.builtin == kTflAdd ? 0 : (op.builtin == kTflSub ? 1 : 2);
-    Shape4(in.shape, p.shape_a);
-    Shape4(b.shape, p.shape_b);
-    Shape4(out.shape, p.shape_o);
-    p.act_min = act == 1 || act == 3 ? 0.f : (act == 2 ? -1.f : -std::numeric_limits<float>::infinity());
-    p.act_max = act == 3 ? 6.f : (act == 2 ? 1.f : std::numeric_limits<float>::infinity());
-    p.a = static_cast<const float*>(in_ptr);
-    p.b = static_cast<const float*>(b_ptr);
-    p.out = static_cast<float*>(out_ptr);
-    L.kind = Launch::kEltwiseF32;
-    L.kernel = "eltwise_f32_host";
   } else if (op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) {
     const TflTensor& b = T(op.inputs[1]);
     void* b_ptr = nullptr;
@@ -1589,7 +1873,18 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
     case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
     case Launch::kZeroInsert: rc = bh_zero_insert(&l.zi, stream_); break;
-    case Launch::kEltwiseF32:
+    case Launch::kConvF32: rc = bh_conv2d_f32(&l.convf, stream_); break;
+    case Launch::kFcF32: rc = bh_fc_f32(&l.fcf, stream_); break;
+    case Launch::kEltwiseF32: rc = bh_eltwise_f32(&l.eltf, stream_); break;
+    case Launch::kPoolF32: rc = bh_pool_f32(&l.poolf, stream_); break;
+    case Launch::kUnaryF32:
+      rc = bh_unary_f32(l.unary_kind, static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.lo,
+                        l.hi, stream_);
+      break;
+    case Launch::kSoftmaxF32:
+      rc = bh_softmax_f32(static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.depth, l.beta,
+                          stream_);
+      break;
     case Launch::kDetectionPost: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
@@ -1641,7 +1936,16 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
       case Launch::kResizeBilinear: CpuResizeBilinear(l.rbil); break;
       case Launch::kSoftmax: CpuSoftmax(l.softmax); break;
       case Launch::kZeroInsert: CpuZeroInsert(l.zi); break;
-      case Launch::kEltwiseF32: CpuEltwiseFloat(l.eltf); break;
+      case Launch::kConvF32: CpuConvF32(l.convf, pool); break;
+      case Launch::kFcF32: CpuFcF32(l.fcf, pool); break;
+      case Launch::kEltwiseF32: CpuEltwiseF32(l.eltf); break;
+      case Launch::kPoolF32: CpuPoolF32(l.poolf); break;
+      case Launch::kUnaryF32:
+        CpuUnaryF32(l.unary_kind, static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.lo, l.hi);
+        break;
+      case Launch::kSoftmaxF32:
+        CpuSoftmaxF32(static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.depth, l.beta);
+        break;
       case Launch::kDetectionPost: CpuDetectionPostprocess(l.det, pool); break;
       default: return absl::InternalError(std::string("no host implementation of ") + l.kernel);
     }

@@ -38,7 +38,7 @@ struct Launch {
   enum Kind {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
-    kEltwiseF32,     // CPU-only (float graphs, e.g. the reference's add.tflite)
+    kConvF32, kFcF32, kEltwiseF32, kPoolF32, kUnaryF32, kSoftmaxF32,  // float32 graphs
     kDetectionPost   // CPU-only TFLite_Detection_PostProcess
   } kind;
   int op_index = -1;
@@ -55,7 +55,13 @@ struct Launch {
   bh_resize_bilinear_params rbil{};
   bh_softmax_params softmax{};
   bh_zero_insert_params zi{};
-  CpuEltwiseF32 eltf{};
+  bh_conv_f32_params convf{};
+  bh_fc_f32_params fcf{};
+  bh_eltwise_f32_params eltf{};
+  bh_pool_f32_params poolf{};
+  int unary_kind = 0;
+  float lo = 0.f, hi = 0.f, beta = 1.f;
+  int depth = 0;
   CpuDetectionParams det{};
   const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
   long count = 0;               // kLut* / kQuantF32: elements
@@ -150,6 +156,8 @@ class HipModelExecutor : public interface::IModelExecutor {
   // across executors by `key`
   absl::Status UploadConst(const std::string& key, const void* data, size_t bytes, PreparedSubgraph* sg,
                            const void** dev);
+  absl::Status LowerFloat(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,
+                          PreparedSubgraph* sg, Launch* l, bool* emit);
   absl::Status LowerTransposeConv(const HipModel& model, int op_index, void* out_ptr, const std::string& ckey,
                                   PreparedSubgraph* sg, Launch* l);
   absl::Status LowerGlue(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,

@@ -1,0 +1,249 @@
+// float32 kernels for fp16-weight TFLite models (post-training float16
+// quantization: fp16 constants behind DEQUANTIZE, float32 compute; the host
+// folds the DEQUANTIZEs).  Semantics of TFLite 2.9.2 reference_ops float
+// Conv / DepthwiseConv / FullyConnected / Add / Sub / Mul / AveragePool /
+// MaxPool / Logistic / Softmax; results agree with the reference within a
+// tolerance (the reduction order differs), not bit-exactly.
+//
+// Batch-1 float layers are small: these kernels aim at one memory round
+// trip per operand and coalesced weight loads, not MFMA.
+#include "common.hpp"
+
+namespace bh {
+
+__device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
+
+// CONV_2D: one thread = one output pixel x 4 output channels; weights are
+// [K][out_c] so the 4-channel loads of neighbouring threads coalesce
+__global__ __launch_bounds__(256) void conv_f32_kernel(bh_conv_f32_params p, FastDiv groups, FastDiv ow,
+                                                       FastDiv oh, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t pix = groups.div((uint32_t)i);
+  const int c0 = 4 * (int)((uint32_t)i - pix * groups.d);
+  const uint32_t t = ow.div(pix);
+  const int ox = (int)(pix - t * p.out_w);
+  const uint32_t n = oh.div(t);
+  const int oy = (int)(t - n * p.out_h);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool vec = (p.out_c % 4) == 0;
+  const int nc = min(4, p.out_c - c0);
+  for (int fy = 0; fy < p.k_h; ++fy) {
+    const int y = oy * p.stride_h - p.pad_h + fy * p.dil_h;
+    if (y < 0 || y >= p.in_h) continue;
+    for (int fx = 0; fx < p.k_w; ++fx) {
+      const int x = ox * p.stride_w - p.pad_w + fx * p.dil_w;
+      if (x < 0 || x >= p.in_w) continue;
+      const float* src = p.input + (((long)n * p.in_h + y) * p.in_w + x) * p.in_c;
+      const float* w = p.weights + (long)((fy * p.k_w + fx) * p.in_c) * p.out_c + c0;
+      for (int ci = 0; ci < p.in_c; ++ci) {
+        const float xv = src[ci];
+        if (vec) {
+          const float4 wv = *(const float4*)(w + (long)ci * p.out_c);
+          acc[0] = fmaf(xv, wv.x, acc[0]);
+          acc[1] = fmaf(xv, wv.y, acc[1]);
+          acc[2] = fmaf(xv, wv.z, acc[2]);
+          acc[3] = fmaf(xv, wv.w, acc[3]);
+        } else {
+          for (int c = 0; c < nc; ++c) acc[c] = fmaf(xv, w[(long)ci * p.out_c + c], acc[c]);
+        }
+      }
+    }
+  }
+  float* out = p.output + (long)pix * p.out_c + c0;
+  for (int c = 0; c < nc; ++c) out[c] = clampf(acc[c] + (p.bias ? p.bias[c0 + c] : 0.f), p.act_min, p.act_max);
+}
+
+// DEPTHWISE_CONV_2D: one thread = one output pixel x 4 channels
+__global__ __launch_bounds__(256) void dwconv_f32_kernel(bh_conv_f32_params p, FastDiv groups, FastDiv ow,
+                                                         FastDiv oh, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t pix = groups.div((uint32_t)i);
+  const int c0 = 4 * (int)((uint32_t)i - pix * groups.d);
+  const uint32_t t = ow.div(pix);
+  const int ox = (int)(pix - t * p.out_w);
+  const uint32_t n = oh.div(t);
+  const int oy = (int)(t - n * p.out_h);
+  const int nc = min(4, p.out_c - c0);
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int fy = 0; fy < p.k_h; ++fy) {
+    const int y = oy * p.stride_h - p.pad_h + fy * p.dil_h;
+    if (y < 0 || y >= p.in_h) continue;
+    for (int fx = 0; fx < p.k_w; ++fx) {
+      const int x = ox * p.stride_w - p.pad_w + fx * p.dil_w;
+      if (x < 0 || x >= p.in_w) continue;
+      const float* src = p.input + (((long)n * p.in_h + y) * p.in_w + x) * p.in_c;
+      const float* w = p.weights + (long)(fy * p.k_w + fx) * p.out_c + c0;
+      for (int c = 0; c < nc; ++c) acc[c] = fmaf(src[(c0 + c) / p.depth_multiplier], w[c], acc[c]);
+    }
+  }
+  float* out = p.output + (long)pix * p.out_c + c0;
+  for (int c = 0; c < nc; ++c) out[c] = clampf(acc[c] + (p.bias ? p.bias[c0 + c] : 0.f), p.act_min, p.act_max);
+}
+
+// FULLY_CONNECTED: one wave per (row, unit), lanes stride the depth
+__global__ __launch_bounds__(256) void fc_f32_kernel(bh_fc_f32_params p, long total) {
+  const long wv = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (wv >= total) return;
+  const long r = wv / p.units;
+  const int u = (int)(wv - r * p.units);
+  const float* x = p.input + r * p.depth;
+  const float* w = p.weights + (long)u * p.depth;
+  float acc = 0.f;
+  for (int k = lane; k < p.depth; k += 64) acc = fmaf(x[k], w[k], acc);
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+  if (lane == 0) p.output[wv] = clampf(acc + (p.bias ? p.bias[u] : 0.f), p.act_min, p.act_max);
+}
+
+__global__ __launch_bounds__(256) void eltwise_f32_kernel(bh_eltwise_f32_params p, long n) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int* so = p.shape_o;
+  const long i3 = i % so[3], t = i / so[3];
+  const long i2 = t % so[2], t2 = t / so[2];
+  const long i1 = t2 % so[1], i0 = t2 / so[1];
+  const int* sa = p.shape_a;
+  const int* sb = p.shape_b;
+  const long ia = (((sa[0] == 1 ? 0 : i0) * sa[1] + (sa[1] == 1 ? 0 : i1)) * sa[2] + (sa[2] == 1 ? 0 : i2)) * sa[3] +
+                  (sa[3] == 1 ? 0 : i3);
+  const long ib = (((sb[0] == 1 ? 0 : i0) * sb[1] + (sb[1] == 1 ? 0 : i1)) * sb[2] + (sb[2] == 1 ? 0 : i2)) * sb[3] +
+                  (sb[3] == 1 ? 0 : i3);
+  const float a = p.a[ia], b = p.b[ib];
+  const float v = p.kind == BH_ELTF_ADD ? a + b : (p.kind == BH_ELTF_SUB ? a - b : a * b);
+  p.out[i] = clampf(v, p.act_min, p.act_max);
+}
+
+__global__ __launch_bounds__(256) void pool_f32_kernel(bh_pool_f32_params p, long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = (int)(i % p.channels);
+  const long pix = i / p.channels;
+  const int ox = (int)(pix % p.out_w);
+  const long t = pix / p.out_w;
+  const int oy = (int)(t % p.out_h);
+  const int n = (int)(t / p.out_h);
+  const int y0 = oy * p.stride_h - p.pad_h, x0 = ox * p.stride_w - p.pad_w;
+  const int fy0 = max(0, -y0), fy1 = min(p.f_h, p.in_h - y0);
+  const int fx0 = max(0, -x0), fx1 = min(p.f_w, p.in_w - x0);
+  float acc = p.kind == BH_POOL_AVG ? 0.f : -INFINITY;
+  int cnt = 0;
+  for (int fy = fy0; fy < fy1; ++fy)
+    for (int fx = fx0; fx < fx1; ++fx) {
+      const float v = p.input[(((long)n * p.in_h + y0 + fy) * p.in_w + x0 + fx) * p.channels + c];
+      acc = p.kind == BH_POOL_AVG ? acc + v : fmaxf(acc, v);
+      ++cnt;
+    }
+  if (p.kind == BH_POOL_AVG) acc = acc / (float)cnt;
+  p.output[i] = clampf(acc, p.act_min, p.act_max);
+}
+
+__global__ __launch_bounds__(256) void unary_f32_kernel(int kind, const float* in, float* out, long n, float lo,
+                                                        float hi) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float x = in[i];
+  out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + expf(-x)) : clampf(x, lo, hi);
+}
+
+// one wave per row: max, sum of exp, normalise
+__global__ __launch_bounds__(256) void softmax_f32_kernel(const float* in, float* out, long rows, int depth,
+                                                          float beta) {
+  const long r = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* x = in + r * depth;
+  float* y = out + r * depth;
+  float mx = -INFINITY;
+  for (int k = lane; k < depth; k += 64) mx = fmaxf(mx, x[k]);
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  float sum = 0.f;
+  for (int k = lane; k < depth; k += 64) sum += expf((x[k] - mx) * beta);
+  for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+  const float inv = 1.0f / sum;
+  for (int k = lane; k < depth; k += 64) y[k] = expf((x[k] - mx) * beta) * inv;
+}
+
+inline unsigned blocks(long n, int per = 256) { return (unsigned)((n + per - 1) / per); }
+
+}  // namespace bh
+
+extern "C" int bh_conv2d_f32(const bh_conv_f32_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->weights || pp->out_c <= 0 || pp->in_c <= 0 || pp->stride_h <= 0 ||
+      pp->stride_w <= 0 || (pp->depthwise && pp->out_c != pp->in_c * pp->depth_multiplier)) {
+    bh_set_last_error("bh_conv2d_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_conv_f32_params& p = *pp;
+  const long pixels = (long)p.batch * p.out_h * p.out_w;
+  const int groups = (p.out_c + 3) / 4;
+  const long total = pixels * groups;
+  if (total <= 0 || total > INT32_MAX) {
+    bh_set_last_error("bh_conv2d_f32: size out of range");
+    return BH_EINVAL;
+  }
+  bh::FastDiv dg((uint32_t)groups), dw((uint32_t)p.out_w), dh((uint32_t)p.out_h);
+  if (p.depthwise)
+    hipLaunchKernelGGL(bh::dwconv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
+                       total);
+  else
+    hipLaunchKernelGGL(bh::conv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
+                       total);
+  return bh_check_launch(p.depthwise ? "dwconv_f32_kernel" : "conv_f32_kernel");
+}
+
+extern "C" int bh_fc_f32(const bh_fc_f32_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->weights || pp->rows <= 0 || pp->depth <= 0 || pp->units <= 0) {
+    bh_set_last_error("bh_fc_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  const long total = (long)pp->rows * pp->units;
+  hipLaunchKernelGGL(bh::fc_f32_kernel, dim3(bh::blocks(total, 4)), dim3(256), 0, (hipStream_t)s, *pp, total);
+  return bh_check_launch("fc_f32_kernel");
+}
+
+extern "C" int bh_eltwise_f32(const bh_eltwise_f32_params* pp, bh_stream_t s) {
+  if (!pp || !pp->a || !pp->b || !pp->out) {
+    bh_set_last_error("bh_eltwise_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  const int* so = pp->shape_o;
+  const long n = (long)so[0] * so[1] * so[2] * so[3];
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(bh::eltwise_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, *pp, n);
+  return bh_check_launch("eltwise_f32_kernel");
+}
+
+extern "C" int bh_pool_f32(const bh_pool_f32_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || pp->channels <= 0 || pp->stride_h <= 0 || pp->stride_w <= 0) {
+    bh_set_last_error("bh_pool_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  const long total = (long)pp->batch * pp->out_h * pp->out_w * pp->channels;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(bh::pool_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, *pp, total);
+  return bh_check_launch("pool_f32_kernel");
+}
+
+extern "C" int bh_unary_f32(int kind, const float* in, float* out, long n, float lo, float hi, bh_stream_t s) {
+  if (!in || !out || n < 0 || (kind != BH_UNARY_CLAMP && kind != BH_UNARY_LOGISTIC)) {
+    bh_set_last_error("bh_unary_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(bh::unary_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, kind, in, out, n, lo,
+                     hi);
+  return bh_check_launch("unary_f32_kernel");
+}
+
+extern "C" int bh_softmax_f32(const float* in, float* out, long rows, int depth, float beta, bh_stream_t s) {
+  if (!in || !out || rows < 0 || depth <= 0) {
+    bh_set_last_error("bh_softmax_f32: invalid parameters");
+    return BH_EINVAL;
+  }
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(bh::softmax_f32_kernel, dim3(bh::blocks(rows, 4)), dim3(256), 0, (hipStream_t)s, in, out, rows,
+                     depth, beta);
+  return bh_check_launch("softmax_f32_kernel");
+}

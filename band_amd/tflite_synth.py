@@ -16,8 +16,8 @@ import struct
 import numpy as np
 
 # schema enums
-T_FLOAT32, T_INT32, T_UINT8, T_INT8 = 0, 2, 3, 9
-NP_TO_SCHEMA = {np.dtype(np.float32): T_FLOAT32, np.dtype(np.int32): T_INT32,
+T_FLOAT32, T_FLOAT16, T_INT32, T_UINT8, T_INT8 = 0, 1, 2, 3, 9
+NP_TO_SCHEMA = {np.dtype(np.float32): T_FLOAT32, np.dtype(np.float16): T_FLOAT16, np.dtype(np.int32): T_INT32,
                 np.dtype(np.uint8): T_UINT8, np.dtype(np.int8): T_INT8}
 ACT = {"NONE": 0, "RELU": 1, "RELU_N1_TO_1": 2, "RELU6": 3}
 OPC = dict(ADD=0, AVERAGE_POOL_2D=1, CONCATENATION=2, CONV_2D=3, DEPTHWISE_CONV_2D=4,
@@ -584,6 +584,8 @@ class QGraph:
                                    h_scale=float(scales[2]), w_scale=float(scales[3])))
         self.mb.op("CUSTOM", [boxes_f, scores_f, a], outs, custom="TFLite_Detection_PostProcess",
                    custom_options=opts)
+        for t, shp in zip(outs, ([1, max_detections, 4], [1, max_detections], [1, max_detections], [1])):
+            self.fshape[t] = shp
         return outs
 
     def quantize_float(self, xf, scale, zp=None):
@@ -596,6 +598,143 @@ class QGraph:
         return self.mb.build()
 
 
+class FGraph:
+    """Float graph builder with QGraph's method names: a TFLite fp16 model
+    (post-training float16 quantization) - float32 activations, every
+    constant stored as float16 behind a DEQUANTIZE op, float32 compute.
+    Weights are He-initialised so activations stay O(1) through ReLU6."""
+
+    def __init__(self, seed=0, name="model"):
+        self.dtype = np.dtype(np.float16)
+        self.rng = np.random.default_rng(seed)
+        self.mb = ModelBuilder(name)
+        self.n = 0
+        self.meta = {}  # tensor -> (shape, None, None)
+
+    def _name(self, kind):
+        self.n += 1
+        return "%s_%d" % (kind, self.n)
+
+    def _act(self, shape, kind="act"):
+        t = self.mb.tensor(self._name(kind), list(shape), np.float32)
+        self.meta[t] = (list(shape), None, None)
+        return t
+
+    def _const(self, values, kind):
+        """float16 constant + DEQUANTIZE -> float32 tensor"""
+        v = np.asarray(values, np.float32)
+        c = self.mb.tensor(self._name(kind + "_fp16"), list(v.shape), np.float16, data=v.astype(np.float16))
+        y = self.mb.tensor(self._name(kind), list(v.shape), np.float32)
+        self.mb.op("DEQUANTIZE", [c], [y], OPT["DequantizeOptions"], Table())
+        return y
+
+    def input(self, shape, scale=None, zp=None):
+        t = self._act(shape, "input")
+        self.mb.inputs.append(t)
+        return t
+
+    def output(self, t):
+        self.mb.outputs.append(t)
+
+    def conv(self, x, out_c, k=1, stride=1, act="RELU6", padding="SAME", dilation=1, out_scale=None,
+             bias_offset_lsb=0):
+        b, h, w, c = self.meta[x][0]
+        K = k * k * c
+        wt = self._const(self.rng.normal(0, np.sqrt(2.0 / K), (out_c, k, k, c)), "weights")
+        bt = self._const(self.rng.normal(0, 0.05, out_c) + (bias_offset_lsb * 0.05 if bias_offset_lsb else 0), "bias")
+        eff = (k - 1) * dilation + 1
+        oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
+        ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
+        y = self._act([b, oh, ow, out_c])
+        self.mb.op("CONV_2D", [x, wt, bt], [y], OPT["Conv2DOptions"], conv_options(padding, stride, act, dilation))
+        return y
+
+    def dwconv(self, x, k=3, stride=1, act="RELU6", padding="SAME", dm=1, dilation=1):
+        b, h, w, c = self.meta[x][0]
+        out_c = c * dm
+        wt = self._const(self.rng.normal(0, np.sqrt(2.0 / (k * k)), (1, k, k, out_c)), "dw_weights")
+        bt = self._const(self.rng.normal(0, 0.05, out_c), "dw_bias")
+        eff = (k - 1) * dilation + 1
+        oh = (h + stride - 1) // stride if padding == "SAME" else (h + stride - eff) // stride
+        ow = (w + stride - 1) // stride if padding == "SAME" else (w + stride - eff) // stride
+        y = self._act([b, oh, ow, out_c])
+        self.mb.op("DEPTHWISE_CONV_2D", [x, wt, bt], [y], OPT["DepthwiseConv2DOptions"],
+                   dw_options(padding, stride, act, dm, dilation))
+        return y
+
+    def add(self, a, b, act="NONE"):
+        y = self._act(self.meta[a][0])
+        self.mb.op("ADD", [a, b], [y], OPT["AddOptions"], act_options(act))
+        return y
+
+    def mul(self, a, b, act="NONE"):
+        y = self._act(self.meta[a][0])
+        self.mb.op("MUL", [a, b], [y], OPT["MulOptions"], act_options(act))
+        return y
+
+    def _pool(self, kind, x, filt, stride, padding):
+        b, h, w, c = self.meta[x][0]
+        oh = (h + stride - filt[0]) // stride if padding == "VALID" else (h + stride - 1) // stride
+        ow = (w + stride - filt[1]) // stride if padding == "VALID" else (w + stride - 1) // stride
+        y = self._act([b, oh, ow, c])
+        self.mb.op(kind, [x], [y], OPT["Pool2DOptions"], pool_options(padding, stride, filt))
+        return y
+
+    def avgpool(self, x, filt, stride=1, padding="VALID"):
+        return self._pool("AVERAGE_POOL_2D", x, filt, stride, padding)
+
+    def maxpool(self, x, filt, stride, padding="SAME"):
+        return self._pool("MAX_POOL_2D", x, filt, stride, padding)
+
+    def reshape(self, x, shape):
+        st = self.mb.tensor(self._name("shape"), [len(shape)], np.int32, data=np.array(shape, np.int32))
+        y = self._act(list(shape))
+        self.mb.op("RESHAPE", [x, st], [y], OPT["ReshapeOptions"], Table().set(0, "o", Vec("i", list(shape))))
+        return y
+
+    def fully_connected(self, x, units, act="NONE"):
+        shp = self.meta[x][0]
+        depth = shp[-1]
+        rows = int(np.prod(shp)) // depth
+        wt = self._const(self.rng.normal(0, np.sqrt(1.0 / depth), (units, depth)), "fc_weights")
+        bt = self._const(self.rng.normal(0, 0.05, units), "fc_bias")
+        y = self._act([rows, units])
+        self.mb.op("FULLY_CONNECTED", [x, wt, bt], [y], OPT["FullyConnectedOptions"], act_options(act))
+        return y
+
+    def concat(self, xs, axis=3):
+        shp = list(self.meta[xs[0]][0])
+        shp[axis] = sum(self.meta[t][0][axis] for t in xs)
+        y = self._act(shp)
+        self.mb.op("CONCATENATION", list(xs), [y], OPT["ConcatenationOptions"], Table().set(0, "i", axis))
+        return y
+
+    def logistic(self, x):
+        y = self._act(self.meta[x][0])
+        self.mb.op("LOGISTIC", [x], [y])
+        return y
+
+    def softmax(self, x, beta=1.0):
+        y = self._act(self.meta[x][0])
+        self.mb.op("SOFTMAX", [x], [y], OPT["SoftmaxOptions"], Table().set(0, "f", float(beta)))
+        return y
+
+    def relu(self, x, kind="RELU"):
+        y = self._act(self.meta[x][0])
+        self.mb.op(kind, [x], [y])
+        return y
+
+    def build(self):
+        return self.mb.build()
+
+
+def _graph(dtype, seed, name):
+    """QGraph for 8-bit models, FGraph for fp16-weight float models"""
+    if np.dtype(dtype) == np.float16:
+        return FGraph(seed, name)
+    return QGraph(dtype, seed, name)
+
+
 # ---------------------------------------------------------------------------
 # BASELINE models
 # ---------------------------------------------------------------------------
@@ -606,7 +745,7 @@ MNV2_BLOCKS = [(1, 16, 1, 1), (6, 24, 2, 2), (6, 32, 3, 2), (6, 64, 4, 2), (6, 9
 def mobilenet_v2(dtype=np.int8, seed=0, size=224, batch=1, classes=1001, width=1.0):
     """MobileNetV2-1.0 with the topology of mobilenet_v2_1.0_224_quant.tflite
     (65 ops: 36 CONV_2D, 17 DEPTHWISE_CONV_2D, 10 ADD, AVERAGE_POOL_2D, RESHAPE)."""
-    g = QGraph(dtype, seed, "mobilenet_v2_%s" % np.dtype(dtype).name)
+    g = _graph(dtype, seed, "mobilenet_v2_%s" % np.dtype(dtype).name)
     ch = lambda c: max(8, int(c * width + 4) // 8 * 8)
     x = g.input([batch, size, size, 3])
     x = g.conv(x, ch(32), k=3, stride=2)
@@ -635,7 +774,7 @@ def mobilenet_v2(dtype=np.int8, seed=0, size=224, batch=1, classes=1001, width=1
 
 def mobilenet_v1(dtype=np.int8, seed=0, size=224, batch=1, classes=1001):
     """MobileNetV1-1.0 (config C1): conv + 13 depthwise-separable blocks."""
-    g = QGraph(dtype, seed, "mobilenet_v1_%s" % np.dtype(dtype).name)
+    g = _graph(dtype, seed, "mobilenet_v1_%s" % np.dtype(dtype).name)
     x = g.input([batch, size, size, 3])
     x = g.conv(x, 32, k=3, stride=2)
     for c, s in [(64, 1), (128, 2), (128, 1), (256, 2), (256, 1), (512, 2), (512, 1), (512, 1),
@@ -688,7 +827,7 @@ def ssd_mobilenet_v2(dtype=np.int8, seed=1, size=224, batch=1, classes=91):
     RESHAPE + CONCATENATION of all anchors, LOGISTIC class scores.  The
     TFLite_Detection_PostProcess custom op (CPU NMS) is left out: outputs are
     box encodings [1,N,4] and class scores [1,N,classes]."""
-    g = QGraph(dtype, seed, "ssd_mobilenet_v2_%s" % np.dtype(dtype).name)
+    g = _graph(dtype, seed, "ssd_mobilenet_v2_%s" % np.dtype(dtype).name)
     x = g.input([batch, size, size, 3])
     feat, taps = _mnv2_trunk(g, x, tap_expansion_at=13)
     maps = [taps["expansion"], g.conv(feat, 1280, k=1)]

@@ -28,6 +28,10 @@
  *   bh_resize_bilinear_i8 <- RESIZE_BILINEAR int8 (reference_ops::ResizeBilinearInteger)
  *   bh_softmax_i8     <- SOFTMAX 8-bit      (optimized_ops::Softmax, lookup-table path)
  *   bh_zero_insert + bh_conv2d_i8 <- TRANSPOSE_CONV int8 (reference_integer_ops::TransposeConv)
+ *   bh_conv2d_f32 / bh_fc_f32 / bh_eltwise_f32 / bh_pool_f32 / bh_unary_f32 / bh_softmax_f32
+ *                     <- the float32 forms of CONV_2D, DEPTHWISE_CONV_2D, FULLY_CONNECTED,
+ *                        ADD/SUB/MUL, AVERAGE/MAX_POOL_2D, LOGISTIC/RELU*, SOFTMAX
+ *                        (reference_ops float kernels) for fp16-weight models
  *
  * Quantised tensors live on the device as raw bytes in their TFLite type
  * (int8 or uint8).  Kernels work in the "int8 domain": a uint8 input is
@@ -288,6 +292,64 @@ int bh_lut_f32(const void* in, void* out, long n, const float* table, bh_stream_
 /* float32 -> 8-bit: clamp((int)roundf(x / scale) + zp) */
 int bh_quantize_f32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed,
                     bh_stream_t s);
+
+/* ---- float32 graphs ------------------------------------------------------
+ * TFLite fp16 models (post-training float16 quantization) compute in float32
+ * with fp16 constant weights behind DEQUANTIZE ops; the host folds those
+ * DEQUANTIZEs and hands these kernels float32 operands.  Float results match
+ * the reference within a stated tolerance (summation order differs), not
+ * bit-exactly.  act_min / act_max are the fused activation's float bounds
+ * (+-inf for NONE). */
+typedef struct {
+  int batch, in_h, in_w, in_c, out_h, out_w, out_c, k_h, k_w;
+  int stride_h, stride_w, dil_h, dil_w, pad_h, pad_w;
+  int depthwise, depth_multiplier;   /* depthwise: out_c = in_c * depth_multiplier */
+  float act_min, act_max;
+  const float* input;
+  float* output;
+  const float* weights; /* conv: [k_h*k_w*in_c][out_c]; depthwise: [k_h*k_w][out_c] */
+  const float* bias;    /* [out_c] or NULL */
+} bh_conv_f32_params;
+int bh_conv2d_f32(const bh_conv_f32_params* p, bh_stream_t s);
+
+typedef struct {
+  int rows, depth, units;
+  float act_min, act_max;
+  const float* input;   /* [rows][depth] */
+  float* output;        /* [rows][units] */
+  const float* weights; /* [units][depth] */
+  const float* bias;    /* [units] or NULL */
+} bh_fc_f32_params;
+int bh_fc_f32(const bh_fc_f32_params* p, bh_stream_t s);
+
+#define BH_ELTF_ADD 0
+#define BH_ELTF_SUB 1
+#define BH_ELTF_MUL 2
+typedef struct {
+  int kind;
+  int shape_a[4], shape_b[4], shape_o[4]; /* 4-D, broadcast dims are 1 */
+  float act_min, act_max;
+  const float* a;
+  const float* b;
+  float* out;
+} bh_eltwise_f32_params;
+int bh_eltwise_f32(const bh_eltwise_f32_params* p, bh_stream_t s);
+
+typedef struct {
+  int kind; /* BH_POOL_AVG / BH_POOL_MAX */
+  int batch, in_h, in_w, channels, out_h, out_w, f_h, f_w, stride_h, stride_w, pad_h, pad_w;
+  float act_min, act_max;
+  const float* input;
+  float* output;
+} bh_pool_f32_params;
+int bh_pool_f32(const bh_pool_f32_params* p, bh_stream_t s);
+
+#define BH_UNARY_CLAMP 0    /* RELU / RELU6 / RELU_N1_TO_1: min(max(x, lo), hi) */
+#define BH_UNARY_LOGISTIC 1 /* 1 / (1 + exp(-x)) */
+int bh_unary_f32(int kind, const float* in, float* out, long n, float lo, float hi, bh_stream_t s);
+
+/* reference_ops::Softmax (float): per row exp((x - max) * beta) / sum */
+int bh_softmax_f32(const float* in, float* out, long rows, int depth, float beta, bh_stream_t s);
 
 #define BH_CONCAT_MAX_INPUTS 16
 typedef struct {

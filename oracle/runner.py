@@ -425,11 +425,78 @@ class OracleInterpreter:
                 vals[idx] = np.asarray(val).reshape(m.tensors[idx].shape).astype(m.tensors[idx].np_dtype, copy=False)
         return vals
 
+    _FLOAT_OPS = ("CONV_2D", "DEPTHWISE_CONV_2D", "FULLY_CONNECTED", "ADD", "SUB", "MUL", "AVERAGE_POOL_2D",
+                  "MAX_POOL_2D", "RELU", "RELU6", "RELU_N1_TO_1", "LOGISTIC", "SOFTMAX", "CONCATENATION")
+
+    def _op_float(self, o, vals):
+        """float32 graphs (oracle/float_ref.py)"""
+        from . import float_ref as F
+        T = self.model.tensors
+        opt = o.options
+        code = o.builtin
+        x = vals[o.inputs[0]]
+        to = T[o.outputs[0]]
+        if code in (OP["CONV_2D"], OP["DEPTHWISE_CONV_2D"]):
+            dw = code == OP["DEPTHWISE_CONV_2D"]
+            w = vals[o.inputs[1]]
+            bias = vals.get(o.inputs[2]) if len(o.inputs) > 2 and o.inputs[2] >= 0 else None
+            same = opt.scalar(0, "b", 0) == 0
+            sw, sh = opt.scalar(1, "i", 1), opt.scalar(2, "i", 1)
+            if dw:
+                dm, act = opt.scalar(3, "i", 1), opt.scalar(4, "b", 0)
+                dw_, dh_ = opt.scalar(5, "i", 1), opt.scalar(6, "i", 1)
+                kh, kw = w.shape[1], w.shape[2]
+            else:
+                act = opt.scalar(3, "b", 0)
+                dw_, dh_ = opt.scalar(4, "i", 1), opt.scalar(5, "i", 1)
+                kh, kw = w.shape[1], w.shape[2]
+            ih, iw = x.shape[1], x.shape[2]
+            oh, ow = out_size(same, ih, kh, sh, dh_), out_size(same, iw, kw, sw, dw_)
+            pad = (padding(sh, dh_, ih, kh, oh), padding(sw, dw_, iw, kw, ow))
+            lo, hi = _f32_act(act)
+            if dw:
+                return [F.dwconv2d_f32(x, w, bias, dm, (sh, sw), (dh_, dw_), pad, (oh, ow), lo, hi)]
+            return [F.conv2d_f32(x, w, bias, (sh, sw), (dh_, dw_), pad, (oh, ow), lo, hi)]
+        if code == OP["FULLY_CONNECTED"]:
+            w = vals[o.inputs[1]]
+            bias = vals.get(o.inputs[2]) if len(o.inputs) > 2 and o.inputs[2] >= 0 else None
+            lo, hi = _f32_act(opt.scalar(0, "b", 0) if opt is not None else 0)
+            return [F.fully_connected_f32(x, w, bias, lo, hi)]
+        if code in (OP["ADD"], OP["SUB"], OP["MUL"]):
+            lo, hi = _f32_act(opt.scalar(0, "b", 0) if opt is not None else 0)
+            kind = {OP["ADD"]: "add", OP["SUB"]: "sub", OP["MUL"]: "mul"}[code]
+            return [F.eltwise_f32(x, vals[o.inputs[1]], kind, lo, hi)]
+        if code in (OP["AVERAGE_POOL_2D"], OP["MAX_POOL_2D"]):
+            same = opt.scalar(0, "b", 0) == 0
+            sw, sh = opt.scalar(1, "i", 1), opt.scalar(2, "i", 1)
+            fw, fh = opt.scalar(3, "i", 1), opt.scalar(4, "i", 1)
+            lo, hi = _f32_act(opt.scalar(5, "b", 0))
+            ih, iw = x.shape[1], x.shape[2]
+            oh, ow = out_size(same, ih, fh, sh, 1), out_size(same, iw, fw, sw, 1)
+            pad = (padding(sh, 1, ih, fh, oh), padding(sw, 1, iw, fw, ow))
+            kind = "avg" if code == OP["AVERAGE_POOL_2D"] else "max"
+            return [F.pool2d_f32(x, kind, (fh, fw), (sh, sw), pad, (oh, ow), lo, hi)]
+        if code in (OP["RELU"], OP["RELU6"], OP["RELU_N1_TO_1"]):
+            lo, hi = {OP["RELU"]: (0.0, np.inf), OP["RELU6"]: (0.0, 6.0), OP["RELU_N1_TO_1"]: (-1.0, 1.0)}[code]
+            return [np.clip(x, lo, hi).astype(np.float32)]
+        if code == OP["LOGISTIC"]:
+            return [F.logistic_f32(x)]
+        if code == OP["SOFTMAX"]:
+            return [F.softmax_f32(x, opt.scalar(0, "f", 1.0) if opt is not None else 1.0)]
+        if code == OP["CONCATENATION"]:
+            return [np.concatenate([vals[i] for i in o.inputs], axis=opt.scalar(0, "i", 0))]
+        raise NotImplementedError("oracle: float op %s" % o.name)
+
     def _op(self, o, vals):
         m = self.model
         T = m.tensors
         opt = o.options
         code = o.builtin
+        if (o.inputs and o.inputs[0] >= 0 and T[o.inputs[0]].np_dtype == np.float32 and
+                o.name in self._FLOAT_OPS):
+            return self._op_float(o, vals)
+        if code == OP["DEQUANTIZE"] and T[o.inputs[0]].np_dtype == np.float16:
+            return [vals[o.inputs[0]].astype(np.float32)]
         if code in (OP["CONV_2D"], OP["DEPTHWISE_CONV_2D"]):
             dw = code == OP["DEPTHWISE_CONV_2D"]
             x, w = vals[o.inputs[0]], vals[o.inputs[1]]

@@ -55,20 +55,50 @@ def tconv_zoo(seed=7):
 
 
 def split_zoo(dtype=np.int8, seed=11):
-    """A model the model analyzer must split: two GPU runs of >= 7 ops around
-    a float32 ADD only the CPU worker runs (DEQUANTIZE -> ADD(x, x) ->
-    QUANTIZE), plus a side output from the first run."""
+    """A model the model analyzer must split GPU -> CPU -> GPU: a GPU run of
+    >= 7 ops, then TFLite_Detection_PostProcess (CPU worker only) on
+    DEQUANTIZEd box / class maps, then a GPU run over the QUANTIZEd
+    detection scores, plus side outputs from both GPU runs."""
     g = QGraph(dtype, seed=seed, name="split_zoo")
     x = g.input([1, 16, 16, 8], scale=0.05)
     a = g.conv(x, 16, k=3, act="RELU6")
     for _ in range(3):
         a = g.add(g.conv(g.dwconv(a), 16, k=1, act="NONE"), a)
-    f = g.dequantize(a)
-    f = g.float_add(f, f)
-    q = g.quantize_float(f, 0.1)
-    b = g.conv(q, 24, k=3, stride=2, act="RELU6")
+    n = 16 * 16
+    boxes = g.dequantize(g.reshape(g.conv(a, 4, k=1, act="NONE"), [1, n, 4]))
+    scores = g.dequantize(g.logistic(g.reshape(g.conv(a, 3, k=1, act="NONE", bias_offset_lsb=-20), [1, n, 3])))
+    rng = np.random.default_rng(seed)
+    anchors = np.concatenate([rng.uniform(0.1, 0.9, (n, 2)), rng.uniform(0.05, 0.3, (n, 2))], 1)
+    det_boxes, det_classes, det_scores, num = g.detection_postprocess(boxes, scores, anchors, 3, max_detections=8,
+                                                                      score_threshold=0.3)
+    q = g.quantize_float(det_scores, 1.0 / 256)
+    q4 = g.reshape(q, [1, 1, 1, 8])
+    b = g.conv(q4, 24, k=1, act="RELU6")
     for _ in range(3):
         b = g.add(g.conv(g.dwconv(b), 24, k=1, act="NONE"), b)
-    g.output(g.fully_connected(g.reshape(g.avgpool(b, (8, 8)), [1, 24]), 10))
+    g.output(g.fully_connected(g.reshape(b, [1, 24]), 10))
     g.output(g.logistic(a))
+    g.output(det_boxes)
+    g.output(num)
+    return g.build()
+
+
+def float_zoo(seed=13):
+    """float32 op variety for the fp16 path: odd channel counts, depth
+    multiplier 2, dilation, strides, VALID padding, broadcast MUL, pools,
+    FC, SOFTMAX, LOGISTIC, RELU_N1_TO_1"""
+    from band_amd.tflite_synth import FGraph
+    g = FGraph(seed=seed, name="float_zoo")
+    x = g.input([1, 13, 11, 5])
+    a = g.conv(x, 6, k=3, stride=2, act="RELU")                  # 7x6x6, out_c % 4 != 0
+    b = g.dwconv(a, k=3, dm=2, act="RELU6")                     # 12 channels
+    c = g.dwconv(b, k=3, dilation=2, act="NONE")
+    d = g.conv(c, 7, k=2, padding="VALID", act="NONE")
+    gate = g.logistic(g.avgpool(d, (6, 5)))                      # [1,1,1,7]
+    e = g.mul(d, gate)                                           # broadcast
+    f = g.maxpool(e, (2, 2), 2)
+    h = g.relu(f, "RELU_N1_TO_1")
+    v = g.reshape(h, [1, int(np.prod(g.meta[h][0]))])
+    g.output(g.softmax(g.fully_connected(v, 9), beta=0.8))
+    g.output(e)
     return g.build()

@@ -6,6 +6,8 @@
 #include <cstdarg>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <random>
 #include <mutex>
 #include <thread>
 #include <list>
@@ -380,13 +382,17 @@ int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandModel* model, int 
   return engine->impl->GetExpected(band::SubgraphKey(model->impl->GetId(), worker_id, units));
 }
 
-BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
-                                    int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
-                                    double* wall_s) {
+namespace {
+// request driver shared by the closed-loop and Poisson entry points:
+// `next_arrival(j)` returns the time (us since start) job j may be submitted
+// (0 = as soon as the in-flight bound allows) and its model index
+BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models, int n_jobs,
+                         int max_inflight, const std::function<std::pair<int64_t, int>(int)>& next_arrival,
+                         double* latency_us, int* worker_ids, int* model_index, double* wall_s) {
   if (!engine || !models || n_models <= 0 || n_jobs < 0 || max_inflight <= 0) return kBandErr;
   band::Engine& e = *engine->impl;
   // per model: one input tensor (copied into the request ring at submit)
-  // and one output tensor (the waiter copies results out of the ring)
+  // and one output tensor per waiter use
   std::vector<std::vector<std::unique_ptr<band::Tensor>>> own_in(n_models), outs(n_models);
   std::vector<band::Tensors> in_ptrs(n_models), out_ptrs(n_models);
   for (int m = 0; m < n_models; ++m) {
@@ -410,7 +416,11 @@ BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, Band
   }
   std::mutex mu;
   std::condition_variable cv;
-  std::deque<std::pair<int, band::JobId>> pending;  // (job index, handle)
+  struct Pending {
+    int index, model;
+    band::JobId id;
+  };
+  std::deque<Pending> pending;
   int inflight = 0;
   bool failed = false;
   const int64_t t0 = band::time::NowMicros();
@@ -418,35 +428,65 @@ BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, Band
     for (int done = 0; done < n_jobs; ++done) {
       std::unique_lock<std::mutex> l(mu);
       cv.wait(l, [&] { return !pending.empty(); });
-      auto item = pending.front();
+      Pending item = pending.front();
       pending.pop_front();
       l.unlock();
-      const int m = item.first % n_models;
-      absl::Status s = item.second >= 0 ? e.Wait(item.second, out_ptrs[m]) : absl::InternalError("submit");
-      band::Job j = item.second >= 0 ? e.GetFinishedJob(item.second) : band::Job();
+      absl::Status s = item.id >= 0 ? e.Wait(item.id, out_ptrs[item.model]) : absl::InternalError("submit");
+      band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
       l.lock();
-      if (!s.ok() || j.job_id != item.second || j.status != band::JobStatus::kSuccess) failed = true;
-      if (latency_us) latency_us[item.first] = static_cast<double>(j.end_time - j.enqueue_time);
-      if (worker_ids) worker_ids[item.first] = j.subgraph_key.GetWorkerId();
+      if (!s.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) failed = true;
+      if (latency_us) latency_us[item.index] = static_cast<double>(j.end_time - j.enqueue_time);
+      if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
+      if (model_index) model_index[item.index] = item.model;
       --inflight;
       cv.notify_all();
     }
   });
   for (int j = 0; j < n_jobs; ++j) {
+    const auto arrival = next_arrival(j);
+    const int64_t now = band::time::NowMicros() - t0;
+    if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
     {
       std::unique_lock<std::mutex> l(mu);
       cv.wait(l, [&] { return inflight < max_inflight; });
       ++inflight;
     }
-    const int m = j % n_models;
+    const int m = arrival.second;
     auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
     std::lock_guard<std::mutex> l(mu);
-    pending.emplace_back(j, id.ok() ? id.value() : -1);
+    pending.push_back({j, m, id.ok() ? id.value() : -1});
     cv.notify_all();
   }
   waiter.join();
   if (wall_s) *wall_s = (band::time::NowMicros() - t0) * 1e-6;
   return failed ? kBandErr : kBandOk;
+}
+}  // namespace
+
+BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
+                                    int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
+                                    double* wall_s) {
+  return DriveRequests(
+      engine, models, inputs, n_models, n_jobs, max_inflight,
+      [&](int j) { return std::make_pair(int64_t(0), j % std::max(n_models, 1)); }, latency_us, worker_ids,
+      nullptr, wall_s);
+}
+
+BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
+                                 int n_jobs, double rate_per_s, uint64_t seed, int max_inflight, double* latency_us,
+                                 int* worker_ids, int* model_index, double* wall_s) {
+  if (!(rate_per_s > 0)) return kBandErr;
+  std::mt19937_64 rng(seed);
+  std::exponential_distribution<double> gap(rate_per_s);
+  std::uniform_int_distribution<int> pick(0, std::max(n_models, 1) - 1);
+  double t = 0;
+  return DriveRequests(
+      engine, models, inputs, n_models, n_jobs, max_inflight,
+      [&](int) {
+        t += gap(rng) * 1e6;
+        return std::make_pair(static_cast<int64_t>(t), pick(rng));
+      },
+      latency_us, worker_ids, model_index, wall_s);
 }
 
 void BandxEngineWaitAll(BandEngine* engine) {

@@ -135,6 +135,8 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
                                          POINTER(c_double), POINTER(c_int), POINTER(c_double)]),
+    "BandxEngineRunPoisson": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_double, c_uint64,
+                                      c_int, POINTER(c_double), POINTER(c_int), POINTER(c_int), POINTER(c_double)]),
 })
 
 
@@ -389,6 +391,25 @@ class Engine:
         if rc != kBandOk:
             raise _abi.BandHipError("BandxEngineRunClosedLoop: a job failed")
         return lat[:n_jobs], wid[:n_jobs], wall.value
+
+    def RunPoisson(self, models, n_jobs, rate_per_s, seed=5489, max_inflight=64, inputs=None):
+        """Native open-loop Poisson driver (BandxEngineRunPoisson).  Returns
+        (latency_us, worker ids, model index per job, wall seconds)."""
+        ms = (c_void_p * len(models))(*[m.handle.value for m in models])
+        ins = None
+        if inputs is not None:
+            ins = (c_void_p * len(models))(*[t.handle.value if t is not None else None for t in inputs])
+        lat = np.zeros(max(n_jobs, 1), np.float64)
+        wid = np.zeros(max(n_jobs, 1), np.int32)
+        mid = np.zeros(max(n_jobs, 1), np.int32)
+        wall = c_double(0)
+        rc = self.lib.BandxEngineRunPoisson(self.handle, ms, ins, len(models), int(n_jobs), float(rate_per_s),
+                                            int(seed), int(max_inflight), lat.ctypes.data_as(POINTER(c_double)),
+                                            wid.ctypes.data_as(POINTER(c_int)), mid.ctypes.data_as(POINTER(c_int)),
+                                            ctypes.byref(wall))
+        if rc != kBandOk:
+            raise _abi.BandHipError("BandxEngineRunPoisson: a job failed")
+        return lat[:n_jobs], wid[:n_jobs], mid[:n_jobs], wall.value
 
     def close(self):
         if getattr(self, "handle", None):

@@ -44,7 +44,9 @@ def parse():
     p.add_argument("--model", default="mix_c3",
                    choices=["mix_c3", "mobilenet_v2_int8", "mobilenet_v2_uint8", "mobilenet_v1_int8",
                             "ssd_mobilenet_v2_int8", "deeplab_v3_mobilenet_v2_int8", "posenet_mobilenet_v1_int8",
-                            "efficientdet_lite2_int8"])
+                            "efficientdet_lite2_int8", "mix_c5"])
+    p.add_argument("--rate", type=float, default=0.0,
+                   help="mix_c5: Poisson arrival rate (requests/s per GPU); default 0.8 x the closed-loop capacity")
     p.add_argument("--cpu-workers", type=int, default=-1,
                    help="Band CPU workers (worker ids first); default: 1 when the model has CPU-only ops")
     p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
@@ -72,6 +74,15 @@ def model_list(name):
         return [(name, S.mobilenet_v1(np.int8, seed=0))]
     if name == "efficientdet_lite2_int8":
         return [(name, S.efficientdet_lite2(np.int8, size=448))]
+    if name == "mix_c5":
+        # 8 DNNs, int8 + fp16 (float16 weights, float32 compute)
+        return [("mobilenet_v1_int8", S.mobilenet_v1(np.int8)), ("mobilenet_v2_int8", S.mobilenet_v2(np.int8)),
+                ("ssd_mobilenet_v2_int8", S.ssd_mobilenet_v2(np.int8)),
+                ("deeplab_v3_mobilenet_v2_int8", S.deeplab_v3_mobilenet_v2(np.int8)),
+                ("posenet_mobilenet_v1_int8", S.posenet_mobilenet_v1(np.int8)),
+                ("efficientdet_lite2_int8", S.efficientdet_lite2(np.int8, size=448)),
+                ("mobilenet_v2_fp16", S.mobilenet_v2(np.float16)),
+                ("ssd_mobilenet_v2_fp16", S.ssd_mobilenet_v2(np.float16))]
     base = name[:-len("_int8")]
     return [(name, getattr(S, base)(np.int8))]
 
@@ -165,7 +176,10 @@ def main():
     # this rank's Band engine: [CPU workers] + W GPU workers, all GPU
     # workers on the local MI355X (worker id -> device ordinal; each worker
     # owns one HIP stream)
-    n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if args.model == "efficientdet_lite2_int8" else 0)
+    needs_cpu = args.model in ("efficientdet_lite2_int8", "mix_c5")
+    n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if needs_cpu else 0)
+    if args.model == "mix_c5" and args.scheduler == "round_robin":
+        args.scheduler = "shortest_expected_latency"  # C5: SEL + latency estimator
     workers = [DeviceFlag.kCPU] * n_cpu + [DeviceFlag.kGPU] * W
     for w in range(n_cpu, n_cpu + W):
         band_amd.SetWorkerDevice(w, D.local_rank)
@@ -187,15 +201,32 @@ def main():
         # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
         t = engine.CreateInputTensor(m, 0)
         arr = t.data()
-        lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
-        arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
+        if arr.dtype == np.float32:  # f32 U(-0.5, 0.5) (band/tool/benchmark.cc:279-287)
+            arr[...] = rng.uniform(-0.5, 0.5, arr.shape).astype(np.float32)
+        else:
+            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
+            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
         inputs.append(t)
     inflight = args.inflight or 2 * W
 
     engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
+    poisson = None
+    if args.model == "mix_c5":
+        # C5: open-loop Poisson arrivals at 0.8 x this engine's closed-loop capacity
+        # (or --rate), uniform over the 8 models
+        rate = args.rate
+        if rate <= 0:
+            _, _, cap_wall = engine.RunClosedLoop(band_models, max(args.steps // 4, 8 * M), inflight, inputs)
+            rate = 0.8 * max(args.steps // 4, 8 * M) / cap_wall
+        poisson = dict(rate_per_s_per_gpu=rate, seed=5489 + D.rank)
     D.barrier()
     t0 = time.perf_counter()
-    lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, args.steps, inflight, inputs)
+    if poisson:
+        lat_us, worker_ids, model_idx, _ = engine.RunPoisson(band_models, args.steps, poisson["rate_per_s_per_gpu"],
+                                                            seed=poisson["seed"], max_inflight=max(64, inflight),
+                                                            inputs=inputs)
+    else:
+        lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, args.steps, inflight, inputs)
     t1 = time.perf_counter()
     D.barrier()
     elapsed = D.max(t1 - t0)
@@ -275,12 +306,16 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "uint8" if args.model.endswith("uint8") else "int8",
+            "dtype": "uint8" if args.model.endswith("uint8") else ("int8+fp16" if args.model == "mix_c5" else "int8"),
             "data": "synthetic (seeded int8 inputs and weights; no checkpoint)",
             "config": {"workload": ("C3: 4-DNN int8 mix (%s), 224x224 batch-1 jobs through the Band engine, "
                                     "%s over %d Band GPU worker(s) per MI355X" %
                                     (", ".join(nm for nm, _ in models), args.scheduler, W))
-                       if M > 1 else (("C4: EfficientDet-Lite2 int8 448x448 batch-1 jobs through the Band engine, "
+                       if M > 1 and args.model != "mix_c5" else
+                       ("C5: 8-DNN int8 + fp16 mix (%s), open-loop Poisson arrivals at %.0f req/s per GPU, %s + "
+                        "latency estimator over [%d CPU, %d GPU] Band workers per MI355X"
+                        % (", ".join(nm for nm, _ in models), poisson["rate_per_s_per_gpu"], args.scheduler, n_cpu, W))
+                       if args.model == "mix_c5" else (("C4: EfficientDet-Lite2 int8 448x448 batch-1 jobs through the Band engine, "
                                        "model_analyzer split (network on GPU workers, TFLite_Detection_PostProcess "
                                        "on %d CPU worker(s)), %s over %d Band GPU worker(s) per MI355X"
                                        % (n_cpu, args.scheduler, W)) if args.model == "efficientdet_lite2_int8" else

@@ -219,6 +219,16 @@ BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandMod
                                                      int n_models, int n_jobs, int max_inflight, double* latency_us,
                                                      int* worker_ids, double* wall_s);
 
+/* Open-loop Poisson driver (BASELINE config C5): n_jobs arrivals with
+ * exponential inter-arrival times at rate_per_s (all models together, seeded
+ * std::mt19937_64), each arrival a model drawn uniformly; arrivals beyond
+ * max_inflight outstanding wait for a completion (the request rings hold
+ * 128 requests per model).  Outputs as BandxEngineRunClosedLoop. */
+BAND_CAPI_EXPORT BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTensor** inputs,
+                                                  int n_models, int n_jobs, double rate_per_s, uint64_t seed,
+                                                  int max_inflight, double* latency_us, int* worker_ids,
+                                                  int* model_index, double* wall_s);
+
 /* The benchmark tool (band/tool/benchmark.cc) driven by a JSON config in the
  * reference's format (band/test/data/benchmark_config.json: "models",
  * "schedulers", "workers", "execution_mode" periodic|stream|workload, ...).

@@ -186,3 +186,43 @@ def test_benchmark_tool_periodic_and_workload(golden_dir):
     assert r["completed"] > 20
     with pytest.raises(Exception):
         BenchmarkRun(dict(base, execution_mode="bogus", models=[{"graph": g}]))
+
+
+def test_native_request_drivers(golden_dir):
+    """closed-loop and Poisson drivers (bench.py / config C5) over SEL"""
+    e = Engine(make_config([SchedulerType.kShortestExpectedLatency], [DeviceFlag.kCPU, DeviceFlag.kCPU]))
+    ms = []
+    for _ in range(2):
+        m = Model()
+        assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+        assert e.RegisterModel(m)
+        ms.append(m)
+    lat, wid, wall = e.RunClosedLoop(ms, 100, 4)
+    assert len(lat) == 100 and (lat >= 0).all() and set(wid) <= {0, 1}
+    lat, wid, mid, wall = e.RunPoisson(ms, 300, 3000.0, seed=7)
+    assert len(lat) == 300 and set(mid) == {0, 1}
+    assert 0.05 < wall < 2.0  # ~0.1 s of arrivals
+
+
+def test_c1_mobilenet_v1_int8_cpu_worker_fixed(tmp_path):
+    """BASELINE config C1: MobileNetV1 224x224 int8 on 1 CPU worker,
+    fixed_worker ("fixed_device" falls back to kFixedWorker, band/common.h:61-71),
+    bit-exact vs the oracle"""
+    from band_amd import tflite_synth as S
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    buf = S.mobilenet_v1(np.int8)
+    p = str(tmp_path / "mnv1.tflite")
+    open(p, "wb").write(buf)
+    e = Engine(make_config([SchedulerType.kFixedWorker], [DeviceFlag.kCPU], num_threads=[8]))
+    assert e.GetNumWorkers() == 1 and e.GetWorkerDevice(0) == DeviceFlag.kCPU
+    m = Model()
+    assert m.FromPath(p)
+    assert e.RegisterModel(m)
+    i, o = e.CreateInputTensor(m, 0), e.CreateOutputTensor(m, 0)
+    x = np.random.default_rng(0).integers(-127, 128, i.dims()).astype(np.int8)
+    i.data()[...] = x
+    assert e.RequestSync(m, [i], [o]) == kBandOk
+    om = OModel(buf)
+    ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]]
+    np.testing.assert_array_equal(o.data().reshape(-1), ref.reshape(-1))

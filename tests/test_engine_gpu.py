@@ -55,7 +55,9 @@ def _run_and_check(e, m, path, xs, expect_workers=None):
         assert r.status == JobStatus.kSuccess
         workers.add(r.worker_id)
         ref = OracleInterpreter(om).run({om.inputs[0]: x})
-        for k, t in enumerate(om.outputs):
+        # the engine orders a model's outputs by tensor index (ModelSpec
+        # holds them in a std::set, band/model_spec.h)
+        for k, t in enumerate(sorted(om.outputs)):
             np.testing.assert_array_equal(o[k].data().reshape(-1), ref[t].reshape(-1), err_msg="output %d" % k)
     if expect_workers is not None:
         assert workers == set(expect_workers)

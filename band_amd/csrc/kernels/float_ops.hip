@@ -13,45 +13,92 @@ namespace bh {
 
 __device__ __forceinline__ float clampf(float v, float lo, float hi) { return fminf(fmaxf(v, lo), hi); }
 
-// CONV_2D: one thread = one output pixel x 4 output channels; weights are
-// [K][out_c] so the 4-channel loads of neighbouring threads coalesce
+// CONV_2D as an implicit GEMM on VALU: an item = one output pixel x 4
+// output channels (items of one pixel are consecutive, so their float4
+// weight loads from [K][out_c] coalesce and their input loads broadcast).
+// A workgroup holds 256 / ks items and splits the reduction over ks slices
+// of the filter taps (ks chosen on the host so deep, narrow layers still
+// fill the chip); slices meet in LDS.
 __global__ __launch_bounds__(256) void conv_f32_kernel(bh_conv_f32_params p, FastDiv groups, FastDiv ow,
-                                                       FastDiv oh, long total) {
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
-  if (i >= total) return;
-  const uint32_t pix = groups.div((uint32_t)i);
-  const int c0 = 4 * (int)((uint32_t)i - pix * groups.d);
-  const uint32_t t = ow.div(pix);
-  const int ox = (int)(pix - t * p.out_w);
-  const uint32_t n = oh.div(t);
-  const int oy = (int)(t - n * p.out_h);
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  const bool vec = (p.out_c % 4) == 0;
-  const int nc = min(4, p.out_c - c0);
-  for (int fy = 0; fy < p.k_h; ++fy) {
-    const int y = oy * p.stride_h - p.pad_h + fy * p.dil_h;
-    if (y < 0 || y >= p.in_h) continue;
-    for (int fx = 0; fx < p.k_w; ++fx) {
+                                                       FastDiv oh, long total, int ks) {
+  __shared__ float4 part[256];
+  const int iw = 256 / ks;  // items per workgroup
+  const int item_in_wg = threadIdx.x % iw;
+  const int slice = threadIdx.x / iw;
+  const long i = (long)blockIdx.x * iw + item_in_wg;
+  const bool live = i < total;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  uint32_t pix = 0;
+  int c0 = 0;
+  if (live) {
+    pix = groups.div((uint32_t)i);
+    c0 = 4 * (int)((uint32_t)i - pix * groups.d);
+    const uint32_t t = ow.div(pix);
+    const int ox = (int)(pix - t * p.out_w);
+    const uint32_t n = oh.div(t);
+    const int oy = (int)(t - n * p.out_h);
+    const int K = p.k_h * p.k_w * p.in_c;
+    const int per = (K + ks - 1) / ks;
+    const int k0 = slice * per, k1 = min(K, k0 + per);
+    const bool vec = (p.out_c % 4) == 0;
+    const int nc = min(4, p.out_c - c0);
+    // walk k = (fy * k_w + fx) * in_c + ci over this slice
+    int ci = k0 % p.in_c;
+    int tap = k0 / p.in_c;
+    int fy = tap / p.k_w, fx = tap - (tap / p.k_w) * p.k_w;
+    for (int k = k0; k < k1;) {
+      const int y = oy * p.stride_h - p.pad_h + fy * p.dil_h;
       const int x = ox * p.stride_w - p.pad_w + fx * p.dil_w;
-      if (x < 0 || x >= p.in_w) continue;
-      const float* src = p.input + (((long)n * p.in_h + y) * p.in_w + x) * p.in_c;
-      const float* w = p.weights + (long)((fy * p.k_w + fx) * p.in_c) * p.out_c + c0;
-      for (int ci = 0; ci < p.in_c; ++ci) {
-        const float xv = src[ci];
+      const int run = min(k1 - k, p.in_c - ci);  // channels left in this tap
+      if (y >= 0 && y < p.in_h && x >= 0 && x < p.in_w) {
+        const float* src = p.input + (((long)n * p.in_h + y) * p.in_w + x) * p.in_c + ci;
+        const float* w = p.weights + (long)k * p.out_c + c0;
         if (vec) {
-          const float4 wv = *(const float4*)(w + (long)ci * p.out_c);
-          acc[0] = fmaf(xv, wv.x, acc[0]);
-          acc[1] = fmaf(xv, wv.y, acc[1]);
-          acc[2] = fmaf(xv, wv.z, acc[2]);
-          acc[3] = fmaf(xv, wv.w, acc[3]);
+#pragma unroll 4
+          for (int j = 0; j < run; ++j) {
+            const float xv = src[j];
+            const float4 wv = *(const float4*)(w + (long)j * p.out_c);
+            acc.x = fmaf(xv, wv.x, acc.x);
+            acc.y = fmaf(xv, wv.y, acc.y);
+            acc.z = fmaf(xv, wv.z, acc.z);
+            acc.w = fmaf(xv, wv.w, acc.w);
+          }
         } else {
-          for (int c = 0; c < nc; ++c) acc[c] = fmaf(xv, w[(long)ci * p.out_c + c], acc[c]);
+          for (int j = 0; j < run; ++j) {
+            const float xv = src[j];
+            const float* wr = w + (long)j * p.out_c;
+            acc.x = fmaf(xv, wr[0], acc.x);
+            if (nc > 1) acc.y = fmaf(xv, wr[1], acc.y);
+            if (nc > 2) acc.z = fmaf(xv, wr[2], acc.z);
+            if (nc > 3) acc.w = fmaf(xv, wr[3], acc.w);
+          }
         }
+      }
+      k += run;
+      ci = 0;
+      if (++fx == p.k_w) {
+        fx = 0;
+        ++fy;
       }
     }
   }
+  if (ks > 1) {
+    part[threadIdx.x] = acc;
+    __syncthreads();
+    if (slice != 0) return;
+    for (int s2 = 1; s2 < ks; ++s2) {
+      const float4 o = part[s2 * iw + item_in_wg];
+      acc.x += o.x;
+      acc.y += o.y;
+      acc.z += o.z;
+      acc.w += o.w;
+    }
+  }
+  if (!live) return;
+  const int nc = min(4, p.out_c - c0);
+  const float r[4] = {acc.x, acc.y, acc.z, acc.w};
   float* out = p.output + (long)pix * p.out_c + c0;
-  for (int c = 0; c < nc; ++c) out[c] = clampf(acc[c] + (p.bias ? p.bias[c0 + c] : 0.f), p.act_min, p.act_max);
+  for (int c = 0; c < nc; ++c) out[c] = clampf(r[c] + (p.bias ? p.bias[c0 + c] : 0.f), p.act_min, p.act_max);
 }
 
 // DEPTHWISE_CONV_2D: one thread = one output pixel x 4 channels
@@ -184,12 +231,18 @@ extern "C" int bh_conv2d_f32(const bh_conv_f32_params* pp, bh_stream_t s) {
     return BH_EINVAL;
   }
   bh::FastDiv dg((uint32_t)groups), dw((uint32_t)p.out_w), dh((uint32_t)p.out_h);
-  if (p.depthwise)
+  if (p.depthwise) {
     hipLaunchKernelGGL(bh::dwconv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
                        total);
-  else
-    hipLaunchKernelGGL(bh::conv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
-                       total);
+  } else {
+    // split the reduction until ~1024 workgroups or 16 taps-channels per slice
+    const int K = p.k_h * p.k_w * p.in_c;
+    int ks = 1;
+    while (ks < 16 && (total * ks) / 256 < 1024 && K / (2 * ks) >= 16) ks *= 2;
+    const long items_per_wg = 256 / ks;
+    hipLaunchKernelGGL(bh::conv_f32_kernel, dim3((unsigned)((total + items_per_wg - 1) / items_per_wg)), dim3(256),
+                       0, (hipStream_t)s, p, dg, dw, dh, total, ks);
+  }
   return bh_check_launch(p.depthwise ? "dwconv_f32_kernel" : "conv_f32_kernel");
 }
 

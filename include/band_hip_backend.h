@@ -107,7 +107,10 @@ int bhx_run_jobs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mas
 /* --- extensions (measurement / tuning; not part of Band's interface) --- */
 int bhx_executor_set_graph(bhx_executor* e, int enabled);
 int bhx_executor_device(bhx_executor* e, int* ordinal);
-/* per-launch HIP-event timing of a prepared subgraph, averaged over iters */
+/* per-launch HIP-event timing of a prepared subgraph: the launch sequence is
+ * queued behind a spin kernel, each launch issued 8 times back to back
+ * between its events (its duration plus a share of the dependent-dispatch
+ * gap, comparable with rocprofv3's kernel durations); averaged over iters */
 int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
                          bhx_op_timing* out, int cap, int* n);
 /* A Band GPU worker serving a mixed request stream (BASELINE C3): worker

@@ -58,33 +58,40 @@ def parse():
                    choices=["round_robin", "fixed_worker", "shortest_expected_latency",
                             "heterogeneous_earliest_finish_time"])
     p.add_argument("--inflight", type=int, default=0, help="outstanding requests (default 2 x workers)")
+    p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
+                   help="cpu: --workers-per-gpu Band CPU workers instead of GPU workers (C1 / CPU tests; no roofline)")
+    p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
     return p.parse_args()
 
 
-def model_list(name):
-    """[(model name, .tflite bytes)] of the workload"""
+def model_list(name, size=0):
+    """[(model name, .tflite bytes)] of the workload (size 0: the configs'
+    224x224, EfficientDet-Lite2 448x448)"""
     from band_amd import tflite_synth as S
+    sz = size or 224
+    ed = size or 448
     if name == "mix_c3":
-        return [(m, getattr(S, m)(np.int8)) for m in S.MIX_C3]
+        return [(m, getattr(S, m)(np.int8, size=sz)) for m in S.MIX_C3]
     if name == "mobilenet_v2_int8":
-        return [(name, S.mobilenet_v2(np.int8, seed=0))]
+        return [(name, S.mobilenet_v2(np.int8, seed=0, size=sz))]
     if name == "mobilenet_v2_uint8":
-        return [(name, S.mobilenet_v2(np.uint8, seed=0))]
+        return [(name, S.mobilenet_v2(np.uint8, seed=0, size=sz))]
     if name == "mobilenet_v1_int8":
-        return [(name, S.mobilenet_v1(np.int8, seed=0))]
+        return [(name, S.mobilenet_v1(np.int8, seed=0, size=sz))]
     if name == "efficientdet_lite2_int8":
-        return [(name, S.efficientdet_lite2(np.int8, size=448))]
+        return [(name, S.efficientdet_lite2(np.int8, size=ed))]
     if name == "mix_c5":
         # 8 DNNs, int8 + fp16 (float16 weights, float32 compute)
-        return [("mobilenet_v1_int8", S.mobilenet_v1(np.int8)), ("mobilenet_v2_int8", S.mobilenet_v2(np.int8)),
-                ("ssd_mobilenet_v2_int8", S.ssd_mobilenet_v2(np.int8)),
-                ("deeplab_v3_mobilenet_v2_int8", S.deeplab_v3_mobilenet_v2(np.int8)),
-                ("posenet_mobilenet_v1_int8", S.posenet_mobilenet_v1(np.int8)),
-                ("efficientdet_lite2_int8", S.efficientdet_lite2(np.int8, size=448)),
-                ("mobilenet_v2_fp16", S.mobilenet_v2(np.float16)),
-                ("ssd_mobilenet_v2_fp16", S.ssd_mobilenet_v2(np.float16))]
+        return [("mobilenet_v1_int8", S.mobilenet_v1(np.int8, size=sz)),
+                ("mobilenet_v2_int8", S.mobilenet_v2(np.int8, size=sz)),
+                ("ssd_mobilenet_v2_int8", S.ssd_mobilenet_v2(np.int8, size=sz)),
+                ("deeplab_v3_mobilenet_v2_int8", S.deeplab_v3_mobilenet_v2(np.int8, size=sz)),
+                ("posenet_mobilenet_v1_int8", S.posenet_mobilenet_v1(np.int8, size=sz)),
+                ("efficientdet_lite2_int8", S.efficientdet_lite2(np.int8, size=ed)),
+                ("mobilenet_v2_fp16", S.mobilenet_v2(np.float16, size=sz)),
+                ("ssd_mobilenet_v2_fp16", S.ssd_mobilenet_v2(np.float16, size=sz))]
     base = name[:-len("_int8")]
-    return [(name, getattr(S, base)(np.int8))]
+    return [(name, getattr(S, base)(np.int8, size=sz))]
 
 
 class Dist:
@@ -124,7 +131,7 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(models, seconds):
+def cpu_baseline(models, seconds, edge=224):
     """Oracle (scalar C port of TFLite's reference kernels) on the host, the
     same round-robin request stream over the models."""
     from oracle.runner import OracleInterpreter
@@ -147,7 +154,89 @@ def cpu_baseline(models, seconds):
     dt = time.perf_counter() - t0
     names = "+".join(name for name, _ in models)
     return dict(value=n / dt, unit="inferences/s", cores=1, kind="port",
-                sample="%d round-robin jobs of %s (224x224 int8) on 1 host core, %.1f s" % (n, names, dt))
+                sample="%d round-robin jobs of %s (%dx%d) on 1 host core, %.1f s" % (n, names, edge, edge, dt))
+
+
+def workload_label(args, models, n_cpu, W, poisson):
+    """config.workload: which BASELINE config (C1-C5) this run measures"""
+    names = ", ".join(nm for nm, _ in models)
+    edge = args.size or 224
+    if args.device == "cpu":
+        return ("%s%s %dx%d batch-1 jobs through the Band engine, %s over %d Band CPU worker(s) (%d threads each)"
+                % ("C1: " if args.model == "mobilenet_v1_int8" and W == 1 else "", names, edge, edge,
+                   args.scheduler, W, args.cpu_threads))
+    if args.model == "mix_c5":
+        return ("C5: 8-DNN int8 + fp16 mix (%s), open-loop Poisson arrivals at %.0f req/s per GPU, %s + "
+                "latency estimator over [%d CPU, %d GPU] Band workers per MI355X"
+                % (names, poisson["rate_per_s_per_gpu"], args.scheduler, n_cpu, W))
+    if len(models) > 1:
+        return ("C3: 4-DNN int8 mix (%s), %dx%d batch-1 jobs through the Band engine, %s over %d Band GPU "
+                "worker(s) per MI355X" % (names, edge, edge, args.scheduler, W))
+    if args.model == "efficientdet_lite2_int8":
+        e = args.size or 448
+        return ("C4: EfficientDet-Lite2 int8 %dx%d batch-1 jobs through the Band engine, model_analyzer split "
+                "(network on GPU workers, TFLite_Detection_PostProcess on %d CPU worker(s)), %s over %d Band GPU "
+                "worker(s) per MI355X" % (e, e, n_cpu, args.scheduler, W))
+    return ("C2: %s %dx%d batch-1 jobs through the Band engine, %s over %d Band GPU worker(s) per MI355X"
+            % (args.model, edge, edge, args.scheduler, W))
+
+
+def profile_roofline(args, D, models, paths):
+    """per-launch roofline of the dominant kernel + device time per model
+    (GPU runs only)"""
+    import band_amd
+    from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
+    M = len(models)
+    # profiling executors (outside the engine, same backend code) for the
+    # per-kernel roofline and the device-side floor of a job
+    prof_wid = 1000
+    band_amd.SetWorkerDevice(prof_wid, D.local_rank)
+    execs0, keys0 = [], []
+    for mid, path in enumerate(paths):
+        hm = HipModel(100 + mid)
+        assert hm.FromPath(path).ok()
+        ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
+        if args.no_graph:
+            ex.SetUseGraph(False)
+        spec = ex.InvestigateModelSpec(hm)
+        gpu_ops = [i for i in range(spec.num_ops) if i not in spec.unsupported_ops[DeviceFlag.kGPU]]
+        # a split model: profile its GPU part (ops before the first CPU-only op)
+        assert ex.PrepareSubgraph(hm, gpu_ops if len(gpu_ops) < spec.num_ops else ()).ok()
+        execs0.append(ex)
+        keys0.append(SubgraphKey(100 + mid, prof_wid))
+        ex._model_ref = hm
+
+    # roofline of the dominant kernel: per-launch HIP events on the worker's
+    # stream, over one inference of each model (the mix is uniform)
+    by_k = {}
+    for ex, key in zip(execs0, keys0):
+        for r in ex.ProfileSubgraph(key, iters=args.profile_iters):
+            # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
+            # with its residual epilogue), as rocprofv3 reports them
+            k = by_k.setdefault(r["kernel"].split("+")[0], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
+            k["ms"] += r["ms"] / M
+            k["bytes"] += r["alg_bytes"] / M
+            k["ops"] += r["alg_ops"] / M
+            k["launches"] += 1.0 / M
+    dom_name = max(by_k, key=lambda k: by_k[k]["ms"])
+    dom = by_k[dom_name]
+    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
+    # passes (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
+    # corrections of MI355X_MICROARCH.md), per launch; null when absent
+    traffic, traffic_src = None, None
+    import glob
+    pmc = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic.json")))
+    if pmc:
+        with open(pmc[-1]) as f:
+            tj = json.load(f)
+        if dom_name in tj:
+            traffic, traffic_src = tj[dom_name]["traffic_bytes_per_launch"], os.path.basename(pmc[-1])
+    # device-side floor of one job: each model's passes replayed back to back
+    # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
+    # host launch + sync wakeup
+    device_us = {name: ex.TimeSubgraph(key, iters=100) for (name, _), ex, key in zip(models, execs0, keys0)}
+
+    return dom_name, dom, by_k, traffic, traffic_src, device_us
 
 
 def main():
@@ -161,7 +250,7 @@ def main():
     from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
     from band_amd.engine import Engine, Model, SchedulerType, make_config
 
-    models = model_list(args.model)
+    models = model_list(args.model, args.size)
     M = len(models)
     W = max(1, args.workers_per_gpu)
     paths = []
@@ -180,16 +269,21 @@ def main():
     n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if needs_cpu else 0)
     if args.model == "mix_c5" and args.scheduler == "round_robin":
         args.scheduler = "shortest_expected_latency"  # C5: SEL + latency estimator
-    workers = [DeviceFlag.kCPU] * n_cpu + [DeviceFlag.kGPU] * W
+    on_gpu = args.device == "gpu"
+    if not on_gpu:
+        n_cpu = 0
+    workers = [DeviceFlag.kCPU] * n_cpu + [DeviceFlag.kGPU if on_gpu else DeviceFlag.kCPU] * W
     for w in range(n_cpu, n_cpu + W):
-        band_amd.SetWorkerDevice(w, D.local_rank)
+        if on_gpu:
+            band_amd.SetWorkerDevice(w, D.local_rank)
     sched = {"round_robin": SchedulerType.kRoundRobin, "fixed_worker": SchedulerType.kFixedWorker,
              "shortest_expected_latency": SchedulerType.kShortestExpectedLatency,
              "heterogeneous_earliest_finish_time": SchedulerType.kHeterogeneousEarliestFinishTime}[args.scheduler]
     if n_cpu and args.scheduler in ("round_robin", "fixed_worker"):
         sched = SchedulerType.kHeterogeneousEarliestFinishTime  # a split model needs fallback subgraphs
         args.scheduler = "heterogeneous_earliest_finish_time"
-    engine = Engine(make_config([sched], workers, num_threads=[args.cpu_threads] * n_cpu + [1] * W,
+    engine = Engine(make_config([sched], workers,
+                                num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
                                 num_warmups=3, num_runs=5))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + D.rank)
@@ -233,63 +327,26 @@ def main():
     all_lat = [x for part in D.gather((lat_us * 1e-6).tolist()) for x in part]
     jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
 
-    # profiling executors (outside the engine, same backend code) for the
-    # per-kernel roofline and the device-side floor of a job
-    prof_wid = 1000
-    band_amd.SetWorkerDevice(prof_wid, D.local_rank)
-    execs0, keys0 = [], []
-    for mid, path in enumerate(paths):
-        hm = HipModel(100 + mid)
-        assert hm.FromPath(path).ok()
-        ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
-        if args.no_graph:
-            ex.SetUseGraph(False)
-        spec = ex.InvestigateModelSpec(hm)
-        gpu_ops = [i for i in range(spec.num_ops) if i not in spec.unsupported_ops[DeviceFlag.kGPU]]
-        # a split model: profile its GPU part (ops before the first CPU-only op)
-        assert ex.PrepareSubgraph(hm, gpu_ops if len(gpu_ops) < spec.num_ops else ()).ok()
-        execs0.append(ex)
-        keys0.append(SubgraphKey(100 + mid, prof_wid))
-        ex._model_ref = hm
-
-    # roofline of the dominant kernel: per-launch HIP events on the worker's
-    # stream, over one inference of each model (the mix is uniform)
-    by_k = {}
-    for ex, key in zip(execs0, keys0):
-        for r in ex.ProfileSubgraph(key, iters=args.profile_iters):
-            # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
-            # with its residual epilogue), as rocprofv3 reports them
-            k = by_k.setdefault(r["kernel"].split("+")[0], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
-            k["ms"] += r["ms"] / M
-            k["bytes"] += r["alg_bytes"] / M
-            k["ops"] += r["alg_ops"] / M
-            k["launches"] += 1.0 / M
-    dom_name = max(by_k, key=lambda k: by_k[k]["ms"])
-    dom = by_k[dom_name]
-    avg_ms = dom["ms"] / dom["launches"]
-    bytes_per_launch = dom["bytes"] / dom["launches"]
-    ops_per_launch = dom["ops"] / dom["launches"]
-    achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-    gpu_ms_total = sum(v["ms"] for v in by_k.values())
-    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
-    # passes (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
-    # corrections of MI355X_MICROARCH.md), per launch; null when absent
-    traffic, traffic_src = None, None
-    import glob
-    pmc = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic.json")))
-    if pmc:
-        with open(pmc[-1]) as f:
-            tj = json.load(f)
-        if dom_name in tj:
-            traffic, traffic_src = tj[dom_name]["traffic_bytes_per_launch"], os.path.basename(pmc[-1])
-    # device-side floor of one job: each model's passes replayed back to back
-    # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
-    # host launch + sync wakeup
-    device_us = {name: ex.TimeSubgraph(key, iters=100) for (name, _), ex, key in zip(models, execs0, keys0)}
+    roof, dev = None, None
+    if on_gpu:
+        dom_name, dom, by_k, traffic, traffic_src, device_us = profile_roofline(args, D, models, paths)
+        avg_ms = dom["ms"] / dom["launches"]
+        bytes_per_launch = dom["bytes"] / dom["launches"]
+        ops_per_launch = dom["ops"] / dom["launches"]
+        achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
+        roof = {
+            "kernel": dom_name, "bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
+            "frac": achieved_gbs / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
+            "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
+            "launches_per_inference": dom["launches"],
+            "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,
+            "mfma_i8_frac": ops_per_launch / (avg_ms * 1e-3) / 5.0e15,
+        }
+        dev = dict(gpu_ms_total=sum(v["ms"] for v in by_k.values()), device_us=device_us)
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(models, args.cpu_baseline_seconds)
+        cpu = cpu_baseline(models, args.cpu_baseline_seconds, args.size or 224)
 
     if D.rank == 0:
         n = D.world
@@ -307,20 +364,9 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8" if args.model.endswith("uint8") else ("int8+fp16" if args.model == "mix_c5" else "int8"),
-            "data": "synthetic (seeded int8 inputs and weights; no checkpoint)",
-            "config": {"workload": ("C3: 4-DNN int8 mix (%s), 224x224 batch-1 jobs through the Band engine, "
-                                    "%s over %d Band GPU worker(s) per MI355X" %
-                                    (", ".join(nm for nm, _ in models), args.scheduler, W))
-                       if M > 1 and args.model != "mix_c5" else
-                       ("C5: 8-DNN int8 + fp16 mix (%s), open-loop Poisson arrivals at %.0f req/s per GPU, %s + "
-                        "latency estimator over [%d CPU, %d GPU] Band workers per MI355X"
-                        % (", ".join(nm for nm, _ in models), poisson["rate_per_s_per_gpu"], args.scheduler, n_cpu, W))
-                       if args.model == "mix_c5" else (("C4: EfficientDet-Lite2 int8 448x448 batch-1 jobs through the Band engine, "
-                                       "model_analyzer split (network on GPU workers, TFLite_Detection_PostProcess "
-                                       "on %d CPU worker(s)), %s over %d Band GPU worker(s) per MI355X"
-                                       % (n_cpu, args.scheduler, W)) if args.model == "efficientdet_lite2_int8" else
-                                      ("C2: %s 224x224 batch-1 jobs through the Band engine, %s over %d Band GPU "
-                                       "worker(s) per MI355X" % (args.model, args.scheduler, W))),
+            "data": "synthetic (seeded inputs and weights; no checkpoint)",
+            "device": args.device,
+            "config": {"workload": workload_label(args, models, n_cpu, W, poisson),
                        "harness": "native Band engine (planner + workers + %s), %d requests in flight"
                                   % (args.scheduler, inflight),
                        "jobs_per_worker_rank0": jobs_per_worker,
@@ -329,17 +375,10 @@ def main():
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
             "p50_job_latency_ms": float(np.percentile(lat_ms, 50)),
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)),
-            "gpu_kernel_ms_per_inference": gpu_ms_total,
-            "device_us_per_inference": float(np.mean(list(device_us.values()))),
-            "device_us_per_model": device_us,
-            "roofline": {
-                "kernel": dom_name, "bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
-                "frac": achieved_gbs / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
-                "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
-                "launches_per_inference": dom["launches"],
-                "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,
-                "mfma_i8_frac": ops_per_launch / (avg_ms * 1e-3) / 5.0e15,
-            },
+            "gpu_kernel_ms_per_inference": dev["gpu_ms_total"] if dev else None,
+            "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
+            "device_us_per_model": dev["device_us"] if dev else None,
+            "roofline": roof,
             "cpu_baseline": cpu,
             "host": platform.node(),
         }

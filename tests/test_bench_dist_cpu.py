@@ -1,0 +1,68 @@
+"""bench.py's multi-rank path on the CPU (gloo, world_size 2), and the C1 line.
+
+The N>1 bench is one process per GPU with no data-path collective: each
+rank serves its own job stream, a gloo group provides only the barrier,
+the max-over-ranks time and the latency gather (bench.py `Dist`).  With
+`--device cpu` the same code runs its engine on Band CPU workers, so the
+whole launch / barrier / reduction / JSON contract is exercised here
+without a GPU.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _json_line(out):
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def _env():
+    env = dict(os.environ)
+    env["OMP_NUM_THREADS"] = "1"
+    return env
+
+
+def test_bench_two_ranks_gloo():
+    steps = 12
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--device", "cpu", "--model", "mix_c3", "--size", "64", "--workers-per-gpu", "1",
+           "--cpu-threads", "2", "--steps", str(steps), "--warmup", "4"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 2 and line["steps"] == steps and line["scaling"] == "weak"
+    # value = all ranks' jobs / max-over-ranks time; ms_per_step is that time / steps
+    elapsed_s = line["ms_per_step"] * steps / 1e3
+    assert abs(line["value"] - 2 * steps / elapsed_s) < 1e-6 * line["value"]
+    assert sum(line["config"]["jobs_per_worker_rank0"]) == steps
+    assert line["p99_job_latency_ms"] >= line["p50_job_latency_ms"] > 0
+    assert line["cpu_baseline"] is None  # rank 0 at N=1 only
+    assert line["roofline"] is None  # no GPU kernels on CPU workers
+    assert "no collective" in line["config"]["parallelism"]
+
+
+def test_bench_c1_cpu_worker_line():
+    """C1: MobileNetV1 int8 on one Band CPU worker, fixed_worker"""
+    cmd = [sys.executable, "bench.py", "--device", "cpu", "--model", "mobilenet_v1_int8", "--size", "64",
+           "--workers-per-gpu", "1", "--scheduler", "fixed_worker", "--cpu-threads", "2", "--steps", "8",
+           "--warmup", "2", "--cpu-baseline-seconds", "0.5"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    assert line["n_gpus"] == 1 and line["config"]["workload"].startswith("C1: ")
+    assert line["config"]["jobs_per_worker_rank0"] == [8]
+    cb = line["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0

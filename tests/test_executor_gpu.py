@@ -136,10 +136,19 @@ def test_error_behaviour(gpu_lib, golden_dir):
     assert not st.ok() and st.message() == "Cannot find subgraph"
     wrong = HipModelExecutor(6, 1, DeviceFlag.kGPU)
     assert not wrong.PrepareSubgraph(model).ok()
-    # float ADD is outside the int8 kernel set: reported, and refused on kGPU
+    # float ADD is in the float32 kernel set: the whole model prepares on kGPU
     spec = ex.InvestigateModelSpec(model)
-    assert spec.unsupported_ops[DeviceFlag.kGPU] == {0, 1}
-    assert not ex.PrepareSubgraph(model).ok()
+    assert spec.unsupported_ops[DeviceFlag.kGPU] == set()
+    assert ex.PrepareSubgraph(model).ok()
+    # TFLite_Detection_PostProcess is CPU-only: reported, and a whole-model
+    # subgraph containing it is refused on kGPU
+    from tests.glue_models import split_zoo
+    split = HipModel(7)
+    assert split.FromBuffer(split_zoo()).ok()
+    ex7 = HipModelExecutor(7, 1, DeviceFlag.kGPU)
+    bad = ex7.InvestigateModelSpec(split).unsupported_ops[DeviceFlag.kGPU]
+    assert len(bad) == 1
+    assert not ex7.PrepareSubgraph(split).ok()
 
 
 @pytest.mark.parametrize("arch,dtype,batch", [

@@ -66,6 +66,10 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_executor_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
     "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int)]),
     "bhx_time_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(ctypes.c_double)]),
+    "bhx_prepare_job_batches": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_uint64, c_int]),
+    "bhx_max_job_batch": (c_int, _KEY + [ctypes.POINTER(c_int)]),
+    "bhx_job_slot_view": (c_int, _KEY + [c_int, c_int, c_int, ctypes.POINTER(TensorInfo)]),
+    "bhx_execute_job_batch": (c_int, _KEY + [c_int]),
     "bhx_run_mixed_jobs": (c_int, [c_int, ctypes.POINTER(c_void_p), ctypes.POINTER(c_int), c_int, ctypes.c_uint64,
                                    ctypes.POINTER(c_void_p), c_int, c_int, ctypes.POINTER(ctypes.c_double),
                                    ctypes.POINTER(c_int)]),
@@ -386,6 +390,24 @@ class HipModelExecutor:
 
     def ExecuteSubgraph(self, key):
         return Status.from_rc(self.lib.bhx_execute_subgraph(self.handle, *key._args()))
+
+    # ---- job batching (band/interface/job_batching.h) -------------------
+    def PrepareJobBatches(self, model, key, max_batch):
+        return Status.from_rc(self.lib.bhx_prepare_job_batches(self.handle, model.handle, *key._args(),
+                                                               int(max_batch)))
+
+    def MaxJobBatch(self, key):
+        n = c_int(1)
+        _abi.check(self.lib.bhx_max_job_batch(self.handle, *key._args(), ctypes.byref(n)), "MaxJobBatch")
+        return n.value
+
+    def GetJobSlotView(self, key, index, n, slot):
+        info = TensorInfo()
+        rc = self.lib.bhx_job_slot_view(self.handle, *key._args(), int(index), int(n), int(slot), ctypes.byref(info))
+        return None if rc != 0 else HipTensorView(info, self)
+
+    def ExecuteJobBatch(self, key, n):
+        return Status.from_rc(self.lib.bhx_execute_job_batch(self.handle, *key._args(), int(n)))
 
     # ---- extensions -----------------------------------------------------
     def RunJobs(self, key, inputs, n_jobs, out=None):

@@ -193,9 +193,8 @@ size_t bhx_get_num_nodes(bhx_executor* e, int mid, int wid, uint64_t mask) {
   return e ? e->exec->GetNumNodes(Key(mid, wid, mask)) : 0;
 }
 
-int bhx_get_tensor_view(bhx_executor* e, int mid, int wid, uint64_t mask, int t, bhx_tensor_info* info) {
-  if (!e || !info) return Fail("null argument");
-  auto v = e->exec->GetTensorView(Key(mid, wid, mask), t);
+namespace {
+int FillInfo(const std::shared_ptr<band::interface::ITensorView>& v, bhx_tensor_info* info) {
   if (!v) return Fail("Cannot find tensor view");
   std::memset(info, 0, sizeof(*info));
   info->type = static_cast<int>(v->GetType());
@@ -214,6 +213,12 @@ int bhx_get_tensor_view(bhx_executor* e, int mid, int wid, uint64_t mask, int t,
     info->quantized_dimension = a->quantized_dimension;
   }
   return 0;
+}
+}  // namespace
+
+int bhx_get_tensor_view(bhx_executor* e, int mid, int wid, uint64_t mask, int t, bhx_tensor_info* info) {
+  if (!e || !info) return Fail("null argument");
+  return FillInfo(e->exec->GetTensorView(Key(mid, wid, mask), t), info);
 }
 
 int bhx_get_largest_subgraph_key(bhx_executor* e, int* mid, int* wid, uint64_t* mask) {
@@ -341,6 +346,34 @@ int bhx_profile_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int i
   for (int i = 0; i < cap && i < static_cast<int>(t.size()); ++i)
     out[i] = bhx_op_timing{t[i].op_index, t[i].kernel, t[i].ms, t[i].alg_bytes, t[i].alg_ops};
   return 0;
+}
+
+int bhx_prepare_job_batches(bhx_executor* e, bhx_model* m, int mid, int wid, uint64_t mask, int max_batch) {
+  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  if (!b || !m) return Fail("executor without job batching");
+  auto s = b->PrepareJobBatches(m->model.get(), Key(mid, wid, mask), max_batch);
+  return s.ok() ? 0 : Fail(s);
+}
+
+int bhx_max_job_batch(bhx_executor* e, int mid, int wid, uint64_t mask, int* max_batch) {
+  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  if (!max_batch) return Fail("null argument");
+  *max_batch = b ? b->MaxJobBatch(Key(mid, wid, mask)) : 1;
+  return 0;
+}
+
+int bhx_job_slot_view(bhx_executor* e, int mid, int wid, uint64_t mask, int t, int n, int slot,
+                      bhx_tensor_info* info) {
+  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  if (!b || !info) return Fail("executor without job batching");
+  return FillInfo(b->GetJobSlotView(Key(mid, wid, mask), t, n, slot), info);
+}
+
+int bhx_execute_job_batch(bhx_executor* e, int mid, int wid, uint64_t mask, int n) {
+  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  if (!b) return Fail("executor without job batching");
+  auto s = b->ExecuteJobBatch(Key(mid, wid, mask), n);
+  return s.ok() ? 0 : Fail(s);
 }
 
 int bhx_time_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int iters, double* us) {

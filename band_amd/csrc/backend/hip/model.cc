@@ -50,5 +50,32 @@ absl::Status HipModel::FromBuffer(const char* buffer, size_t buffer_size) {
   return s.ok() ? s : absl::InternalError("Cannot load from buffer.");
 }
 
+absl::Status HipModel::CloneWithJobBatch(int batch, std::unique_ptr<HipModel>* out) const {
+  if (!initialized_) return absl::InternalError("job batching: model not loaded");
+  if (batch < 1) return absl::InternalError("job batching: batch must be >= 1");
+  for (const TflOperator& op : desc_.ops) {
+    if (op.builtin == kTflCustom) return absl::InternalError("job batching: CUSTOM op " + op.custom_code);
+    if (op.builtin == kTflConcatenation && op.options.valid() && !op.outputs.empty()) {
+      const int rank = static_cast<int>(desc_.tensors[op.outputs[0]].shape.size());
+      int axis = op.options.Int(0, 0);
+      if (axis < 0) axis += rank;
+      if (axis == 0) return absl::InternalError("job batching: CONCATENATION on the batch axis");
+    }
+  }
+  for (const TflTensor& t : desc_.tensors)
+    if (!t.is_const() && (t.shape.empty() || t.shape[0] != 1))
+      return absl::InternalError("job batching: tensor '" + t.name + "' has no unit batch dimension");
+  auto m = std::make_unique<HipModel>(id_);
+  m->path_ = path_;
+  std::vector<uint8_t> bytes = bytes_;
+  absl::Status loaded = m->Load(std::move(bytes));
+  if (!loaded.ok()) return loaded;
+  for (TflTensor& t : m->desc_.tensors)
+    if (!t.is_const()) t.shape[0] = batch;
+  m->serial_ = serial_;
+  *out = std::move(m);
+  return absl::OkStatus();
+}
+
 }  // namespace hip
 }  // namespace band

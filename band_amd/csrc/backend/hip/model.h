@@ -9,6 +9,7 @@
 #include <vector>
 
 #include "absl/status/status.h"
+#include <string>
 #include "backend/hip/tflite_reader.h"
 #include "band/interface/model.h"
 
@@ -26,6 +27,13 @@ class HipModel : public interface::IModel {
   const TflModel& desc() const { return desc_; }
   // process-unique id of the loaded contents (keys the device weight cache)
   uint64_t serial() const { return serial_; }
+
+  // Job batching (HipModelExecutor::PrepareJobBatches): a copy of this model
+  // whose activation tensors carry a leading batch of `batch` jobs.  Every
+  // non-constant tensor must have dim 0 == 1 and no op may mix the batch
+  // axis (CONCATENATION on axis 0, CUSTOM ops); otherwise an error says why.
+  // The copy keeps this model's serial, so device weights stay shared.
+  absl::Status CloneWithJobBatch(int batch, std::unique_ptr<HipModel>* out) const;
 
  private:
   absl::Status Load(std::vector<uint8_t>&& bytes);

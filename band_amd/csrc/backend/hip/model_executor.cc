@@ -1985,6 +1985,72 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   return absl::OkStatus();
 }
 
+absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const SubgraphKey& key, int max_batch) {
+  if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("job batching needs a kGPU executor");
+  PreparedSubgraph* base = Find(key);
+  if (!base) return absl::InternalError("Cannot find subgraph");
+  auto* hm = dynamic_cast<HipModel*>(model);
+  if (!hm || hm != model_) return absl::InternalError("job batching: not the model this executor prepared");
+  job_batches_.erase(key);
+  if (max_batch <= 1) return absl::OkStatus();
+  std::vector<int> sizes;
+  for (int b = 2; b < max_batch; b *= 2) sizes.push_back(b);
+  sizes.push_back(max_batch);
+  // a whole-model subgraph is prepared as one (model-order I/O), not as its op set
+  std::set<int> ops;
+  if (base->ops.size() != hm->desc().ops.size()) ops.insert(base->ops.begin(), base->ops.end());
+  const std::set<int> units = key.GetUnitIndicesSet();
+  std::vector<JobBatchVariant> variants;
+  for (int b : sizes) {
+    JobBatchVariant v;
+    v.batch = b;
+    RETURN_STATUS_IF(hm->CloneWithJobBatch(b, &v.model));
+    v.exec = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
+                                                num_threads_);
+    v.exec->use_graph_ = use_graph_;
+    // the base subgraph's op set (a whole-model key prepares all ops)
+    RETURN_STATUS_IF(v.exec->PrepareSubgraph(v.model.get(), ops, units));
+    PreparedSubgraph* vs = v.exec->Find(key);
+    if (!vs || vs->inputs != base->inputs || vs->outputs != base->outputs)
+      return absl::InternalError("job batching: variant I/O differs from the subgraph's");
+    variants.push_back(std::move(v));
+  }
+  job_batches_[key] = std::move(variants);
+  return absl::OkStatus();
+}
+
+int HipModelExecutor::MaxJobBatch(const SubgraphKey& key) const {
+  auto it = job_batches_.find(key);
+  return it == job_batches_.end() || it->second.empty() ? 1 : it->second.back().batch;
+}
+
+const HipModelExecutor::JobBatchVariant* HipModelExecutor::VariantFor(const SubgraphKey& key, int n) const {
+  auto it = job_batches_.find(key);
+  if (it == job_batches_.end()) return nullptr;
+  for (const JobBatchVariant& v : it->second)
+    if (v.batch >= n) return &v;
+  return nullptr;
+}
+
+std::shared_ptr<interface::ITensorView> HipModelExecutor::GetJobSlotView(const SubgraphKey& key, int index, int n,
+                                                                          int slot) {
+  if (n == 1 && slot == 0) return GetTensorView(key, index);
+  const JobBatchVariant* v = VariantFor(key, n);
+  if (!v || n < 1 || slot < 0 || slot >= n || index < 0 || index >= static_cast<int>(meta_.size())) return nullptr;
+  PreparedSubgraph* vs = v->exec->Find(key);
+  auto h = vs ? vs->host.find(index) : decltype(vs->host.end()){};
+  if (!vs || h == vs->host.end()) return nullptr;  // slot views exist for boundary tensors only
+  TensorMeta* m = meta_[index].get();
+  return std::make_shared<HipTensorView>(m, h->second->data() + static_cast<size_t>(slot) * m->bytes);
+}
+
+absl::Status HipModelExecutor::ExecuteJobBatch(const SubgraphKey& key, int n) {
+  if (n == 1) return ExecuteSubgraph(key);
+  const JobBatchVariant* v = VariantFor(key, n);
+  if (!v || n < 1) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
+  return v->exec->ExecuteSubgraph(key);
+}
+
 absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, double* us) {
   PreparedSubgraph* sg = Find(key);
   if (!sg) return absl::InternalError("Cannot find subgraph");

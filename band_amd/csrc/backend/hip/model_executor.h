@@ -28,6 +28,7 @@
 #include "backend/hip/device.h"
 #include "backend/hip/model.h"
 #include "backend/hip/tensor.h"
+#include "band/interface/job_batching.h"
 #include "band/interface/model_executor.h"
 #include "band_hip_kernels.h"
 
@@ -100,7 +101,7 @@ struct PreparedSubgraph {
   int runs = 0;
 };
 
-class HipModelExecutor : public interface::IModelExecutor {
+class HipModelExecutor : public interface::IModelExecutor, public interface::IJobBatching {
  public:
   HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceFlag device_flag,
                    CpuSet thread_affinity_mask, int num_threads);
@@ -121,6 +122,16 @@ class HipModelExecutor : public interface::IModelExecutor {
   SubgraphKey GetLargestSubgraphKey() const override;
   absl::Status ExecuteSubgraph(const SubgraphKey& key) override;
   void ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) override;
+
+  // --- job batching (band/interface/job_batching.h; kGPU executors) ---
+  // Variants for 2, 4, 8, ... and max_batch jobs: each is an executor of a
+  // batch-B copy of the model (HipModel::CloneWithJobBatch) over the same op
+  // set, on this executor's stream, sharing its device weights.
+  absl::Status PrepareJobBatches(interface::IModel* model, const SubgraphKey& key, int max_batch) override;
+  int MaxJobBatch(const SubgraphKey& key) const override;
+  std::shared_ptr<interface::ITensorView> GetJobSlotView(const SubgraphKey& key, int index, int n,
+                                                         int slot) override;
+  absl::Status ExecuteJobBatch(const SubgraphKey& key, int n) override;
 
   // --- extensions used by the C ABI / bench (not part of Band's interface) ---
   void SetUseGraph(bool on) { use_graph_ = on; }
@@ -165,6 +176,15 @@ class HipModelExecutor : public interface::IModelExecutor {
   absl::Status Enqueue(PreparedSubgraph* sg);
   absl::Status ExecuteOnHost(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
+
+  struct JobBatchVariant {
+    int batch = 1;
+    std::unique_ptr<HipModel> model;
+    std::unique_ptr<HipModelExecutor> exec;
+  };
+  // variant running n jobs (smallest batch >= n), or null
+  const JobBatchVariant* VariantFor(const SubgraphKey& key, int n) const;
+  std::map<SubgraphKey, std::vector<JobBatchVariant>> job_batches_;  // ascending batch
 
   const HipModel* model_ = nullptr;
   std::vector<std::unique_ptr<TensorMeta>> meta_;

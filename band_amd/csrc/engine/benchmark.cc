@@ -195,6 +195,7 @@ absl::Status Benchmark::Parse(const std::string& text) {
   }
   r.worker_config.availability_check_interval_ms =
       static_cast<int>(num(root, "availability_check_interval_ms", 30000));
+  r.worker_config.max_job_batch = static_cast<int>(num(root, "max_job_batch", 1));  // extension
   r.subgraph_config.minimum_subgraph_size = static_cast<int>(num(root, "minimum_subgraph_size", 7));
   r.subgraph_config.subgraph_preparation_type =
       FromString<SubgraphPreparationType>(str(root, "subgraph_preparation_type", "merge_unit_subgraph"));

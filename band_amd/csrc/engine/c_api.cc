@@ -92,6 +92,7 @@ absl::Status Validate(const band::RuntimeConfig& c) {
     return absl::InvalidArgumentError("[WorkerConfigBuilder] num_threads_.size() == workers_.size()");
   for (int t : w.num_threads)
     if (t < 0) return absl::InvalidArgumentError("[WorkerConfigBuilder] num_threads_[i] >= 0");
+  if (w.max_job_batch < 1) return absl::InvalidArgumentError("max_job_batch >= 1");
   if (w.availability_check_interval_ms <= 0)
     return absl::InvalidArgumentError("[WorkerConfigBuilder] availability_check_interval_ms_ > 0");
   if (c.subgraph_config.minimum_subgraph_size <= 0)
@@ -170,6 +171,7 @@ void BandAddConfig(BandConfigBuilder* b, int field, int count, ...) {
       break;  // no resource monitor on this platform
     case BAND_RESOURCE_MONITOR_INTERVAL_MS: (void)va_arg(vl, int); break;
     case BAND_RESOURCE_MONITOR_LOG_PATH: (void)va_arg(vl, const char*); break;
+    case BANDX_WORKER_MAX_JOB_BATCH: c.worker_config.max_job_batch = va_arg(vl, int); break;
     default: BAND_LOG(LogSeverity::kWarning, "unknown config field %d", field);
   }
   va_end(vl);

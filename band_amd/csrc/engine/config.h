@@ -36,6 +36,10 @@ struct WorkerConfig {
   std::vector<int> num_threads;
   bool allow_worksteal = false;
   int availability_check_interval_ms = 30000;
+  // Extension (not in band/config.h): a device-queue worker runs up to this
+  // many queued whole-model jobs of one subgraph as one batched pass when
+  // the executor implements interface::IJobBatching.  1 = Band's behaviour.
+  int max_job_batch = 1;
 };
 
 struct SubgraphConfig {

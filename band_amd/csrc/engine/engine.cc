@@ -1,5 +1,7 @@
 #include "engine/engine.h"
 
+#include "band/interface/job_batching.h"
+
 #include <algorithm>
 #include <cassert>
 #include <cstdio>
@@ -49,6 +51,7 @@ absl::Status Engine::Init(const RuntimeConfig& config) {
     for (DeviceFlag f : util->GetAvailableDevices()) valid.insert(f);
   }
   const bool global = planner_->GetWorkerType() == static_cast<int>(WorkerType::kGlobalQueue);
+  max_job_batch_ = std::max(1, config.worker_config.max_job_batch);
   for (DeviceFlag flag : config.worker_config.workers) {
     if (!valid.count(flag)) {
       BAND_LOG(LogSeverity::kWarning, "%s worker is not created (device unavailable)", ToString(flag));
@@ -126,6 +129,16 @@ absl::Status Engine::RegisterModel(Model* model) {
       const std::set<int> eout_set(eout.begin(), eout.end());
       if (!std::includes(outputs.begin(), outputs.end(), eout_set.begin(), eout_set.end()))
         return absl::InternalError("Output format is not correct for worker " + std::to_string(def.worker_id));
+      // job batching for whole-model subgraphs on GPU workers (config extension)
+      if (max_job_batch_ > 1 && GetWorkerDevice(def.worker_id) == DeviceFlag::kGPU &&
+          static_cast<int>(def.op_indices.size()) == spec.num_ops) {
+        if (auto* jb = dynamic_cast<interface::IJobBatching*>(exec)) {
+          absl::Status bs = jb->PrepareJobBatches(backend_model, key, max_job_batch_);
+          if (!bs.ok())
+            BAND_LOG(LogSeverity::kWarning, "model %d runs unbatched on worker %d: %s", model_id, def.worker_id,
+                     bs.message().c_str());
+        }
+      }
       unit_subgraphs_to_subgraph_keys_[model_id][*def.unit_subgraph_indices.begin()]
                                       [*def.unit_subgraph_indices.rbegin()]
                                           .push_back(key);
@@ -544,6 +557,12 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
   const SubgraphKey& key = job.subgraph_key;
   interface::IModelExecutor* exec = GetModelExecutor(key);
   if (!exec) return absl::InternalError("no executor for " + key.ToString());
+  return CopyInputs(job, [&](int t) { return exec->GetTensorView(key, t); });
+}
+
+absl::Status Engine::CopyInputs(const Job& job, const ViewFn& view) {
+  const SubgraphKey& key = job.subgraph_key;
+  interface::IModelExecutor* exec = GetModelExecutor(key);
   std::set<int> unresolved(exec->GetInputs(key).begin(), exec->GetInputs(key).end());
   if (job.intermediates) {
     for (auto it = unresolved.begin(); it != unresolved.end();) {
@@ -552,7 +571,7 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
         ++it;
         continue;
       }
-      auto dst = exec->GetTensorView(key, *it);
+      auto dst = view(*it);
       if (!dst || dst->GetBytes() != hit->second.size())
         return absl::InternalError("intermediate tensor " + std::to_string(*it) + " does not fit its view");
       std::memcpy(dst->GetData(), hit->second.data(), hit->second.size());
@@ -565,7 +584,7 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
     for (int t : pexec->GetOutputs(prev)) {
       if (!unresolved.count(t)) continue;
       auto src = pexec->GetTensorView(prev, t);
-      auto dst = exec->GetTensorView(key, t);
+      auto dst = view(t);
       if (!src || !dst || !dst->CopyDataFrom(src.get()).ok())
         return absl::InternalError("Tensor data copy failure for tensor " + std::to_string(t));
       unresolved.erase(t);
@@ -579,7 +598,7 @@ absl::Status Engine::TryCopyInputTensors(const Job& job) {
       ++it;
       continue;
     }
-    auto dst = exec->GetTensorView(key, *it);
+    auto dst = view(*it);
     if (!dst || !ring->second->GetTensorFromHandle(dst.get(), *it, job.input_handle).ok())
       return absl::InternalError("Failed to copy input tensor " + std::to_string(*it) + " for model " +
                                  std::to_string(job.model_id));
@@ -614,17 +633,51 @@ absl::Status Engine::TryCopyOutputTensors(const Job& job) {
   const SubgraphKey& key = job.subgraph_key;
   interface::IModelExecutor* exec = GetModelExecutor(key);
   if (!exec) return absl::InternalError("no executor for " + key.ToString());
+  return CopyOutputs(job, [&](int t) { return exec->GetTensorView(key, t); });
+}
+
+absl::Status Engine::CopyOutputs(const Job& job, const ViewFn& view) {
+  const SubgraphKey& key = job.subgraph_key;
+  interface::IModelExecutor* exec = GetModelExecutor(key);
   auto ring = model_output_buffer_.find(job.model_id);
   if (ring == model_output_buffer_.end())
     return absl::InternalError("Failed to find output tensor ring buffer for model " + std::to_string(job.model_id));
   for (int t : exec->GetOutputs(key)) {
     if (!ring->second->IsTensorIndexValid(t)) continue;
-    auto src = exec->GetTensorView(key, t);
+    auto src = view(t);
     if (!src || !ring->second->PutTensorToHandle(src.get(), t, job.output_handle).ok())
       return absl::InternalError("Failed to copy output tensor " + std::to_string(t) + " for model " +
                                  std::to_string(job.model_id));
   }
   return absl::OkStatus();
+}
+
+int Engine::MaxJobBatch(const SubgraphKey& key) const {
+  if (max_job_batch_ <= 1) return 1;
+  auto* jb = dynamic_cast<const interface::IJobBatching*>(GetModelExecutor(key));
+  return jb ? jb->MaxJobBatch(key) : 1;
+}
+
+absl::Status Engine::TryCopyInputTensorsToSlot(const Job& job, int n, int slot) {
+  if (job.input_handle < 0) return absl::OkStatus();
+  const SubgraphKey& key = job.subgraph_key;
+  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
+  return CopyInputs(job, [&](int t) { return jb->GetJobSlotView(key, t, n, slot); });
+}
+
+absl::Status Engine::InvokeJobBatch(const SubgraphKey& key, int n) {
+  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
+  return jb->ExecuteJobBatch(key, n);
+}
+
+absl::Status Engine::TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) {
+  if (job.output_handle < 0) return absl::OkStatus();
+  const SubgraphKey& key = job.subgraph_key;
+  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
+  return CopyOutputs(job, [&](int t) { return jb->GetJobSlotView(key, t, n, slot); });
 }
 
 }  // namespace band

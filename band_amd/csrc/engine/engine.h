@@ -13,6 +13,7 @@
 //  * the model analyzer resolves op support by device flag (see
 //    model_analyzer.cc).
 #pragma once
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -103,6 +104,10 @@ class Engine : public IEngine {
   absl::Status TryCopyInputTensors(const Job& job) override;
   absl::Status TryCopyOutputTensors(const Job& job) override;
   absl::Status SaveIntermediates(Job& job) override;
+  int MaxJobBatch(const SubgraphKey& key) const override;
+  absl::Status TryCopyInputTensorsToSlot(const Job& job, int n, int slot) override;
+  absl::Status InvokeJobBatch(const SubgraphKey& key, int n) override;
+  absl::Status TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) override;
   void UpdateLatency(const SubgraphKey& key, int64_t latency) override { latency_estimator_->UpdateLatency(key, latency); }
   int64_t GetProfiled(const SubgraphKey& key) const override { return latency_estimator_->GetProfiled(key); }
   int64_t GetExpected(const SubgraphKey& key) const override { return latency_estimator_->GetExpected(key); }
@@ -135,6 +140,10 @@ class Engine : public IEngine {
   const interface::IModelExecutor* GetModelExecutor(const SubgraphKey& key) const;
 
   SubgraphConfig subgraph_config_;
+  int max_job_batch_ = 1;
+  using ViewFn = std::function<std::shared_ptr<interface::ITensorView>(int)>;
+  absl::Status CopyInputs(const Job& job, const ViewFn& view);
+  absl::Status CopyOutputs(const Job& job, const ViewFn& view);
   std::vector<std::unique_ptr<Worker>> workers_;
   mutable WorkerWaitingTime workers_waiting_;
   std::unique_ptr<LatencyEstimator> latency_estimator_;

@@ -57,6 +57,17 @@ class IEngine {
   // snapshot a non-final subgraph's outputs into the job's following jobs
   virtual absl::Status SaveIntermediates(Job& job) { return absl::OkStatus(); }
 
+  // job batching (interface/job_batching.h): n jobs of one subgraph, job i
+  // in slot i; MaxJobBatch == 1 means the worker never batches `key`
+  virtual int MaxJobBatch(const SubgraphKey& key) const { return 1; }
+  virtual absl::Status TryCopyInputTensorsToSlot(const Job& job, int n, int slot) {
+    return absl::InternalError("job batching unsupported");
+  }
+  virtual absl::Status InvokeJobBatch(const SubgraphKey& key, int n) { return absl::InternalError("job batching unsupported"); }
+  virtual absl::Status TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) {
+    return absl::InternalError("job batching unsupported");
+  }
+
   // latency estimator
   virtual void UpdateLatency(const SubgraphKey& key, int64_t latency) = 0;
   virtual int64_t GetProfiled(const SubgraphKey& key) const = 0;

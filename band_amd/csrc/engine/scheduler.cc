@@ -64,9 +64,20 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
     });
     if (it == requests.end()) continue;
     Job job = std::move(*it);
-    requests.erase(it);
+    it = requests.erase(it);
     const SubgraphKey key = engine_.GetLargestSubgraphKey(job.model_id, w);
     ok &= engine_.EnqueueToWorker({job, key});
+    // job batching (extension): the idle worker also takes the next queued
+    // requests of the same model, up to its batch, and runs them in one pass
+    for (int more = engine_.MaxJobBatch(key) - 1; more > 0 && it != requests.end();) {
+      if (it->model_id == key.GetModelId()) {
+        ok &= engine_.EnqueueToWorker({*it, key});
+        it = requests.erase(it);
+        --more;
+      } else {
+        ++it;
+      }
+    }
     next_ = w + 1;
   }
   return ok;

@@ -50,6 +50,9 @@ class FixedWorkerGlobalQueueScheduler : public IScheduler {
 // part 3).  Here the waiting times are refreshed and the scan starts after
 // the worker served last, so arrivals rotate over the idle workers; a job
 // with no idle worker waits in the planner until a worker frees up.
+// Job batching (extension, WorkerConfig::max_job_batch > 1): an idle worker
+// also takes the following queued requests of the same model, up to its
+// executor's batch, which its DeviceQueueWorker runs as one pass.
 class RoundRobinScheduler : public IScheduler {
  public:
   using IScheduler::IScheduler;

@@ -95,6 +95,17 @@ void Worker::Work() {
     }
 
     const SubgraphKey key = job->subgraph_key;
+    const int max_batch = engine_->MaxJobBatch(key);
+    if (max_batch > 1 && Batchable(*job)) {
+      std::vector<Job> partners;
+      lock.lock();
+      TakeBatchPartners(*job, max_batch - 1, &partners);
+      lock.unlock();
+      if (!partners.empty()) {
+        WorkBatch(job, partners);
+        continue;
+      }
+    }
     if (engine_->TryCopyInputTensors(*job).ok()) {
       lock.lock();
       job->invoke_time = time::NowMicros();
@@ -126,6 +137,76 @@ void Worker::Work() {
     lock.unlock();
     engine_->Trigger();
   }
+}
+
+// A batch is the head job plus queued jobs of the same whole-model subgraph
+// (no split job state to carry).  All of them get the batch's invoke / end
+// times; the latency estimator is not fed batched passes (they are not the
+// per-job latency it models).
+void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
+  std::vector<Job*> jobs{head};
+  for (Job& p : partners) jobs.push_back(&p);
+  const int n = static_cast<int>(jobs.size());
+  const SubgraphKey key = head->subgraph_key;
+  std::vector<bool> copied(n, false);
+  for (int i = 0; i < n; ++i) {
+    copied[i] = engine_->TryCopyInputTensorsToSlot(*jobs[i], n, i).ok();
+    if (!copied[i]) {
+      BAND_LOG(LogSeverity::kError, "worker %d failed to copy input of job %d", worker_id_, jobs[i]->job_id);
+      jobs[i]->status = JobStatus::kInputCopyFailure;
+    }
+  }
+  const int64_t invoke_time = time::NowMicros();
+  {
+    std::lock_guard<std::mutex> lock(device_mtx_);
+    head->invoke_time = invoke_time;
+  }
+  const absl::Status status = engine_->InvokeJobBatch(key, n);
+  const int64_t end_time = time::NowMicros();
+  for (int i = 0; i < n; ++i) {
+    Job& j = *jobs[i];
+    j.invoke_time = invoke_time;
+    j.end_time = end_time;
+    if (!copied[i]) continue;
+    if (!status.ok()) {
+      j.status = JobStatus::kInvokeFailure;
+      continue;
+    }
+    const absl::Status out = engine_->TryCopyOutputTensorsFromSlot(j, n, i);
+    j.status = out.ok() ? JobStatus::kSuccess : JobStatus::kOutputCopyFailure;
+    if (!out.ok()) BAND_LOG(LogSeverity::kWarning, "%s", out.message().c_str());
+  }
+  if (!status.ok())
+    BAND_LOG(LogSeverity::kError, "worker %d failed to invoke a batch of %d jobs: %s", worker_id_, n,
+             status.message().c_str());
+  for (int i = 1; i < n; ++i) engine_->EnqueueFinishedJob(*jobs[i]);
+  engine_->EnqueueFinishedJob(*head);
+  {
+    std::lock_guard<std::mutex> lock(device_mtx_);
+    EndEnqueue();
+  }
+  engine_->Trigger();
+}
+
+bool Worker::Batchable(const Job& job) {
+  return job.following_jobs.empty() && job.previous_subgraph_keys.empty() && !job.intermediates;
+}
+
+void DeviceQueueWorker::TakeBatchPartners(const Job& head, int max, std::vector<Job>* out) {
+  if (requests_.size() < 2 || max <= 0) return;
+  // the head stays at the front (GetWaitingTime counts it); partners are
+  // moved out of the queue in FIFO order
+  JobQueue rest;
+  auto it = std::next(requests_.begin());
+  for (; it != requests_.end(); ++it) {
+    if (static_cast<int>(out->size()) < max && it->subgraph_key == head.subgraph_key && IsValid(*it) &&
+        Batchable(*it))
+      out->push_back(std::move(*it));
+    else
+      rest.push_back(std::move(*it));
+  }
+  requests_.erase(std::next(requests_.begin()), requests_.end());
+  for (Job& j : rest) requests_.push_back(std::move(j));
 }
 
 bool DeviceQueueWorker::EnqueueJob(Job& job) {

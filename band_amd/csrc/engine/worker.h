@@ -11,6 +11,7 @@
 #include <cstdint>
 #include <mutex>
 #include <thread>
+#include <vector>
 
 #include "band/device/cpu.h"
 #include "engine/config.h"
@@ -51,8 +52,14 @@ class Worker {
  protected:
   virtual Job* GetCurrentJob() = 0;
   virtual void EndEnqueue() = 0;
+  // Job batching (extension; device_mtx_ held): moves up to `max` queued
+  // jobs that can share one batched pass with `head` into `out`.
+  virtual void TakeBatchPartners(const Job& head, int max, std::vector<Job>* out) {}
   void Work();
+  // runs `head` + `partners` as one batched pass (device_mtx_ not held)
+  void WorkBatch(Job* head, std::vector<Job>& partners);
   static bool IsValid(const Job& job);
+  static bool Batchable(const Job& job);
 
   IEngine* const engine_;
   const WorkerId worker_id_;
@@ -84,6 +91,7 @@ class DeviceQueueWorker : public Worker {
  protected:
   Job* GetCurrentJob() override { return requests_.empty() ? nullptr : &requests_.front(); }
   void EndEnqueue() override { requests_.pop_front(); }
+  void TakeBatchPartners(const Job& head, int max, std::vector<Job>* out) override;
 
  private:
   JobQueue requests_;  // deque: pointers to elements survive push_back

@@ -61,23 +61,28 @@ def parse():
     p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                    help="cpu: --workers-per-gpu Band CPU workers instead of GPU workers (C1 / CPU tests; no roofline)")
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
+    p.add_argument("--job-batch", type=int, default=1,
+                   help="max queued jobs of one model a GPU worker runs as one batched pass "
+                        "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
     return p.parse_args()
 
 
-def model_list(name, size=0):
+def model_list(name, size=0, batch=1):
     """[(model name, .tflite bytes)] of the workload (size 0: the configs'
-    224x224, EfficientDet-Lite2 448x448)"""
+    224x224, EfficientDet-Lite2 448x448); batch > 1: the same models with a
+    leading batch (profiling the passes job batching runs)"""
     from band_amd import tflite_synth as S
     sz = size or 224
     ed = size or 448
+    b = batch
     if name == "mix_c3":
-        return [(m, getattr(S, m)(np.int8, size=sz)) for m in S.MIX_C3]
+        return [(m, getattr(S, m)(np.int8, size=sz, batch=b)) for m in S.MIX_C3]
     if name == "mobilenet_v2_int8":
-        return [(name, S.mobilenet_v2(np.int8, seed=0, size=sz))]
+        return [(name, S.mobilenet_v2(np.int8, seed=0, size=sz, batch=b))]
     if name == "mobilenet_v2_uint8":
-        return [(name, S.mobilenet_v2(np.uint8, seed=0, size=sz))]
+        return [(name, S.mobilenet_v2(np.uint8, seed=0, size=sz, batch=b))]
     if name == "mobilenet_v1_int8":
-        return [(name, S.mobilenet_v1(np.int8, seed=0, size=sz))]
+        return [(name, S.mobilenet_v1(np.int8, seed=0, size=sz, batch=b))]
     if name == "efficientdet_lite2_int8":
         return [(name, S.efficientdet_lite2(np.int8, size=ed))]
     if name == "mix_c5":
@@ -91,7 +96,7 @@ def model_list(name, size=0):
                 ("mobilenet_v2_fp16", S.mobilenet_v2(np.float16, size=sz)),
                 ("ssd_mobilenet_v2_fp16", S.ssd_mobilenet_v2(np.float16, size=sz))]
     base = name[:-len("_int8")]
-    return [(name, getattr(S, base)(np.int8, size=sz))]
+    return [(name, getattr(S, base)(np.int8, size=sz, batch=b))]
 
 
 class Dist:
@@ -187,6 +192,16 @@ def profile_roofline(args, D, models, paths):
     import band_amd
     from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
     M = len(models)
+    # with job batching the workers run batch-B passes: profile those (the
+    # same models with a leading batch of B), per-inference figures / B
+    B = args.job_batch if args.job_batch > 1 and args.model not in ("efficientdet_lite2_int8", "mix_c5") else 1
+    if B > 1:
+        paths = []
+        for name, buf in model_list(args.model, args.size, batch=B):
+            tmp = tempfile.NamedTemporaryFile(prefix="band_prof_%s_" % name, suffix=".tflite", delete=False)
+            tmp.write(buf)
+            tmp.close()
+            paths.append(tmp.name)
     # profiling executors (outside the engine, same backend code) for the
     # per-kernel roofline and the device-side floor of a job
     prof_wid = 1000
@@ -234,9 +249,15 @@ def profile_roofline(args, D, models, paths):
     # device-side floor of one job: each model's passes replayed back to back
     # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
     # host launch + sync wakeup
-    device_us = {name: ex.TimeSubgraph(key, iters=100) for (name, _), ex, key in zip(models, execs0, keys0)}
-
-    return dom_name, dom, by_k, traffic, traffic_src, device_us
+    device_us = {name: ex.TimeSubgraph(key, iters=100) / B for (name, _), ex, key in zip(models, execs0, keys0)}
+    if B > 1:
+        for path in paths:
+            os.unlink(path)
+    # per inference: kernel time of a batch-B pass / B
+    for k in by_k.values():
+        for f in ("ms", "bytes", "ops", "launches"):
+            k[f] /= B
+    return dom_name, dom, by_k, traffic, traffic_src, device_us, B
 
 
 def main():
@@ -284,7 +305,8 @@ def main():
         args.scheduler = "heterogeneous_earliest_finish_time"
     engine = Engine(make_config([sched], workers,
                                 num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
-                                num_warmups=3, num_runs=5))
+                                num_warmups=3, num_runs=5,
+                                max_job_batch=args.job_batch if args.job_batch > 1 else None))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + D.rank)
     for path in paths:
@@ -301,7 +323,7 @@ def main():
             lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
             arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
         inputs.append(t)
-    inflight = args.inflight or 2 * W
+    inflight = args.inflight or 2 * W * max(1, args.job_batch)
 
     engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
     poisson = None
@@ -329,7 +351,7 @@ def main():
 
     roof, dev = None, None
     if on_gpu:
-        dom_name, dom, by_k, traffic, traffic_src, device_us = profile_roofline(args, D, models, paths)
+        dom_name, dom, by_k, traffic, traffic_src, device_us, prof_batch = profile_roofline(args, D, models, paths)
         avg_ms = dom["ms"] / dom["launches"]
         bytes_per_launch = dom["bytes"] / dom["launches"]
         ops_per_launch = dom["ops"] / dom["launches"]
@@ -339,6 +361,7 @@ def main():
             "frac": achieved_gbs / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
             "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
             "launches_per_inference": dom["launches"],
+            "profiled_pass_batch": prof_batch,
             "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,
             "mfma_i8_frac": ops_per_launch / (avg_ms * 1e-3) / 5.0e15,
         }
@@ -366,11 +389,14 @@ def main():
             "dtype": "uint8" if args.model.endswith("uint8") else ("int8+fp16" if args.model == "mix_c5" else "int8"),
             "data": "synthetic (seeded inputs and weights; no checkpoint)",
             "device": args.device,
-            "config": {"workload": workload_label(args, models, n_cpu, W, poisson),
+            "config": {"workload": workload_label(args, models, n_cpu, W, poisson) + (
+                           "; each GPU worker runs up to %d queued jobs of one model as one batched pass "
+                           "(job batching)" % args.job_batch if args.job_batch > 1 else ""),
                        "harness": "native Band engine (planner + workers + %s), %d requests in flight"
                                   % (args.scheduler, inflight),
                        "jobs_per_worker_rank0": jobs_per_worker,
-                       "model": args.model, "global_batch": n * W, "seq_len": None,
+                       "max_job_batch": args.job_batch,
+                       "model": args.model, "global_batch": n * W * max(1, args.job_batch), "seq_len": None,
                        "parallelism": "job-sharded x%d (no collective)" % n, "hipgraph": not args.no_graph,
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
             "p50_job_latency_ms": float(np.percentile(lat_ms, 50)),

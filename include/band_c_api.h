@@ -92,6 +92,9 @@ typedef enum BandConfigField {
   BAND_RESOURCE_MONITOR_DEVICE_PATH,
   BAND_RESOURCE_MONITOR_INTERVAL_MS,
   BAND_RESOURCE_MONITOR_LOG_PATH,
+  /* extension: a GPU device-queue worker runs up to this many queued
+   * whole-model jobs of one model as one batched pass (default 1 = Band) */
+  BANDX_WORKER_MAX_JOB_BATCH = 1000,
 } BandConfigField;
 
 typedef struct BandRequestOption {

@@ -126,6 +126,18 @@ int bhx_run_mixed_jobs(int n_models, bhx_executor* const* execs, const int* mode
  * back to back on the executor's stream (graph replay when captured) */
 int bhx_time_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters, double* us);
 
+/* --- job batching (extension, band/interface/job_batching.h) -------------
+ * Not in the reference interface: Band runs one job per ExecuteSubgraph
+ * (band/worker.cc:222-323).  A prepared kGPU subgraph gets batch variants
+ * for up to max_batch jobs; slot views are batch-1 views into a variant's
+ * pinned boundary mirrors; execute runs n jobs in one pass. */
+int bhx_prepare_job_batches(bhx_executor* e, bhx_model* m, int model_id, int worker_id, uint64_t unit_mask,
+                            int max_batch);
+int bhx_max_job_batch(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int* max_batch);
+int bhx_job_slot_view(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int tensor_index, int n,
+                      int slot, bhx_tensor_info* info);
+int bhx_execute_job_batch(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int n);
+
 #ifdef __cplusplus
 }
 #endif

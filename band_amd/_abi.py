@@ -22,7 +22,7 @@ class ConvParams(ctypes.Structure):
         (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift", "residual")] + [
         (n, c_int32) for n in ("add_y_off", "add_r_off", "add_o_off", "add_left_shift", "add_y_mult",
                                "add_y_shift", "add_r_mult", "add_r_shift", "add_o_mult", "add_o_shift",
-                               "add_act_min", "add_act_max")] + [("out_table", c_void_p)]
+                               "add_act_min", "add_act_max")] + [("out_table", c_void_p), ("requant_fast", c_int32)]
 
 
 class DwConvParams(ctypes.Structure):
@@ -30,7 +30,8 @@ class DwConvParams(ctypes.Structure):
         "batch", "in_h", "in_w", "in_c", "out_h", "out_w", "out_c", "depth_multiplier",
         "k_h", "k_w", "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "in_xor")] + [
         (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
-        (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift", "out_table")]
+        (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift", "out_table", "taps")] + [
+        ("requant_fast", c_int32)]
 
 
 class FcParams(ctypes.Structure):
@@ -163,7 +164,10 @@ KERNEL_SYMBOLS = {
     "bh_pack_conv_weights": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_int32, c_int32, c_void_p, c_void_p]),
     "bh_conv_packed_geometry": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "bh_pack_dw_taps": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int32, c_void_p]),
+    "bh_conv_requant_fast_ok": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_int64]),
     "bh_conv2d_i8": (c_int, [ctypes.POINTER(ConvParams), c_void_p]),
+    "bh_conv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(ConvParams)]),
     "bh_lut_u8": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
     "bh_lut_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
     "bh_quantize_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, ctypes.c_float, c_int32, c_int, c_void_p]),

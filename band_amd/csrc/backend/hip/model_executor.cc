@@ -79,6 +79,24 @@ HipModelExecutor::~HipModelExecutor() {
 }
 
 namespace {
+// "<conv kernel>+add": a conv launch with the following ADD in its epilogue
+const char* WithAdd(const char* k) {
+  static const char* const names[][2] = {{"conv_mfma_kernel", "conv_mfma_kernel+add"},
+                                         {"conv_xs_kernel", "conv_xs_kernel+add"},
+                                         {"conv_rows_kernel", "conv_rows_kernel+add"},
+                                         {"conv_direct_kernel", "conv_direct_kernel+add"},
+                                         {"conv_stem_kernel", "conv_stem_kernel+add"}};
+  for (const auto& n : names)
+    if (std::strcmp(k, n[0]) == 0) return n[1];
+  return k;
+}
+
+int64_t MaxAbs(const int32_t* v, int n) {
+  int64_t m = 0;
+  for (int i = 0; v && i < n; ++i) m = std::max<int64_t>(m, v[i] < 0 ? -(int64_t)v[i] : (int64_t)v[i]);
+  return m;
+}
+
 // TFLite fp16 post-training quantization keeps constants in float16 behind
 // DEQUANTIZE ops; such a tensor is a constant of the float graph
 const TflOperator* ProducerOf(const TflModel& m, int t) {
@@ -587,8 +605,9 @@ absl::Status HipModelExecutor::LowerTransposeConv(const HipModel& model, int oi,
   p.input = scratch->ptr(); p.output = out_ptr;
   p.weights = static_cast<const int8_t*>(blob->ptr());
   p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+  p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, K, MaxAbs(bias, oc));
   L->kind = Launch::kConv;
-  L->kernel = (kh * kw * ic <= 64 && ic < 8) ? "conv_direct_kernel" : "conv_mfma_kernel";
+  L->kernel = bh_conv2d_i8_kernel(&p);
   const double M = static_cast<double>(b) * oh * ow;
   L->alg_ops = 2.0 * M * oc * K;
   L->alg_bytes = static_cast<double>(b) * uh * uw * ic + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
@@ -1209,7 +1228,7 @@ bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, Prepare
   const int act = add.options.valid() ? add.options.Int8(0, 0) : 0;
   ActivationRangeQuantized(act, Scale(to), Zp(to), to.type == DataType::kInt8, &p.add_act_min, &p.add_act_max);
   L->alg_bytes += static_cast<double>(tr.num_elements());  // residual read; y never stored
-  L->kernel = std::strcmp(L->kernel, "conv_direct_kernel") == 0 ? "conv_direct_kernel+add" : "conv_mfma_kernel+add";
+  L->kernel = WithAdd(L->kernel);
   sg->fused_ops.insert(j);
   L->out_tensor = add.outputs[0];
   sg->fused_tensors.insert(t);
@@ -1481,11 +1500,9 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
       p.input = in_ptr; p.output = out_ptr;
       p.weights = static_cast<const int8_t*>(blob->ptr());
       p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+      p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, K, MaxAbs(bias, oc));
       L.kind = Launch::kConv;
-      // mirrors bh_conv2d_i8's dispatch (conv_mfma.hip): small-K layers with
-      // few input channels run the direct VALU kernel
-      const bool direct = !(kh == 1 && kw == 1 && ph == 0 && pw == 0) && kh * kw * ic <= 64 && ic < 8;
-      L.kernel = direct ? "conv_direct_kernel" : "conv_mfma_kernel";
+      L.kernel = bh_conv2d_i8_kernel(&p);  // the kernel bh_conv2d_i8 dispatches to
       L.alg_ops = 2.0 * M * oc * K;
       L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
     } else {
@@ -1493,6 +1510,9 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
       const size_t wbytes = static_cast<size_t>(kh) * kw * oc;
       const size_t wpad = (wbytes + 15) / 16 * 16;
       const size_t tbytes = 12ull * oc;
+      // 3x3 / dm 1 layers also get the dot4 kernel's tap table (bh_pack_dw_taps)
+      const bool dot = kh == 3 && kw == 3 && dm == 1 && oc % 4 == 0;
+      const size_t pbytes = dot ? 16ull * oc : 0;
       auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
       if (!blob) {
         std::vector<uint8_t> wd(wpad, 0);
@@ -1501,9 +1521,13 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
         for (int c = 0; c < oc; ++c) tables[c] = bias ? bias[c] : 0;
         std::copy(mult.begin(), mult.end(), tables.begin() + oc);
         std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
-        blob = std::make_shared<DeviceBlob>(ordinal_, wpad + tbytes);
+        std::vector<int32_t> taps(pbytes / 4);
+        if (dot && bh_pack_dw_taps(reinterpret_cast<const int8_t*>(wd.data()), oc, tables.data(), in_zp, w_zp,
+                                   taps.data()) != 0)
+          return absl::InternalError("depthwise tap packing failed");
+        blob = std::make_shared<DeviceBlob>(ordinal_, wpad + tbytes + pbytes);
         if (!blob->ok() || !blob->Upload(0, wd.data(), wpad) ||
-            !blob->Upload(wpad, tables.data(), tbytes))
+            !blob->Upload(wpad, tables.data(), tbytes) || (dot && !blob->Upload(wpad + tbytes, taps.data(), pbytes)))
           return HipErr(1, "upload depthwise operands");
         DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
       }
@@ -1518,6 +1542,8 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
       p.act_min = amin; p.act_max = amax; p.input = in_ptr; p.output = out_ptr;
       p.weights = static_cast<const int8_t*>(blob->ptr());
       p.bias = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
+      if (dot && !blob->host()) p.taps = tab + 3 * oc;
+      p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, kh * kw, MaxAbs(bias, oc));
       L.kind = Launch::kDwConv;
       L.kernel = "dwconv_kernel";
       L.alg_ops = 2.0 * M * oc * kh * kw;

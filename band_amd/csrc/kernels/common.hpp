@@ -84,6 +84,49 @@ struct FastDiv {
   __device__ __forceinline__ uint32_t mod(uint32_t n) const { return n - div(n) * d; }
 };
 
+// TFLite requantisation of one accumulator to the clamped output value.
+// FAST: the single-step identity of bh_conv_requant_fast_ok (one
+// v_mad_i64_i32, a funnel shift and four 32-bit ops; checked against the
+// two-step reference on 1.9e8 values incl. every rounding tie class).
+struct ChanQ {
+  int32_t mu, sh;        // multiplier / TFLite shift
+  int32_t e, emask, zpe; // FAST: right shift, sign-correction mask, zp << e
+  int64_t c0;
+};
+
+__device__ __forceinline__ ChanQ chan_q(int32_t mu, int32_t sh, int32_t zp) {
+  ChanQ q;
+  q.mu = mu;
+  q.sh = sh;
+  q.e = -sh;
+  q.emask = q.e > 0 ? -1 : 0;
+  q.zpe = (int32_t)((uint32_t)zp << (q.e & 31));
+  q.c0 = (1ll << 30) + (q.e > 0 ? (1ll << (30 + q.e)) : 0ll);
+  return q;
+}
+
+template <bool FAST>
+__device__ __forceinline__ int32_t requant_out(int32_t acc, const ChanQ& q, int32_t zp, int32_t lo, int32_t hi) {
+  int32_t v;
+  if constexpr (FAST) {
+    const int64_t z = (int64_t)acc * q.mu + q.c0;
+    const int32_t u = (int32_t)(z >> 31);
+    v = (u + ((acc >> 31) & q.emask) + q.zpe) >> q.e;
+  } else {
+    v = requant(acc, q.mu, q.sh) + zp;
+  }
+  return min(max(v, lo), hi);
+}
+
+// Workgroup id -> logical id such that each XCD (hardware ids i % 8 run on
+// XCD i % 8) gets one contiguous run of logical ids; the ids of an
+// incomplete last round keep their own number.  Neighbouring tiles (e.g. the
+// halo rows of a convolution) then share one L2.
+__device__ __forceinline__ int xcd_block(int hw, int total) {
+  const int per = total >> 3;
+  return hw < (per << 3) ? (hw & 7) * per + (hw >> 3) : hw;
+}
+
 }  // namespace bh
 
 // thread-local last-error plumbing for the C ABI (defined in capi_runtime.hip)

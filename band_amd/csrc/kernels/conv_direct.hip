@@ -90,6 +90,99 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(bh_conv_params p, int 
   }
 }
 
+// The 3x3 RGB stem (k_w * in_c == 9 contiguous bytes per window row,
+// dil_w 1) with one thread per output pixel over ALL output channels: the
+// window is gathered once - three aligned dword loads per row and
+// v_alignbyte / v_perm_b32 into the k-ordered byte stream
+// (k = (fy*3 + fx)*3 + ci, seven dwords) - instead of 27 byte loads per
+// 8-channel group.  Filter dwords, bias and multipliers are uniform per
+// channel group (scalar loads).  Threads whose window leaves the image
+// horizontally, or whose aligned loads would run past the tensor, take the
+// byte path of conv_direct_kernel.
+template <bool FAST>
+__global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M, DirectDivs dv) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const int t = dv.out_w.div(m);
+  const int ox = m - t * p.out_w;
+  const int n = dv.out_h.div(t);
+  const int oy = t - n * p.out_h;
+  const int y0 = oy * p.stride_h - p.pad_h;
+  const int x0 = ox * p.stride_w - p.pad_w;
+  const long img = (long)p.in_h * p.in_w * 3;
+  const uint8_t* in = (const uint8_t*)p.input + n * img;
+  const uint8_t* end = (const uint8_t*)p.input + p.batch * img;
+  const uint32_t xorw = splat_byte(p.in_xor);
+  const uint32_t padw = splat_byte(p.in_zp);
+
+  uint32_t r[3][3];  // row fy: window bytes 0-3, 4-7, 8 (int8 domain)
+  const bool colok = x0 >= 0 && x0 + 3 <= p.in_w;
+#pragma unroll
+  for (int fy = 0; fy < 3; ++fy) {
+    const int y = y0 + fy * p.dil_h;
+    const bool rowok = y >= 0 && y < p.in_h;
+    const uint8_t* a = in + ((long)y * p.in_w + x0) * 3;
+    const uintptr_t ai = (uintptr_t)a;
+    const uint32_t* base = (const uint32_t*)(ai & ~(uintptr_t)3);
+    if (rowok && colok && (const uint8_t*)(base + 3) <= end) {
+      const uint32_t o = (uint32_t)(ai & 3);
+      const uint32_t d0 = base[0], d1 = base[1], d2 = base[2];
+      r[fy][0] = __builtin_amdgcn_alignbyte(d1, d0, o) ^ xorw;
+      r[fy][1] = __builtin_amdgcn_alignbyte(d2, d1, o) ^ xorw;
+      r[fy][2] = ((d2 >> (8 * o)) ^ xorw) & 0xffu;
+    } else if (!rowok) {
+      r[fy][0] = padw;
+      r[fy][1] = padw;
+      r[fy][2] = padw & 0xffu;
+    } else {
+      uint32_t b[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int x = x0 + k / 3;
+        b[k] = (x >= 0 && x < p.in_w) ? (uint32_t)(a[k] ^ (uint8_t)p.in_xor) : (padw & 0xffu);
+      }
+      r[fy][0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+      r[fy][1] = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+      r[fy][2] = b[8];
+    }
+  }
+  // k-ordered stream: rows of 9 bytes back to back, one zero byte of tail
+  uint32_t xw[7];
+  xw[0] = r[0][0];
+  xw[1] = r[0][1];
+  xw[2] = __builtin_amdgcn_perm(r[1][0], r[0][2], 0x06050400u);  // R0[8] R1[0..2]
+  xw[3] = __builtin_amdgcn_alignbyte(r[1][1], r[1][0], 3);        // R1[3..6]
+  {
+    const uint32_t u = __builtin_amdgcn_perm(r[1][2], r[1][1], 0x0c0c0403u);  // R1[7] R1[8] 0 0
+    xw[4] = u | (r[2][0] << 16);                                             // .. R2[0] R2[1]
+  }
+  xw[5] = __builtin_amdgcn_alignbyte(r[2][1], r[2][0], 2);  // R2[2..5]
+  xw[6] = __builtin_amdgcn_alignbyte(r[2][2], r[2][1], 2);  // R2[6..8] 0
+  int rowsum = 0;
+  if (p.w_zp != 0) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) rowsum = __builtin_amdgcn_sdot4((int)xw[j], 0x01010101, rowsum, false);
+  }
+  uint8_t* out = (uint8_t*)p.output + (long)m * p.out_c;
+  const uint8_t* tab = (const uint8_t*)p.out_table;
+  for (int c0 = 0; c0 < p.out_c; c0 += 8) {
+    uint32_t packed[2] = {0u, 0u};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int oc = c0 + c;
+      const int* wrow = (const int*)(p.weights + (long)oc * p.k_pad);
+      int acc = p.bias_eff[oc];
+#pragma unroll
+      for (int j = 0; j < 7; ++j) acc = __builtin_amdgcn_sdot4((int)xw[j], wrow[j], acc, false);
+      if (p.w_zp != 0) acc -= p.w_zp * rowsum;
+      int32_t v = requant_out<FAST>(acc, chan_q(p.mult[oc], p.shift[oc], p.out_zp), p.out_zp, p.act_min, p.act_max);
+      const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
+      packed[c >> 2] |= byte << (8 * (c & 3));
+    }
+    *(v2i*)(out + c0) = (v2i){(int)packed[0], (int)packed[1]};
+  }
+}
+
 }  // namespace bh
 
 // Launched by bh_conv2d_i8 for small-K layers (conv_mfma.hip); returns
@@ -103,4 +196,18 @@ int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s) 
   if (K <= 32) hipLaunchKernelGGL(bh::conv_direct_kernel<8>, grid, dim3(256), 0, s, p, M, K, dv);
   else hipLaunchKernelGGL(bh::conv_direct_kernel<16>, grid, dim3(256), 0, s, p, M, K, dv);
   return bh_check_launch("conv_direct_kernel");
+}
+
+// 3x3 / in_c 3 / dil_w 1 stems, out_c % 8 == 0, no residual (conv_mfma.hip
+// routes them here); anything else takes conv_direct_kernel
+int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
+  if (p.k_h != 3 || p.k_w != 3 || p.in_c != 3 || p.dil_w != 1 || p.out_c % 8 || p.residual || p.k_pad < 28)
+    return bh_conv_direct_launch(p, M, K, s);
+  bh::DirectDivs dv;
+  dv.out_w = bh::FastDiv(p.out_w);
+  dv.out_h = bh::FastDiv(p.out_h);
+  const dim3 grid((unsigned)((M + 255) / 256));
+  if (p.requant_fast) hipLaunchKernelGGL(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv);
+  else hipLaunchKernelGGL(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv);
+  return bh_check_launch("conv_stem_kernel");
 }

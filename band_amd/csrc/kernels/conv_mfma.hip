@@ -23,6 +23,8 @@
 // enough workgroups exist, deep-K layers split K across the 4 waves of a
 // workgroup (partials reduced through LDS), and each wave issues the loads
 // of up to 4 K-steps before their MFMAs.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace bh {
@@ -328,6 +330,56 @@ static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_
 }  // namespace bh
 
 int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  // conv_direct.hip
+int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s);    // conv_direct.hip
+int bh_conv_rows_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);  // conv_rows.hip
+int bh_conv_xs_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);    // conv_rows.hip
+
+namespace {
+// batched 1x1 layers (K <= 320) at or above this many output pixels take the
+// x-stationary kernel conv_xs_kernel: measured faster than conv_mfma_kernel
+// on every MobileNetV2 1x1 shape from M = 3136 up (gpurun_out/lb_conv_*,
+// DESIGN.md); BH_CONV_XS_MIN_M overrides (diagnostics / tuning)
+long XsMinM() {
+  static const long v = [] {
+    const char* e = std::getenv("BH_CONV_XS_MIN_M");
+    return e ? std::atol(e) : 2048L;
+  }();
+  return v;
+}
+// conv_rows_kernel (any K) is opt-in: BH_CONV_ROWS_MIN_M = the M from which
+// deep-K batched 1x1 layers take it (default: never; slower than
+// conv_mfma_kernel on every K > 320 MobileNet shape measured)
+long RowsMinM() {
+  static const long v = [] {
+    const char* e = std::getenv("BH_CONV_ROWS_MIN_M");
+    return e ? std::atol(e) : -1L;
+  }();
+  return v;
+}
+
+enum Route { kDirect, kStem, kXs, kRows, kMfma };
+
+Route route(const bh_conv_params& p, long M, int K, int N) {
+  const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
+  // RGB-stem-like layers (tiny K, byte-granular gather): direct VALU kernel
+  if (!is1x1 && K <= 64 && p.in_c < 8) {
+    const bool stem = p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && N % 8 == 0 && !p.residual;
+    return stem && !std::getenv("BH_CONV_NO_STEM") ? kStem : kDirect;
+  }
+  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0) {
+    if (K <= 320 && M >= XsMinM()) return kXs;
+    if (RowsMinM() >= 0 && M >= RowsMinM()) return kRows;
+  }
+  return kMfma;
+}
+}  // namespace
+
+extern "C" const char* bh_conv2d_i8_kernel(const bh_conv_params* p) {
+  if (!p) return "";
+  static const char* const names[] = {"conv_direct_kernel", "conv_stem_kernel", "conv_xs_kernel",
+                                      "conv_rows_kernel", "conv_mfma_kernel"};
+  return names[route(*p, (long)p->batch * p->out_h * p->out_w, p->k_h * p->k_w * p->in_c, p->out_c)];
+}
 
 extern "C" int bh_conv_packed_geometry(int out_c, int k, int* k_pad, int* n_pad) {
   if (out_c <= 0 || k <= 0 || !k_pad || !n_pad) return BH_EINVAL;
@@ -372,8 +424,13 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
   hipStream_t s = (hipStream_t)stream;
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
   const int c = p.in_c;
-  // RGB-stem-like layers (tiny K, byte-granular gather): direct VALU kernel
-  if (!is1x1 && K <= 64 && c < 8) return bh_conv_direct_launch(p, M, K, s);
+  switch (route(p, M, K, N)) {
+    case kDirect: return bh_conv_direct_launch(p, M, K, s);
+    case kStem: return bh_conv_stem_launch(p, M, K, s);
+    case kXs: return bh_conv_xs_launch(p, M, K, N, s);
+    case kRows: return bh_conv_rows_launch(p, M, K, N, s);
+    case kMfma: break;
+  }
   if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);
   if (is1x1 && c % 8 == 0) return bh::launch_shape<true, 8>(p, M, K, N, s);
   if (is1x1 && c % 4 == 0) return bh::launch_shape<true, 4>(p, M, K, N, s);

@@ -9,6 +9,8 @@
 // NHWC), the 3x3 taps are fully unrolled with every in-bounds tap load
 // issued before the arithmetic, and (x' - zp_in) * (w' - zp_w) accumulates
 // exactly in int32.  Taps outside the image are skipped, as TFLite does.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace bh {
@@ -43,12 +45,14 @@ struct Vec<16> {
 // thread index -> (pixel, channel group) divisors (FastDiv, host-built)
 struct DwDivs {
   FastDiv groups, out_w, out_h, dm;
+  int xcd;  // 1: XCD-contiguous workgroup order (xcd_block)
 };
 
 template <int CV>
 __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int total, DwDivs dv) {
   constexpr int NW = CV / 4;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int idx = blk * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int pix = dv.groups.div(idx);
   const int c0 = (idx - pix * (int)dv.groups.d) * CV;
@@ -109,9 +113,105 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int 
   Vec<CV>::st((uint8_t*)p.output + (((long)n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0, packed);
 }
 
+// 3x3 / dm 1 with the host-packed tap table (bh_pack_dw_taps): the nine
+// per-channel products are summed with v_dot4_i32_i8 instead of 36 byte
+// extracts and multiply-adds per 4 channels.  The tap dwords a thread loads
+// hold 4 CHANNELS of one tap; two 4x4 byte transposes (8 v_perm_b32 each)
+// turn taps 0-3 and 4-7 into dwords holding 4 TAPS of one channel, which
+// dot with that channel's packed filter dwords; tap 8 dots untransposed
+// against a filter dword carrying w[8][c] in byte c % 4 only.  Out-of-image
+// taps read as the input zero point, so (x - zp_in) vanishes for them
+// exactly as TFLite's skipped taps do, and the zero-point terms fold into
+// the table's bias:
+//   sum (x - zx)(w - zw) = sum x*w - zw * sum x - zx * sum w + 9 * zx * zw.
+template <int CV, bool FAST, bool WZP>
+__global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, int total, DwDivs dv) {
+  constexpr int NW = CV / 4;
+  const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int idx = blk * blockDim.x + threadIdx.x;
+  if (idx >= total) return;
+  const int pix = dv.groups.div(idx);
+  const int c0 = (idx - pix * (int)dv.groups.d) * CV;
+  const int t = dv.out_w.div(pix);
+  const int ox = pix - t * p.out_w;
+  const int n = dv.out_h.div(t);
+  const int oy = t - n * p.out_h;
+  const uint8_t* base = (const uint8_t*)p.input;
+  const uint8_t* in = base + (long)n * p.in_h * p.in_w * p.in_c + c0;
+  const uint32_t xorw = splat_byte(p.in_xor);
+  const uint32_t zfill = splat_byte(p.in_zp);
+  const int y0 = oy * p.stride_h - p.pad_h;
+  const int x0 = ox * p.stride_w - p.pad_w;
+
+  // all nine tap loads issue before any arithmetic; out-of-image taps load
+  // from the tensor base (always readable) and are replaced afterwards
+  uint32_t xv[9][NW];
+#pragma unroll
+  for (int fy = 0; fy < 3; ++fy) {
+#pragma unroll
+    for (int fx = 0; fx < 3; ++fx) {
+      const int tap = fy * 3 + fx;
+      const int y = y0 + fy * p.dil_h;
+      const int x = x0 + fx * p.dil_w;
+      const bool ok = y >= 0 && y < p.in_h && x >= 0 && x < p.in_w;
+      Vec<CV>::ld(ok ? in + ((long)y * p.in_w + x) * p.in_c : base, xv[tap]);
+#pragma unroll
+      for (int d = 0; d < NW; ++d) xv[tap][d] = ok ? xv[tap][d] ^ xorw : zfill;
+    }
+  }
+  const v4i* tp = (const v4i*)p.taps + c0;
+  uint32_t packed[NW];
+#pragma unroll
+  for (int d = 0; d < NW; ++d) {
+    uint32_t T[4], U[4];
+    {
+      const uint32_t l01 = __builtin_amdgcn_perm(xv[1][d], xv[0][d], 0x05010400u);
+      const uint32_t h01 = __builtin_amdgcn_perm(xv[1][d], xv[0][d], 0x07030602u);
+      const uint32_t l23 = __builtin_amdgcn_perm(xv[3][d], xv[2][d], 0x05010400u);
+      const uint32_t h23 = __builtin_amdgcn_perm(xv[3][d], xv[2][d], 0x07030602u);
+      T[0] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
+      T[1] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
+      T[2] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
+      T[3] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
+    }
+    {
+      const uint32_t l01 = __builtin_amdgcn_perm(xv[5][d], xv[4][d], 0x05010400u);
+      const uint32_t h01 = __builtin_amdgcn_perm(xv[5][d], xv[4][d], 0x07030602u);
+      const uint32_t l23 = __builtin_amdgcn_perm(xv[7][d], xv[6][d], 0x05010400u);
+      const uint32_t h23 = __builtin_amdgcn_perm(xv[7][d], xv[6][d], 0x07030602u);
+      U[0] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
+      U[1] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
+      U[2] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
+      U[3] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
+    }
+    const v4i mm = *(const v4i*)(p.mult + c0 + 4 * d);
+    const v4i ss = *(const v4i*)(p.shift + c0 + 4 * d);
+    uint32_t o = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const v4i w = tp[4 * d + j];  // filter taps 0-3, 4-7, 8 (byte j), folded bias
+      int32_t acc = __builtin_amdgcn_sdot4((int)T[j], w.x, w.w, false);
+      acc = __builtin_amdgcn_sdot4((int)U[j], w.y, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xv[8][d], w.z, acc, false);
+      if constexpr (WZP) {
+        int32_t sx = __builtin_amdgcn_sdot4((int)T[j], 0x01010101, 0, false);
+        sx = __builtin_amdgcn_sdot4((int)U[j], 0x01010101, sx, false);
+        sx = __builtin_amdgcn_sdot4((int)xv[8][d], (int)(1u << (8 * j)), sx, false);
+        acc -= p.w_zp * sx;
+      }
+      int32_t r = requant_out<FAST>(acc, chan_q(mm[j], ss[j], p.out_zp), p.out_zp, p.act_min, p.act_max);
+      const uint32_t byte = p.out_table ? ((const uint8_t*)p.out_table)[(uint8_t)r] : ((uint32_t)r & 0xffu);
+      o |= byte << (8 * j);
+    }
+    packed[d] = o;
+  }
+  Vec<CV>::st((uint8_t*)p.output + (((long)n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0, packed);
+}
+
 // general filter size / depth multiplier: one output channel per thread
 __global__ __launch_bounds__(256) void dwconv_generic_kernel(bh_dwconv_params p, int total, DwDivs dv) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int idx = blk * blockDim.x + threadIdx.x;
   if (idx >= total) return;
   const int pix = dv.groups.div(idx);
   const int c = idx - pix * p.out_c;
@@ -148,14 +248,28 @@ static DwDivs dw_divs(const bh_dwconv_params& p, int groups) {
   dv.out_w = FastDiv(p.out_w);
   dv.out_h = FastDiv(p.out_h);
   dv.dm = FastDiv(p.depth_multiplier);
+  static const int xcd = [] {
+    const char* e = std::getenv("BH_DW_XCD");
+    return e ? std::atoi(e) : 1;
+  }();
+  dv.xcd = xcd;
   return dv;
 }
 
 template <int CV>
 static void launch3x3(const bh_dwconv_params& p, long pixels, hipStream_t s) {
   const int total = (int)(pixels * (p.out_c / CV));
-  hipLaunchKernelGGL(dwconv3x3_kernel<CV>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total,
-                     dw_divs(p, p.out_c / CV));
+  const dim3 grid((unsigned)((total + 255) / 256));
+  const DwDivs dv = dw_divs(p, p.out_c / CV);
+  if (!p.taps) {
+    hipLaunchKernelGGL(dwconv3x3_kernel<CV>, grid, dim3(256), 0, s, p, total, dv);
+  } else if (p.w_zp != 0) {
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, true, true>), grid, dim3(256), 0, s, p, total, dv);
+    else hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, false, true>), grid, dim3(256), 0, s, p, total, dv);
+  } else {
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, true, false>), grid, dim3(256), 0, s, p, total, dv);
+    else hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, false, false>), grid, dim3(256), 0, s, p, total, dv);
+  }
 }
 
 }  // namespace bh
@@ -176,6 +290,10 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
     return BH_EINVAL;
   }
   const bool fast = p.depth_multiplier == 1 && p.k_h == 3 && p.k_w == 3 && p.out_c % 4 == 0;
+  if (p.taps && !fast) {
+    bh_set_last_error("bh_dwconv2d_i8: a tap table needs a 3x3, depth multiplier 1, out_c % 4 == 0 layer");
+    return BH_EINVAL;
+  }
   if (fast) {
     // widest vector that still leaves enough threads to fill the chip
     if (p.out_c % 16 == 0 && pixels * (p.out_c / 16) >= 65536) bh::launch3x3<16>(p, pixels, s);
@@ -187,4 +305,28 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
                        bh::dw_divs(p, p.out_c));
   }
   return bh_check_launch("dwconv_kernel");
+}
+
+extern "C" int bh_pack_dw_taps(const int8_t* w, int c, const int32_t* bias, int32_t in_zp, int32_t w_zp,
+                               int32_t* taps) {
+  if (!w || !taps || c <= 0 || c % 4) {
+    bh_set_last_error("bh_pack_dw_taps: invalid parameters");
+    return BH_EINVAL;
+  }
+  for (int ch = 0; ch < c; ++ch) {
+    uint32_t d[3] = {0, 0, 0};
+    int32_t wsum = 0;
+    for (int tap = 0; tap < 9; ++tap) {
+      const int8_t v = w[(long)tap * c + ch];
+      wsum += v;
+      if (tap < 8) d[tap / 4] |= (uint32_t)(uint8_t)v << (8 * (tap % 4));
+      else d[2] = (uint32_t)(uint8_t)v << (8 * (ch % 4));
+    }
+    int32_t* o = taps + 4L * ch;
+    o[0] = (int32_t)d[0];
+    o[1] = (int32_t)d[1];
+    o[2] = (int32_t)d[2];
+    o[3] = (bias ? bias[ch] : 0) - in_zp * wsum + 9 * in_zp * w_zp;
+  }
+  return 0;
 }

@@ -13,8 +13,17 @@ A "step" is one Band job, end to end through the harness: RequestAsync
 scheduler -> worker queue (band/planner.cc:268-365) -> Worker::Work: input
 copy into the executor's view, IModelExecutor::ExecuteSubgraph on the GPU,
 output copy (band/worker.cc:222-323) -> Wait.  A native closed-loop driver
-(BandxEngineRunClosedLoop) keeps 2 x workers requests in flight.  Job
-latency = end - enqueue of the planner's job record (band/common.h:351-353).
+(BandxEngineRunClosedLoop) keeps 2 x workers x job-batch requests in
+flight.  Job latency = end - enqueue of the planner's job record
+(band/common.h:351-353).
+
+Job batching (--job-batch B, default 16; BANDX_WORKER_MAX_JOB_BATCH): an
+idle GPU worker takes up to B queued requests of one model from round_robin
+and runs them as ONE pass over a batch-B variant of the model's subgraph
+(every job still gets its own input copy, its own outputs, its own job
+record).  Band itself runs one job per ExecuteSubgraph; that configuration
+(8 GPU workers, no batching) is measured in the same run and reported as
+"band_one_job_per_pass".  --job-batch 1 makes it the headline instead.
 
 N>1: one process per GPU (torchrun), each with its own engine over its GPU;
 jobs shard across GPUs with no data-path collective (weak scaling); a gloo
@@ -61,7 +70,9 @@ def parse():
     p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                    help="cpu: --workers-per-gpu Band CPU workers instead of GPU workers (C1 / CPU tests; no roofline)")
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
-    p.add_argument("--job-batch", type=int, default=1,
+    p.add_argument("--no-batch1", action="store_true",
+                   help="skip the one-job-per-pass (Band semantics) line reported beside a job-batched run")
+    p.add_argument("--job-batch", type=int, default=16,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
     return p.parse_args()
@@ -260,6 +271,34 @@ def profile_roofline(args, D, models, paths):
     return dom_name, dom, by_k, traffic, traffic_src, device_us, B
 
 
+def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch):
+    """this rank's Band engine with the models registered and one synthetic
+    request tensor per model"""
+    from band_amd.engine import Engine, Model, make_config
+    on_gpu = args.device == "gpu"
+    engine = Engine(make_config([sched], workers,
+                                num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
+                                num_warmups=3, num_runs=5,
+                                max_job_batch=job_batch if job_batch > 1 else None))
+    band_models, inputs = [], []
+    rng = np.random.default_rng(5489 + D.rank)
+    for path in paths:
+        m = Model()
+        assert m.FromPath(path), path
+        assert engine.RegisterModel(m), path
+        band_models.append(m)
+        # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
+        t = engine.CreateInputTensor(m, 0)
+        arr = t.data()
+        if arr.dtype == np.float32:  # f32 U(-0.5, 0.5) (band/tool/benchmark.cc:279-287)
+            arr[...] = rng.uniform(-0.5, 0.5, arr.shape).astype(np.float32)
+        else:
+            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
+            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
+        inputs.append(t)
+    return engine, band_models, inputs
+
+
 def main():
     args = parse()
     # hardware queues are fixed at HIP runtime init: one per concurrently
@@ -303,26 +342,7 @@ def main():
     if n_cpu and args.scheduler in ("round_robin", "fixed_worker"):
         sched = SchedulerType.kHeterogeneousEarliestFinishTime  # a split model needs fallback subgraphs
         args.scheduler = "heterogeneous_earliest_finish_time"
-    engine = Engine(make_config([sched], workers,
-                                num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
-                                num_warmups=3, num_runs=5,
-                                max_job_batch=args.job_batch if args.job_batch > 1 else None))
-    band_models, inputs = [], []
-    rng = np.random.default_rng(5489 + D.rank)
-    for path in paths:
-        m = Model()
-        assert m.FromPath(path), path
-        assert engine.RegisterModel(m), path
-        band_models.append(m)
-        # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
-        t = engine.CreateInputTensor(m, 0)
-        arr = t.data()
-        if arr.dtype == np.float32:  # f32 U(-0.5, 0.5) (band/tool/benchmark.cc:279-287)
-            arr[...] = rng.uniform(-0.5, 0.5, arr.shape).astype(np.float32)
-        else:
-            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
-            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
-        inputs.append(t)
+    engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch)
     inflight = args.inflight or 2 * W * max(1, args.job_batch)
 
     engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
@@ -348,6 +368,27 @@ def main():
     elapsed = D.max(t1 - t0)
     all_lat = [x for part in D.gather((lat_us * 1e-6).tolist()) for x in part]
     jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
+    engine.close()
+
+    # Band's own semantics beside it: one job per ExecuteSubgraph (no job
+    # batching), the same mix and scheduler over 8 GPU workers per GPU
+    batch1 = None
+    if args.job_batch > 1 and not poisson and on_gpu and not args.no_batch1:
+        W1 = 8
+        e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1)
+        n1 = max(args.steps // 2, 16 * M)
+        e1.RunClosedLoop(bm1, max(args.warmup // 2, 2 * W1 * M), 2 * W1, in1)
+        D.barrier()
+        t0 = time.perf_counter()
+        lat1, _, _ = e1.RunClosedLoop(bm1, n1, 2 * W1, in1)
+        t1 = time.perf_counter()
+        D.barrier()
+        el1 = D.max(t1 - t0)
+        l1 = np.array([x for part in D.gather((lat1 * 1e-3).tolist()) for x in part])
+        batch1 = {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "steps": n1,
+                  "p50_job_latency_ms": float(np.percentile(l1, 50)),
+                  "p99_job_latency_ms": float(np.percentile(l1, 99))}
+        e1.close()
 
     roof, dev = None, None
     if on_gpu:
@@ -404,12 +445,12 @@ def main():
             "gpu_kernel_ms_per_inference": dev["gpu_ms_total"] if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
             "device_us_per_model": dev["device_us"] if dev else None,
+            "band_one_job_per_pass": batch1,
             "roofline": roof,
             "cpu_baseline": cpu,
             "host": platform.node(),
         }
         print(json.dumps(line), flush=True)
-    engine.close()
     for path in paths:
         os.unlink(path)
     D.close()

@@ -132,6 +132,10 @@ typedef struct bh_conv_params {
    * following 8-bit unary op (QUANTIZE / RELU family / LOGISTIC) folded into
    * this epilogue (NULL = none) */
   const void* out_table;
+  /* 1 when bh_conv_requant_fast_ok() holds for this layer's multipliers:
+   * the kernels may then evaluate TFLite's two-step requantisation with one
+   * 64-bit multiply-add and shifts (same results, fewer instructions) */
+  int32_t requant_fast;
 } bh_conv_params;
 
 /* DEPTHWISE_CONV_2D.  weights: int8-domain [k_h][k_w][out_c] (TFLite layout
@@ -156,6 +160,12 @@ typedef struct bh_dwconv_params {
    * following 8-bit unary op (QUANTIZE / RELU family / LOGISTIC) folded into
    * this epilogue (NULL = none) */
   const void* out_table;
+  /* optional [out_c][4] int32 tap table from bh_pack_dw_taps (3x3, depth
+   * multiplier 1, out_c % 4 == 0): the dot4 kernel then replaces the
+   * per-tap one (weights / bias are not read).  NULL = per-tap kernel */
+  const int32_t* taps;
+  /* 1 when bh_conv_requant_fast_ok(mult, shift, out_c, 9, max|bias|) holds */
+  int32_t requant_fast;
 } bh_dwconv_params;
 
 /* FULLY_CONNECTED.  input [rows][depth] bytes, weights int8-domain
@@ -271,9 +281,26 @@ int bh_pack_conv_weights(const void* w, int w_signed, int out_c, int k,
 
 /* Tile geometry the conv launcher expects for a layer (k_pad, n_pad). */
 int bh_conv_packed_geometry(int out_c, int k, int* k_pad, int* n_pad);
+/* DEPTHWISE_CONV_2D 3x3 / depth multiplier 1 tap table: for channel c,
+ * taps[4c..4c+3] = {w[0..3][c] as bytes, w[4..7][c] as bytes,
+ * w[8][c] << 8*(c%4), bias[c] - in_zp*sum_t w[t][c] + 9*in_zp*w_zp}.
+ * w: int8-domain [9][c]; in_zp / w_zp int8-domain; c % 4 == 0. */
+int bh_pack_dw_taps(const int8_t* w, int c, const int32_t* bias, int32_t in_zp, int32_t w_zp, int32_t* taps);
+/* Whether a conv layer may use the single-step requantisation identity
+ *   rdbypot(srdhm(x, M), e) + zp == (((x*M + c0) >> 31) + s + (zp << e)) >> e
+ *   c0 = 2^30 + (e > 0 ? 2^(30+e) : 0),  s = (e > 0 && x < 0) ? -1 : 0
+ * (TFLite MultiplyByQuantizedMultiplier with shift = -e <= 0).  Holds when
+ * every multiplier is in (2^30, 2^31), every shift <= 0 and the int32
+ * accumulators are small enough that nothing overflows:
+ *   K * 2^16 + max|bias| + 255 * 2^e < 2^30.  Returns 1 / 0. */
+int bh_conv_requant_fast_ok(const int32_t* mult, const int32_t* shift, int n, int k, int64_t max_abs_bias);
 
 /* ---- launchers ---------------------------------------------------------- */
 int bh_conv2d_i8(const bh_conv_params* p, bh_stream_t s);
+/* Symbol of the kernel bh_conv2d_i8 dispatches these parameters to
+ * ("conv_mfma_kernel", "conv_xs_kernel", "conv_rows_kernel",
+ * "conv_direct_kernel"); static storage.  Profiling attribution only. */
+const char* bh_conv2d_i8_kernel(const bh_conv_params* p);
 int bh_dwconv2d_i8(const bh_dwconv_params* p, bh_stream_t s);
 int bh_fc_i8(const bh_fc_params* p, bh_stream_t s);
 int bh_eltwise_i8(const bh_eltwise_params* p, bh_stream_t s);

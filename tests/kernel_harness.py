@@ -26,8 +26,11 @@ def xor_of(dtype):
 
 class ConvCase:
     def __init__(self, rng, b, ih, iw, ic, oc, kh, kw, stride=(1, 1), dil=(1, 1), same=True,
-                 dtype=np.int8, per_channel=True, act=3, depthwise=False, dm=1):
+                 dtype=np.int8, per_channel=True, act=3, depthwise=False, dm=1, requant_fast=None,
+                 taps=True):
         self.dtype = dtype
+        self.taps = taps
+        self.requant_fast = requant_fast
         self.depthwise = depthwise
         self.dm = dm
         if depthwise:
@@ -106,6 +109,24 @@ class ConvCase:
                 w_zp=w_zp_d, out_zp=self.out_zp, act_min=self.amin, act_max=self.amax,
                 input=dx.value, output=dy.value, weights=dw.value, bias=db.value,
                 mult=dmult.value, shift=dshift.value)
+            m32 = np.ascontiguousarray(self.mult, np.int32)
+            s32 = np.ascontiguousarray(self.shift, np.int32)
+            fast = lib.bh_conv_requant_fast_ok(m32.ctypes.data_as(ctypes.c_void_p),
+                                               s32.ctypes.data_as(ctypes.c_void_p), self.oc, 9,
+                                               int(np.abs(self.bias.astype(np.int64)).max()))
+            p.requant_fast = fast if self.requant_fast is None else int(self.requant_fast and fast)
+            # tap table (dot4 kernel) for 3x3 / dm 1 / C % 4 == 0, as the
+            # executor lowers it; taps=False keeps the per-tap kernel
+            if self.taps and self.kh == 3 and self.kw == 3 and self.dm == 1 and self.oc % 4 == 0:
+                taps = np.zeros((self.oc, 4), np.int32)
+                wt = np.ascontiguousarray(wd.reshape(9, self.oc))
+                bias = np.ascontiguousarray(self.bias, np.int32)
+                _abi.check(lib.bh_pack_dw_taps(wt.ctypes.data_as(ctypes.c_void_p), self.oc,
+                                               bias.ctypes.data_as(ctypes.c_void_p), in_zp_d, w_zp_d,
+                                               taps.ctypes.data_as(ctypes.c_void_p)), "bh_pack_dw_taps")
+                dt = DeviceBuffer.from_array(taps)
+                keep.append(dt)
+                p.taps = dt.value
         else:
             K = self.kh * self.kw * self.ic
             kp, npd = ctypes.c_int(), ctypes.c_int()
@@ -127,6 +148,13 @@ class ConvCase:
                 k_pad=kp.value, n_pad=npd.value, in_xor=xor_of(self.dtype), in_zp=in_zp_d, w_zp=w_zp_d,
                 out_zp=self.out_zp, act_min=self.amin, act_max=self.amax, input=dx.value,
                 output=dy.value, weights=dw.value, bias_eff=db.value, mult=dmult.value, shift=dshift.value)
+            m32 = np.ascontiguousarray(self.mult, np.int32)
+            s32 = np.ascontiguousarray(self.shift, np.int32)
+            fast = lib.bh_conv_requant_fast_ok(m32.ctypes.data_as(ctypes.c_void_p),
+                                               s32.ctypes.data_as(ctypes.c_void_p), self.oc, K,
+                                               int(np.abs(self.bias.astype(np.int64)).max()))
+            # requant_fast: None = what the executor would choose, else forced
+            p.requant_fast = fast if self.requant_fast is None else int(self.requant_fast and fast)
         return p
 
 

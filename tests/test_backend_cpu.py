@@ -219,3 +219,35 @@ def test_gpu_executor_without_device_fails_loudly(golden_dir):
     m = _model(golden_dir, "mobilenet_v2_1.0_224_quant.tflite")
     st = HipModelExecutor(0, 1, DeviceFlag.kGPU).PrepareSubgraph(m)
     assert not st.ok() and "gfx950" in st.message()
+
+
+@pytest.mark.parametrize("dtype", [np.int8, np.uint8])
+def test_dw_tap_table_identity(dtype):
+    """bh_pack_dw_taps (host code, no GPU): the dot4 kernel's sum over the
+    table equals the oracle's accumulator bias + sum (x - zx)(w - zw) over
+    in-image taps, with out-of-image taps read as zx (dwconv.hip)."""
+    import ctypes
+    lib = _abi.load()
+    rng = np.random.default_rng(11)
+    C = 24
+    w = rng.integers(-128, 128, size=(9, C)).astype(np.int8)  # int8-domain
+    bias = rng.integers(-(1 << 15), 1 << 15, size=C).astype(np.int32)
+    zx = int(rng.integers(-128, 128))
+    zw = 0 if dtype == np.int8 else int(rng.integers(-40, 40))
+    taps = np.zeros((C, 4), np.int32)
+    assert lib.bh_pack_dw_taps(w.ctypes.data_as(ctypes.c_void_p), C, bias.ctypes.data_as(ctypes.c_void_p),
+                               zx, zw, taps.ctypes.data_as(ctypes.c_void_p)) == 0
+    tb = taps.view(np.uint8).reshape(C, 4, 4).astype(np.int8).astype(np.int64)
+    for trial in range(20):
+        x = rng.integers(-128, 128, size=(9, C)).astype(np.int64)
+        inside = rng.random(9) < 0.7
+        ref = bias.astype(np.int64) + ((x - zx) * (w.astype(np.int64) - zw) * inside[:, None]).sum(0)
+        xp = np.where(inside[:, None], x, zx)  # padded taps read as zx
+        for c in range(C):
+            j = c % 4
+            tcol = np.concatenate([xp[0:8, c], [xp[8, c - j + 0], xp[8, c - j + 1], xp[8, c - j + 2], xp[8, c - j + 3]]])
+            wcol = np.concatenate([tb[c, 0], tb[c, 1], tb[c, 2]])
+            acc = int(taps[c, 3]) + int((tcol * wcol).sum())
+            if zw:
+                acc -= zw * int(xp[:, c].sum())
+            assert acc == ref[c], (trial, c)

@@ -22,6 +22,39 @@ def test_conv1x1_mnv2_shapes_int8(gpu_lib, spatial, ic, oc):
     np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
 
 
+# batched 1x1 layers (job batching): M = b*h*w >= 32768 output pixels take
+# conv_rows_kernel (channel-major tiles, packed stores); N / K tails, uint8
+# per-tensor filters (row-sum correction), whole-N and chunked-N grids
+@pytest.mark.parametrize("b,spatial,ic,oc,dtype", [
+    (4, 112, 16, 96, np.int8), (4, 112, 32, 16, np.uint8), (12, 56, 24, 144, np.int8),
+    (12, 56, 144, 24, np.uint8), (44, 28, 32, 192, np.int8), (44, 28, 192, 32, np.int8),
+    (170, 14, 64, 384, np.int8), (170, 14, 96, 20, np.uint8), (700, 7, 64, 520, np.int8),
+    (700, 7, 40, 1001 + 3, np.int8), (45, 28, 12, 72, np.uint8)])
+def test_conv1x1_rows_batched(gpu_lib, b, spatial, ic, oc, dtype):
+    rng = np.random.default_rng(4000 + b + spatial + ic + oc)
+    c = ConvCase(rng, b, spatial, spatial, ic, oc, 1, 1, dtype=dtype, act=3)
+    ref = c.oracle()
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+    c.requant_fast = False  # the two-step requantisation path
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+
+
+# the RGB stem kernel (conv_stem_kernel: aligned row gathers + byte path at
+# the image's left / right edge and the tensor's end): SAME / VALID padding,
+# stride 1 / 2, odd widths, batch, uint8 (filter zero point), both
+# requantisation paths
+@pytest.mark.parametrize("b,h,w,oc,stride,same,dtype", [
+    (2, 224, 224, 32, 2, True, np.int8), (3, 37, 41, 16, 2, True, np.uint8), (1, 15, 13, 24, 1, True, np.int8),
+    (2, 20, 23, 8, 1, False, np.uint8), (4, 9, 9, 48, 2, False, np.int8), (1, 224, 224, 64, 2, True, np.uint8)])
+def test_conv_stem(gpu_lib, b, h, w, oc, stride, same, dtype):
+    rng = np.random.default_rng(5000 + b * h * w + oc + stride)
+    c = ConvCase(rng, b, h, w, 3, oc, 3, 3, stride=(stride, stride), same=same, dtype=dtype, act=3)
+    ref = c.oracle()
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+    c.requant_fast = False
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+
+
 def test_conv_first_layer_3x3_s2_int8(gpu_lib):
     rng = np.random.default_rng(7)
     c = ConvCase(rng, 1, 224, 224, 3, 32, 3, 3, stride=(2, 2), act=3)
@@ -60,6 +93,25 @@ def test_dwconv_mnv2_shapes(gpu_lib, spatial, ch, stride):
     rng = np.random.default_rng(3000 + spatial + ch + stride)
     c = ConvCase(rng, 1, spatial, spatial, ch, ch, 3, 3, stride=(stride, stride), depthwise=True)
     np.testing.assert_array_equal(c.gpu(gpu_lib), c.oracle())
+
+
+# the dot4 kernel (tap table) and the per-tap kernel against the oracle:
+# int8 / uint8 (filter zero point), the single-step and two-step
+# requantisation, odd sizes (image-border taps on every side), batch, the
+# three vector widths (C % 16, % 8, % 4) and dilation
+@pytest.mark.parametrize("b,h,w,ch,stride,dil,dtype", [
+    (1, 112, 112, 32, 1, 1, np.int8), (3, 57, 55, 144, 2, 1, np.int8), (2, 28, 28, 192, 1, 1, np.uint8),
+    (5, 15, 13, 24, 2, 1, np.uint8), (2, 9, 9, 12, 1, 1, np.int8), (1, 17, 17, 20, 1, 2, np.int8),
+    (16, 14, 14, 576, 1, 1, np.int8), (4, 7, 7, 960, 1, 1, np.uint8)])
+def test_dwconv_taps_vs_per_tap(gpu_lib, b, h, w, ch, stride, dil, dtype):
+    rng = np.random.default_rng(3100 + b * h * w + ch + stride + dil)
+    c = ConvCase(rng, b, h, w, ch, ch, 3, 3, stride=(stride, stride), dil=(dil, dil), depthwise=True, dtype=dtype)
+    ref = c.oracle()
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+    c.requant_fast = False
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+    c.taps = False
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
 
 
 @pytest.mark.parametrize("args", [

@@ -168,6 +168,7 @@ KERNEL_SYMBOLS = {
     "bh_conv_requant_fast_ok": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_int64]),
     "bh_conv2d_i8": (c_int, [ctypes.POINTER(ConvParams), c_void_p]),
     "bh_conv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(ConvParams)]),
+    "bh_dwconv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(DwConvParams)]),
     "bh_lut_u8": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
     "bh_lut_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
     "bh_quantize_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, ctypes.c_float, c_int32, c_int, c_void_p]),

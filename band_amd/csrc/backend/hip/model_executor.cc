@@ -1545,7 +1545,7 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
       if (dot && !blob->host()) p.taps = tab + 3 * oc;
       p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, kh * kw, MaxAbs(bias, oc));
       L.kind = Launch::kDwConv;
-      L.kernel = "dwconv_kernel";
+      L.kernel = bh_dwconv2d_i8_kernel(&p);  // the kernel bh_dwconv2d_i8 dispatches to
       L.alg_ops = 2.0 * M * oc * kh * kw;
       L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(wbytes) + 12.0 * oc;
     }

@@ -127,6 +127,77 @@ __device__ __forceinline__ int rowsum16(v4i a, int s) {
   return __builtin_amdgcn_sdot4(a.w, 0x01010101, s, false);
 }
 
+// Epilogue of one transposed 16x16 tile: the lane holds output channels
+// nb..nb+3 of pixel m (D^T = W x X^T on the MFMA), so its four requantised
+// bytes leave as one dword store when N % 4 == 0.  acc excludes the folded
+// bias; rsum is pixel m's input row sum (uint8 filters).
+__device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc, int rsum, int m, int nb, int M,
+                                               int N) {
+  if (m >= M || nb >= N) return;
+  // dword path: N % 4 == 0 (then nb + 3 < N too) and 4-byte aligned output /
+  // residual bases (a concat-elided output may start at any byte)
+  const bool vec = (N & 3) == 0 && (((uintptr_t)p.output | (uintptr_t)p.residual) & 3) == 0;
+  int32_t be[4], mu[4], sh[4];
+  if (vec) {
+    const v4i b4 = *(const v4i*)(p.bias_eff + nb);
+    const v4i m4 = *(const v4i*)(p.mult + nb);
+    const v4i s4 = *(const v4i*)(p.shift + nb);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      be[r] = b4[r];
+      mu[r] = m4[r];
+      sh[r] = s4[r];
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = nb + r < N ? nb + r : nb;
+      be[r] = p.bias_eff[n];
+      mu[r] = p.mult[n];
+      sh[r] = p.shift[n];
+    }
+  }
+  const long o = (long)m * N + nb;
+  const uint8_t* res = (const uint8_t*)p.residual;
+  const bool res_signed = p.in_xor == 0;  // residual shares the activation type
+  const uint8_t* tab = (const uint8_t*)p.out_table;
+  uint32_t rq = 0;
+  if (res) {
+    if (vec) {
+      rq = *(const uint32_t*)(res + o);
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (nb + r < N) rq |= (uint32_t)res[o + r] << (8 * r);
+    }
+  }
+  uint32_t packed = 0;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    int32_t a = acc[r] + be[r];
+    if (p.w_zp != 0) a -= p.w_zp * rsum;
+    int32_t v = p.requant_fast ? requant_out<true>(a, chan_q(mu[r], sh[r], p.out_zp), p.out_zp, p.act_min, p.act_max)
+                               : requant_out<false>(a, chan_q(mu[r], sh[r], p.out_zp), p.out_zp, p.act_min, p.act_max);
+    if (res) {
+      const uint32_t qb = (rq >> (8 * r)) & 0xffu;
+      const int32_t q = res_signed ? (int32_t)(int8_t)qb : (int32_t)qb;
+      const int32_t sy = requant_lt1((v + p.add_y_off) * (1 << p.add_left_shift), p.add_y_mult, p.add_y_shift);
+      const int32_t sr = requant_lt1((q + p.add_r_off) * (1 << p.add_left_shift), p.add_r_mult, p.add_r_shift);
+      v = clamp_i32(requant_lt1(sy + sr, p.add_o_mult, p.add_o_shift) + p.add_o_off, p.add_act_min, p.add_act_max);
+    }
+    const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
+    packed |= byte << (8 * r);
+  }
+  uint8_t* out = (uint8_t*)p.output + o;
+  if (vec) {
+    *(uint32_t*)out = packed;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (nb + r < N) out[r] = (uint8_t)(packed >> (8 * r));
+  }
+}
+
 constexpr int KU = 4;  // K-steps whose loads are issued together
 
 // WM x WN 16x16 tiles per wave; waves arranged WAVES_M x WAVES_N x SPLITK.
@@ -203,7 +274,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
         for (int wm = 0; wm < WM; ++wm)
 #pragma unroll
           for (int wn = 0; wn < WN; ++wn)
-            acc[wm][wn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[u][wm], b[u][wn], acc[wm][wn], 0, 0, 0);
+            acc[wm][wn] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[u][wn], a[u][wm], acc[wm][wn], 0, 0, 0);
         if (wzp) {
 #pragma unroll
           for (int wm = 0; wm < WM; ++wm) rs[wm] = rowsum16(a[u][wm], rs[wm]);
@@ -212,77 +283,48 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
     }
   }
 
-  if constexpr (SPLITK > 1) {
-    // reduce the K-split partials of the WAVES_M*WAVES_N tiles through LDS
-    __shared__ int red[SPLITK - 1][WAVES_M * WAVES_N][NACC + WM][64];
-    if (kz > 0) {
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) red[kz - 1][wt][(i * WN + j) * 4 + r][lane] = acc[i][j][r];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) red[kz - 1][wt][NACC + i][lane] = rs[i];
-    }
-    __syncthreads();
-    if (kz > 0) return;
-#pragma unroll
-    for (int z = 0; z < SPLITK - 1; ++z) {
-#pragma unroll
-      for (int i = 0; i < WM; ++i)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) acc[i][j][r] += red[z][wt][(i * WN + j) * 4 + r][lane];
-#pragma unroll
-      for (int i = 0; i < WM; ++i) rs[i] += red[z][wt][NACC + i][lane];
-    }
-  }
-
-  int rowsum[WM][4];
+  // pixel row sums (uint8 filters): lane (g, r16) holds a 16-byte K slice of
+  // pixel r16; the 4 slices of a K-step sit in lanes r16 + 16g
   if (wzp) {
 #pragma unroll
     for (int wm = 0; wm < WM; ++wm) {
-      int s = rs[wm];
-      s += __shfl_xor(s, 16);
-      s += __shfl_xor(s, 32);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rowsum[wm][r] = __shfl(s, 4 * g + r);
+      rs[wm] += __shfl_xor(rs[wm], 16);
+      rs[wm] += __shfl_xor(rs[wm], 32);
     }
   }
-
-  uint8_t* out = (uint8_t*)p.output;
-  const uint8_t* res = (const uint8_t*)p.residual;
-  const bool res_signed = p.in_xor == 0;  // residual shares the activation type
-  const uint8_t* tab = (const uint8_t*)p.out_table;
+  if constexpr (SPLITK > 1) {
+    // every wave parks its K-split partials in LDS; after one barrier wave w
+    // sums and finishes tiles w, w+4, ... so the epilogue runs on all waves
+    static_assert(WAVES_M * WAVES_N == 1, "split-K workgroups hold one wave tile");
+    __shared__ int red[SPLITK][NACC + WM][64];
 #pragma unroll
-  for (int wn = 0; wn < WN; ++wn) {
-    const int n = n0 + wn * 16 + r16;
-    if (n >= N) continue;
-    const int32_t be = p.bias_eff[n];
-    const int32_t mu = p.mult[n];
-    const int32_t sh = p.shift[n];
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-    for (int wm = 0; wm < WM; ++wm) {
+      for (int j = 0; j < WN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * 16 + 4 * g + r;
-        if (m >= M) continue;
-        int32_t v = acc[wm][wn][r] + be;
-        if (wzp) v -= p.w_zp * rowsum[wm][r];
-        v = clamp_i32(requant(v, mu, sh) + p.out_zp, p.act_min, p.act_max);
-        const long o = (long)m * N + n;
-        if (res) {
-          const int32_t q = res_signed ? (int32_t)(int8_t)res[o] : (int32_t)res[o];
-          const int32_t sy = requant_lt1((v + p.add_y_off) * (1 << p.add_left_shift), p.add_y_mult, p.add_y_shift);
-          const int32_t sr = requant_lt1((q + p.add_r_off) * (1 << p.add_left_shift), p.add_r_mult, p.add_r_shift);
-          v = clamp_i32(requant_lt1(sy + sr, p.add_o_mult, p.add_o_shift) + p.add_o_off, p.add_act_min,
-                        p.add_act_max);
-        }
-        out[o] = tab ? tab[(uint8_t)v] : (uint8_t)v;
+        for (int r = 0; r < 4; ++r) red[kz][(i * WN + j) * 4 + r][lane] = acc[i][j][r];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) red[kz][NACC + i][lane] = rs[i];
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < WM * WN; ++t) {
+      if (t % SPLITK != kz) continue;
+      const int i = t / WN, j = t % WN;
+      v4i sum = {0, 0, 0, 0};
+      int rsum = 0;
+#pragma unroll
+      for (int z = 0; z < SPLITK; ++z) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sum[r] += red[z][t * 4 + r][lane];
+        rsum += red[z][NACC + i][lane];
       }
+      conv_epilogue4(p, sum, rsum, m0 + i * 16 + r16, n0 + j * 16 + 4 * g, M, N);
     }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) conv_epilogue4(p, acc[i][j], rs[i], m0 + i * 16 + r16, n0 + j * 16 + 4 * g, M, N);
   }
 }
 
@@ -366,7 +408,8 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
     const bool stem = p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && N % 8 == 0 && !p.residual;
     return stem && !std::getenv("BH_CONV_NO_STEM") ? kStem : kDirect;
   }
-  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0) {
+  const bool aligned = (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.input) & 3) == 0;
+  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0 && aligned) {
     if (K <= 320 && M >= XsMinM()) return kXs;
     if (RowsMinM() >= 0 && M >= RowsMinM()) return kRows;
   }

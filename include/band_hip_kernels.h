@@ -302,6 +302,10 @@ int bh_conv2d_i8(const bh_conv_params* p, bh_stream_t s);
  * "conv_direct_kernel"); static storage.  Profiling attribution only. */
 const char* bh_conv2d_i8_kernel(const bh_conv_params* p);
 int bh_dwconv2d_i8(const bh_dwconv_params* p, bh_stream_t s);
+/* Symbol of the kernel bh_dwconv2d_i8 dispatches these parameters to
+ * ("dwconv3x3_run_kernel", "dwconv3x3_dot_kernel", "dwconv3x3_kernel",
+ * "dwconv_generic_kernel"); static storage.  Profiling attribution only. */
+const char* bh_dwconv2d_i8_kernel(const bh_dwconv_params* p);
 int bh_fc_i8(const bh_fc_params* p, bh_stream_t s);
 int bh_eltwise_i8(const bh_eltwise_params* p, bh_stream_t s);
 int bh_pool_i8(const bh_pool_params* p, bh_stream_t s);

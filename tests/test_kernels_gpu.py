@@ -102,7 +102,11 @@ def test_dwconv_mnv2_shapes(gpu_lib, spatial, ch, stride):
 @pytest.mark.parametrize("b,h,w,ch,stride,dil,dtype", [
     (1, 112, 112, 32, 1, 1, np.int8), (3, 57, 55, 144, 2, 1, np.int8), (2, 28, 28, 192, 1, 1, np.uint8),
     (5, 15, 13, 24, 2, 1, np.uint8), (2, 9, 9, 12, 1, 1, np.int8), (1, 17, 17, 20, 1, 2, np.int8),
-    (16, 14, 14, 576, 1, 1, np.int8), (4, 7, 7, 960, 1, 1, np.uint8)])
+    (16, 14, 14, 576, 1, 1, np.int8), (4, 7, 7, 960, 1, 1, np.uint8),
+    # grids >= 40k threads: the run kernel (4 pixels x 4 channels per thread),
+    # both strides, widths not a multiple of 4, uint8
+    (4, 112, 112, 32, 1, 1, np.int8), (8, 57, 55, 144, 2, 1, np.int8), (6, 28, 27, 192, 1, 1, np.uint8),
+    (32, 29, 30, 96, 2, 1, np.uint8), (64, 7, 7, 960, 1, 1, np.int8)])
 def test_dwconv_taps_vs_per_tap(gpu_lib, b, h, w, ch, stride, dil, dtype):
     rng = np.random.default_rng(3100 + b * h * w + ch + stride + dil)
     c = ConvCase(rng, b, h, w, ch, ch, 3, 3, stride=(stride, stride), dil=(dil, dil), depthwise=True, dtype=dtype)

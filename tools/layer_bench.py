@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--dtype", default="int8")
+    ap.add_argument("--layer", type=int, default=-1, help="only this row of the MNV2 table (0-based)")
     ap.add_argument("--no-taps", action="store_true", help="depthwise: the per-tap kernel (no tap table)")
     a = ap.parse_args()
     from band_amd import _abi
@@ -51,8 +52,10 @@ def main():
     rng = np.random.default_rng(0)
     dt = np.int8 if a.dtype == "int8" else np.uint8
     tot = {}
-    for kind, sp, ci, co, k, st in MNV2:
+    for li, (kind, sp, ci, co, k, st) in enumerate(MNV2):
         if a.only and kind != a.only:
+            continue
+        if a.layer >= 0 and li != a.layer:
             continue
         dw = kind == "dw"
         c = ConvCase(rng, a.batch, sp, sp, ci, co, k, k, stride=(st, st), depthwise=dw, dtype=dt,

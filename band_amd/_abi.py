@@ -69,7 +69,7 @@ class IrbParams(ctypes.Structure):
         ("has_residual", c_int)] + [(n, c_int32) for n in (
             "add_p_off", "add_x_off", "add_o_off", "add_left_shift", "add_p_mult", "add_p_shift", "add_x_mult",
             "add_x_shift", "add_o_mult", "add_o_shift", "add_act_min", "add_act_max")] + [
-        ("input", c_void_p), ("output", c_void_p), ("debug_stamps", c_void_p)]
+        ("input", c_void_p), ("output", c_void_p), ("debug_stamps", c_void_p), ("requant_fast", c_int32)]
 
 
 # symbol -> (restype, argtypes)

@@ -990,6 +990,7 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
       q.add_x_mult = pc.add_r_mult; q.add_x_shift = pc.add_r_shift;
       q.add_o_mult = pc.add_o_mult; q.add_o_shift = pc.add_o_shift;
       q.add_act_min = pc.add_act_min; q.add_act_max = pc.add_act_max;
+      q.requant_fast = (ec && ec->requant_fast ? 1 : 0) | (dw.requant_fast ? 2 : 0) | (pc.requant_fast ? 4 : 0);
       q.input = ec ? ec->input : dw.input;
       q.output = pc.output;
       // Tile edge: measured on this device when possible (each feasible

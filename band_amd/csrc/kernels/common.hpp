@@ -118,6 +118,13 @@ __device__ __forceinline__ int32_t requant_out(int32_t acc, const ChanQ& q, int3
   return min(max(v, lo), hi);
 }
 
+// requant + zero point + clamp, the single-step identity when `fast`
+// (uniform per layer) and TFLite's two-step form otherwise
+__device__ __forceinline__ int32_t requant_clamp(int32_t acc, int32_t mu, int32_t sh, int32_t zp, int32_t lo,
+                                                 int32_t hi, bool fast) {
+  return fast ? requant_out<true>(acc, chan_q(mu, sh, zp), zp, lo, hi) : clamp_i32(requant(acc, mu, sh) + zp, lo, hi);
+}
+
 // Workgroup id -> logical id such that each XCD (hardware ids i % 8 run on
 // XCD i % 8) gets one contiguous run of logical ids; the ids of an
 // incomplete last round keep their own number.  Neighbouring tiles (e.g. the

@@ -234,7 +234,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
       for (int r = 0; r < 4; ++r) {
         const int row = mt * 16 + 4 * g + r;
         if (row < G.R) {
-          const int32_t v = clamp_i32(requant(acc[r] + be1, mu1, sh1) + p.e_zp, p.e_act_min, p.e_act_max);
+          const int32_t v = requant_clamp(acc[r] + be1, mu1, sh1, p.e_zp, p.e_act_min, p.e_act_max, p.requant_fast & 1);
           el[row * G.es + col] = (unsigned char)v;
         }
       }
@@ -290,7 +290,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
         const v4i ss = *(const v4i*)(dwt + 2 * G.ce16 + c0);
 #pragma unroll
         for (int b = 0; b < 4; ++b) {
-          const int32_t v = clamp_i32(requant(acc[b] + bb[b], mm[b], ss[b]) + p.d_zp, p.d_act_min, p.d_act_max);
+          const int32_t v = requant_clamp(acc[b] + bb[b], mm[b], ss[b], p.d_zp, p.d_act_min, p.d_act_max, p.requant_fast & 2);
           packed |= ((uint32_t)v & 0xffu) << (8 * b);
         }
       }
@@ -318,8 +318,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
             acc += ((int32_t)(int8_t)el[er * G.es + c] - p.e_zp) * (int32_t)(int8_t)wl[(fy * 3 + fx) * G.ce16 + c];
           }
         }
-        v = clamp_i32(requant(acc + dwt[c], dwt[G.ce16 + c], dwt[2 * G.ce16 + c]) + p.d_zp, p.d_act_min,
-                      p.d_act_max);
+        v = requant_clamp(acc + dwt[c], dwt[G.ce16 + c], dwt[2 * G.ce16 + c], p.d_zp, p.d_act_min, p.d_act_max,
+                          p.requant_fast & 2);
       }
       dl[pi * G.ds + c] = (unsigned char)v;
     }
@@ -397,7 +397,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(bh_irb_params p, int kspli
         const int pi = pis[j];
         const int col = cols[j];
         int32_t v = accl[pi * G.np3 + col] + pjt[col];
-        v = clamp_i32(requant(v, pjt[p.out_c + col], pjt[2 * p.out_c + col]) + p.p_zp, p.p_act_min, p.p_act_max);
+        v = requant_clamp(v, pjt[p.out_c + col], pjt[2 * p.out_c + col], p.p_zp, p.p_act_min, p.p_act_max,
+                          p.requant_fast & 4);
         if (p.has_residual) {
           const int32_t sp = requant_lt1((v + p.add_p_off) * (1 << p.add_left_shift), p.add_p_mult, p.add_p_shift);
           const int32_t sx = requant_lt1((q[j] + p.add_x_off) * (1 << p.add_left_shift), p.add_x_mult, p.add_x_shift);

@@ -261,6 +261,9 @@ typedef struct bh_irb_params {
    * s_memrealtime stamps (100 MHz) at phase boundaries to
    * debug_stamps[16 * workgroup] (slots 0-7 used); NULL in production */
   void* debug_stamps;
+  /* single-step requantisation allowed (bh_conv_requant_fast_ok) per stage:
+   * bit 0 expand, bit 1 depthwise, bit 2 project */
+  int32_t requant_fast;
 } bh_irb_params;
 
 /* LDS bytes one workgroup of bh_irb_i8 needs for a tile (0 if unsupported) */

@@ -19,7 +19,8 @@ MNV2_BLOCKS = [
 
 
 class IrbCase:
-    def __init__(self, rng, b, h, w, cin, ce, cout, stride, has_expand=True, residual=None):
+    def __init__(self, rng, b, h, w, cin, ce, cout, stride, has_expand=True, residual=None, fast=True):
+        self.fast = fast
         self.b, self.h, self.w, self.cin, self.ce, self.cout, self.stride = b, h, w, cin, ce, cout, stride
         self.has_expand = has_expand
         if residual is None:
@@ -131,6 +132,18 @@ class IrbCase:
             q.add_p_mult, q.add_p_shift, q.add_x_mult, q.add_x_shift, q.add_o_mult, q.add_o_shift = prm[:6]
             q.add_left_shift = prm[6]
             q.add_act_min, q.add_act_max = orc.act_range(0, self.o_s, self.o_zp, True)
+        # single-step requant per stage, as the executor decides it
+        # (fast=False forces the two-step form everywhere)
+        def fast_ok(s_in, ws, n, k, s_out, bias):
+            m, sh = orc.conv_multipliers(s_in, ws, n, s_out, False)
+            m = np.ascontiguousarray(m, np.int32)
+            sh = np.ascontiguousarray(sh, np.int32)
+            return int(lib.bh_conv_requant_fast_ok(m.ctypes.data_as(ctypes.c_void_p), sh.ctypes.data_as(ctypes.c_void_p),
+                                                   n, k, int(np.abs(np.asarray(bias, np.int64)).max())))
+        if self.fast:
+            q.requant_fast = ((fast_ok(self.x_s, self.we_s, self.ce, self.cin, self.e_s, self.be) if self.has_expand
+                               else 0) | (fast_ok(self.e_s, self.wd_s, self.ce, 9, self.d_s, self.bd) << 1) |
+                              (fast_ok(self.d_s, self.wp_s, self.cout, self.ce, self.p_s, self.bp) << 2))
         q.input = dev(self.x)
         self.out_shape = (self.b, oh, ow, self.cout)
         from band_amd.device import DeviceBuffer as DB

@@ -19,6 +19,8 @@ def test_irb_mnv2_blocks(gpu_lib, h, cin, t, cout, s):
         if tile > 1 and not c.supported(gpu_lib, tile):
             continue
         np.testing.assert_array_equal(c.gpu(gpu_lib, tile), ref, err_msg="tile %d" % tile)
+    c.fast = False  # TFLite's two-step requantisation in every stage
+    np.testing.assert_array_equal(c.gpu(gpu_lib, 1), ref, err_msg="two-step requant")
 
 
 @pytest.mark.parametrize("args", [

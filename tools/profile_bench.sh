@@ -22,12 +22,13 @@ ARGS="--steps 2000 --warmup 200 --workers-per-gpu 1 $*"
 timeout -k 10 300 python3 bench.py $ARGS > "$O/${TAG}_bench.json"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${TAG}_trace" -o run -- \
   python3 bench.py $ARGS --no-graph --no-cpu-baseline > "$O/${TAG}_bench_profiled.json" 2> "$O/${TAG}_trace.err"
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcf" -o run -- \
-  python3 bench.py --steps 64 --warmup 16 --workers-per-gpu 1 --no-graph --no-cpu-baseline --no-batch1 --profile-iters 2 $* \
-  > /dev/null 2> "$O/${TAG}_pmcf.err"
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcw" -o run -- \
-  python3 bench.py --steps 64 --warmup 16 --workers-per-gpu 1 --no-graph --no-cpu-baseline --no-batch1 --profile-iters 2 $* \
-  > /dev/null 2> "$O/${TAG}_pmcw.err"
+# PMC passes: tools/pmc_pass.py replays the bench's batched passes from one
+# thread (bench.py itself crashed inside rocprofv3's PMC dispatch hook)
+JB=$(python3 -c "import sys; a=sys.argv[1:]; print(a[a.index('--job-batch')+1] if '--job-batch' in a else 16)" $*)
+timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcf" -o run -- \
+  python3 tools/pmc_pass.py --batch $JB > "$O/${TAG}_pmcf.log" 2> "$O/${TAG}_pmcf.err"
+timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcw" -o run -- \
+  python3 tools/pmc_pass.py --batch $JB > "$O/${TAG}_pmcw.log" 2> "$O/${TAG}_pmcw.err"
 python3 tools/pmc_traffic.py "$O/${TAG}_pmcf" "$O/${TAG}_pmcw" "$O/${TAG}_pmc_traffic.json" > "$O/${TAG}_pmc_traffic.txt"
 cp "$O/${TAG}_trace/run_kernel_stats.csv" "$O/${TAG}_kernel_stats.csv"
 echo "profile $TAG done"

@@ -81,3 +81,36 @@ def test_padding_rules():
     assert orc.padding(2, 1, 224, 3, 112) == 0
     assert orc.out_size(True, 7, 3, 1, 1) == 7 and orc.padding(1, 1, 7, 3, 7) == 1
     assert orc.out_size(False, 7, 7, 1, 1) == 1
+
+
+def test_single_step_requant_identity():
+    """The kernels' single-step requantisation (common.hpp requant_out<true>,
+    enabled per layer by bh_conv_requant_fast_ok) equals TFLite's two-step
+    MultiplyByQuantizedMultiplier (the oracle's tfl_mbqm) plus the zero point
+    for M in (2^30, 2^31), shift -e <= 0 and |x| inside the fast_ok bound;
+    random multipliers, multipliers with zeroed low bits (rounding ties are
+    then frequent) and exact half-way accumulators."""
+    L = orc.lib()
+    rng = np.random.default_rng(2024)
+    n = 0
+    for trial in range(400):
+        e = int(rng.integers(0, 21))
+        if trial % 3 == 0:
+            M = int(rng.integers((1 << 30) + 1, 1 << 31))
+        else:  # low bits zero: x*M lands on .5 boundaries often
+            M = (1 << 30) + (int(rng.integers(1, 1 << 10)) << 20)
+        zp = int(rng.integers(-128, 128))
+        bound = (1 << 30) - 255 * (1 << e) - 1
+        xs = rng.integers(-bound, bound + 1, size=200).tolist()
+        # accumulators whose product with M is an exact multiple of 2^30 (ties)
+        xs += [int(k) << 10 for k in rng.integers(-(bound >> 10), (bound >> 10) + 1, size=50)]
+        xs += [0, 1, -1, bound, -bound]
+        for x in xs:
+            z = x * M + (1 << 30) + ((1 << (30 + e)) if e > 0 else 0)
+            u = z >> 31
+            s = -1 if (e > 0 and x < 0) else 0
+            v = (u + s + (zp << e)) >> e
+            ref = L.tfl_mbqm(x, M, -e) + zp
+            assert v == ref, (x, M, e, zp, v, ref)
+            n += 1
+    assert n > 100000

@@ -31,6 +31,17 @@ MNV2 = [
     ("conv", 7, 960, 320, 1, 1), ("conv", 7, 320, 1280, 1, 1),
 ]
 
+# MobileNetV1-1.0-224 (PoseNet's backbone), deduplicated
+MNV1 = [
+    ("stem", 224, 3, 32, 3, 2),
+    ("dw", 112, 32, 32, 3, 1), ("conv", 112, 32, 64, 1, 1), ("dw", 112, 64, 64, 3, 2),
+    ("conv", 56, 64, 128, 1, 1), ("dw", 56, 128, 128, 3, 1), ("conv", 56, 128, 128, 1, 1),
+    ("dw", 56, 128, 128, 3, 2), ("conv", 28, 128, 256, 1, 1), ("dw", 28, 256, 256, 3, 1),
+    ("conv", 28, 256, 256, 1, 1), ("dw", 28, 256, 256, 3, 2), ("conv", 14, 256, 512, 1, 1),
+    ("dw", 14, 512, 512, 3, 1), ("conv", 14, 512, 512, 1, 1), ("dw", 14, 512, 512, 3, 2),
+    ("conv", 7, 512, 1024, 1, 1), ("dw", 7, 1024, 1024, 3, 1), ("conv", 7, 1024, 1024, 1, 1),
+]
+
 
 def main():
     ap = argparse.ArgumentParser()
@@ -38,6 +49,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--only", default="")
     ap.add_argument("--dtype", default="int8")
+    ap.add_argument("--net", default="mnv2", choices=["mnv2", "mnv1"])
     ap.add_argument("--layer", type=int, default=-1, help="only this row of the MNV2 table (0-based)")
     ap.add_argument("--no-taps", action="store_true", help="depthwise: the per-tap kernel (no tap table)")
     a = ap.parse_args()
@@ -52,7 +64,7 @@ def main():
     rng = np.random.default_rng(0)
     dt = np.int8 if a.dtype == "int8" else np.uint8
     tot = {}
-    for li, (kind, sp, ci, co, k, st) in enumerate(MNV2):
+    for li, (kind, sp, ci, co, k, st) in enumerate(MNV2 if a.net == "mnv2" else MNV1):
         if a.only and kind != a.only:
             continue
         if a.layer >= 0 and li != a.layer:

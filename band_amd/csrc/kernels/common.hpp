@@ -125,6 +125,18 @@ __device__ __forceinline__ int32_t requant_clamp(int32_t acc, int32_t mu, int32_
   return fast ? requant_out<true>(acc, chan_q(mu, sh, zp), zp, lo, hi) : clamp_i32(requant(acc, mu, sh) + zp, lo, hi);
 }
 
+// Read-only operand tables (filters, folded biases, multipliers) seen
+// through the constant address space: a wave-uniform index then compiles to
+// s_load (scalar cache, no texture-unit work) even though the kernel also
+// stores through other pointers, which keeps the compiler from proving the
+// generic pointer unclobbered.
+template <typename T>
+using cst_ptr = const T __attribute__((address_space(4)))*;
+template <typename T>
+__device__ __forceinline__ cst_ptr<T> as_const(const T* p) {
+  return (cst_ptr<T>)(uintptr_t)p;
+}
+
 // Workgroup id -> logical id such that each XCD (hardware ids i % 8 run on
 // XCD i % 8) gets one contiguous run of logical ids; the ids of an
 // incomplete last round keep their own number.  Neighbouring tiles (e.g. the

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void conv_direct_kernel(bh_conv_params p, int 
 // horizontally, or whose aligned loads would run past the tensor, take the
 // byte path of conv_direct_kernel.
 template <bool FAST>
-__global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M, DirectDivs dv) {
+__global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M, DirectDivs dv, int ch_per_y) {
   const int m = blockIdx.x * 256 + threadIdx.x;
   if (m >= M) return;
   const int t = dv.out_w.div(m);
@@ -165,17 +165,24 @@ __global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M,
   }
   uint8_t* out = (uint8_t*)p.output + (long)m * p.out_c;
   const uint8_t* tab = (const uint8_t*)p.out_table;
-  for (int c0 = 0; c0 < p.out_c; c0 += 8) {
+  const cst_ptr<int32_t> wts = as_const((const int32_t*)p.weights);
+  const cst_ptr<int32_t> bias = as_const(p.bias_eff), mult = as_const(p.mult), shift = as_const(p.shift);
+  const int kpw = p.k_pad >> 2;
+  // grid.y splits the channels when the pixels alone give too few
+  // workgroups (batch 1): this workgroup's range [cb, ce)
+  const int cb = blockIdx.y * ch_per_y;
+  const int ce = min(p.out_c, cb + ch_per_y);
+  for (int c0 = cb; c0 < ce; c0 += 8) {
     uint32_t packed[2] = {0u, 0u};
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
       const int oc = c0 + c;
-      const int* wrow = (const int*)(p.weights + (long)oc * p.k_pad);
-      int acc = p.bias_eff[oc];
+      const cst_ptr<int32_t> wrow = wts + oc * kpw;  // uniform: scalar loads
+      int acc = bias[oc];
 #pragma unroll
       for (int j = 0; j < 7; ++j) acc = __builtin_amdgcn_sdot4((int)xw[j], wrow[j], acc, false);
       if (p.w_zp != 0) acc -= p.w_zp * rowsum;
-      int32_t v = requant_out<FAST>(acc, chan_q(p.mult[oc], p.shift[oc], p.out_zp), p.out_zp, p.act_min, p.act_max);
+      int32_t v = requant_out<FAST>(acc, chan_q(mult[oc], shift[oc], p.out_zp), p.out_zp, p.act_min, p.act_max);
       const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
       packed[c >> 2] |= byte << (8 * (c & 3));
     }
@@ -206,8 +213,15 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   bh::DirectDivs dv;
   dv.out_w = bh::FastDiv(p.out_w);
   dv.out_h = bh::FastDiv(p.out_h);
-  const dim3 grid((unsigned)((M + 255) / 256));
-  if (p.requant_fast) hipLaunchKernelGGL(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv);
-  else hipLaunchKernelGGL(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv);
+  // >= ~512 workgroups: split the output channels over grid.y (8 at a time)
+  const int gx = (M + 255) / 256;
+  const int groups = p.out_c / 8;
+  int gy = (512 + gx - 1) / gx;
+  gy = gy < 1 ? 1 : (gy > groups ? groups : gy);
+  const int ch_per_y = (groups + gy - 1) / gy * 8;
+  gy = (p.out_c + ch_per_y - 1) / ch_per_y;
+  const dim3 grid((unsigned)gx, (unsigned)gy);
+  if (p.requant_fast) hipLaunchKernelGGL(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+  else hipLaunchKernelGGL(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
   return bh_check_launch("conv_stem_kernel");
 }

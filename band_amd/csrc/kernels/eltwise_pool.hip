@@ -275,7 +275,7 @@ extern "C" int bh_pool_i8(const bh_pool_params* pp, bh_stream_t stream) {
   bh::PoolDivs dv;
   dv.out_w = bh::FastDiv(p.out_w);
   dv.out_h = bh::FastDiv(p.out_h);
-  if (p.channels % 4 == 0 && pixels * (p.channels / 4) <= 4096 && p.f_h * p.f_w >= 16 && pixels <= 65535) {
+  if (p.channels % 4 == 0 && pixels * (p.channels / 4) <= 65536 && p.f_h * p.f_w >= 16 && pixels <= 65535) {
     dv.groups = bh::FastDiv(p.channels / 4);
     const dim3 grid((unsigned)pixels, (unsigned)((p.channels / 4 + 63) / 64));
     hipLaunchKernelGGL(bh::pool_wide_kernel, grid, dim3(256), 0, s, p, dv);

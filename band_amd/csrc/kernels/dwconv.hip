@@ -61,7 +61,9 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int 
   const int ox = pix - t * p.out_w;
   const int n = dv.out_h.div(t);
   const int oy = t - n * p.out_h;
-  const uint8_t* in = (const uint8_t*)p.input + (long)n * p.in_h * p.in_w * p.in_c + c0;
+  // 32-bit offsets (tensor sizes < 2^31, checked by the launcher): no
+  // 64-bit multiplies in the address math
+  const uint8_t* in = (const uint8_t*)p.input + (n * p.in_h * p.in_w * p.in_c + c0);
   const uint8_t* wt = (const uint8_t*)p.weights + c0;
   const uint32_t xorw = splat_byte(p.in_xor);
   const int y0 = oy * p.stride_h - p.pad_h;
@@ -77,8 +79,8 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int 
       const int y = y0 + fy * p.dil_h;
       const int x = x0 + fx * p.dil_w;
       ok[tap] = y >= 0 && y < p.in_h && x >= 0 && x < p.in_w;
-      Vec<CV>::ld(wt + (long)tap * p.out_c, wv[tap]);
-      if (ok[tap]) Vec<CV>::ld(in + ((long)y * p.in_w + x) * p.in_c, xv[tap]);
+      Vec<CV>::ld(wt + tap * p.out_c, wv[tap]);
+      if (ok[tap]) Vec<CV>::ld(in + (y * p.in_w + x) * p.in_c, xv[tap]);
     }
   }
   int32_t acc[CV];
@@ -111,7 +113,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_kernel(bh_dwconv_params p, int 
     }
     packed[d] = o;
   }
-  Vec<CV>::st((uint8_t*)p.output + (((long)n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0, packed);
+  Vec<CV>::st((uint8_t*)p.output + (((n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0), packed);
 }
 
 // 3x3 / dm 1 with the host-packed tap table (bh_pack_dw_taps): the nine
@@ -138,7 +140,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, 
   const int n = dv.out_h.div(t);
   const int oy = t - n * p.out_h;
   const uint8_t* base = (const uint8_t*)p.input;
-  const uint8_t* in = base + (long)n * p.in_h * p.in_w * p.in_c + c0;
+  const uint8_t* in = base + (n * p.in_h * p.in_w * p.in_c + c0);
   const uint32_t xorw = splat_byte(p.in_xor);
   const uint32_t zfill = splat_byte(p.in_zp);
   const int y0 = oy * p.stride_h - p.pad_h;
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, 
       const int y = y0 + fy * p.dil_h;
       const int x = x0 + fx * p.dil_w;
       const bool ok = y >= 0 && y < p.in_h && x >= 0 && x < p.in_w;
-      Vec<CV>::ld(ok ? in + ((long)y * p.in_w + x) * p.in_c : base, xv[tap]);
+      Vec<CV>::ld(ok ? in + (y * p.in_w + x) * p.in_c : base, xv[tap]);
 #pragma unroll
       for (int d = 0; d < NW; ++d) xv[tap][d] = ok ? xv[tap][d] ^ xorw : zfill;
     }
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, 
     }
     packed[d] = o;
   }
-  Vec<CV>::st((uint8_t*)p.output + (((long)n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0, packed);
+  Vec<CV>::st((uint8_t*)p.output + (((n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0), packed);
 }
 
 // dot4 kernel, run form (dil 1, stride S in {1, 2}): a thread owns a RUN of
@@ -233,11 +235,14 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
   const int n = dv.out_h.div(t);
   const int oy = t - n * p.out_h;
   const uint8_t* base = (const uint8_t*)p.input;
-  const uint8_t* in = base + (long)n * p.in_h * p.in_w * p.in_c + c0;
   const uint32_t xorw = splat_byte(p.in_xor);
   const uint32_t zfill = splat_byte(p.in_zp);
   const int y0 = oy * S - p.pad_h;
   const int x0 = ox0 * S - p.pad_w;
+  // 32-bit offsets (tensor sizes < 2^31, checked by the launcher), one
+  // multiply per row: the columns step by in_c
+  const int rstride = p.in_w * p.in_c;
+  const int off0 = n * p.in_h * rstride + y0 * rstride + x0 * p.in_c + c0;
 
   uint32_t X[3][NCOL][NW];
 #pragma unroll
@@ -248,7 +253,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
     for (int col = 0; col < NCOL; ++col) {
       const int x = x0 + col;
       const bool ok = yok && x >= 0 && x < p.in_w;
-      Vec<CV>::ld(ok ? in + ((long)y * p.in_w + x) * p.in_c : base, X[fy][col]);
+      Vec<CV>::ld(ok ? base + (off0 + fy * rstride + col * p.in_c) : base, X[fy][col]);
 #pragma unroll
       for (int d = 0; d < NW; ++d) X[fy][col][d] = ok ? X[fy][col][d] ^ xorw : zfill;
     }
@@ -268,7 +273,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
     }
   }
   const uint8_t* otab = (const uint8_t*)p.out_table;
-  uint8_t* out = (uint8_t*)p.output + (((long)n * p.out_h + oy) * p.out_w + ox0) * p.out_c + c0;
+  uint8_t* out = (uint8_t*)p.output + (((n * p.out_h + oy) * p.out_w + ox0) * p.out_c + c0);
 #pragma unroll
   for (int px = 0; px < PX; ++px) {
     if (ox0 + px >= p.out_w) break;
@@ -320,7 +325,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
       }
       packed[d] = o;
     }
-    Vec<CV>::st(out + (long)px * p.out_c, packed);
+    Vec<CV>::st(out + px * p.out_c, packed);
   }
 }
 
@@ -458,7 +463,7 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
   }
   hipStream_t s = (hipStream_t)stream;
   const long pixels = (long)p.batch * p.out_h * p.out_w;
-  if (pixels * p.out_c >= INT32_MAX) {
+  if (pixels * p.out_c >= INT32_MAX || (long)p.batch * p.in_h * p.in_w * p.in_c >= INT32_MAX) {
     bh_set_last_error("bh_dwconv2d_i8: tensor too large for 32-bit indexing");
     return BH_EINVAL;
   }

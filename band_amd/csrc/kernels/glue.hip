@@ -151,15 +151,18 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(bh_resize_bilinear
   const int y = (int)(t - n * p.out_h);
   const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1], iy = p.y_tab[3 * y + 2];
   const int x0 = p.x_tab[3 * x], x1 = p.x_tab[3 * x + 1], ix = p.x_tab[3 * x + 2];
-  const int8_t* in = (const int8_t*)p.input + (long)n * p.in_h * p.in_w * p.channels + ch;
-  const long r0 = (long)y0 * p.in_w, r1 = (long)y1 * p.in_w;
-  const int64_t v00 = in[(r0 + x0) * p.channels], v10 = in[(r1 + x0) * p.channels];
-  const int64_t v01 = in[(r0 + x1) * p.channels], v11 = in[(r1 + x1) * p.channels];
+  // 32-bit throughout: |s| <= 128 * 2^20 (the four weights sum to 2^20), so
+  // TFLite's int64 accumulation never leaves int32 range; offsets < 2^31
+  // (checked by the launcher)
+  const int8_t* in = (const int8_t*)p.input + ((int)n * p.in_h * p.in_w * p.channels + ch);
+  const int r0 = y0 * p.in_w, r1 = y1 * p.in_w;
+  const int32_t v00 = in[(r0 + x0) * p.channels], v10 = in[(r1 + x0) * p.channels];
+  const int32_t v01 = in[(r0 + x1) * p.channels], v11 = in[(r1 + x1) * p.channels];
   constexpr int32_t one = 1 << 10;
   const int32_t fy = iy - one * y0, fx = ix - one * x0;
-  const int64_t s = v00 * ((one - fy) * (one - fx)) + v10 * (fy * (one - fx)) + v01 * ((one - fy) * fx) +
+  const int32_t s = v00 * ((one - fy) * (one - fx)) + v10 * (fy * (one - fx)) + v01 * ((one - fy) * fx) +
                     v11 * (fy * fx);
-  const int64_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
+  const int32_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
   ((int8_t*)p.output)[i] = (int8_t)((s + rnd) / (1 << 20));
 }
 
@@ -355,7 +358,7 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
   }
   const bh_resize_bilinear_params& p = *pp;
   const long total = (long)p.batch * p.out_h * p.out_w * p.channels;
-  if (total >= INT32_MAX) {
+  if (total >= INT32_MAX || (long)p.batch * p.in_h * p.in_w * p.channels >= INT32_MAX) {
     bh_set_last_error("bh_resize_bilinear_i8: tensor too large for 32-bit indexing");
     return BH_EINVAL;
   }

@@ -17,7 +17,7 @@ output copy (band/worker.cc:222-323) -> Wait.  A native closed-loop driver
 flight.  Job latency = end - enqueue of the planner's job record
 (band/common.h:351-353).
 
-Job batching (--job-batch B, default 16; BANDX_WORKER_MAX_JOB_BATCH): an
+Job batching (--job-batch B, default 24; BANDX_WORKER_MAX_JOB_BATCH): an
 idle GPU worker takes up to B queued requests of one model from round_robin
 and runs them as ONE pass over a batch-B variant of the model's subgraph
 (every job still gets its own input copy, its own outputs, its own job
@@ -72,7 +72,7 @@ def parse():
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
     p.add_argument("--no-batch1", action="store_true",
                    help="skip the one-job-per-pass (Band semantics) line reported beside a job-batched run")
-    p.add_argument("--job-batch", type=int, default=16,
+    p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
     return p.parse_args()
@@ -343,7 +343,10 @@ def main():
         sched = SchedulerType.kHeterogeneousEarliestFinishTime  # a split model needs fallback subgraphs
         args.scheduler = "heterogeneous_earliest_finish_time"
     engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch)
-    inflight = args.inflight or 2 * W * max(1, args.job_batch)
+    # 2 x workers x job batch requests in flight, at most 120 per model: Band's
+    # per-model output ring buffers hold 128 slots (TensorRingBuffer), and a
+    # request whose slot was reused before its output was copied fails
+    inflight = args.inflight or min(2 * W * max(1, args.job_batch), 120 * M)
 
     engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
     poisson = None

@@ -9,7 +9,7 @@ each (eager launches, the tuning decisions of BAND_HIP_TUNE_FILE), `iters`
 ExecuteSubgraph calls per model.  tools/pmc_traffic.py then reads the
 per-dispatch FETCH_SIZE / WRITE_SIZE.
 
-usage: python3 tools/pmc_pass.py [--model mix_c3] [--batch 16] [--iters 3]
+usage: python3 tools/pmc_pass.py [--model mix_c3] [--batch 24] [--iters 3]
 """
 import argparse
 import os
@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="mix_c3")
-    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--iters", type=int, default=3)
     a = ap.parse_args()
     import tempfile

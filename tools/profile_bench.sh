@@ -24,7 +24,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/${
   python3 bench.py $ARGS --no-graph --no-cpu-baseline > "$O/${TAG}_bench_profiled.json" 2> "$O/${TAG}_trace.err"
 # PMC passes: tools/pmc_pass.py replays the bench's batched passes from one
 # thread (bench.py itself crashed inside rocprofv3's PMC dispatch hook)
-JB=$(python3 -c "import sys; a=sys.argv[1:]; print(a[a.index('--job-batch')+1] if '--job-batch' in a else 16)" $*)
+JB=$(python3 -c "import sys; a=sys.argv[1:]; print(a[a.index('--job-batch')+1] if '--job-batch' in a else 24)" $*)
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcf" -o run -- \
   python3 tools/pmc_pass.py --batch $JB > "$O/${TAG}_pmcf.log" 2> "$O/${TAG}_pmcf.err"
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$O/${TAG}_pmcw" -o run -- \

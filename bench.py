@@ -342,11 +342,14 @@ def main():
     if n_cpu and args.scheduler in ("round_robin", "fixed_worker"):
         sched = SchedulerType.kHeterogeneousEarliestFinishTime  # a split model needs fallback subgraphs
         args.scheduler = "heterogeneous_earliest_finish_time"
+    if not (on_gpu and n_cpu == 0 and args.scheduler == "round_robin"):
+        args.job_batch = 1  # job batching applies to round_robin over GPU workers only
+    batching = args.job_batch > 1
     engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch)
     # 2 x workers x job batch requests in flight, at most 120 per model: Band's
     # per-model output ring buffers hold 128 slots (TensorRingBuffer), and a
     # request whose slot was reused before its output was copied fails
-    inflight = args.inflight or min(2 * W * max(1, args.job_batch), 120 * M)
+    inflight = args.inflight or min(2 * W * (args.job_batch if batching else 1), 120 * M)
 
     engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
     poisson = None
@@ -376,7 +379,8 @@ def main():
     # Band's own semantics beside it: one job per ExecuteSubgraph (no job
     # batching), the same mix and scheduler over 8 GPU workers per GPU
     batch1 = None
-    if args.job_batch > 1 and not poisson and on_gpu and not args.no_batch1:
+    # (only where job batching applies: round_robin over GPU workers alone)
+    if batching and not poisson and not args.no_batch1:
         W1 = 8
         e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1)
         n1 = max(args.steps // 2, 16 * M)

@@ -202,7 +202,8 @@ constexpr int KU = 4;  // K-steps whose loads are issued together
 
 // WM x WN 16x16 tiles per wave; waves arranged WAVES_M x WAVES_N x SPLITK.
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv) {
+__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv,
+                                                        int nblocks, int xcd) {
   static_assert(WAVES_M * WAVES_N * SPLITK == 4, "4 waves per workgroup");
   constexpr int TM = WAVES_M * WM * 16;
   constexpr int TN = WAVES_N * WN * 16;
@@ -213,8 +214,14 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   const int wt = wave % (WAVES_M * WAVES_N);
   const int wave_m = wt % WAVES_M;
   const int wave_n = wt / WAVES_M;
-  const int m0 = blockIdx.x * TM + wave_m * WM * 16;
-  const int n0 = blockIdx.y * TN + wave_n * WN * 16;
+  // 1-D grid, N-blocks fastest; with xcd each XCD (hardware ids i % 8) runs
+  // a contiguous run of logical blocks, so all N-blocks of a pixel block -
+  // which read the same input rows - share one L2
+  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int bm = logical / nblocks;
+  const int bn = logical - bm * nblocks;
+  const int m0 = bm * TM + wave_m * WM * 16;
+  const int n0 = bn * TN + wave_n * WN * 16;
   const int r16 = lane & 15;
   const int g = lane >> 4;
   const bool wzp = p.w_zp != 0;
@@ -339,9 +346,13 @@ static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t 
   dv.out_h = FastDiv(p.out_h);
   dv.in_c = FastDiv(p.in_c);
   dv.k_w = FastDiv(p.k_w);
-  dim3 grid((M + TM - 1) / TM, (N + TN - 1) / TN);
-  hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), grid, dim3(256), 0, s,
-                     p, M, K, N, kchunk, dv);
+  const int gm = (M + TM - 1) / TM, gn = (N + TN - 1) / TN;
+  static const int xcd = [] {
+    const char* e = std::getenv("BH_CONV_XCD");  // A-B runs: 0 = plain order
+    return e ? std::atoi(e) : 1;
+  }();
+  hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
+                     s, p, M, K, N, kchunk, dv, gn, xcd);
   return bh_check_launch("conv_mfma_kernel");
 }
 

@@ -211,7 +211,8 @@ __global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, 
   Vec<CV>::st((uint8_t*)p.output + (((n * p.out_h + oy) * p.out_w + ox) * p.out_c + c0), packed);
 }
 
-// dot4 kernel, run form (dil 1, stride S in {1, 2}): a thread owns a RUN of
+// dot4 kernel, run form (dil 1 with stride S in {1, 2}, or dil D = 2 with
+// stride 1): a thread owns a RUN of
 // 4 horizontally adjacent output pixels x CV channels.  The run's input
 // columns (3 + 3*S) are loaded once and shared by its pixels' windows
 // (18 / 27 loads for 4 pixels instead of 36), and the channel operands -
@@ -220,11 +221,11 @@ __global__ __launch_bounds__(256) void dwconv3x3_dot_kernel(bh_dwconv_params p, 
 // texture-unit bound (TA busy ~60%, waves parked on vmcnt 86% of their
 // cycles) with 33 bytes of L1 traffic per output byte; the run form needs
 // about 10.
-template <int CV, int S, bool FAST, bool WZP>
+template <int CV, int S, int D, bool FAST, bool WZP>
 __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, int total, DwDivs dv) {
   constexpr int NW = CV / 4;
   constexpr int PX = 4;
-  constexpr int NCOL = 3 + (PX - 1) * S;
+  constexpr int NCOL = 1 + 2 * D + (PX - 1) * S;  // input columns of the run (dilation D)
   const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   const int idx = blk * blockDim.x + threadIdx.x;
   if (idx >= total) return;
@@ -247,13 +248,13 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
   uint32_t X[3][NCOL][NW];
 #pragma unroll
   for (int fy = 0; fy < 3; ++fy) {
-    const int y = y0 + fy;
+    const int y = y0 + fy * D;
     const bool yok = y >= 0 && y < p.in_h;
 #pragma unroll
     for (int col = 0; col < NCOL; ++col) {
       const int x = x0 + col;
       const bool ok = yok && x >= 0 && x < p.in_w;
-      Vec<CV>::ld(ok ? base + (off0 + fy * rstride + col * p.in_c) : base, X[fy][col]);
+      Vec<CV>::ld(ok ? base + (off0 + fy * D * rstride + col * p.in_c) : base, X[fy][col]);
 #pragma unroll
       for (int d = 0; d < NW; ++d) X[fy][col][d] = ok ? X[fy][col][d] ^ xorw : zfill;
     }
@@ -281,7 +282,7 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
 #pragma unroll
     for (int d = 0; d < NW; ++d) {
       // window taps (fy, fx) in row-major order: 0-3, 4-7 transposed, 8 as is
-#define TAP(k) X[(k) / 3][px * S + (k) % 3][d]
+#define TAP(k) X[(k) / 3][px * S + ((k) % 3) * D][d]
       uint32_t T[4], U[4];
       {
         const uint32_t l01 = __builtin_amdgcn_perm(TAP(1), TAP(0), 0x05010400u);
@@ -377,7 +378,7 @@ static DwDivs dw_divs(const bh_dwconv_params& p, int groups) {
   return dv;
 }
 
-template <int CV, int S>
+template <int CV, int S, int D>
 static void launch_run(const bh_dwconv_params& p, hipStream_t s) {
   const int runs_w = (p.out_w + 3) / 4;
   const int total = (int)((long)p.batch * p.out_h * runs_w * (p.out_c / CV));
@@ -385,11 +386,11 @@ static void launch_run(const bh_dwconv_params& p, hipStream_t s) {
   dv.runs_w = FastDiv(runs_w);
   const dim3 grid((unsigned)((total + 255) / 256));
   if (p.w_zp != 0) {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, true, true>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, false, true>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, true, true>), grid, dim3(256), 0, s, p, total, dv);
+    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, false, true>), grid, dim3(256), 0, s, p, total, dv);
   } else {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, true, false>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, false, false>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, true, false>), grid, dim3(256), 0, s, p, total, dv);
+    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, false, false>), grid, dim3(256), 0, s, p, total, dv);
   }
 }
 
@@ -399,8 +400,9 @@ static bool run_ok(const bh_dwconv_params& p) {
     const char* e = std::getenv("BH_DW_NO_RUN");
     return e ? std::atoi(e) : 0;
   }();
-  return !off && p.taps && p.dil_h == 1 && p.dil_w == 1 && p.stride_h == p.stride_w &&
-         (p.stride_h == 1 || p.stride_h == 2);
+  // dil 1 with stride 1 / 2, or dil 2 with stride 1 (DeepLab's atrous layers)
+  return !off && p.taps && p.dil_h == p.dil_w && p.stride_h == p.stride_w &&
+         ((p.dil_h == 1 && (p.stride_h == 1 || p.stride_h == 2)) || (p.dil_h == 2 && p.stride_h == 1));
 }
 
 template <int CV>
@@ -422,7 +424,7 @@ static void launch3x3(const bh_dwconv_params& p, long pixels, hipStream_t s) {
 }  // namespace bh
 
 namespace {
-enum DwRoute { kRun1, kRun2, kDot16, kDot8, kDot4, kTap16, kTap8, kTap4, kGeneric };
+enum DwRoute { kRun1, kRun2, kRunD2, kDot16, kDot8, kDot4, kTap16, kTap8, kTap4, kGeneric };
 
 DwRoute dw_route(const bh_dwconv_params& p) {
   const long pixels = (long)p.batch * p.out_h * p.out_w;
@@ -433,7 +435,7 @@ DwRoute dw_route(const bh_dwconv_params& p) {
   // (MobileNetV2 depthwise layers, batch 16 / 64); below it, at batch 1, the
   // per-pixel kernels' shorter per-thread chains win
   if (bh::run_ok(p) && (long)p.batch * p.out_h * ((p.out_w + 3) / 4) * (p.out_c / 4) >= 40000)
-    return p.stride_h == 1 ? kRun1 : kRun2;
+    return p.dil_h == 2 ? kRunD2 : (p.stride_h == 1 ? kRun1 : kRun2);
   // per-pixel kernels: widest vector that still leaves enough threads to fill the chip
   const int base = p.taps ? kDot16 : kTap16;
   if (p.out_c % 16 == 0 && pixels * (p.out_c / 16) >= 65536) return (DwRoute)base;
@@ -445,7 +447,7 @@ DwRoute dw_route(const bh_dwconv_params& p) {
 extern "C" const char* bh_dwconv2d_i8_kernel(const bh_dwconv_params* p) {
   if (!p) return "";
   switch (dw_route(*p)) {
-    case kRun1: case kRun2: return "dwconv3x3_run_kernel";
+    case kRun1: case kRun2: case kRunD2: return "dwconv3x3_run_kernel";
     case kDot16: case kDot8: case kDot4: return "dwconv3x3_dot_kernel";
     case kTap16: case kTap8: case kTap4: return "dwconv3x3_kernel";
     default: return "dwconv_generic_kernel";
@@ -473,8 +475,9 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
     return BH_EINVAL;
   }
   switch (dw_route(p)) {
-    case kRun1: bh::launch_run<4, 1>(p, s); break;
-    case kRun2: bh::launch_run<4, 2>(p, s); break;
+    case kRun1: bh::launch_run<4, 1, 1>(p, s); break;
+    case kRun2: bh::launch_run<4, 2, 1>(p, s); break;
+    case kRunD2: bh::launch_run<4, 1, 2>(p, s); break;
     case kDot16: case kTap16: bh::launch3x3<16>(p, pixels, s); break;
     case kDot8: case kTap8: bh::launch3x3<8>(p, pixels, s); break;
     case kDot4: case kTap4: bh::launch3x3<4>(p, pixels, s); break;

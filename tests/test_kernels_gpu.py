@@ -106,7 +106,9 @@ def test_dwconv_mnv2_shapes(gpu_lib, spatial, ch, stride):
     # grids >= 40k threads: the run kernel (4 pixels x 4 channels per thread),
     # both strides, widths not a multiple of 4, uint8
     (4, 112, 112, 32, 1, 1, np.int8), (8, 57, 55, 144, 2, 1, np.int8), (6, 28, 27, 192, 1, 1, np.uint8),
-    (32, 29, 30, 96, 2, 1, np.uint8), (64, 7, 7, 960, 1, 1, np.int8)])
+    (32, 29, 30, 96, 2, 1, np.uint8), (64, 7, 7, 960, 1, 1, np.int8),
+    # dilation 2 (DeepLab's atrous depthwise layers) in the run form
+    (24, 14, 14, 576, 1, 2, np.int8), (32, 17, 15, 96, 1, 2, np.uint8)])
 def test_dwconv_taps_vs_per_tap(gpu_lib, b, h, w, ch, stride, dil, dtype):
     rng = np.random.default_rng(3100 + b * h * w + ch + stride + dil)
     c = ConvCase(rng, b, h, w, ch, ch, 3, 3, stride=(stride, stride), dil=(dil, dil), depthwise=True, dtype=dtype)

@@ -244,6 +244,8 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
   // multiply per row: the columns step by in_c
   const int rstride = p.in_w * p.in_c;
   const int off0 = n * p.in_h * rstride + y0 * rstride + x0 * p.in_c + c0;
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, p.batch * p.in_h * rstride, 0x00020000);
 
   uint32_t X[3][NCOL][NW];
 #pragma unroll
@@ -254,7 +256,15 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
     for (int col = 0; col < NCOL; ++col) {
       const int x = x0 + col;
       const bool ok = yok && x >= 0 && x < p.in_w;
-      Vec<CV>::ld(ok ? base + (off0 + fy * D * rstride + col * p.in_c) : base, X[fy][col]);
+      const int off = off0 + fy * D * rstride + col * p.in_c;
+      if constexpr (CV == 4) {
+        // raw buffer load: 32-bit offset, no 64-bit address math and no
+        // address select - an out-of-image tap's offset may be anything
+        // (negative ones are out of range and read 0); it is replaced below
+        X[fy][col][0] = __builtin_amdgcn_raw_buffer_load_b32(rsrc, off, 0, 0);
+      } else {
+        Vec<CV>::ld(ok ? base + off : base, X[fy][col]);
+      }
 #pragma unroll
       for (int d = 0; d < NW; ++d) X[fy][col][d] = ok ? X[fy][col][d] ^ xorw : zfill;
     }

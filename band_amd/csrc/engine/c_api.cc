@@ -388,9 +388,18 @@ namespace {
 // request driver shared by the closed-loop and Poisson entry points:
 // `next_arrival(j)` returns the time (us since start) job j may be submitted
 // (0 = as soon as the in-flight bound allows) and its model index
+//
+// Latency: closed loop, end - enqueue of the job record; open loop (Poisson),
+// end - the job's SCHEDULED arrival, so time a request waited to be submitted
+// (in-flight bound, ring back-pressure) counts as the queueing it is rather
+// than vanishing from the percentiles (no coordinated omission).
+// Outputs are read in submission order; a model never has more unread
+// requests than its request ring has slots, so no result is overwritten
+// before it is read (the engine's own back-pressure covers unfinished ones).
 BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models, int n_jobs,
-                         int max_inflight, const std::function<std::pair<int64_t, int>(int)>& next_arrival,
-                         double* latency_us, int* worker_ids, int* model_index, double* wall_s) {
+                         int max_inflight, bool open_loop,
+                         const std::function<std::pair<int64_t, int>(int)>& next_arrival, double* latency_us,
+                         int* worker_ids, int* model_index, double* wall_s) {
   if (!engine || !models || n_models <= 0 || n_jobs < 0 || max_inflight <= 0) return kBandErr;
   band::Engine& e = *engine->impl;
   // per model: one input tensor (copied into the request ring at submit)
@@ -421,9 +430,12 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   struct Pending {
     int index, model;
     band::JobId id;
+    int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
   };
   std::deque<Pending> pending;
   int inflight = 0;
+  std::vector<int> unread(n_models, 0), ring(n_models, 0);
+  for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
   bool failed = false;
   const int64_t t0 = band::time::NowMicros();
   std::thread waiter([&] {
@@ -437,10 +449,12 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
       band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
       l.lock();
       if (!s.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) failed = true;
-      if (latency_us) latency_us[item.index] = static_cast<double>(j.end_time - j.enqueue_time);
+      if (latency_us)
+        latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
       if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
       if (model_index) model_index[item.index] = item.model;
       --inflight;
+      --unread[item.model];
       cv.notify_all();
     }
   });
@@ -448,15 +462,16 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     const auto arrival = next_arrival(j);
     const int64_t now = band::time::NowMicros() - t0;
     if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
+    const int m = arrival.second;
     {
       std::unique_lock<std::mutex> l(mu);
-      cv.wait(l, [&] { return inflight < max_inflight; });
+      cv.wait(l, [&] { return inflight < max_inflight && unread[m] < ring[m]; });
       ++inflight;
+      ++unread[m];
     }
-    const int m = arrival.second;
     auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
     std::lock_guard<std::mutex> l(mu);
-    pending.push_back({j, m, id.ok() ? id.value() : -1});
+    pending.push_back({j, m, id.ok() ? id.value() : -1, t0 + arrival.first});
     cv.notify_all();
   }
   waiter.join();
@@ -469,7 +484,7 @@ BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, Band
                                     int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
                                     double* wall_s) {
   return DriveRequests(
-      engine, models, inputs, n_models, n_jobs, max_inflight,
+      engine, models, inputs, n_models, n_jobs, max_inflight, false,
       [&](int j) { return std::make_pair(int64_t(0), j % std::max(n_models, 1)); }, latency_us, worker_ids,
       nullptr, wall_s);
 }
@@ -483,7 +498,7 @@ BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTen
   std::uniform_int_distribution<int> pick(0, std::max(n_models, 1) - 1);
   double t = 0;
   return DriveRequests(
-      engine, models, inputs, n_models, n_jobs, max_inflight,
+      engine, models, inputs, n_models, n_jobs, max_inflight, true,
       [&](int) {
         t += gap(rng) * 1e6;
         return std::make_pair(static_cast<int64_t>(t), pick(rng));

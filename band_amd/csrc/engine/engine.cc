@@ -260,7 +260,8 @@ absl::StatusOr<JobId> Engine::RequestAsync(ModelId model_id, RequestOption optio
   return ids.value()[0];
 }
 
-// band/engine.cc:455-529
+// band/engine.cc:455-529.  Every request is validated before any ring slot
+// is taken, so a refused call leaves no slot held.
 absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> model_ids,
                                                         std::vector<RequestOption> options,
                                                         std::vector<Tensors> inputs) {
@@ -287,20 +288,33 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
                                    std::to_string(options[i].target_worker) + ")");
       job.target_worker_id = options[i].target_worker;
     }
-    if (i < inputs.size()) {
-      auto in_it = model_input_buffer_.find(model_ids[i]);
-      auto out_it = model_output_buffer_.find(model_ids[i]);
-      if (in_it == model_input_buffer_.end() || out_it == model_output_buffer_.end())
-        return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
-      const int handle = in_it->second->Alloc();
-      if (!in_it->second->PutTensorsToHandle(inputs[i], handle).ok())
-        return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
-      job.input_handle = handle;
-      job.output_handle = out_it->second->Alloc();
-    }
+    if (i < inputs.size() && (!model_input_buffer_.count(model_ids[i]) || !model_output_buffer_.count(model_ids[i])))
+      return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
     jobs.push_back(std::move(job));
   }
+  for (size_t i = 0; i < jobs.size() && i < inputs.size(); ++i) {
+    TensorRingBuffer* in_ring = model_input_buffer_.at(model_ids[i]).get();
+    // blocks while the model has a full ring of unfinished requests
+    const int handle = in_ring->AllocBlocking();
+    if (!in_ring->PutTensorsToHandle(inputs[i], handle).ok()) {
+      for (size_t k = 0; k <= i; ++k) model_input_buffer_.at(model_ids[k])->Release();
+      return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
+    }
+    jobs[i].input_handle = handle;
+    jobs[i].output_handle = model_output_buffer_.at(model_ids[i])->Alloc();
+  }
   return EnqueueBatch(std::move(jobs));
+}
+
+void Engine::ReleaseRequest(const Job& job) {
+  if (job.input_handle < 0) return;
+  auto it = model_input_buffer_.find(job.model_id);
+  if (it != model_input_buffer_.end()) it->second->Release();
+}
+
+int Engine::RequestRingSize(ModelId model_id) const {
+  auto it = model_input_buffer_.find(model_id);
+  return it == model_input_buffer_.end() ? 0 : it->second->size();
 }
 
 absl::Status Engine::Wait(JobId job_id, Tensors outputs) {

@@ -119,6 +119,9 @@ class Engine : public IEngine {
   }
   void PrepareReenqueue(Job& job) override { planner_->PrepareReenqueue(job); }
   void EnqueueFinishedJob(Job& job) override { planner_->EnqueueFinishedJob(job); }
+  void ReleaseRequest(const Job& job) override;
+  // request-ring slots per model: the most unfinished requests it can have
+  int RequestRingSize(ModelId model_id) const;
   bool EnqueueToWorker(const ScheduleAction& action) override { return planner_->EnqueueToWorker({action}); }
   bool EnqueueToWorkerBatch(const std::vector<ScheduleAction>& actions) override {
     return planner_->EnqueueToWorker(actions);

@@ -80,6 +80,8 @@ class IEngine {
   virtual std::vector<JobId> EnqueueBatch(std::vector<Job> jobs, bool push_front = false) = 0;
   virtual void PrepareReenqueue(Job& job) = 0;
   virtual void EnqueueFinishedJob(Job& job) = 0;
+  // a finished request frees its request-ring slot (ring back-pressure)
+  virtual void ReleaseRequest(const Job& job) {}
   virtual bool EnqueueToWorker(const ScheduleAction& action) = 0;
   virtual bool EnqueueToWorkerBatch(const std::vector<ScheduleAction>& actions) = 0;
 };

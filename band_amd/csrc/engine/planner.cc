@@ -141,6 +141,7 @@ void Planner::EnqueueFinishedJob(Job& job) {
     const absl::Status s = job.status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
     for (auto& cb : on_end_request_callbacks_) cb.second(job.job_id, s);
   }
+  if (finished) engine_.ReleaseRequest(job);
 }
 
 void Planner::PrepareReenqueue(Job& job) {
@@ -224,6 +225,7 @@ void Planner::CopyToLocalQueues() {
 // (the reference notifies immediately and spins the planner thread).
 bool Planner::EnqueueToWorker(const std::vector<ScheduleAction>& actions) {
   bool ok = true;
+  std::vector<Job> rejected;  // back to the queue head in their original order
   for (const auto& action : actions) {
     Job job = action.first;
     const SubgraphKey& key = action.second;
@@ -245,10 +247,14 @@ bool Planner::EnqueueToWorker(const std::vector<ScheduleAction>& actions) {
         worker->EnqueueJob(job);
       } else {
         lock.unlock();
-        std::lock_guard<std::mutex> rl(requests_mtx_);
-        requests_.push_front(std::move(job));
+        rejected.push_back(std::move(job));
       }
     }
+  }
+  if (!rejected.empty()) {
+    std::lock_guard<std::mutex> rl(requests_mtx_);
+    requests_.insert(requests_.begin(), std::make_move_iterator(rejected.begin()),
+                     std::make_move_iterator(rejected.end()));
   }
   return ok;
 }

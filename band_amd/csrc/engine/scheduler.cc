@@ -66,18 +66,20 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
     Job job = std::move(*it);
     it = requests.erase(it);
     const SubgraphKey key = engine_.GetLargestSubgraphKey(job.model_id, w);
-    ok &= engine_.EnqueueToWorker({job, key});
     // job batching (extension): the idle worker also takes the next queued
-    // requests of the same model, up to its batch, and runs them in one pass
+    // requests of the same model, up to its batch, and runs them in one pass;
+    // one EnqueueToWorkerBatch call keeps their FIFO order if it is refused
+    std::vector<ScheduleAction> actions{{std::move(job), key}};
     for (int more = engine_.MaxJobBatch(key) - 1; more > 0 && it != requests.end();) {
       if (it->model_id == key.GetModelId()) {
-        ok &= engine_.EnqueueToWorker({*it, key});
+        actions.emplace_back(std::move(*it), key);
         it = requests.erase(it);
         --more;
       } else {
         ++it;
       }
     }
+    ok &= engine_.EnqueueToWorkerBatch(actions);
     next_ = w + 1;
   }
   return ok;

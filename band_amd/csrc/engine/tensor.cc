@@ -95,6 +95,26 @@ int TensorRingBuffer::Alloc() {
   return head_++;
 }
 
+int TensorRingBuffer::AllocBlocking() {
+  std::unique_lock<std::mutex> lock(head_mtx_);
+  slot_cv_.wait(lock, [this] { return outstanding_ < size_; });
+  ++outstanding_;
+  return head_++;
+}
+
+void TensorRingBuffer::Release() {
+  {
+    std::lock_guard<std::mutex> lock(head_mtx_);
+    if (outstanding_ > 0) --outstanding_;
+  }
+  slot_cv_.notify_one();
+}
+
+int TensorRingBuffer::Outstanding() const {
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  return outstanding_;
+}
+
 bool TensorRingBuffer::IsHandleValid(int handle) const {
   std::lock_guard<std::mutex> lock(head_mtx_);
   return handle >= 0 && head_ - size_ <= handle && handle < head_;

@@ -3,6 +3,7 @@
 // buffers and of the C API's BandTensor.  Affine quantization parameters are
 // deep-copied in the TfLiteAffineQuantization layout the views hand out.
 #pragma once
+#include <condition_variable>
 #include <memory>
 #include <mutex>
 #include <map>
@@ -47,11 +48,23 @@ class Tensor : public interface::ITensor {
 // Only the handle bookkeeping is under the lock - the memcpy of a slot runs
 // outside it, so copies of different requests of one model proceed in
 // parallel (the reference copies under the ring's mutex).
+//
+// Back-pressure (deviation): the reference's Alloc never waits, so a model
+// with more than `size` unfinished requests reuses the slot of a request
+// that has not run yet and that job later fails its input or output copy.
+// AllocBlocking() waits until fewer than `size` requests taken with it are
+// unfinished; Release() is called once per such request when its job is
+// finished (Planner::EnqueueFinishedJob, after the end-request callbacks).
 class TensorRingBuffer {
  public:
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
                    int size = 128);
   int Alloc();
+  // Alloc() once fewer than size() AllocBlocking()-ed requests are unfinished
+  int AllocBlocking();
+  void Release();
+  int size() const { return size_; }
+  int Outstanding() const;
   bool IsTensorIndexValid(int tensor_index) const { return tensor_to_buffer_.count(tensor_index) != 0; }
   bool IsHandleValid(int handle) const;
   int GetTensorsLength() const { return static_cast<int>(num_tensors_); }
@@ -67,7 +80,9 @@ class TensorRingBuffer {
   std::vector<std::vector<std::unique_ptr<Tensor>>> slots_;
   std::map<int, int> tensor_to_buffer_;
   mutable std::mutex head_mtx_;
+  std::condition_variable slot_cv_;
   int head_ = 0;
+  int outstanding_ = 0;
 };
 
 }  // namespace band

@@ -100,6 +100,8 @@ void Worker::Work() {
       std::vector<Job> partners;
       lock.lock();
       TakeBatchPartners(*job, max_batch - 1, &partners);
+      partners_expected_us_ = 0;
+      for (const Job& p : partners) partners_expected_us_ += engine_->GetExpected(p.subgraph_key);
       lock.unlock();
       if (!partners.empty()) {
         WorkBatch(job, partners);
@@ -183,6 +185,7 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   engine_->EnqueueFinishedJob(*head);
   {
     std::lock_guard<std::mutex> lock(device_mtx_);
+    partners_expected_us_ = 0;
     EndEnqueue();
   }
   engine_->Trigger();
@@ -221,7 +224,7 @@ bool DeviceQueueWorker::EnqueueJob(Job& job) {
 int64_t DeviceQueueWorker::GetWaitingTime() {
   std::lock_guard<std::mutex> lock(device_mtx_);
   if (!IsAvailable()) return kLargeWaitingTime;
-  int64_t total = 0;
+  int64_t total = partners_expected_us_;
   for (auto it = requests_.begin(); it != requests_.end(); ++it) {
     const int64_t expected = engine_->GetExpected(it->subgraph_key);
     total += expected;

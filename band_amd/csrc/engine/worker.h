@@ -73,6 +73,11 @@ class Worker {
   CpuSet cpu_set_;
   int num_threads_ = -1;
   int availability_check_interval_ms_ = 30000;
+  // expected latency of the batch partners of the running pass (device_mtx_):
+  // they left the queue but the worker has not finished them, so
+  // GetWaitingTime keeps counting them (at their one-job latency, an upper
+  // bound of their share of the batched pass)
+  int64_t partners_expected_us_ = 0;
 
  private:
   std::thread thread_;

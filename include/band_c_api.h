@@ -215,6 +215,8 @@ BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
  * over the n_models models (model j % n_models), with at most max_inflight
  * outstanding, and waits for all of them.  Inputs are the engine-created
  * tensors of each model (caller fills them first, or NULL for zeros).
+ * A model never has more outstanding requests than its request ring holds
+ * (128), so no result is overwritten before it is read.
  * latency_us[j] = end - enqueue of job j (band/common.h:351-353);
  * worker_ids[j] = worker that ran its last subgraph (may be NULL);
  * *wall_s = submission of the first job to completion of the last. */
@@ -225,8 +227,10 @@ BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandMod
 /* Open-loop Poisson driver (BASELINE config C5): n_jobs arrivals with
  * exponential inter-arrival times at rate_per_s (all models together, seeded
  * std::mt19937_64), each arrival a model drawn uniformly; arrivals beyond
- * max_inflight outstanding wait for a completion (the request rings hold
- * 128 requests per model).  Outputs as BandxEngineRunClosedLoop. */
+ * max_inflight outstanding wait for a completion, and so do arrivals of a
+ * model with a full request ring (128 requests).  latency_us[j] = end - the
+ * SCHEDULED arrival of job j, so submission delays count as queueing (no
+ * coordinated omission).  Other outputs as BandxEngineRunClosedLoop. */
 BAND_CAPI_EXPORT BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTensor** inputs,
                                                   int n_models, int n_jobs, double rate_per_s, uint64_t seed,
                                                   int max_inflight, double* latency_us, int* worker_ids,

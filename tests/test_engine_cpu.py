@@ -226,3 +226,76 @@ def test_c1_mobilenet_v1_int8_cpu_worker_fixed(tmp_path):
     om = OModel(buf)
     ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]]
     np.testing.assert_array_equal(o.data().reshape(-1), ref.reshape(-1))
+
+
+def _slow_cpu_model(tmp_path):
+    """a whole MobileNetV2 at 96x96 on one CPU thread: a few ms per job, so a
+    fast submitter builds a backlog of several hundred requests"""
+    from band_amd import tflite_synth as S
+    buf = S.mobilenet_v2(np.int8, size=96)
+    p = str(tmp_path / "mnv2_96.tflite")
+    open(p, "wb").write(buf)
+    return p, buf
+
+
+def test_request_ring_back_pressure(tmp_path):
+    """More than the 128-slot request ring in flight: RequestAsync waits for
+    a slot instead of letting a later request overwrite an unfinished one
+    (band/tensor_ring_buffer.cc:58-106 has no such wait); every job succeeds
+    and the newest results stay readable"""
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    path, buf = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], num_threads=[1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    om = OModel(buf)
+    rng = np.random.default_rng(9)
+    xs = [rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8) for _ in range(4)]
+    t = e.CreateInputTensor(m, 0)
+    hs = []
+    for j in range(300):
+        t.data()[...] = xs[j % 4]
+        hs.append(e.RequestAsync(m, [t]))
+    assert all(h >= 0 for h in hs)
+    e.WaitAll()
+    recs = [e.GetJobRecord(h) for h in hs]
+    assert all(r is not None and r.status == JobStatus.kSuccess for r in recs), \
+        [JobStatus(r.status).name for r in recs if r is not None and r.status != JobStatus.kSuccess][:4]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]].reshape(-1) for x in xs]
+    o = e.CreateOutputTensor(m, 0)
+    for j in range(300 - 100, 300):  # the last 100 results are still in the ring
+        assert e.Wait(hs[j], [o]) == kBandOk
+        np.testing.assert_array_equal(o.data().reshape(-1), refs[j % 4])
+    e.close()
+
+
+def test_closed_loop_beyond_ring_capacity(tmp_path):
+    """the native driver with 600 requests allowed in flight on one model (the
+    bench no longer caps it at the ring size): no failed job"""
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU, DeviceFlag.kCPU], num_threads=[1, 1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    lat, wid, wall = e.RunClosedLoop([m], 400, 600)
+    assert len(lat) == 400 and (lat > 0).all() and set(wid) == {0, 1}
+    e.close()
+
+
+def test_poisson_latency_counts_submission_delay(golden_dir):
+    """open loop: latency runs from each request's scheduled arrival, so an
+    arrival held back by the in-flight bound still shows its wait (no
+    coordinated omission).  With max_inflight 1 and arrivals far faster than
+    the worker, late jobs wait for every job before them."""
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU]))
+    m = Model()
+    assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+    assert e.RegisterModel(m)
+    lat, _, _, wall = e.RunPoisson([m], 200, 1e6, seed=3, max_inflight=1)
+    # ~all 200 arrivals are due within the first ~0.2 ms, so the last job's
+    # latency is close to the whole run, not to one job's service time
+    assert lat[-1] > 0.5 * wall * 1e6
+    assert np.median(lat[100:]) > 10 * np.median(lat[:5])
+    e.close()

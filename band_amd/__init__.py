@@ -6,7 +6,7 @@ IBackendUtil, behind the C ABIs in include/).  This package is the Python
 mirror of that interface (ctypes), used by tests and bench.py.
 """
 from .backend import (DataType, DeviceFlag, GetAvailableDevices, HipModel, HipModelExecutor,  # noqa: F401
-                      HipTensorView, ModelSpec, RunMixedJobs, SetWorkerDevice, Status, SubgraphKey)
+                      HipTensorView, ModelSpec, RunMixedJobs, SetWorkerDevice, Status, SubgraphKey, WorkerDevice)
 
 __all__ = ["DataType", "DeviceFlag", "GetAvailableDevices", "HipModel", "HipModelExecutor",
-           "HipTensorView", "ModelSpec", "RunMixedJobs", "SetWorkerDevice", "Status", "SubgraphKey"]
+           "HipTensorView", "ModelSpec", "RunMixedJobs", "SetWorkerDevice", "Status", "SubgraphKey", "WorkerDevice"]

@@ -35,6 +35,7 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_last_error": (ctypes.c_char_p, []),
     "bhx_available_devices": (c_int, [ctypes.POINTER(ctypes.c_uint32)]),
     "bhx_set_worker_device": (c_int, [c_int, c_int]),
+    "bhx_worker_device": (c_int, [c_int]),
     "bhx_model_create": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "bhx_model_from_path": (c_int, [c_void_p, ctypes.c_char_p]),
     "bhx_model_from_buffer": (c_int, [c_void_p, ctypes.c_char_p, c_size_t]),
@@ -64,7 +65,8 @@ _abi.BACKEND_SYMBOLS.update({
                                     ctypes.POINTER(ctypes.c_double)]),
     "bhx_executor_set_graph": (c_int, [c_void_p, c_int]),
     "bhx_executor_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
-    "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int)]),
+    "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int),
+                                            ctypes.POINTER(ctypes.c_double)]),
     "bhx_time_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(ctypes.c_double)]),
     "bhx_prepare_job_batches": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_uint64, c_int]),
     "bhx_max_job_batch": (c_int, _KEY + [ctypes.POINTER(c_int)]),
@@ -218,6 +220,11 @@ def GetAvailableDevices():
 
 def SetWorkerDevice(worker_id, ordinal):
     _abi.load().bhx_set_worker_device(int(worker_id), int(ordinal))
+
+
+def WorkerDevice(worker_id):
+    """the GPU ordinal worker `worker_id`'s executors use (DeviceRegistry)"""
+    return int(_abi.load().bhx_worker_device(int(worker_id)))
 
 
 class HipModel:
@@ -432,14 +439,18 @@ class HipModelExecutor:
         _abi.check(self.lib.bhx_executor_device(self.handle, ctypes.byref(o)), "device")
         return o.value
 
-    def ProfileSubgraph(self, key, iters=10):
+    def ProfileSubgraph(self, key, iters=10, with_floor=False):
+        """per-launch event timing in program order (ms each); with_floor:
+        also the per-launch floor (us) an empty launch chain measures"""
         n = c_int(0)
         cap = 4096
         arr = (OpTiming * cap)()
-        _abi.check(self.lib.bhx_profile_subgraph(self.handle, *key._args(), int(iters), arr, cap, ctypes.byref(n)),
-                   "ProfileSubgraph")
-        return [dict(op_index=arr[i].op_index, kernel=arr[i].kernel.decode(), ms=arr[i].ms,
+        floor = ctypes.c_double(0)
+        _abi.check(self.lib.bhx_profile_subgraph(self.handle, *key._args(), int(iters), arr, cap, ctypes.byref(n),
+                                                 ctypes.byref(floor)), "ProfileSubgraph")
+        rows = [dict(op_index=arr[i].op_index, kernel=arr[i].kernel.decode(), ms=arr[i].ms,
                      alg_bytes=arr[i].alg_bytes, alg_ops=arr[i].alg_ops) for i in range(min(n.value, cap))]
+        return (rows, floor.value) if with_floor else rows
 
     def TimeSubgraph(self, key, iters=100):
         """device microseconds per subgraph pass, passes issued back to back"""

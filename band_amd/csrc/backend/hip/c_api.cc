@@ -72,6 +72,8 @@ int bhx_set_worker_device(int worker_id, int ordinal) {
   return 0;
 }
 
+int bhx_worker_device(int worker_id) { return band::hip::DeviceRegistry::Get().OrdinalForWorker(worker_id); }
+
 int bhx_model_create(int model_id, bhx_model** out) {
   if (!out) return Fail("null out");
   auto* m = BackendFactory::CreateModel(BackendType::kTfLite, model_id);
@@ -336,11 +338,11 @@ int bhx_executor_device(bhx_executor* e, int* ordinal) {
 }
 
 int bhx_profile_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int iters, bhx_op_timing* out, int cap,
-                         int* n) {
+                         int* n, double* floor_us) {
   auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;
   if (!h) return Fail("not a HIP executor");
   std::vector<band::hip::OpTiming> t;
-  auto s = h->ProfileSubgraph(Key(mid, wid, mask), iters, &t);
+  auto s = h->ProfileSubgraph(Key(mid, wid, mask), iters, &t, floor_us);
   if (!s.ok()) return Fail(s);
   if (n) *n = static_cast<int>(t.size());
   for (int i = 0; i < cap && i < static_cast<int>(t.size()); ++i)

@@ -95,11 +95,13 @@ int DeviceRegistry::OrdinalForWorker(int worker_id) {
 bh_stream_t DeviceRegistry::StreamForWorker(int worker_id) {
   const int ord = OrdinalForWorker(worker_id);
   std::lock_guard<std::mutex> l(mu_);
-  auto it = streams_.find(worker_id);
+  // keyed by (worker, ordinal): a later engine may map the same worker id
+  // to another device (bench.py's single-engine line after the per-GPU ones)
+  auto it = streams_.find({worker_id, ord});
   if (it != streams_.end()) return it->second;
   bh_stream_t s = nullptr;
   if (bh_set_device(ord) != 0 || bh_stream_create(&s) != 0) return nullptr;
-  streams_[worker_id] = s;
+  streams_[{worker_id, ord}] = s;
   return s;
 }
 

@@ -87,7 +87,7 @@ class DeviceRegistry {
   bool gfx950_ = false;
   std::map<int, int> worker_ordinal_;
   int next_auto_ = 0;
-  std::map<int, bh_stream_t> streams_;
+  std::map<std::pair<int, int>, bh_stream_t> streams_;  // (worker id, ordinal)
   std::map<std::pair<int, std::string>, std::weak_ptr<DeviceBlob>> consts_;
 };
 

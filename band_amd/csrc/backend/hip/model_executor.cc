@@ -2107,7 +2107,8 @@ absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, d
   return status;
 }
 
-absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out) {
+absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out,
+                                              double* floor_us) {
   PreparedSubgraph* sg = Find(key);
   if (!sg) return absl::InternalError("Cannot find subgraph");
   if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("profiling needs a GPU executor");
@@ -2117,24 +2118,31 @@ absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters
   for (auto& e : ev)
     if (bh_event_create(&e) != 0) return HipErr(1, "event create");
   std::vector<double> acc(n, 0.0);
+  double floor_acc = 0.0;
   absl::Status status = absl::OkStatus();
-  // every launch repeated kRepeat times back to back between its events:
-  // the per-launch figure is then the kernel's duration plus only a share
-  // of the dependent-dispatch gap, close to what rocprofv3 reports
-  constexpr int kRepeat = 8;
+  // The launches run once each, in program order, with an event between
+  // consecutive ones: every kernel then sees the cache state of a real pass
+  // (its input just written by its producer).  The same chain of EMPTY
+  // launches is timed alongside; its per-launch figure (dispatch + gap +
+  // event) is the floor a caller subtracts to compare with rocprofv3's
+  // kernel-only durations.
   for (int it = 0; it < iters && status.ok(); ++it) {
-    // head start (see TimeLaunches): per-launch events then time execution
-    if (bh_spin_us(stream_, 300 + 40 * kRepeat * static_cast<int>(n)) != 0) status = HipErr(1, "spin");
-    bh_event_record(ev[0], stream_);
-    for (size_t i = 0; i < n && status.ok(); ++i) {
-      for (int r = 0; r < kRepeat && status.ok(); ++r) status = EnqueueLaunch(sg->launches[i]);
-      bh_event_record(ev[i + 1], stream_);
-    }
-    if (bh_stream_sync(stream_) != 0) status = HipErr(1, "sync");
-    for (size_t i = 0; i < n && status.ok(); ++i) {
-      float ms = 0;
-      bh_event_elapsed_ms(ev[i], ev[i + 1], &ms);
-      acc[i] += ms / kRepeat;
+    for (int pass = 0; pass < 2 && status.ok(); ++pass) {
+      // head start (see TimeLaunches): per-launch events then time execution
+      if (bh_spin_us(stream_, 300 + 40 * static_cast<int>(n)) != 0) status = HipErr(1, "spin");
+      bh_event_record(ev[0], stream_);
+      for (size_t i = 0; i < n && status.ok(); ++i) {
+        if (pass == 0) status = EnqueueLaunch(sg->launches[i]);
+        else if (bh_empty_launch(stream_) != 0) status = HipErr(1, "empty launch");
+        bh_event_record(ev[i + 1], stream_);
+      }
+      if (bh_stream_sync(stream_) != 0) status = HipErr(1, "sync");
+      for (size_t i = 0; i < n && status.ok(); ++i) {
+        float ms = 0;
+        bh_event_elapsed_ms(ev[i], ev[i + 1], &ms);
+        if (pass == 0) acc[i] += ms;
+        else floor_acc += ms * 1e3 / n;
+      }
     }
   }
   for (auto e : ev) bh_event_destroy(e);
@@ -2144,6 +2152,7 @@ absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters
     const Launch& l = sg->launches[i];
     out->push_back({l.op_index, l.kernel, acc[i] / std::max(iters, 1), l.alg_bytes, l.alg_ops});
   }
+  if (floor_us) *floor_us = floor_acc / std::max(iters, 1);
   return absl::OkStatus();
 }
 

@@ -136,8 +136,11 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   // --- extensions used by the C ABI / bench (not part of Band's interface) ---
   void SetUseGraph(bool on) { use_graph_ = on; }
   // Times every launch of `key` with HIP events on the executor's stream
-  // (eager enqueue, averaged over `iters`).
-  absl::Status ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out);
+  // (eager enqueue in program order, averaged over `iters`); *floor_us = the
+  // per-launch time of an equal chain of empty launches (event + dispatch
+  // + gap), what an event figure holds beyond the kernel itself.
+  absl::Status ProfileSubgraph(const SubgraphKey& key, int iters, std::vector<OpTiming>* out,
+                               double* floor_us = nullptr);
   // Device time of one subgraph pass (us) with `iters` passes issued back to
   // back (replayed hipGraph when captured, else the launch sequence): no host
   // gaps, H2D/D2H included.  The latency floor of ExecuteSubgraph's device side.

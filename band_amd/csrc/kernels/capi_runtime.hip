@@ -133,3 +133,13 @@ extern "C" int bh_spin_us(bh_stream_t s, int us) {
   hipLaunchKernelGGL(bh_spin_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, (unsigned long long)us * 100ull);
   return bh_check_launch("bh_spin_kernel");
 }
+
+__global__ void bh_empty_kernel(int) {}
+
+// One empty single-wave launch: profilers time chains of these exactly like
+// a real launch sequence to learn what an event pair measures beyond a
+// kernel's own duration (dispatch + inter-kernel gap).
+extern "C" int bh_empty_launch(bh_stream_t s) {
+  hipLaunchKernelGGL(bh_empty_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, 0);
+  return bh_check_launch("bh_empty_kernel");
+}

@@ -6,15 +6,21 @@ Workload (default, N=1): BASELINE config C3 - the 4-DNN int8 mix
 224x224, synthetic seeded weights with TFLite-converter-shaped quantisation)
 served by the native Band engine (band_amd/csrc/engine) with round_robin over
 `--workers-per-gpu` Band GPU workers of one MI355X (AddWorkers({kGPU, ...})).
-`--model mobilenet_v2_int8` etc. run single-model configs (C2).
+`--model mobilenet_v2_int8` etc. run single-model configs (C2); C4 / C5 have
+their own models (`efficientdet_lite2_int8`, `mix_c5`).
 
-A "step" is one Band job, end to end through the harness: RequestAsync
-(user tensor -> request ring, band/engine.cc:455-529) -> planner thread ->
+A job is one Band request end to end through the harness: RequestAsync (user
+tensor -> request ring, band/engine.cc:455-529) -> planner thread ->
 scheduler -> worker queue (band/planner.cc:268-365) -> Worker::Work: input
 copy into the executor's view, IModelExecutor::ExecuteSubgraph on the GPU,
 output copy (band/worker.cc:222-323) -> Wait.  A native closed-loop driver
-(BandxEngineRunClosedLoop) keeps 2 x workers x job-batch requests in
-flight.  Job latency = end - enqueue of the planner's job record
+(BandxEngineRunClosedLoop) keeps 2 x workers x job-batch requests in flight;
+the engine's request rings apply back-pressure beyond 128 per model.
+
+A STEP is one round of `--jobs-per-step` jobs (default 1024, 256 of each mix
+model): `--steps K --warmup W` times exactly K x 1024 jobs after W x 1024
+warm-up jobs, so the driver's `--steps 20 --warmup 5` times 20,480 jobs in
+steady state.  Job latency = end - enqueue of the planner's job record
 (band/common.h:351-353).
 
 Job batching (--job-batch B, default 24; BANDX_WORKER_MAX_JOB_BATCH): an
@@ -23,16 +29,31 @@ and runs them as ONE pass over a batch-B variant of the model's subgraph
 (every job still gets its own input copy, its own outputs, its own job
 record).  Band itself runs one job per ExecuteSubgraph; that configuration
 (8 GPU workers, no batching) is measured in the same run and reported as
-"band_one_job_per_pass".  --job-batch 1 makes it the headline instead.
+"band_one_job_per_pass".
 
-N>1: one process per GPU (torchrun), each with its own engine over its GPU;
-jobs shard across GPUs with no data-path collective (weak scaling); a gloo
-process group only provides the barrier and the max-over-ranks timing.  The
-GPU is driven exclusively through libband_hip.so; torch never touches it.
+N>1 (torchrun, one process per GPU): each rank serves its own job stream
+with its own engine over its GPU; jobs shard across GPUs with no data-path
+collective (weak scaling); a gloo group only provides the barrier and the
+max-over-ranks timing.  After that line is measured, rank 0 alone runs ONE
+Band engine whose GPU workers span all N GPUs (worker w -> GPU w % N,
+round_robin, Band's single planner thread) and reports it as
+"single_engine" beside the per-process value (the other ranks have closed
+their engines and wait at the barrier).  `--single-engine` makes that the
+headline.  The GPU is driven exclusively through libband_hip.so.
 
-Prints ONE JSON line on rank 0.
+Roofline: every launch of the profiled passes (the same models at the job
+batch) is timed with HIP events in program order (HipModelExecutor::
+ProfileSubgraph); an equal chain of empty launches gives the per-launch
+floor (dispatch + gap) that is subtracted for a kernel-only duration, the
+quantity rocprofv3 reports.  The dominant kernel (largest total time) and
+the next two are reported with their algorithmic bytes and ops per launch.
+
+Prints ONE JSON line on rank 0.  `--profile-only` runs just the profiled
+passes (for rocprofv3 kernel traces / PMC passes of exactly those launches).
 """
 import argparse
+import glob
+import hashlib
 import json
 import os
 import platform
@@ -41,12 +62,15 @@ import time
 
 import numpy as np
 
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20000, help="jobs per rank in the timed region")
-    p.add_argument("--warmup", type=int, default=2000)
+    p.add_argument("--steps", type=int, default=20, help="timed steps (one step = --jobs-per-step jobs)")
+    p.add_argument("--warmup", type=int, default=5, help="untimed warm-up steps")
+    p.add_argument("--jobs-per-step", type=int, default=1024)
     p.add_argument("--workers-per-gpu", type=int, default=8)
     p.add_argument("--hw-queues", type=int, default=4,
                    help="GPU_MAX_HW_QUEUES for this process (HIP default 4; <= 32)")
@@ -61,12 +85,12 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-baseline-seconds", type=float, default=12.0)
+    p.add_argument("--cpu-baseline-seconds", type=float, default=8.0, help="per CPU-baseline mode")
     p.add_argument("--profile-iters", type=int, default=20)
     p.add_argument("--scheduler", default="round_robin",
                    choices=["round_robin", "fixed_worker", "shortest_expected_latency",
                             "heterogeneous_earliest_finish_time"])
-    p.add_argument("--inflight", type=int, default=0, help="outstanding requests (default 2 x workers)")
+    p.add_argument("--inflight", type=int, default=0, help="outstanding requests (default 2 x workers x job batch)")
     p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                    help="cpu: --workers-per-gpu Band CPU workers instead of GPU workers (C1 / CPU tests; no roofline)")
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
@@ -75,6 +99,11 @@ def parse():
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
+    p.add_argument("--single-engine", action="store_true",
+                   help="headline = one process, one Band engine, GPU workers over all --gpus GPUs")
+    p.add_argument("--no-single-engine", action="store_true", help="N>1: skip the single-engine line")
+    p.add_argument("--profile-only", action="store_true",
+                   help="run only the profiled batch passes (rocprofv3 traces); prints their per-kernel table")
     return p.parse_args()
 
 
@@ -108,6 +137,16 @@ def model_list(name, size=0, batch=1):
                 ("ssd_mobilenet_v2_fp16", S.ssd_mobilenet_v2(np.float16, size=sz))]
     base = name[:-len("_int8")]
     return [(name, getattr(S, base)(np.int8, size=sz, batch=b))]
+
+
+def write_models(models, prefix):
+    paths = []
+    for name, buf in models:
+        tmp = tempfile.NamedTemporaryFile(prefix="%s_%s_" % (prefix, name), suffix=".tflite", delete=False)
+        tmp.write(buf)
+        tmp.close()
+        paths.append(tmp.name)
+    return paths
 
 
 class Dist:
@@ -147,30 +186,239 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def cpu_baseline(models, seconds, edge=224):
-    """Oracle (scalar C port of TFLite's reference kernels) on the host, the
-    same round-robin request stream over the models."""
+def host_cores():
+    """host cores this process may use: its affinity set, capped by the
+    per-job CPU share the box grants (OMP_NUM_THREADS, 16 on the GPU box)"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        cap = int(os.environ.get("OMP_NUM_THREADS", "0"))
+    except ValueError:
+        cap = 0
+    return min(n, cap) if cap > 0 else n
+
+
+def host_info():
+    """nproc / lscpu facts of the host, read from /proc (no subprocess)"""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+    try:
+        with open("/proc/cpuinfo") as f:
+            txt = f.read()
+        models = [l.split(":", 1)[1].strip() for l in txt.splitlines() if l.startswith("model name")]
+        phys = {(l1, l2) for l1, l2 in zip([l for l in txt.splitlines() if l.startswith("physical id")],
+                                           [l for l in txt.splitlines() if l.startswith("core id")])}
+        info["cpu_model"] = models[0] if models else platform.processor()
+        info["physical_cores_total"] = len(phys) or None
+    except OSError:
+        pass
+    return info
+
+
+def cpu_baseline(args, models, paths, seconds):
+    """The product's own kCPU path (the same lowered program and integer
+    arithmetic on the host, backend/hip/cpu_kernels.cc) through the same Band
+    harness, as BASELINE.md section 2 prescribes: (i) one CPU worker with
+    every core as its thread pool, (ii) one single-threaded CPU worker per
+    core; round_robin over the same models and request stream, each mode run
+    for about `seconds`.  Plus the scalar oracle port on one core (test
+    infrastructure, kept as a reference point)."""
+    from band_amd import DeviceFlag
+    from band_amd.engine import Engine, Model, SchedulerType, make_config
+    T = host_cores()
+    M = len(models)
+    modes = []
+    for label, n_workers, threads in (("1 CPU worker x %d threads" % T, 1, T),
+                                      ("%d CPU workers x 1 thread" % T, T, 1)):
+        prof = os.path.join(tempfile.gettempdir(), "band_bench_cpu_profile_%d.json" % os.getpid())
+        e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU] * n_workers,
+                               num_threads=[threads] * n_workers, online=False, profile_path=prof))
+        ms, ins = [], []
+        rng = np.random.default_rng(5489)
+        for path in paths:
+            m = Model()
+            assert m.FromPath(path), path
+            assert e.RegisterModel(m), path
+            t = e.CreateInputTensor(m, 0)
+            arr = t.data()
+            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
+            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
+            ms.append(m)
+            ins.append(t)
+        inflight = 2 * n_workers
+        n0 = max(M, 2 * n_workers) // M * M
+        _, _, w0 = e.RunClosedLoop(ms, n0, inflight, ins)  # warm + calibrate
+        n = max(n0, int(seconds * n0 / max(w0, 1e-6)) // M * M)
+        lat, _, wall = e.RunClosedLoop(ms, n, inflight, ins)
+        modes.append(dict(mode=label, workers=n_workers, threads_per_worker=threads, value=n / wall, jobs=n,
+                          seconds=wall, p99_job_latency_ms=float(np.percentile(lat * 1e-3, 99))))
+        e.close()
+    best = max(modes, key=lambda m: m["value"])
+    # scalar oracle port (test infrastructure) on one core, a short sample
     from oracle.runner import OracleInterpreter
-    from oracle.tflite_fb import Model
+    from oracle.tflite_fb import Model as OModel
     rng = np.random.default_rng(5489)
     runs = []
     for _, buf in models:
-        m = Model(buf)
-        t_in = m.tensors[m.inputs[0]]
+        om = OModel(buf)
+        t_in = om.tensors[om.inputs[0]]
         lo, hi = (-127, 128) if t_in.np_dtype == np.int8 else (0, 255)
-        x = rng.integers(lo, hi, t_in.shape).astype(t_in.np_dtype)
-        interp = OracleInterpreter(m)
-        interp.run({m.inputs[0]: x})  # warm
-        runs.append((interp, {m.inputs[0]: x}))
+        runs.append((OracleInterpreter(om), {om.inputs[0]: rng.integers(lo, hi, t_in.shape).astype(t_in.np_dtype)}))
     n, t0 = 0, time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
+    while time.perf_counter() - t0 < min(3.0, seconds) or n < len(runs):
         interp, feed = runs[n % len(runs)]
         interp.run(feed)
         n += 1
-    dt = time.perf_counter() - t0
+    oracle = dict(value=n / (time.perf_counter() - t0), cores=1, jobs=n)
     names = "+".join(name for name, _ in models)
-    return dict(value=n / dt, unit="inferences/s", cores=1, kind="port",
-                sample="%d round-robin jobs of %s (%dx%d) on 1 host core, %.1f s" % (n, names, edge, edge, dt))
+    return dict(value=best["value"], unit="inferences/s", cores=T, kind="port",
+                sample="Band engine kCPU workers (the product's host kernels), round_robin over %s 224x224 int8; "
+                       "best of BASELINE.md modes (i) 1 worker x %d threads and (ii) %d workers x 1 thread, ~%.0f s "
+                       "each; best: %s" % (names, T, T, seconds, best["mode"]),
+                modes=modes, oracle_scalar_port_1core=oracle, host=host_info())
+
+
+def kernel_source_tag():
+    """hash of the kernel sources: PMC traffic figures are only reported for
+    the tree they were measured on"""
+    h = hashlib.sha1()
+    for f in sorted(glob.glob(os.path.join(ROOT, "band_amd", "csrc", "kernels", "*"))) + \
+            [os.path.join(ROOT, "include", "band_hip_kernels.h")]:
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:12]
+
+
+def profiled_batch(args):
+    return args.job_batch if args.job_batch > 1 and args.model not in ("efficientdet_lite2_int8", "mix_c5") else 1
+
+
+def profile_executors(args, D, models, paths):
+    """profiling executors (outside the engine, same backend code) over the
+    passes the workers run: with job batching, the same models with a
+    leading batch of B"""
+    import band_amd
+    from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
+    B = profiled_batch(args)
+    tmp = []
+    if B > 1:
+        paths = tmp = write_models(model_list(args.model, args.size, batch=B), "band_prof")
+    prof_wid = 1000
+    band_amd.SetWorkerDevice(prof_wid, D.local_rank)
+    execs = []
+    for mid, path in enumerate(paths):
+        hm = HipModel(100 + mid)
+        assert hm.FromPath(path).ok()
+        ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
+        if args.no_graph:
+            ex.SetUseGraph(False)
+        spec = ex.InvestigateModelSpec(hm)
+        gpu_ops = [i for i in range(spec.num_ops) if i not in spec.unsupported_ops[DeviceFlag.kGPU]]
+        # a split model: profile its GPU part (ops before the first CPU-only op)
+        assert ex.PrepareSubgraph(hm, gpu_ops if len(gpu_ops) < spec.num_ops else ()).ok()
+        ex._model_ref = hm
+        execs.append((ex, SubgraphKey(100 + mid, prof_wid)))
+    for path in tmp:
+        os.unlink(path)
+    return execs, B
+
+
+def profile_roofline(args, D, models, paths):
+    """per-launch roofline of the dominant kernels + device time per model
+    (GPU runs only)"""
+    execs, B = profile_executors(args, D, models, paths)
+    M = len(models)
+    by_k, floors = {}, []
+    for ex, key in execs:
+        rows, floor_us = ex.ProfileSubgraph(key, iters=args.profile_iters, with_floor=True)
+        floors.append(floor_us)
+        for r in rows:
+            # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
+            # with its residual epilogue), as rocprofv3 reports them
+            k = by_k.setdefault(r["kernel"].split("+")[0], dict(us=0.0, event_us=0.0, bytes=0.0, ops=0.0,
+                                                                launches=0))
+            k["event_us"] += r["ms"] * 1e3
+            k["us"] += max(r["ms"] * 1e3 - floor_us, 0.0)
+            k["bytes"] += r["alg_bytes"]
+            k["ops"] += r["alg_ops"]
+            k["launches"] += 1
+    # device-side floor of one job: each model's passes replayed back to back
+    # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
+    # host launch + sync wakeup
+    device_us = {name: ex.TimeSubgraph(key, iters=100) / B for (name, _), (ex, key) in zip(models, execs)}
+    total_us = sum(k["us"] for k in by_k.values())
+    ranked = sorted(by_k.items(), key=lambda kv: -kv[1]["us"])
+    # HBM traffic per launch from the committed rocprofv3 PMC passes
+    # (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, the gfx950
+    # corrections of MI355X_MICROARCH.md), only when measured on this
+    # kernel source tree and at this pass batch
+    tag = kernel_source_tag()
+    pmc = {}
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json"))):
+        with open(f) as fh:
+            tj = json.load(fh)
+        meta = tj.get("_meta", {})
+        if meta.get("kernel_source_tag") == tag and meta.get("pass_batch") == B:
+            pmc = dict(tj, _file=os.path.basename(f))
+
+    def roof(name, k):
+        us = k["us"] / k["launches"]
+        b = k["bytes"] / k["launches"]
+        o = k["ops"] / k["launches"]
+        gbs = b / (us * 1e-6) / 1e9
+        t = pmc.get(name, {}).get("traffic_bytes_per_launch")
+        return {"kernel": name, "bound": "hbm", "achieved": gbs, "peak": 8000.0, "unit": "GB/s", "frac": gbs / 8000.0,
+                "traffic": t, "traffic_over_algorithmic": (t / b) if t else None,
+                "traffic_source": pmc.get("_file") if t else
+                "null: no PMC file measured on this kernel tree (tag %s) at pass batch %d" % (tag, B),
+                "alg_bytes_per_launch": b, "alg_ops_per_launch": o, "avg_launch_us": us,
+                "avg_launch_us_event": k["event_us"] / k["launches"],
+                "launches_per_pass": k["launches"] / M, "share_of_kernel_time": k["us"] / total_us,
+                "mfma_i8_tops": o / (us * 1e-6) / 1e12, "mfma_i8_frac": o / (us * 1e-6) / 5.0e15}
+
+    top = [roof(n, k) for n, k in ranked[:3]]
+    dom = dict(top[0])
+    dom.update(profiled_pass_batch=B, launch_floor_us=float(np.mean(floors)), kernel_source_tag=tag,
+               next_kernels=top[1:])
+    return dom, dict(gpu_us_per_inference=total_us / M / B, device_us=device_us), execs
+
+
+def profile_only(args, D, models, paths):
+    """only the profiled passes (graph replays of the batch-B variants),
+    for rocprofv3: its per-kernel averages then describe exactly the launches
+    the roofline line reports"""
+    execs, B = profile_executors(args, D, models, paths)
+    for ex, key in execs:
+        ex.TimeSubgraph(key, iters=max(10, args.profile_iters))
+    dom, dev, _ = profile_roofline(args, D, models, paths)
+    print(json.dumps({"profile_only": True, "pass_batch": B, "roofline": dom, "device": dev}), flush=True)
+
+
+def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch, seed_offset=0):
+    """a Band engine with the models registered and one synthetic request
+    tensor per model"""
+    from band_amd.engine import Engine, Model, make_config
+    on_gpu = args.device == "gpu"
+    engine = Engine(make_config([sched], workers,
+                                num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
+                                num_warmups=3, num_runs=5,
+                                max_job_batch=job_batch if job_batch > 1 else None))
+    band_models, inputs = [], []
+    rng = np.random.default_rng(5489 + seed_offset)
+    for path in paths:
+        m = Model()
+        assert m.FromPath(path), path
+        assert engine.RegisterModel(m), path
+        band_models.append(m)
+        # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
+        t = engine.CreateInputTensor(m, 0)
+        arr = t.data()
+        if arr.dtype == np.float32:  # f32 U(-0.5, 0.5) (band/tool/benchmark.cc:279-287)
+            arr[...] = rng.uniform(-0.5, 0.5, arr.shape).astype(np.float32)
+        else:
+            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
+            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
+        inputs.append(t)
+    return engine, band_models, inputs
 
 
 def workload_label(args, models, n_cpu, W, poisson):
@@ -197,106 +445,46 @@ def workload_label(args, models, n_cpu, W, poisson):
             % (args.model, edge, edge, args.scheduler, W))
 
 
-def profile_roofline(args, D, models, paths):
-    """per-launch roofline of the dominant kernel + device time per model
-    (GPU runs only)"""
+def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
+    """warm-up, barrier, exactly n_timed jobs, barrier; max over ranks"""
+    engine.RunClosedLoop(band_models, n_warm, inflight, inputs)
+    D.barrier()
+    t0 = time.perf_counter()
+    lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
+    t1 = time.perf_counter()
+    D.barrier()
+    return D.max(t1 - t0), lat_us, worker_ids
+
+
+def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
+    """ONE Band engine over n_gpus GPUs in this process: W GPU workers per GPU,
+    worker w on GPU w % n_gpus (so round_robin's rotation alternates GPUs),
+    one planner thread (band/engine.cc:681-713, band/planner.cc:268-293)"""
     import band_amd
-    from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
-    M = len(models)
-    # with job batching the workers run batch-B passes: profile those (the
-    # same models with a leading batch of B), per-inference figures / B
-    B = args.job_batch if args.job_batch > 1 and args.model not in ("efficientdet_lite2_int8", "mix_c5") else 1
-    if B > 1:
-        paths = []
-        for name, buf in model_list(args.model, args.size, batch=B):
-            tmp = tempfile.NamedTemporaryFile(prefix="band_prof_%s_" % name, suffix=".tflite", delete=False)
-            tmp.write(buf)
-            tmp.close()
-            paths.append(tmp.name)
-    # profiling executors (outside the engine, same backend code) for the
-    # per-kernel roofline and the device-side floor of a job
-    prof_wid = 1000
-    band_amd.SetWorkerDevice(prof_wid, D.local_rank)
-    execs0, keys0 = [], []
-    for mid, path in enumerate(paths):
-        hm = HipModel(100 + mid)
-        assert hm.FromPath(path).ok()
-        ex = HipModelExecutor(100 + mid, prof_wid, DeviceFlag.kGPU)
-        if args.no_graph:
-            ex.SetUseGraph(False)
-        spec = ex.InvestigateModelSpec(hm)
-        gpu_ops = [i for i in range(spec.num_ops) if i not in spec.unsupported_ops[DeviceFlag.kGPU]]
-        # a split model: profile its GPU part (ops before the first CPU-only op)
-        assert ex.PrepareSubgraph(hm, gpu_ops if len(gpu_ops) < spec.num_ops else ()).ok()
-        execs0.append(ex)
-        keys0.append(SubgraphKey(100 + mid, prof_wid))
-        ex._model_ref = hm
+    from band_amd import DeviceFlag
+    n_workers = W * n_gpus
+    for w in range(n_workers):
+        band_amd.SetWorkerDevice(w, w % n_gpus)
 
-    # roofline of the dominant kernel: per-launch HIP events on the worker's
-    # stream, over one inference of each model (the mix is uniform)
-    by_k = {}
-    for ex, key in zip(execs0, keys0):
-        for r in ex.ProfileSubgraph(key, iters=args.profile_iters):
-            # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
-            # with its residual epilogue), as rocprofv3 reports them
-            k = by_k.setdefault(r["kernel"].split("+")[0], dict(ms=0.0, bytes=0.0, ops=0.0, launches=0))
-            k["ms"] += r["ms"] / M
-            k["bytes"] += r["alg_bytes"] / M
-            k["ops"] += r["alg_ops"] / M
-            k["launches"] += 1.0 / M
-    dom_name = max(by_k, key=lambda k: by_k[k]["ms"])
-    dom = by_k[dom_name]
-    # HBM traffic of the dominant kernel from the committed rocprofv3 PMC
-    # passes (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950
-    # corrections of MI355X_MICROARCH.md), per launch; null when absent
-    traffic, traffic_src = None, None
-    import glob
-    pmc = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic.json")))
-    if pmc:
-        with open(pmc[-1]) as f:
-            tj = json.load(f)
-        if dom_name in tj:
-            traffic, traffic_src = tj[dom_name]["traffic_bytes_per_launch"], os.path.basename(pmc[-1])
-    # device-side floor of one job: each model's passes replayed back to back
-    # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
-    # host launch + sync wakeup
-    device_us = {name: ex.TimeSubgraph(key, iters=100) / B for (name, _), ex, key in zip(models, execs0, keys0)}
-    if B > 1:
-        for path in paths:
-            os.unlink(path)
-    # per inference: kernel time of a batch-B pass / B
-    for k in by_k.values():
-        for f in ("ms", "bytes", "ops", "launches"):
-            k[f] /= B
-    return dom_name, dom, by_k, traffic, traffic_src, device_us, B
+    class Local:  # no barrier partners: this process alone drives the GPUs
+        def barrier(self):
+            pass
 
+        def max(self, v):
+            return v
 
-def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch):
-    """this rank's Band engine with the models registered and one synthetic
-    request tensor per model"""
-    from band_amd.engine import Engine, Model, make_config
-    on_gpu = args.device == "gpu"
-    engine = Engine(make_config([sched], workers,
-                                num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
-                                num_warmups=3, num_runs=5,
-                                max_job_batch=job_batch if job_batch > 1 else None))
-    band_models, inputs = [], []
-    rng = np.random.default_rng(5489 + D.rank)
-    for path in paths:
-        m = Model()
-        assert m.FromPath(path), path
-        assert engine.RegisterModel(m), path
-        band_models.append(m)
-        # synthetic requests: int8 U{-127..127} / uint8 U{0..254} (band/tool/benchmark.cc:279-287)
-        t = engine.CreateInputTensor(m, 0)
-        arr = t.data()
-        if arr.dtype == np.float32:  # f32 U(-0.5, 0.5) (band/tool/benchmark.cc:279-287)
-            arr[...] = rng.uniform(-0.5, 0.5, arr.shape).astype(np.float32)
-        else:
-            lo, hi = (-127, 128) if arr.dtype == np.int8 else (0, 255)
-            arr[...] = rng.integers(lo, hi, arr.shape).astype(arr.dtype)
-        inputs.append(t)
-    return engine, band_models, inputs
+    e, bm, ins = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * n_workers, 0, n_workers, args.job_batch)
+    inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
+    el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
+    e.close()
+    per_gpu = np.bincount(np.asarray(wid) % n_gpus, minlength=n_gpus).tolist()
+    for w in range(n_workers):  # back to the per-process mapping
+        band_amd.SetWorkerDevice(w, D.local_rank)
+    return {"value": n_timed / el, "unit": "inferences/s", "n_gpus": n_gpus, "jobs": n_timed,
+            "ms_per_step": el * 1e3 / max(1, n_timed // args.jobs_per_step),
+            "workers": n_workers, "worker_to_gpu": "w %% %d" % n_gpus, "jobs_per_gpu": per_gpu,
+            "p50_job_latency_ms": float(np.percentile(lat * 1e-3, 50)),
+            "p99_job_latency_ms": float(np.percentile(lat * 1e-3, 99))}
 
 
 def main():
@@ -305,26 +493,25 @@ def main():
     # running Band GPU worker stream (must be set before libband_hip loads)
     # (explicit assignment: the GPU box exports HIP's default of 4)
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
+    hinfo = host_info()  # before any GPU runtime is touched
     D = Dist()
     import band_amd
-    from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
-    from band_amd.engine import Engine, Model, SchedulerType, make_config
+    from band_amd import DeviceFlag
+    from band_amd.engine import SchedulerType
 
     models = model_list(args.model, args.size)
     M = len(models)
     W = max(1, args.workers_per_gpu)
-    paths = []
-    for name, buf in models:
-        tmp = tempfile.NamedTemporaryFile(prefix="band_bench_%s_" % name, suffix=".tflite", delete=False)
-        tmp.write(buf)
-        tmp.close()
-        paths.append(tmp.name)
+    paths = write_models(models, "band_bench")
     if args.no_graph:
         os.environ["BAND_HIP_GRAPH"] = "0"
+    if args.profile_only:
+        profile_only(args, D, models, paths)
+        for path in paths:
+            os.unlink(path)
+        D.close()
+        return
 
-    # this rank's Band engine: [CPU workers] + W GPU workers, all GPU
-    # workers on the local MI355X (worker id -> device ordinal; each worker
-    # owns one HIP stream)
     needs_cpu = args.model in ("efficientdet_lite2_int8", "mix_c5")
     n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if needs_cpu else 0)
     if args.model == "mix_c5" and args.scheduler == "round_robin":
@@ -345,91 +532,91 @@ def main():
     if not (on_gpu and n_cpu == 0 and args.scheduler == "round_robin"):
         args.job_batch = 1  # job batching applies to round_robin over GPU workers only
     batching = args.job_batch > 1
-    engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch)
-    # 2 x workers x job batch requests in flight, at most 120 per model: Band's
-    # per-model output ring buffers hold 128 slots (TensorRingBuffer), and a
-    # request whose slot was reused before its output was copied fails
-    inflight = args.inflight or min(2 * W * (args.job_batch if batching else 1), 120 * M)
+    jps = max(M, args.jobs_per_step // M * M)
+    args.jobs_per_step = jps
+    n_warm, n_timed = max(1, args.warmup) * jps, max(1, args.steps) * jps
+    # 2 x workers x job batch requests in flight (the engine's request rings
+    # hold back a model's 129th unfinished request)
+    inflight = args.inflight or 2 * W * (args.job_batch if batching else 1)
 
-    engine.RunClosedLoop(band_models, max(args.warmup, 2 * W * M), inflight, inputs)
     poisson = None
-    if args.model == "mix_c5":
-        # C5: open-loop Poisson arrivals at 0.8 x this engine's closed-loop capacity
-        # (or --rate), uniform over the 8 models
-        rate = args.rate
-        if rate <= 0:
-            _, _, cap_wall = engine.RunClosedLoop(band_models, max(args.steps // 4, 8 * M), inflight, inputs)
-            rate = 0.8 * max(args.steps // 4, 8 * M) / cap_wall
-        poisson = dict(rate_per_s_per_gpu=rate, seed=5489 + D.rank)
-    D.barrier()
-    t0 = time.perf_counter()
-    if poisson:
-        lat_us, worker_ids, model_idx, _ = engine.RunPoisson(band_models, args.steps, poisson["rate_per_s_per_gpu"],
-                                                            seed=poisson["seed"], max_inflight=max(64, inflight),
-                                                            inputs=inputs)
+    single = None
+    if args.single_engine:
+        # headline: one process, one engine over all --gpus GPUs
+        assert D.world == 1, "--single-engine runs in one process (no torchrun)"
+        single = single_engine_line(args, D, paths, sched, W, max(1, args.gpus), n_warm, n_timed)
+        elapsed, lat_us, worker_ids = n_timed / single["value"], None, []
+        jobs_per_worker = single["jobs_per_gpu"]
+        n_ranks = 1
     else:
-        lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, args.steps, inflight, inputs)
-    t1 = time.perf_counter()
-    D.barrier()
-    elapsed = D.max(t1 - t0)
-    all_lat = [x for part in D.gather((lat_us * 1e-6).tolist()) for x in part]
-    jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
-    engine.close()
+        engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch,
+                                                  seed_offset=D.rank)
+        if args.model == "mix_c5":
+            # C5: open-loop Poisson arrivals at 0.8 x this engine's closed-loop
+            # capacity (or --rate), uniform over the 8 models; latency from
+            # each request's scheduled arrival
+            engine.RunClosedLoop(band_models, n_warm, inflight, inputs)
+            rate = args.rate
+            if rate <= 0:
+                _, _, cap_wall = engine.RunClosedLoop(band_models, n_timed // 4, inflight, inputs)
+                rate = 0.8 * (n_timed // 4) / cap_wall
+            poisson = dict(rate_per_s_per_gpu=rate, seed=5489 + D.rank)
+            D.barrier()
+            t0 = time.perf_counter()
+            lat_us, worker_ids, _, _ = engine.RunPoisson(band_models, n_timed, rate, seed=poisson["seed"],
+                                                         max_inflight=1 << 20, inputs=inputs)
+            t1 = time.perf_counter()
+            D.barrier()
+            elapsed = D.max(t1 - t0)
+        else:
+            elapsed, lat_us, worker_ids = run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D)
+        jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
+        engine.close()
+        n_ranks = D.world
+    all_lat = [x for part in D.gather((lat_us * 1e-6).tolist() if lat_us is not None else []) for x in part]
 
     # Band's own semantics beside it: one job per ExecuteSubgraph (no job
     # batching), the same mix and scheduler over 8 GPU workers per GPU
     batch1 = None
-    # (only where job batching applies: round_robin over GPU workers alone)
-    if batching and not poisson and not args.no_batch1:
+    if batching and not poisson and not args.no_batch1 and not args.single_engine:
         W1 = 8
-        e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1)
-        n1 = max(args.steps // 2, 16 * M)
-        e1.RunClosedLoop(bm1, max(args.warmup // 2, 2 * W1 * M), 2 * W1, in1)
-        D.barrier()
-        t0 = time.perf_counter()
-        lat1, _, _ = e1.RunClosedLoop(bm1, n1, 2 * W1, in1)
-        t1 = time.perf_counter()
-        D.barrier()
-        el1 = D.max(t1 - t0)
+        e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1, seed_offset=D.rank)
+        n1 = max(n_timed // 4, 16 * M)
+        el1, lat1, _ = run_closed(e1, bm1, in1, max(n_warm // 4, 2 * W1 * M), n1, 2 * W1, D)
         l1 = np.array([x for part in D.gather((lat1 * 1e-3).tolist()) for x in part])
-        batch1 = {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "steps": n1,
+        batch1 = {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "jobs": n1,
                   "p50_job_latency_ms": float(np.percentile(l1, 50)),
                   "p99_job_latency_ms": float(np.percentile(l1, 99))}
         e1.close()
 
+    # N > 1: the same C3 workload through ONE engine spanning every GPU
+    if D.world > 1 and not args.no_single_engine and not poisson and on_gpu:
+        D.barrier()  # every rank has closed its engines
+        if D.rank == 0:
+            single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world)
+        D.barrier()
+
     roof, dev = None, None
-    if on_gpu:
-        dom_name, dom, by_k, traffic, traffic_src, device_us, prof_batch = profile_roofline(args, D, models, paths)
-        avg_ms = dom["ms"] / dom["launches"]
-        bytes_per_launch = dom["bytes"] / dom["launches"]
-        ops_per_launch = dom["ops"] / dom["launches"]
-        achieved_gbs = bytes_per_launch / (avg_ms * 1e-3) / 1e9
-        roof = {
-            "kernel": dom_name, "bound": "hbm", "achieved": achieved_gbs, "peak": 8000.0, "unit": "GB/s",
-            "frac": achieved_gbs / 8000.0, "traffic": traffic, "traffic_source": traffic_src,
-            "alg_bytes_per_launch": bytes_per_launch, "avg_launch_us": avg_ms * 1e3,
-            "launches_per_inference": dom["launches"],
-            "profiled_pass_batch": prof_batch,
-            "mfma_i8_tops": ops_per_launch / (avg_ms * 1e-3) / 1e12,
-            "mfma_i8_frac": ops_per_launch / (avg_ms * 1e-3) / 5.0e15,
-        }
-        dev = dict(gpu_ms_total=sum(v["ms"] for v in by_k.values()), device_us=device_us)
+    if on_gpu and D.rank == 0:
+        roof, dev, _ = profile_roofline(args, D, models, paths)
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(models, args.cpu_baseline_seconds, args.size or 224)
+        cpu = cpu_baseline(args, models, paths, args.cpu_baseline_seconds)
 
     if D.rank == 0:
-        n = D.world
-        total_jobs = args.steps * n
-        lat_ms = np.array(all_lat) * 1e3
+        total_jobs = n_timed * n_ranks
+        value = total_jobs / elapsed if not args.single_engine else single["value"]
+        lat_ms = np.array(all_lat) * 1e3 if all_lat else None
         line = {
             "metric": "multi-DNN inferences/sec + p99 job latency, 4-model int8 mix @1/2/4/8 GPU",
-            "value": total_jobs / elapsed,
+            "value": value,
             "unit": "inferences/s",
-            "n_gpus": n,
+            "n_gpus": n_ranks if not args.single_engine else max(1, args.gpus),
             "steps": args.steps,
             "warmup": args.warmup,
+            "jobs_per_step": jps,
+            "jobs_timed": total_jobs,
             "ms_per_step": elapsed * 1e3 / args.steps,
             "higher_is_better": True,
             "scaling": "weak",
@@ -440,22 +627,30 @@ def main():
             "config": {"workload": workload_label(args, models, n_cpu, W, poisson) + (
                            "; each GPU worker runs up to %d queued jobs of one model as one batched pass "
                            "(job batching)" % args.job_batch if args.job_batch > 1 else ""),
-                       "harness": "native Band engine (planner + workers + %s), %d requests in flight"
-                                  % (args.scheduler, inflight),
+                       "harness": ("ONE native Band engine over %d GPUs (single planner)" % max(1, args.gpus)
+                                   if args.single_engine else
+                                   "native Band engine per GPU (planner + workers + %s)" % args.scheduler) +
+                                  ", %d requests in flight per engine" % inflight,
+                       "step": "%d jobs (%d of each model), round-robin over the models" % (jps, jps // M),
                        "jobs_per_worker_rank0": jobs_per_worker,
                        "max_job_batch": args.job_batch,
-                       "model": args.model, "global_batch": n * W * max(1, args.job_batch), "seq_len": None,
-                       "parallelism": "job-sharded x%d (no collective)" % n, "hipgraph": not args.no_graph,
+                       "model": args.model, "global_batch": n_ranks * W * max(1, args.job_batch), "seq_len": None,
+                       "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus)) if args.single_engine
+                       else "job-sharded x%d (no collective)" % n_ranks,
+                       "hipgraph": not args.no_graph,
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
-            "p50_job_latency_ms": float(np.percentile(lat_ms, 50)),
-            "p99_job_latency_ms": float(np.percentile(lat_ms, 99)),
-            "gpu_kernel_ms_per_inference": dev["gpu_ms_total"] if dev else None,
+            "p50_job_latency_ms": float(np.percentile(lat_ms, 50)) if lat_ms is not None else
+            single["p50_job_latency_ms"],
+            "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
+            single["p99_job_latency_ms"],
+            "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
             "device_us_per_model": dev["device_us"] if dev else None,
             "band_one_job_per_pass": batch1,
+            "single_engine": single,
             "roofline": roof,
             "cpu_baseline": cpu,
-            "host": platform.node(),
+            "host": dict(hinfo, node=platform.node()),
         }
         print(json.dumps(line), flush=True)
     for path in paths:

@@ -58,6 +58,9 @@ const char* bhx_last_error(void);
 int bhx_available_devices(uint32_t* mask);
 /* pin a Band worker id to a GPU ordinal (one process per GPU launchers) */
 int bhx_set_worker_device(int worker_id, int ordinal);
+/* the ordinal a worker's executors use: its bhx_set_worker_device mapping,
+ * else assigned on first use in ascending order modulo the device count */
+int bhx_worker_device(int worker_id);
 
 /* IModel (BackendFactory::CreateModel + FromPath/FromBuffer/IsInitialized) */
 int bhx_model_create(int model_id, bhx_model** out);
@@ -108,11 +111,13 @@ int bhx_run_jobs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mas
 int bhx_executor_set_graph(bhx_executor* e, int enabled);
 int bhx_executor_device(bhx_executor* e, int* ordinal);
 /* per-launch HIP-event timing of a prepared subgraph: the launch sequence is
- * queued behind a spin kernel, each launch issued 8 times back to back
- * between its events (its duration plus a share of the dependent-dispatch
- * gap, comparable with rocprofv3's kernel durations); averaged over iters */
+ * queued behind a spin kernel and runs once in program order with an event
+ * between consecutive launches (each kernel sees a real pass's cache state);
+ * averaged over iters.  *floor_us (may be NULL) = per-launch time of the same
+ * chain of empty launches: subtract it from a launch's figure for a
+ * kernel-only duration comparable with rocprofv3's. */
 int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
-                         bhx_op_timing* out, int cap, int* n);
+                         bhx_op_timing* out, int cap, int* n, double* floor_us);
 /* A Band GPU worker serving a mixed request stream (BASELINE C3): worker
  * `wid` holds one prepared executor per model (as Band creates one executor
  * per (model, worker), band/engine.cc:91-106); job j runs model

@@ -91,6 +91,9 @@ int bh_event_elapsed_ms(bh_event_t start, bh_event_t end, float* ms);
 /* hold the stream for `us` microseconds (<= 100 ms): lets a profiler enqueue
  * a launch sequence before the GPU starts it, so events time execution */
 int bh_spin_us(bh_stream_t s, int us);
+/* one empty single-wave launch (profilers time chains of them to measure
+ * the dispatch + gap an event pair adds around a real launch) */
+int bh_empty_launch(bh_stream_t s);
 
 /* ---- op parameter blocks ------------------------------------------------ */
 

@@ -38,6 +38,7 @@ def lib():
         if not os.path.exists(path):
             build()
         L = ctypes.CDLL(path)
+        L.tfl_set_num_threads.argtypes = [ctypes.c_int]
         L.tfl_srdhm.restype = ctypes.c_int32
         L.tfl_srdhm.argtypes = [ctypes.c_int32, ctypes.c_int32]
         L.tfl_rdbypot.restype = ctypes.c_int32

@@ -42,6 +42,21 @@ static inline int imin(int a, int b) { return a < b ? a : b; }
 static inline int imax(int a, int b) { return a > b ? a : b; }
 
 /* gemmlowp::SaturatingRoundingDoublingHighMul (fixedpoint.h) */
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* threads of the conv / depthwise / fully-connected loops (test speed only;
+ * every output element is computed by one thread, so results never depend
+ * on it).  n <= 0 restores the OpenMP default. */
+void tfl_set_num_threads(int n) {
+#ifdef _OPENMP
+  omp_set_num_threads(n > 0 ? n : omp_get_num_procs());
+#else
+  (void)n;
+#endif
+}
+
 int32_t tfl_srdhm(int32_t a, int32_t b) {
   int overflow = (a == b) && (a == I32MIN);
   int64_t ab = (int64_t)a * (int64_t)b;
@@ -146,6 +161,8 @@ void tfl_conv2d(const uint8_t* in, int in_signed, int b, int ih, int iw, int ic,
                 int pad_h, int pad_w, int32_t in_off, int32_t w_off,
                 int32_t out_off, const int32_t* mult, const int32_t* shift,
                 int32_t amin, int32_t amax) {
+  /* output rows are independent: threads change the schedule, not a value */
+#pragma omp parallel for collapse(2) schedule(static)
   for (int n = 0; n < b; ++n)
     for (int oy = 0; oy < oh; ++oy)
       for (int ox = 0; ox < ow; ++ox) {
@@ -183,6 +200,7 @@ void tfl_dwconv2d(const uint8_t* in, int in_signed, int b, int ih, int iw, int i
                   int32_t out_off, const int32_t* mult, const int32_t* shift,
                   int32_t amin, int32_t amax) {
   const int oc = ic * dm;
+#pragma omp parallel for collapse(2) schedule(static)
   for (int n = 0; n < b; ++n)
     for (int oy = 0; oy < oh; ++oy)
       for (int ox = 0; ox < ow; ++ox)
@@ -215,6 +233,7 @@ void tfl_fully_connected(const uint8_t* in, int in_signed, int rows, int depth,
                          const int32_t* bias, uint8_t* out, int32_t in_off,
                          int32_t w_off, int32_t out_off, const int32_t* mult,
                          const int32_t* shift, int32_t amin, int32_t amax) {
+#pragma omp parallel for collapse(2) schedule(static)
   for (int r = 0; r < rows; ++r)
     for (int u = 0; u < units; ++u) {
       int32_t acc = 0;

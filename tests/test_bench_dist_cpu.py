@@ -39,15 +39,17 @@ def test_bench_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--gpus", "2", "--device", "cpu", "--model", "mix_c3", "--size", "64", "--workers-per-gpu", "1",
-           "--cpu-threads", "2", "--steps", str(steps), "--warmup", "4"]
+           "--cpu-threads", "2", "--steps", str(steps), "--warmup", "4", "--jobs-per-step", "4"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_line(r.stdout)
     assert line["n_gpus"] == 2 and line["steps"] == steps and line["scaling"] == "weak"
     # value = all ranks' jobs / max-over-ranks time; ms_per_step is that time / steps
     elapsed_s = line["ms_per_step"] * steps / 1e3
-    assert abs(line["value"] - 2 * steps / elapsed_s) < 1e-6 * line["value"]
-    assert sum(line["config"]["jobs_per_worker_rank0"]) == steps
+    # (a step = --jobs-per-step jobs: 4, one of each mix model)
+    assert line["jobs_per_step"] == 4 and line["jobs_timed"] == 2 * 4 * steps
+    assert abs(line["value"] - 2 * 4 * steps / elapsed_s) < 1e-6 * line["value"]
+    assert sum(line["config"]["jobs_per_worker_rank0"]) == 4 * steps
     assert line["p99_job_latency_ms"] >= line["p50_job_latency_ms"] > 0
     assert line["cpu_baseline"] is None  # rank 0 at N=1 only
     assert line["roofline"] is None  # no GPU kernels on CPU workers
@@ -58,7 +60,7 @@ def test_bench_c1_cpu_worker_line():
     """C1: MobileNetV1 int8 on one Band CPU worker, fixed_worker"""
     cmd = [sys.executable, "bench.py", "--device", "cpu", "--model", "mobilenet_v1_int8", "--size", "64",
            "--workers-per-gpu", "1", "--scheduler", "fixed_worker", "--cpu-threads", "2", "--steps", "8",
-           "--warmup", "2", "--cpu-baseline-seconds", "0.5"]
+           "--warmup", "2", "--cpu-baseline-seconds", "0.5", "--jobs-per-step", "1"]
     r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_line(r.stdout)
@@ -66,3 +68,6 @@ def test_bench_c1_cpu_worker_line():
     assert line["config"]["jobs_per_worker_rank0"] == [8]
     cb = line["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0
+    # both CPU modes through the Band harness, host facts recorded
+    assert [m["workers"] for m in cb["modes"]] == [1, 1] and cb["host"]["nproc"] >= 1
+    assert cb["oracle_scalar_port_1core"]["value"] > 0

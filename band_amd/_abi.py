@@ -31,7 +31,7 @@ class DwConvParams(ctypes.Structure):
         "k_h", "k_w", "stride_h", "stride_w", "dil_h", "dil_w", "pad_h", "pad_w", "in_xor")] + [
         (n, c_int32) for n in ("in_zp", "w_zp", "out_zp", "act_min", "act_max")] + [
         (n, c_void_p) for n in ("input", "output", "weights", "bias", "mult", "shift", "out_table", "taps")] + [
-        ("requant_fast", c_int32)]
+        ("requant_fast", c_int32), ("kernel_hint", c_int32)]
 
 
 class FcParams(ctypes.Structure):

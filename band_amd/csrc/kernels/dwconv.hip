@@ -340,6 +340,132 @@ __global__ __launch_bounds__(256) void dwconv3x3_run_kernel(bh_dwconv_params p, 
   }
 }
 
+// Depthwise 3x3 on the int8 matrix cores (depth multiplier 1, C % 16 == 0).
+// For one 16-channel group the depthwise layer is a GEMM whose K = taps x
+// channels and whose filter matrix is block diagonal: one
+// v_mfma_i32_16x16x64_i8 contracts 4 taps x 16 channels of 16 pixels, so
+// three of them (taps 0-3, 4-7, 8) produce a 16-pixel x 16-channel tile.  A
+// lane's pixel fragment is the 16 channel bytes of one tap: ONE 16-byte
+// load from NHWC, and no byte transposes (the dot4 forms spend 16
+// v_perm_b32 per pixel and channel quad on them).  Computed transposed
+// (D^T = W x X^T, as conv_xs_kernel) so a lane ends with 4 consecutive
+// channels of one pixel and stores them as one dword.  The filter fragments
+// are 15/16 zeros - the matrix cores do 16x the useful MACs - but at three
+// MFMAs per 256 outputs that is far below the epilogue's VALU work.
+//
+// Out-of-image taps read the input zero point; the zero-point terms fold
+// into the tap table's bias word (bh_pack_dw_taps, word 3) exactly as for
+// the dot4 kernels, and uint8 filters (w_zp != 0) take the per-pixel sum of
+// the nine taps from a second MFMA against a block-diagonal ones matrix:
+//   sum (x - zx)(w - zw) = sum x*w - zw * sum x + (bias word - bias).
+// A wave owns RB x 16 pixels of one channel group; channel groups are the
+// fastest-varying wave index, so a workgroup's waves share input lines.
+template <int RB, bool FAST, bool WZP>
+__global__ __launch_bounds__(256) void dwconv3x3_mfma_kernel(bh_dwconv_params p, int P, int nblocks, DwDivs dv) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  const int lane = threadIdx.x & 63;
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int wv = blk * 4 + (threadIdx.x >> 6);
+  const int pb = dv.groups.div(wv);  // pixel block
+  if (pb >= nblocks) return;
+  const int cg = wv - pb * (int)dv.groups.d;  // 16-channel group
+  const int C = p.out_c;
+  const int c0 = cg * 16;
+
+  // filter fragments of K-steps s = 0..2 (taps 4s..4s+3 x channels c0..+15):
+  // W^T row r16 holds w[tap][c0 + r16] in byte r16 and zeros elsewhere
+  v4i wf[3], of[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int tap = 4 * s + g;
+    const uint32_t wb = tap < 9 ? (uint32_t)(uint8_t)p.weights[tap * C + c0 + r16] : 0u;
+    const uint32_t w = wb << (8 * (r16 & 3));
+    const uint32_t o = (tap < 9 ? 1u : 0u) << (8 * (r16 & 3));
+    const int d = r16 >> 2;
+    wf[s] = (v4i){d == 0 ? (int)w : 0, d == 1 ? (int)w : 0, d == 2 ? (int)w : 0, d == 3 ? (int)w : 0};
+    of[s] = (v4i){d == 0 ? (int)o : 0, d == 1 ? (int)o : 0, d == 2 ? (int)o : 0, d == 3 ? (int)o : 0};
+  }
+  // this lane's tap of each K-step, as an offset from the window origin
+  int tdy[3], tdx[3];
+  bool tok[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int tap = 4 * s + g;
+    const int fy = (tap * 11) >> 5;  // tap / 3 for tap < 12
+    const int fx = tap - 3 * fy;
+    tdy[s] = fy * p.dil_h - p.pad_h;
+    tdx[s] = fx * p.dil_w - p.pad_w;
+    tok[s] = tap < 9;
+  }
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.input, (short)0, p.batch * p.in_h * p.in_w * C, 0x00020000);
+  const uint32_t xorw = splat_byte(p.in_xor);
+  const int zfill = (int)splat_byte(p.in_zp);
+
+  // every pixel fragment load of the wave issues before the first MFMA
+  v4i xf[RB][3];
+  int mpix[RB];
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    const int m = (pb * RB + b) * 16 + r16;
+    mpix[b] = m;
+    const bool valid = m < P;
+    const int mm = valid ? m : 0;
+    const int t = dv.out_w.div(mm);
+    const int ox = mm - t * p.out_w;
+    const int n = dv.out_h.div(t);
+    const int oy = t - n * p.out_h;
+    const int iy = oy * p.stride_h, ix = ox * p.stride_w, row0 = n * p.in_h;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int y = iy + tdy[s], x = ix + tdx[s];
+      const bool ok = valid && tok[s] && y >= 0 && y < p.in_h && x >= 0 && x < p.in_w;
+      const int off = ok ? ((row0 + y) * p.in_w + x) * C + c0 : 0;
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+      xf[b][s] = (v4i){ok ? (int)(v.x ^ xorw) : zfill, ok ? (int)(v.y ^ xorw) : zfill,
+                       ok ? (int)(v.z ^ xorw) : zfill, ok ? (int)(v.w ^ xorw) : zfill};
+    }
+  }
+  // epilogue operands of this lane's 4 output channels
+  const int co = c0 + 4 * g;
+  const v4i* tp = (const v4i*)p.taps;
+  const v4i mm4 = *(const v4i*)(p.mult + co);
+  const v4i ss4 = *(const v4i*)(p.shift + co);
+  int32_t be[4];
+  ChanQ q[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    be[r] = tp[co + r].w;
+    q[r] = chan_q(mm4[r], ss4[r], p.out_zp);
+  }
+  const uint8_t* otab = (const uint8_t*)p.out_table;
+  uint8_t* out = (uint8_t*)p.output;
+#pragma unroll
+  for (int b = 0; b < RB; ++b) {
+    v4i acc = (v4i){0, 0, 0, 0};
+    v4i sx = (v4i){0, 0, 0, 0};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[s], xf[b][s], acc, 0, 0, 0);
+      if constexpr (WZP) sx = __builtin_amdgcn_mfma_i32_16x16x64_i8(of[s], xf[b][s], sx, 0, 0, 0);
+    }
+    if (mpix[b] >= P) continue;
+    int32_t v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      int32_t a = acc[r] + be[r];
+      if constexpr (WZP) a -= p.w_zp * sx[r];
+      v[r] = requant_out<FAST>(a, q[r], p.out_zp, p.act_min, p.act_max);
+      if (otab) v[r] = otab[(uint8_t)v[r]];
+    }
+    const uint32_t lo = __builtin_amdgcn_perm((uint32_t)v[1], (uint32_t)v[0], 0x0c0c0400u);
+    const uint32_t hi = __builtin_amdgcn_perm((uint32_t)v[3], (uint32_t)v[2], 0x04000c0cu);
+    *(uint32_t*)(out + mpix[b] * C + co) = lo | hi;
+  }
+}
+
 // general filter size / depth multiplier: one output channel per thread
 __global__ __launch_bounds__(256) void dwconv_generic_kernel(bh_dwconv_params p, int total, DwDivs dv) {
   const int blk = dv.xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -404,6 +530,34 @@ static void launch_run(const bh_dwconv_params& p, hipStream_t s) {
   }
 }
 
+// pixel tile rows per wave: 4 (64 pixels) when that still gives >= 2048
+// waves, else 1
+static int mfma_rb(const bh_dwconv_params& p) {
+  const long P = (long)p.batch * p.out_h * p.out_w;
+  return ((P + 63) / 64) * (p.out_c / 16) >= 2048 ? 4 : 1;
+}
+
+template <int RB>
+static void launch_mfma(const bh_dwconv_params& p, hipStream_t s) {
+  const int P = p.batch * p.out_h * p.out_w;
+  const int nblocks = (P + RB * 16 - 1) / (RB * 16);
+  const int groups = p.out_c / 16;
+  const long waves = (long)nblocks * groups;
+  DwDivs dv = dw_divs(p, groups);
+  const dim3 grid((unsigned)((waves + 3) / 4));
+  if (p.w_zp != 0) {
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, true, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    else hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, false, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+  } else {
+    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, true, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    else hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, false, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+  }
+}
+
+// the MFMA kernel's shapes: tap table, 3x3 dm 1, C % 16 == 0, any stride /
+// dilation
+static bool mfma_ok(const bh_dwconv_params& p) { return p.taps && p.out_c % 16 == 0; }
+
 // the run kernel's shapes: tap table, dil 1, equal strides 1 / 2
 static bool run_ok(const bh_dwconv_params& p) {
   static const int off = [] {
@@ -434,12 +588,31 @@ static void launch3x3(const bh_dwconv_params& p, long pixels, hipStream_t s) {
 }  // namespace bh
 
 namespace {
-enum DwRoute { kRun1, kRun2, kRunD2, kDot16, kDot8, kDot4, kTap16, kTap8, kTap4, kGeneric };
+enum DwRoute { kRun1, kRun2, kRunD2, kDot16, kDot8, kDot4, kTap16, kTap8, kTap4, kGeneric, kMfma };
+
+// MFMA form from this many 16x16 output tiles (BH_DW_MFMA_MIN_TILES
+// overrides; A-B timing); below it the per-pixel / run forms
+long MfmaMinTiles() {
+  static const long v = [] {
+    const char* e = std::getenv("BH_DW_MFMA_MIN_TILES");
+    return e ? std::atol(e) : 4096L;
+  }();
+  return v;
+}
 
 DwRoute dw_route(const bh_dwconv_params& p) {
   const long pixels = (long)p.batch * p.out_h * p.out_w;
   const bool fast = p.depth_multiplier == 1 && p.k_h == 3 && p.k_w == 3 && p.out_c % 4 == 0;
   if (!fast) return kGeneric;
+  // forced forms (when the shape allows them)
+  if (p.kernel_hint == BH_DW_MFMA && bh::mfma_ok(p)) return kMfma;
+  if (p.kernel_hint == BH_DW_RUN && bh::run_ok(p))
+    return p.dil_h == 2 ? kRunD2 : (p.stride_h == 1 ? kRun1 : kRun2);
+  if (p.kernel_hint == BH_DW_DOT && p.taps) {
+    if (p.out_c % 16 == 0) return kDot16;
+    return p.out_c % 8 == 0 ? kDot8 : kDot4;
+  }
+  if (bh::mfma_ok(p) && (pixels + 15) / 16 * (p.out_c / 16) >= MfmaMinTiles()) return kMfma;
   // run kernel (4 channels x 4 pixels per thread) once the grid has >= ~40k
   // threads: measured 1.5-1.9x faster than the per-pixel kernels from there
   // (MobileNetV2 depthwise layers, batch 16 / 64); below it, at batch 1, the
@@ -458,6 +631,7 @@ extern "C" const char* bh_dwconv2d_i8_kernel(const bh_dwconv_params* p) {
   if (!p) return "";
   switch (dw_route(*p)) {
     case kRun1: case kRun2: case kRunD2: return "dwconv3x3_run_kernel";
+    case kMfma: return "dwconv3x3_mfma_kernel";
     case kDot16: case kDot8: case kDot4: return "dwconv3x3_dot_kernel";
     case kTap16: case kTap8: case kTap4: return "dwconv3x3_kernel";
     default: return "dwconv_generic_kernel";
@@ -485,6 +659,10 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
     return BH_EINVAL;
   }
   switch (dw_route(p)) {
+    case kMfma:
+      if (bh::mfma_rb(p) == 4) bh::launch_mfma<4>(p, s);
+      else bh::launch_mfma<1>(p, s);
+      break;
     case kRun1: bh::launch_run<4, 1, 1>(p, s); break;
     case kRun2: bh::launch_run<4, 2, 1>(p, s); break;
     case kRunD2: bh::launch_run<4, 1, 2>(p, s); break;

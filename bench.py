@@ -254,8 +254,9 @@ def cpu_baseline(args, models, paths, seconds):
         e.close()
     best = max(modes, key=lambda m: m["value"])
     # scalar oracle port (test infrastructure) on one core, a short sample
-    from oracle.runner import OracleInterpreter
+    from oracle.runner import OracleInterpreter, lib as oracle_lib
     from oracle.tflite_fb import Model as OModel
+    oracle_lib().tfl_set_num_threads(1)  # the scalar port on ONE core
     rng = np.random.default_rng(5489)
     runs = []
     for _, buf in models:
@@ -269,6 +270,7 @@ def cpu_baseline(args, models, paths, seconds):
         interp.run(feed)
         n += 1
     oracle = dict(value=n / (time.perf_counter() - t0), cores=1, jobs=n)
+    oracle_lib().tfl_set_num_threads(0)
     names = "+".join(name for name, _ in models)
     return dict(value=best["value"], unit="inferences/s", cores=T, kind="port",
                 sample="Band engine kCPU workers (the product's host kernels), round_robin over %s 224x224 int8; "

@@ -169,7 +169,14 @@ typedef struct bh_dwconv_params {
   const int32_t* taps;
   /* 1 when bh_conv_requant_fast_ok(mult, shift, out_c, 9, max|bias|) holds */
   int32_t requant_fast;
+  /* kernel choice: BH_DW_AUTO (by shape), or force one form where the
+   * shape allows it (parity tests cover every form; A-B timing) */
+  int32_t kernel_hint;
 } bh_dwconv_params;
+#define BH_DW_AUTO 0
+#define BH_DW_RUN 1   /* dwconv3x3_run_kernel: 4 pixels x 4 channels per thread */
+#define BH_DW_DOT 2   /* dwconv3x3_dot_kernel: one pixel per thread */
+#define BH_DW_MFMA 3  /* dwconv3x3_mfma_kernel: block-diagonal MFMA, C % 16 == 0 */
 
 /* FULLY_CONNECTED.  input [rows][depth] bytes, weights int8-domain
  * [units][depth_pad] (depth_pad multiple of 16, zero padded); bias_eff as

@@ -27,9 +27,10 @@ def xor_of(dtype):
 class ConvCase:
     def __init__(self, rng, b, ih, iw, ic, oc, kh, kw, stride=(1, 1), dil=(1, 1), same=True,
                  dtype=np.int8, per_channel=True, act=3, depthwise=False, dm=1, requant_fast=None,
-                 taps=True):
+                 taps=True, kernel_hint=0):
         self.dtype = dtype
         self.taps = taps
+        self.kernel_hint = kernel_hint  # depthwise: BH_DW_* (0 = the shape's own route)
         self.requant_fast = requant_fast
         self.depthwise = depthwise
         self.dm = dm
@@ -115,6 +116,7 @@ class ConvCase:
                                                s32.ctypes.data_as(ctypes.c_void_p), self.oc, 9,
                                                int(np.abs(self.bias.astype(np.int64)).max()))
             p.requant_fast = fast if self.requant_fast is None else int(self.requant_fast and fast)
+            p.kernel_hint = self.kernel_hint
             # tap table (dot4 kernel) for 3x3 / dm 1 / C % 4 == 0, as the
             # executor lowers it; taps=False keeps the per-tap kernel
             if self.taps and self.kh == 3 and self.kw == 3 and self.dm == 1 and self.oc % 4 == 0:

@@ -113,10 +113,31 @@ def test_dwconv_taps_vs_per_tap(gpu_lib, b, h, w, ch, stride, dil, dtype):
     rng = np.random.default_rng(3100 + b * h * w + ch + stride + dil)
     c = ConvCase(rng, b, h, w, ch, ch, 3, 3, stride=(stride, stride), dil=(dil, dil), depthwise=True, dtype=dtype)
     ref = c.oracle()
+    # every form the shape allows: its own route, then each forced one
+    # (BH_DW_RUN / _DOT / _MFMA; a form the shape cannot take falls back)
+    for hint in (0, 1, 2, 3):
+        c.kernel_hint = hint
+        for fast in (None, False):
+            c.requant_fast = fast
+            np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="hint %d requant_fast %s" % (hint, fast))
+    c.kernel_hint, c.taps = 0, False
+    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+
+
+# the MFMA form (block-diagonal filter fragments) on every MobileNetV2
+# depthwise layer at the headline's job batch, int8 and uint8 (w_zp != 0:
+# the ones-matrix row sums), plus pixel counts that are not a multiple of 16
+@pytest.mark.parametrize("h,ch,stride", [(112, 32, 1), (112, 96, 2), (56, 144, 1), (56, 144, 2), (28, 192, 1),
+                                         (28, 192, 2), (14, 384, 1), (14, 576, 1), (14, 576, 2), (7, 960, 1),
+                                         (13, 48, 1), (9, 16, 2)])
+@pytest.mark.parametrize("dtype", [np.int8, np.uint8])
+def test_dwconv_mfma_mnv2_layers(gpu_lib, h, ch, stride, dtype):
+    b = 24 if h >= 14 else 5
+    rng = np.random.default_rng(7700 + h * ch + stride + (dtype == np.uint8))
+    c = ConvCase(rng, b, h, h, ch, ch, 3, 3, stride=(stride, stride), depthwise=True, dtype=dtype, kernel_hint=3)
+    ref = c.oracle()
     np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
     c.requant_fast = False
-    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
-    c.taps = False
     np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
 
 

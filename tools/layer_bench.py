@@ -52,6 +52,7 @@ def main():
     ap.add_argument("--net", default="mnv2", choices=["mnv2", "mnv1"])
     ap.add_argument("--layer", type=int, default=-1, help="only this row of the MNV2 table (0-based)")
     ap.add_argument("--no-taps", action="store_true", help="depthwise: the per-tap kernel (no tap table)")
+    ap.add_argument("--dw-hint", type=int, default=0, help="depthwise kernel: 0 auto, 1 run, 2 dot, 3 mfma")
     a = ap.parse_args()
     from band_amd import _abi
     from tests.kernel_harness import ConvCase
@@ -71,7 +72,7 @@ def main():
             continue
         dw = kind == "dw"
         c = ConvCase(rng, a.batch, sp, sp, ci, co, k, k, stride=(st, st), depthwise=dw, dtype=dt,
-                     taps=not a.no_taps)
+                     taps=not a.no_taps, kernel_hint=a.dw_hint)
         keep = []
         p = c.params(lib, keep)
         fn = lib.bh_dwconv2d_i8 if dw else lib.bh_conv2d_i8

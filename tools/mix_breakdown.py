@@ -46,6 +46,11 @@ def main():
         dev_us = ex.TimeSubgraph(key, iters=50)
         prof, floor = ex.ProfileSubgraph(key, iters=a.iters, with_floor=True)
         floors.append(floor)
+        ex.SetUseGraph(False)
+        eager_us = ex.TimeSubgraph(key, iters=20)
+        ex.SetUseGraph(True)
+        ev_sum = sum(r["ms"] for r in prof) * 1e3
+        ko_sum = sum(max(r["ms"] * 1e3 - floor, 0.0) for r in prof)
         for r in prof:
             op = desc["ops"][r["op_index"]]
             ins = desc["tensors"][op["inputs"][0]]["shape"] if op["inputs"] else []
@@ -57,8 +62,9 @@ def main():
             us = max(r["ms"] * 1e3 - floor, 1e-3)
             rows.append(dict(model=name, op=r["op_index"], kernel=r["kernel"], ins=ins, outs=outs, extra=extra,
                              us=us, bytes=r["alg_bytes"], ops=r["alg_ops"]))
-        print("%-28s graph replay %.1f us per pass, %.2f us per inference; %d launches, floor %.2f us/launch" % (
-            name, dev_us, dev_us / a.batch, len(prof), floor), flush=True)
+        print("%-28s graph replay %.1f us per pass (%.2f per inference), eager %.1f; %d launches; event sum %.1f, "
+              "floor %.2f us/launch, kernel-only sum %.1f" % (name, dev_us, dev_us / a.batch, eager_us, len(prof),
+                                                             ev_sum, floor, ko_sum), flush=True)
         keep.append((m, ex))
     tot = sum(r["us"] for r in rows)
     print("\nsum of kernel-only launch times: %.1f us for one pass of every model (batch %d)" % (tot, a.batch))

@@ -161,6 +161,7 @@ KERNEL_SYMBOLS = {
     "bh_event_sync": (c_int, [c_void_p]),
     "bh_event_elapsed_ms": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "bh_spin_us": (c_int, [c_void_p, c_int]),
+    "bh_empty_launch": (c_int, [c_void_p]),
     "bh_pack_conv_weights": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_int32, c_int32, c_void_p, c_void_p]),
     "bh_conv_packed_geometry": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),

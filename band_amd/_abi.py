@@ -22,7 +22,8 @@ class ConvParams(ctypes.Structure):
         (n, c_void_p) for n in ("input", "output", "weights", "bias_eff", "mult", "shift", "residual")] + [
         (n, c_int32) for n in ("add_y_off", "add_r_off", "add_o_off", "add_left_shift", "add_y_mult",
                                "add_y_shift", "add_r_mult", "add_r_shift", "add_o_mult", "add_o_shift",
-                               "add_act_min", "add_act_max")] + [("out_table", c_void_p), ("requant_fast", c_int32)]
+                               "add_act_min", "add_act_max")] + [("out_table", c_void_p), ("requant_fast", c_int32),
+                                                                  ("kernel_hint", c_int32)]
 
 
 class DwConvParams(ctypes.Structure):
@@ -162,6 +163,7 @@ KERNEL_SYMBOLS = {
     "bh_event_elapsed_ms": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "bh_spin_us": (c_int, [c_void_p, c_int]),
     "bh_empty_launch": (c_int, [c_void_p]),
+    "bh_profile_events": (c_int, [c_void_p, c_void_p]),
     "bh_pack_conv_weights": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                                      c_int32, c_int32, c_void_p, c_void_p]),
     "bh_conv_packed_geometry": (c_int, [c_int, c_int, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),

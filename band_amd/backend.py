@@ -440,8 +440,9 @@ class HipModelExecutor:
         return o.value
 
     def ProfileSubgraph(self, key, iters=10, with_floor=False):
-        """per-launch event timing in program order (ms each); with_floor:
-        also the per-launch floor (us) an empty launch chain measures"""
+        """per-launch kernel durations in program order (ms each; dispatch
+        begin / end timestamps, as rocprofv3 reports them); with_floor: also
+        the duration (us) of an empty single-wave kernel"""
         n = c_int(0)
         cap = 4096
         arr = (OpTiming * cap)()

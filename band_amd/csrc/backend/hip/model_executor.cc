@@ -2087,15 +2087,27 @@ absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, d
   for (int i = 0; i < 2; ++i) RETURN_STATUS_IF(ExecuteSubgraph(key));
   bh_event_t e0 = nullptr, e1 = nullptr;
   if (bh_event_create(&e0) != 0 || bh_event_create(&e1) != 0) return HipErr(1, "event create");
+  // At most kDepth passes queued ahead of the GPU: the host waits for pass
+  // i - kDepth before issuing pass i, so the queue never drains (timing is
+  // unchanged) but the number of outstanding dispatches stays bounded.
+  // Unbounded, 100 queued batch-24 SSD passes (~7,700 kernel dispatches)
+  // crash rocprofv3's kernel-trace interception.
+  constexpr int kDepth = 4;
+  bh_event_t ring[kDepth] = {nullptr};
+  for (auto& e : ring)
+    if (bh_event_create(&e) != 0) return HipErr(1, "event create");
   absl::Status status = absl::OkStatus();
   bh_event_record(e0, stream_);
   for (int i = 0; i < iters && status.ok(); ++i) {
+    if (i >= kDepth && bh_event_sync(ring[i % kDepth]) != 0) status = HipErr(1, "event sync");
+    if (!status.ok()) break;
     if (use_graph_ && sg->graph) {
       const int rc = bh_graph_launch(sg->graph, stream_);
       if (rc) status = HipErr(rc, "graph launch");
     } else {
       status = Enqueue(sg);
     }
+    bh_event_record(ring[i % kDepth], stream_);
   }
   bh_event_record(e1, stream_);
   float ms = 0.f;
@@ -2103,6 +2115,7 @@ absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, d
   if (status.ok() && bh_event_elapsed_ms(e0, e1, &ms) != 0) status = HipErr(1, "elapsed");
   bh_event_destroy(e0);
   bh_event_destroy(e1);
+  for (auto e : ring) bh_event_destroy(e);
   if (status.ok()) *us = 1e3 * ms / iters;
   return status;
 }
@@ -2114,38 +2127,43 @@ absl::Status HipModelExecutor::ProfileSubgraph(const SubgraphKey& key, int iters
   if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("profiling needs a GPU executor");
   if (bh_set_device(ordinal_) != 0) return HipErr(1, "hipSetDevice");
   const size_t n = sg->launches.size();
-  std::vector<bh_event_t> ev(n + 1, nullptr);
-  for (auto& e : ev)
-    if (bh_event_create(&e) != 0) return HipErr(1, "event create");
+  std::vector<bh_event_t> st(n, nullptr), sp(n, nullptr);
+  for (size_t i = 0; i < n; ++i)
+    if (bh_event_create(&st[i]) != 0 || bh_event_create(&sp[i]) != 0) return HipErr(1, "event create");
   std::vector<double> acc(n, 0.0);
   double floor_acc = 0.0;
   absl::Status status = absl::OkStatus();
-  // The launches run once each, in program order, with an event between
-  // consecutive ones: every kernel then sees the cache state of a real pass
-  // (its input just written by its producer).  The same chain of EMPTY
-  // launches is timed alongside; its per-launch figure (dispatch + gap +
-  // event) is the floor a caller subtracts to compare with rocprofv3's
-  // kernel-only durations.
+  // The launches run once each, in program order, queued back to back behind
+  // a spin kernel (so the GPU runs them without host gaps, as in a replayed
+  // graph), each kernel carrying its own dispatch begin / end timestamps
+  // (bh_profile_events -> hipExtLaunchKernel): the kernel-only duration
+  // rocprofv3's kernel trace reports, every kernel seeing the cache state of
+  // a real pass (its input just written by its producer).  A launch that
+  // issues no kernel (a copy) is timed by plain events around it.  The
+  // second pass times empty single-wave kernels the same way: the fixed cost
+  // of a dispatch inside every duration (floor_us).
   for (int it = 0; it < iters && status.ok(); ++it) {
     for (int pass = 0; pass < 2 && status.ok(); ++pass) {
-      // head start (see TimeLaunches): per-launch events then time execution
       if (bh_spin_us(stream_, 300 + 40 * static_cast<int>(n)) != 0) status = HipErr(1, "spin");
-      bh_event_record(ev[0], stream_);
       for (size_t i = 0; i < n && status.ok(); ++i) {
+        bh_event_record(st[i], stream_);
+        bh_profile_events(st[i], sp[i]);
         if (pass == 0) status = EnqueueLaunch(sg->launches[i]);
         else if (bh_empty_launch(stream_) != 0) status = HipErr(1, "empty launch");
-        bh_event_record(ev[i + 1], stream_);
+        if (bh_profile_events(nullptr, nullptr) == 0) bh_event_record(sp[i], stream_);
       }
       if (bh_stream_sync(stream_) != 0) status = HipErr(1, "sync");
       for (size_t i = 0; i < n && status.ok(); ++i) {
         float ms = 0;
-        bh_event_elapsed_ms(ev[i], ev[i + 1], &ms);
+        bh_event_elapsed_ms(st[i], sp[i], &ms);
         if (pass == 0) acc[i] += ms;
         else floor_acc += ms * 1e3 / n;
       }
     }
   }
-  for (auto e : ev) bh_event_destroy(e);
+  bh_profile_events(nullptr, nullptr);
+  for (auto e : st) bh_event_destroy(e);
+  for (auto e : sp) bh_event_destroy(e);
   if (!status.ok()) return status;
   out->clear();
   for (size_t i = 0; i < n; ++i) {

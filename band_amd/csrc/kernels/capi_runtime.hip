@@ -9,6 +9,20 @@
 
 static thread_local char g_last_error[256] = "";
 
+namespace bh {
+thread_local ProfEvents g_prof;
+}
+
+// returns how many kernels the previous setting timed (so a caller can tell
+// a launch that issued no kernel, e.g. a plain copy, from a timed one)
+extern "C" int bh_profile_events(bh_event_t start, bh_event_t stop) {
+  const int n = bh::g_prof.launched;
+  bh::g_prof.start = (hipEvent_t)start;
+  bh::g_prof.stop = (hipEvent_t)stop;
+  bh::g_prof.launched = 0;
+  return n;
+}
+
 extern "C" void bh_set_last_error(const char* msg) {
   snprintf(g_last_error, sizeof(g_last_error), "%s", msg ? msg : "");
 }

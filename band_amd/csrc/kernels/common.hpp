@@ -7,12 +7,39 @@
 // (band/backend/tfl/model_executor.cc:249-255 -> Interpreter::Invoke).
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "band_hip_kernels.h"
 
 namespace bh {
+
+// Per-dispatch timestamps for the profiler (bh_profile_events): while `stop`
+// is set, launches go through hipExtLaunchKernel, whose start / stop events
+// carry the dispatch's own begin / end timestamps - the duration rocprofv3's
+// kernel trace reports, without the event-to-event dispatch gap.  The first
+// kernel of a launcher takes `start`, every kernel re-records `stop`, so a
+// launcher that issues several kernels is timed from the first one's begin
+// to the last one's end.
+struct ProfEvents {
+  hipEvent_t start = nullptr;
+  hipEvent_t stop = nullptr;
+  int launched = 0;  // kernels issued under these events
+};
+extern thread_local ProfEvents g_prof;
+
+#define BH_LAUNCH(kern, grid, block, shmem, stream, ...)                                            \
+  do {                                                                                              \
+    if (::bh::g_prof.stop) {                                                                        \
+      hipExtLaunchKernelGGL(kern, grid, block, shmem, stream, ::bh::g_prof.start, ::bh::g_prof.stop, 0, \
+                            __VA_ARGS__);                                                           \
+      ::bh::g_prof.start = nullptr;                                                                 \
+      ++::bh::g_prof.launched;                                                                      \
+    } else {                                                                                        \
+      hipLaunchKernelGGL(kern, grid, block, shmem, stream, __VA_ARGS__);                            \
+    }                                                                                               \
+  } while (0)
 
 typedef int v4i __attribute__((ext_vector_type(4)));
 typedef int v2i __attribute__((ext_vector_type(2)));

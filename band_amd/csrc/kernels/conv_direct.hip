@@ -200,8 +200,8 @@ int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s) 
   dv.out_w = bh::FastDiv(p.out_w);
   dv.out_h = bh::FastDiv(p.out_h);
   const dim3 grid((unsigned)((M + 255) / 256), (unsigned)((p.out_c + 7) / 8));
-  if (K <= 32) hipLaunchKernelGGL(bh::conv_direct_kernel<8>, grid, dim3(256), 0, s, p, M, K, dv);
-  else hipLaunchKernelGGL(bh::conv_direct_kernel<16>, grid, dim3(256), 0, s, p, M, K, dv);
+  if (K <= 32) BH_LAUNCH(bh::conv_direct_kernel<8>, grid, dim3(256), 0, s, p, M, K, dv);
+  else BH_LAUNCH(bh::conv_direct_kernel<16>, grid, dim3(256), 0, s, p, M, K, dv);
   return bh_check_launch("conv_direct_kernel");
 }
 
@@ -221,7 +221,7 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const int ch_per_y = (groups + gy - 1) / gy * 8;
   gy = (p.out_c + ch_per_y - 1) / ch_per_y;
   const dim3 grid((unsigned)gx, (unsigned)gy);
-  if (p.requant_fast) hipLaunchKernelGGL(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
-  else hipLaunchKernelGGL(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+  if (p.requant_fast) BH_LAUNCH(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+  else BH_LAUNCH(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
   return bh_check_launch("conv_stem_kernel");
 }

@@ -127,24 +127,28 @@ __device__ __forceinline__ int rowsum16(v4i a, int s) {
   return __builtin_amdgcn_sdot4(a.w, 0x01010101, s, false);
 }
 
-// Epilogue of one transposed 16x16 tile: the lane holds output channels
-// nb..nb+3 of pixel m (D^T = W x X^T on the MFMA), so its four requantised
-// bytes leave as one dword store when N % 4 == 0.  acc excludes the folded
-// bias; rsum is pixel m's input row sum (uint8 filters).
-__device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc, int rsum, int m, int nb, int M,
-                                               int N) {
-  if (m >= M || nb >= N) return;
-  // dword path: N % 4 == 0 (then nb + 3 < N too) and 4-byte aligned output /
-  // residual bases (a concat-elided output may start at any byte)
-  const bool vec = (N & 3) == 0 && (((uintptr_t)p.output | (uintptr_t)p.residual) & 3) == 0;
-  int32_t be[4], mu[4], sh[4];
-  if (vec) {
+// Per-lane channel constants of a transposed 16x16 tile's epilogue: the lane
+// owns output channels nb..nb+3 (every pixel row of the tile uses the same
+// four), so kernels that store several pixel tiles per channel group build
+// them once.
+struct Chan4 {
+  int32_t be[4];
+  ChanQ q[4];
+  bool vec;  // dword path: N % 4 == 0 and 4-byte aligned output / residual bases
+};
+
+__device__ __forceinline__ Chan4 chan4(const bh_conv_params& p, int nb, int N) {
+  Chan4 c;
+  // (a concat-elided output may start at any byte)
+  c.vec = (N & 3) == 0 && (((uintptr_t)p.output | (uintptr_t)p.residual) & 3) == 0;
+  int32_t mu[4], sh[4];
+  if (c.vec) {
     const v4i b4 = *(const v4i*)(p.bias_eff + nb);
     const v4i m4 = *(const v4i*)(p.mult + nb);
     const v4i s4 = *(const v4i*)(p.shift + nb);
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      be[r] = b4[r];
+      c.be[r] = b4[r];
       mu[r] = m4[r];
       sh[r] = s4[r];
     }
@@ -152,18 +156,30 @@ __device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc,
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = nb + r < N ? nb + r : nb;
-      be[r] = p.bias_eff[n];
+      c.be[r] = p.bias_eff[n];
       mu[r] = p.mult[n];
       sh[r] = p.shift[n];
     }
   }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) c.q[r] = chan_q(mu[r], sh[r], p.out_zp);
+  return c;
+}
+
+// Epilogue of one transposed 16x16 tile: the lane holds output channels
+// nb..nb+3 of pixel m (D^T = W x X^T on the MFMA), so its four requantised
+// bytes leave as one dword store when N % 4 == 0.  acc excludes the folded
+// bias; rsum is pixel m's input row sum (uint8 filters).
+__device__ __forceinline__ void conv_store4(const bh_conv_params& p, v4i acc, int rsum, int m, int nb, int M, int N,
+                                            const Chan4& c) {
+  if (m >= M || nb >= N) return;
   const long o = (long)m * N + nb;
   const uint8_t* res = (const uint8_t*)p.residual;
   const bool res_signed = p.in_xor == 0;  // residual shares the activation type
   const uint8_t* tab = (const uint8_t*)p.out_table;
   uint32_t rq = 0;
   if (res) {
-    if (vec) {
+    if (c.vec) {
       rq = *(const uint32_t*)(res + o);
     } else {
 #pragma unroll
@@ -174,10 +190,10 @@ __device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc,
   uint32_t packed = 0;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    int32_t a = acc[r] + be[r];
+    int32_t a = acc[r] + c.be[r];
     if (p.w_zp != 0) a -= p.w_zp * rsum;
-    int32_t v = p.requant_fast ? requant_out<true>(a, chan_q(mu[r], sh[r], p.out_zp), p.out_zp, p.act_min, p.act_max)
-                               : requant_out<false>(a, chan_q(mu[r], sh[r], p.out_zp), p.out_zp, p.act_min, p.act_max);
+    int32_t v = p.requant_fast ? requant_out<true>(a, c.q[r], p.out_zp, p.act_min, p.act_max)
+                               : requant_out<false>(a, c.q[r], p.out_zp, p.act_min, p.act_max);
     if (res) {
       const uint32_t qb = (rq >> (8 * r)) & 0xffu;
       const int32_t q = res_signed ? (int32_t)(int8_t)qb : (int32_t)qb;
@@ -189,13 +205,19 @@ __device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc,
     packed |= byte << (8 * r);
   }
   uint8_t* out = (uint8_t*)p.output + o;
-  if (vec) {
+  if (c.vec) {
     *(uint32_t*)out = packed;
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r)
       if (nb + r < N) out[r] = (uint8_t)(packed >> (8 * r));
   }
+}
+
+__device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc, int rsum, int m, int nb, int M,
+                                               int N) {
+  if (m >= M || nb >= N) return;
+  conv_store4(p, acc, rsum, m, nb, M, N, chan4(p, nb, N));
 }
 
 constexpr int KU = 4;  // K-steps whose loads are issued together
@@ -351,9 +373,151 @@ static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t 
     const char* e = std::getenv("BH_CONV_XCD");  // A-B runs: 0 = plain order
     return e ? std::atoi(e) : 1;
   }();
-  hipLaunchKernelGGL((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
+  BH_LAUNCH((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
                      s, p, M, K, N, kchunk, dv, gn, xcd);
   return bh_check_launch("conv_mfma_kernel");
+}
+
+// ---------------------------------------------------------------------------
+// conv_gemm_kernel: the deep / wide batched 1x1 layers (stride 1, int8
+// activations, symmetric int8 filters) as an LDS-staged GEMM.
+//
+// conv_mfma_kernel gives every wave its own fragments straight from L2, so a
+// workgroup tile of 32x32 outputs re-reads its A rows and B rows once per
+// tile: on PoseNet's 14x14 512->1024 layer at batch 24 that is ~300 MB of L2
+// reads for 10 GOP.  Here a workgroup owns a BM x BN output tile (up to
+// 128 x 128) and walks K in 64-byte steps: the step's A rows (pixels) and B
+// rows (filters) go global -> LDS with 16-byte global_load_lds (no VGPR
+// staging), two LDS buffers so the next step's DMA runs under this step's
+// MFMAs, and each of the 4 waves reads its 16-byte fragments back with
+// ds_read_b128 and issues (BM/2/16) x (BN/2/16) v_mfma_i32_16x16x64_i8 per
+// step.  LDS image: staged row r (A rows first, then B rows) is 64 bytes
+// whose four 16-byte chunks are stored XOR-swizzled, chunk c at (c ^ (r>>2))
+// & 3, so the 16 lanes of a ds_read_b128 group (16 consecutive rows, one
+// chunk) hit 16 distinct 4-bank slots; glds writes lane-linear, so the swizzle
+// is applied to each lane's global source address and undone on the read.
+// The K tail reads a harmless in-row address (the packed filters are zero
+// there, so it adds 0).  Epilogue: the conv_mfma_kernel one (transposed D:
+// a lane holds 4 consecutive channels of one pixel, one dword store).
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// vmcnt(n) with n a compile-time count (glds instructions left in flight)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int WM, int WN, int WAVES_M, int WAVES_N, int NB>
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_conv_params p, int M, int K,
+                                                                          int nblocks, int ksteps, int xcd) {
+  constexpr int W = WAVES_M * WAVES_N;
+  static_assert(W == 4 || W == 8, "4 or 8 waves per workgroup");
+  static_assert(NB >= 2 && NB <= 4, "LDS ring depth");
+  constexpr int BM = WAVES_M * WM * 16;
+  constexpr int BN = WAVES_N * WN * 16;
+  constexpr int ROWS = BM + BN;  // 64-byte rows staged per K-step
+  static_assert(ROWS % (16 * W) == 0, "whole staging instructions per wave");
+  constexpr int NI = ROWS / (16 * W);  // glds instructions per wave per K-step (16 rows each)
+  constexpr int STAGE = ROWS * 64;
+  constexpr int D = NB - 1;  // K-steps staged ahead of the one computed
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NB * STAGE];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int bm = logical / nblocks;
+  const int bn = logical - bm * nblocks;
+  const int tm0 = bm * BM;
+  const int tn0 = bn * BN;
+  const int N = p.out_c;
+
+  // this lane's source for each of its wave's staging instructions
+  const uint8_t* src[NI];
+  int kval[NI], goff[NI];
+#pragma unroll
+  for (int j = 0; j < NI; ++j) {
+    const int row = 16 * (wave + W * j) + (lane >> 2);
+    const int g = (lane & 3) ^ ((row >> 2) & 3);
+    goff[j] = 16 * g;
+    if (row < BM) {
+      const int m = min(tm0 + row, M - 1);
+      src[j] = (const uint8_t*)p.input + (long)m * K + 16 * g;
+      kval[j] = K - 16 * g;
+    } else {
+      const int n = min(tn0 + row - BM, p.n_pad - 1);
+      src[j] = (const uint8_t*)p.weights + (long)n * p.k_pad + 16 * g;
+      kval[j] = 0x7fffffff;
+    }
+  }
+  auto stage = [&](int ks) {
+    const int kb = ks * 64;
+    uint8_t* dst = lds + (ks % NB) * STAGE + wave * 1024;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const uint8_t* s = kb < kval[j] ? src[j] + kb : src[j] - goff[j];
+      __builtin_amdgcn_global_load_lds((const void*)s, (lds_void_t*)(dst + j * W * 1024), 16, 0, 0);
+    }
+  };
+
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  const int chunk = ((g ^ (r16 >> 2)) & 3) << 4;
+  const int wm0 = (wave % WAVES_M) * WM * 16;
+  const int wn0 = (wave / WAVES_M) * WN * 16;
+  v4i acc[WM][WN];
+#pragma unroll
+  for (int i = 0; i < WM; ++i)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[i][j] = (v4i){0, 0, 0, 0};
+
+  // prologue: D steps in flight
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+    if (d < ksteps) stage(d);
+  for (int ks = 0; ks < ksteps; ++ks) {
+    // step ks landed: this wave leaves the glds of steps ks+1 .. ks+D-1 in
+    // flight (counted wait, never 0 in the steady state), the raw barrier
+    // then orders every wave's DMA before the reads; it also retires every
+    // wave's reads of step ks-1, whose buffer step ks+D now refills
+    const int ahead = min(D - 1, ksteps - 1 - ks);
+    if (ahead >= 2) wait_vmcnt<2 * NI>();
+    else if (ahead == 1) wait_vmcnt<NI>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (ks + D < ksteps) stage(ks + D);
+    const uint8_t* buf = lds + (ks % NB) * STAGE;
+    v4i a[WM], b[WN];
+#pragma unroll
+    for (int i = 0; i < WM; ++i) a[i] = *(const v4i*)(buf + (wm0 + i * 16 + r16) * 64 + chunk);
+#pragma unroll
+    for (int j = 0; j < WN; ++j) b[j] = *(const v4i*)(buf + (BM + wn0 + j * 16 + r16) * 64 + chunk);
+#pragma unroll
+    for (int i = 0; i < WM; ++i)
+#pragma unroll
+      for (int j = 0; j < WN; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(b[j], a[i], acc[i][j], 0, 0, 0);
+    // this step's reads are done before any wave passes the next barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // channel constants once per channel group, shared by the WM pixel tiles
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int nb = tn0 + wn0 + j * 16 + 4 * g;
+    if (nb >= N) continue;
+    const Chan4 c = chan4(p, nb, N);
+#pragma unroll
+    for (int i = 0; i < WM; ++i) conv_store4(p, acc[i][j], 0, tm0 + wm0 + i * 16 + r16, nb, M, N, c);
+  }
+}
+
+template <int WM, int WN, int WAVES_M, int WAVES_N, int NB>
+static int launch_gemm(const bh_conv_params& p, int M, int K, hipStream_t s) {
+  constexpr int BM = WAVES_M * WM * 16;
+  constexpr int BN = WAVES_N * WN * 16;
+  const int gm = (M + BM - 1) / BM, gn = (p.out_c + BN - 1) / BN;
+  BH_LAUNCH((conv_gemm_kernel<WM, WN, WAVES_M, WAVES_N, NB>), dim3(gm * gn), dim3(WAVES_M * WAVES_N * 64), 0, s,
+            p, M, K, gn, (K + 63) / 64, 1);
+  return bh_check_launch("conv_gemm_kernel");
 }
 
 static inline long wgs(int M, int N, int tm, int tn) { return (long)((M + tm - 1) / tm) * ((N + tn - 1) / tn); }
@@ -378,6 +542,28 @@ static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_
   if (N <= 32 && wgs(M, N, 128, 32) >= kTargetWG) return launch_cfg<2, 2, 4, 1, 1, IS1X1, VEC>(p, M, K, N, s);
   if (wgs(M, N, 64, 64) >= kTargetWG) return launch_cfg<2, 2, 2, 2, 1, IS1X1, VEC>(p, M, K, N, s);
   return launch_cfg<1, 1, 2, 2, 1, IS1X1, VEC>(p, M, K, N, s);
+}
+
+// conv_gemm_kernel configuration (tools/gemm_cfg_sweep.sh, batch-24 C3
+// shapes): 128x128 tiles over 8 waves (64x32 each, 2 LDS buffers) once they
+// still give one workgroup per CU - PoseNet's 512/1024-channel layers, 1.6-2.7x
+// conv_mfma_kernel; otherwise 64x64 tiles over 8 waves (16x32 each, 3 LDS
+// buffers), which keep ~4 waves per SIMD on the mid-size layers.
+// BH_GEMM_CFG=1 selects the first 4-wave form (128x128 ... 64x64, 4 buffers).
+static int launch_gemm_shape(const bh_conv_params& p, int M, int K, hipStream_t s) {
+  const int N = p.out_c;
+  static const int cfg = [] {
+    const char* e = std::getenv("BH_GEMM_CFG");  // A-B experiments
+    return e ? std::atoi(e) : 0;
+  }();
+  if (cfg == 1) {
+    if (wgs(M, N, 128, 128) >= 256) return launch_gemm<4, 4, 2, 2, 4>(p, M, K, s);
+    if (wgs(M, N, 128, 64) >= 256) return launch_gemm<4, 2, 2, 2, 4>(p, M, K, s);
+    if (wgs(M, N, 64, 128) >= 256) return launch_gemm<2, 4, 2, 2, 4>(p, M, K, s);
+    return launch_gemm<2, 2, 2, 2, 4>(p, M, K, s);
+  }
+  if (wgs(M, N, 128, 128) >= 256) return launch_gemm<4, 2, 2, 4, 2>(p, M, K, s);
+  return launch_gemm<1, 2, 4, 2, 3>(p, M, K, s);
 }
 
 }  // namespace bh
@@ -410,7 +596,24 @@ long RowsMinM() {
   return v;
 }
 
-enum Route { kDirect, kStem, kXs, kRows, kMfma };
+// conv_gemm_kernel (LDS-staged GEMM): BH_CONV_GEMM=0 off, 1 (default) the
+// eligible layers of at least GemmMinOps() ops, 2 every eligible layer
+int GemmMode() {
+  static const int v = [] {
+    const char* e = std::getenv("BH_CONV_GEMM");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+double GemmMinOps() {
+  static const double v = [] {
+    const char* e = std::getenv("BH_CONV_GEMM_MIN_GOP");
+    return e ? std::atof(e) * 1e9 : 1.2e9;
+  }();
+  return v;
+}
+
+enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm };
 
 Route route(const bh_conv_params& p, long M, int K, int N) {
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
@@ -420,10 +623,17 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
     return stem && !std::getenv("BH_CONV_NO_STEM") ? kStem : kDirect;
   }
   const bool aligned = (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.input) & 3) == 0;
-  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0 && aligned) {
+  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0 && aligned && p.kernel_hint == 0) {
     if (K <= 320 && M >= XsMinM()) return kXs;
     if (RowsMinM() >= 0 && M >= RowsMinM()) return kRows;
   }
+  // LDS-staged GEMM: int8 activations (glds cannot apply the uint8 XOR),
+  // symmetric filters (no row sums), 16-byte K chunks
+  const bool gemm_ok = is1x1 && p.stride_h == 1 && p.stride_w == 1 && p.in_xor == 0 && p.w_zp == 0 &&
+                       K % 16 == 0 && aligned && ((uintptr_t)p.input & 15) == 0;
+  if (p.kernel_hint == BH_CONV_MFMA) return kMfma;
+  if (p.kernel_hint == BH_CONV_GEMM) return gemm_ok ? kGemm : kMfma;
+  if (gemm_ok && GemmMode() > 0 && (GemmMode() == 2 || 2.0 * M * N * K >= GemmMinOps())) return kGemm;
   return kMfma;
 }
 }  // namespace
@@ -431,7 +641,7 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
 extern "C" const char* bh_conv2d_i8_kernel(const bh_conv_params* p) {
   if (!p) return "";
   static const char* const names[] = {"conv_direct_kernel", "conv_stem_kernel", "conv_xs_kernel",
-                                      "conv_rows_kernel", "conv_mfma_kernel"};
+                                      "conv_rows_kernel", "conv_mfma_kernel", "conv_gemm_kernel"};
   return names[route(*p, (long)p->batch * p->out_h * p->out_w, p->k_h * p->k_w * p->in_c, p->out_c)];
 }
 
@@ -483,6 +693,7 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
     case kStem: return bh_conv_stem_launch(p, M, K, s);
     case kXs: return bh_conv_xs_launch(p, M, K, N, s);
     case kRows: return bh_conv_rows_launch(p, M, K, N, s);
+    case kGemm: return bh::launch_gemm_shape(p, M, K, s);
     case kMfma: break;
   }
   if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);

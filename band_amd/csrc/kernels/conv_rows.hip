@@ -339,10 +339,10 @@ static int launch_xs(const bh_conv_params& p, int M, int K, int N, hipStream_t s
   const int tpc = (tiles + chunks - 1) / chunks;
   chunks = (tiles + tpc - 1) / tpc;
   if (p.requant_fast)
-    hipLaunchKernelGGL((conv_xs_kernel<RB, KS, VEC, true>), dim3(pwgs * chunks), dim3(256), 0, s, p, M, K, N, pwgs,
+    BH_LAUNCH((conv_xs_kernel<RB, KS, VEC, true>), dim3(pwgs * chunks), dim3(256), 0, s, p, M, K, N, pwgs,
                        chunks, tpc);
   else
-    hipLaunchKernelGGL((conv_xs_kernel<RB, KS, VEC, false>), dim3(pwgs * chunks), dim3(256), 0, s, p, M, K, N,
+    BH_LAUNCH((conv_xs_kernel<RB, KS, VEC, false>), dim3(pwgs * chunks), dim3(256), 0, s, p, M, K, N,
                        pwgs, chunks, tpc);
   return bh_check_launch("conv_xs_kernel");
 }
@@ -364,10 +364,10 @@ static int launch_rows(const bh_conv_params& p, int M, int K, int N, hipStream_t
   const int mblocks = (M + 4 * RB * 16 - 1) / (4 * RB * 16);
   const int nchunks = (N + NT * 16 - 1) / (NT * 16);
   if (p.requant_fast)
-    hipLaunchKernelGGL((conv_rows_kernel<RB, NT, VEC, true>), dim3(mblocks * nchunks), dim3(256), 0, s, p, M, K, N,
+    BH_LAUNCH((conv_rows_kernel<RB, NT, VEC, true>), dim3(mblocks * nchunks), dim3(256), 0, s, p, M, K, N,
                        mblocks, nchunks);
   else
-    hipLaunchKernelGGL((conv_rows_kernel<RB, NT, VEC, false>), dim3(mblocks * nchunks), dim3(256), 0, s, p, M, K,
+    BH_LAUNCH((conv_rows_kernel<RB, NT, VEC, false>), dim3(mblocks * nchunks), dim3(256), 0, s, p, M, K,
                        N, mblocks, nchunks);
   return bh_check_launch("conv_rows_kernel");
 }

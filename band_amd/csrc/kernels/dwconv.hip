@@ -522,11 +522,11 @@ static void launch_run(const bh_dwconv_params& p, hipStream_t s) {
   dv.runs_w = FastDiv(runs_w);
   const dim3 grid((unsigned)((total + 255) / 256));
   if (p.w_zp != 0) {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, true, true>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, false, true>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_run_kernel<CV, S, D, true, true>), grid, dim3(256), 0, s, p, total, dv);
+    else BH_LAUNCH((dwconv3x3_run_kernel<CV, S, D, false, true>), grid, dim3(256), 0, s, p, total, dv);
   } else {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, true, false>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_run_kernel<CV, S, D, false, false>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_run_kernel<CV, S, D, true, false>), grid, dim3(256), 0, s, p, total, dv);
+    else BH_LAUNCH((dwconv3x3_run_kernel<CV, S, D, false, false>), grid, dim3(256), 0, s, p, total, dv);
   }
 }
 
@@ -546,11 +546,11 @@ static void launch_mfma(const bh_dwconv_params& p, hipStream_t s) {
   DwDivs dv = dw_divs(p, groups);
   const dim3 grid((unsigned)((waves + 3) / 4));
   if (p.w_zp != 0) {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, true, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
-    else hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, false, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_mfma_kernel<RB, true, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    else BH_LAUNCH((dwconv3x3_mfma_kernel<RB, false, true>), grid, dim3(256), 0, s, p, P, nblocks, dv);
   } else {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, true, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
-    else hipLaunchKernelGGL((dwconv3x3_mfma_kernel<RB, false, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_mfma_kernel<RB, true, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
+    else BH_LAUNCH((dwconv3x3_mfma_kernel<RB, false, false>), grid, dim3(256), 0, s, p, P, nblocks, dv);
   }
 }
 
@@ -575,13 +575,13 @@ static void launch3x3(const bh_dwconv_params& p, long pixels, hipStream_t s) {
   const dim3 grid((unsigned)((total + 255) / 256));
   const DwDivs dv = dw_divs(p, p.out_c / CV);
   if (!p.taps) {
-    hipLaunchKernelGGL(dwconv3x3_kernel<CV>, grid, dim3(256), 0, s, p, total, dv);
+    BH_LAUNCH(dwconv3x3_kernel<CV>, grid, dim3(256), 0, s, p, total, dv);
   } else if (p.w_zp != 0) {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, true, true>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, false, true>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_dot_kernel<CV, true, true>), grid, dim3(256), 0, s, p, total, dv);
+    else BH_LAUNCH((dwconv3x3_dot_kernel<CV, false, true>), grid, dim3(256), 0, s, p, total, dv);
   } else {
-    if (p.requant_fast) hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, true, false>), grid, dim3(256), 0, s, p, total, dv);
-    else hipLaunchKernelGGL((dwconv3x3_dot_kernel<CV, false, false>), grid, dim3(256), 0, s, p, total, dv);
+    if (p.requant_fast) BH_LAUNCH((dwconv3x3_dot_kernel<CV, true, false>), grid, dim3(256), 0, s, p, total, dv);
+    else BH_LAUNCH((dwconv3x3_dot_kernel<CV, false, false>), grid, dim3(256), 0, s, p, total, dv);
   }
 }
 
@@ -671,7 +671,7 @@ extern "C" int bh_dwconv2d_i8(const bh_dwconv_params* pp, bh_stream_t stream) {
     case kDot4: case kTap4: bh::launch3x3<4>(p, pixels, s); break;
     case kGeneric: {
       const int total = (int)(pixels * p.out_c);
-      hipLaunchKernelGGL(bh::dwconv_generic_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total,
+      BH_LAUNCH(bh::dwconv_generic_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total,
                          bh::dw_divs(p, p.out_c));
       break;
     }

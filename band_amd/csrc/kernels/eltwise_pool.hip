@@ -248,13 +248,13 @@ extern "C" int bh_eltwise_i8(const bh_eltwise_params* pp, bh_stream_t stream) {
   const bool aligned = ((uintptr_t)p.a % 4 == 0) && ((uintptr_t)p.b % 4 == 0) && ((uintptr_t)p.out % 4 == 0);
   if (same && n % 4 == 0 && aligned) {
     const long n4 = n / 4;
-    hipLaunchKernelGGL(bh::eltwise_flat4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p, n4);
+    BH_LAUNCH(bh::eltwise_flat4_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, s, p, n4);
   } else {
     bh::BcastDivs dv;
     dv.d3 = bh::FastDiv(p.shape_o[3]);
     dv.d2 = bh::FastDiv(p.shape_o[2]);
     dv.d1 = bh::FastDiv(p.shape_o[1]);
-    hipLaunchKernelGGL(bh::eltwise_bcast_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, (int)n, dv);
+    BH_LAUNCH(bh::eltwise_bcast_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, p, (int)n, dv);
   }
   return bh_check_launch("eltwise_kernel");
 }
@@ -278,15 +278,15 @@ extern "C" int bh_pool_i8(const bh_pool_params* pp, bh_stream_t stream) {
   if (p.channels % 4 == 0 && pixels * (p.channels / 4) <= 65536 && p.f_h * p.f_w >= 16 && pixels <= 65535) {
     dv.groups = bh::FastDiv(p.channels / 4);
     const dim3 grid((unsigned)pixels, (unsigned)((p.channels / 4 + 63) / 64));
-    hipLaunchKernelGGL(bh::pool_wide_kernel, grid, dim3(256), 0, s, p, dv);
+    BH_LAUNCH(bh::pool_wide_kernel, grid, dim3(256), 0, s, p, dv);
   } else if (p.channels % 4 == 0) {
     const int total = (int)(pixels * (p.channels / 4));
     dv.groups = bh::FastDiv(p.channels / 4);
-    hipLaunchKernelGGL(bh::pool_kernel<4>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total, dv);
+    BH_LAUNCH(bh::pool_kernel<4>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total, dv);
   } else {
     const int total = (int)(pixels * p.channels);
     dv.groups = bh::FastDiv(p.channels);
-    hipLaunchKernelGGL(bh::pool_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total, dv);
+    BH_LAUNCH(bh::pool_kernel<1>, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, p, total, dv);
   }
   return bh_check_launch("pool_kernel");
 }

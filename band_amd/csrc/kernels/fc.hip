@@ -93,11 +93,11 @@ extern "C" int bh_fc_i8(const bh_fc_params* pp, bh_stream_t stream) {
   dim3 grid((unsigned)((jobs + 3) / 4));
   const bool vec16 = (p.depth % 16 == 0) && ((uintptr_t)p.input % 16 == 0);
   if (p.w_zp != 0) {
-    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, true>), grid, dim3(256), 0, s, p, units);
-    else hipLaunchKernelGGL((bh::fc_kernel<1, true>), grid, dim3(256), 0, s, p, units);
+    if (vec16) BH_LAUNCH((bh::fc_kernel<16, true>), grid, dim3(256), 0, s, p, units);
+    else BH_LAUNCH((bh::fc_kernel<1, true>), grid, dim3(256), 0, s, p, units);
   } else {
-    if (vec16) hipLaunchKernelGGL((bh::fc_kernel<16, false>), grid, dim3(256), 0, s, p, units);
-    else hipLaunchKernelGGL((bh::fc_kernel<1, false>), grid, dim3(256), 0, s, p, units);
+    if (vec16) BH_LAUNCH((bh::fc_kernel<16, false>), grid, dim3(256), 0, s, p, units);
+    else BH_LAUNCH((bh::fc_kernel<1, false>), grid, dim3(256), 0, s, p, units);
   }
   return bh_check_launch("fc_kernel");
 }

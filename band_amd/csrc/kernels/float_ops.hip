@@ -232,7 +232,7 @@ extern "C" int bh_conv2d_f32(const bh_conv_f32_params* pp, bh_stream_t s) {
   }
   bh::FastDiv dg((uint32_t)groups), dw((uint32_t)p.out_w), dh((uint32_t)p.out_h);
   if (p.depthwise) {
-    hipLaunchKernelGGL(bh::dwconv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
+    BH_LAUNCH(bh::dwconv_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dg, dw, dh,
                        total);
   } else {
     // split the reduction until ~1024 workgroups or 16 taps-channels per slice
@@ -240,7 +240,7 @@ extern "C" int bh_conv2d_f32(const bh_conv_f32_params* pp, bh_stream_t s) {
     int ks = 1;
     while (ks < 16 && (total * ks) / 256 < 1024 && K / (2 * ks) >= 16) ks *= 2;
     const long items_per_wg = 256 / ks;
-    hipLaunchKernelGGL(bh::conv_f32_kernel, dim3((unsigned)((total + items_per_wg - 1) / items_per_wg)), dim3(256),
+    BH_LAUNCH(bh::conv_f32_kernel, dim3((unsigned)((total + items_per_wg - 1) / items_per_wg)), dim3(256),
                        0, (hipStream_t)s, p, dg, dw, dh, total, ks);
   }
   return bh_check_launch(p.depthwise ? "dwconv_f32_kernel" : "conv_f32_kernel");
@@ -252,7 +252,7 @@ extern "C" int bh_fc_f32(const bh_fc_f32_params* pp, bh_stream_t s) {
     return BH_EINVAL;
   }
   const long total = (long)pp->rows * pp->units;
-  hipLaunchKernelGGL(bh::fc_f32_kernel, dim3(bh::blocks(total, 4)), dim3(256), 0, (hipStream_t)s, *pp, total);
+  BH_LAUNCH(bh::fc_f32_kernel, dim3(bh::blocks(total, 4)), dim3(256), 0, (hipStream_t)s, *pp, total);
   return bh_check_launch("fc_f32_kernel");
 }
 
@@ -264,7 +264,7 @@ extern "C" int bh_eltwise_f32(const bh_eltwise_f32_params* pp, bh_stream_t s) {
   const int* so = pp->shape_o;
   const long n = (long)so[0] * so[1] * so[2] * so[3];
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(bh::eltwise_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, *pp, n);
+  BH_LAUNCH(bh::eltwise_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, *pp, n);
   return bh_check_launch("eltwise_f32_kernel");
 }
 
@@ -275,7 +275,7 @@ extern "C" int bh_pool_f32(const bh_pool_f32_params* pp, bh_stream_t s) {
   }
   const long total = (long)pp->batch * pp->out_h * pp->out_w * pp->channels;
   if (total <= 0) return 0;
-  hipLaunchKernelGGL(bh::pool_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, *pp, total);
+  BH_LAUNCH(bh::pool_f32_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, *pp, total);
   return bh_check_launch("pool_f32_kernel");
 }
 
@@ -285,7 +285,7 @@ extern "C" int bh_unary_f32(int kind, const float* in, float* out, long n, float
     return BH_EINVAL;
   }
   if (n == 0) return 0;
-  hipLaunchKernelGGL(bh::unary_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, kind, in, out, n, lo,
+  BH_LAUNCH(bh::unary_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, kind, in, out, n, lo,
                      hi);
   return bh_check_launch("unary_f32_kernel");
 }
@@ -296,7 +296,7 @@ extern "C" int bh_softmax_f32(const float* in, float* out, long rows, int depth,
     return BH_EINVAL;
   }
   if (rows == 0) return 0;
-  hipLaunchKernelGGL(bh::softmax_f32_kernel, dim3(bh::blocks(rows, 4)), dim3(256), 0, (hipStream_t)s, in, out, rows,
+  BH_LAUNCH(bh::softmax_f32_kernel, dim3(bh::blocks(rows, 4)), dim3(256), 0, (hipStream_t)s, in, out, rows,
                      depth, beta);
   return bh_check_launch("softmax_f32_kernel");
 }

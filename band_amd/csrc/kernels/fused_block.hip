@@ -441,7 +441,7 @@ static int launch_irb(const bh_irb_params& p, size_t lds, hipStream_t s) {
   dv.mt3 = FastDiv(G.MT3);
   dv.ksplit = FastDiv(ksplit);
   dim3 grid((p.out_w + p.tile_w - 1) / p.tile_w, (p.out_h + p.tile_h - 1) / p.tile_h, p.batch);
-  hipLaunchKernelGGL(irb_kernel<NW>, grid, dim3(NW * 64), lds, s, p, ksplit, (KS3 + ksplit - 1) / ksplit, dv);
+  BH_LAUNCH(irb_kernel<NW>, grid, dim3(NW * 64), lds, s, p, ksplit, (KS3 + ksplit - 1) / ksplit, dv);
   return bh_check_launch("irb_kernel");
 }
 

@@ -234,7 +234,7 @@ extern "C" int bh_lut_u8(const void* in, void* out, long n, const void* table, b
   const bool al = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
   const long n16 = al ? n / 16 : 0;
   const long threads = n16 + (n - 16 * n16);
-  hipLaunchKernelGGL(bh::lut_u8_kernel, dim3(bh::blocks(threads)), dim3(256), 0, (hipStream_t)s,
+  BH_LAUNCH(bh::lut_u8_kernel, dim3(bh::blocks(threads)), dim3(256), 0, (hipStream_t)s,
                      (const uint8_t*)in, (uint8_t*)out, n, n16, (const uint8_t*)table);
   return bh_check_launch("lut_u8_kernel");
 }
@@ -245,7 +245,7 @@ extern "C" int bh_lut_f32(const void* in, void* out, long n, const float* table,
     return BH_EINVAL;
   }
   if (n == 0) return 0;
-  hipLaunchKernelGGL(bh::lut_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, (const uint8_t*)in,
+  BH_LAUNCH(bh::lut_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, (const uint8_t*)in,
                      (float*)out, n, table);
   return bh_check_launch("lut_f32_kernel");
 }
@@ -257,7 +257,7 @@ extern "C" int bh_quantize_f32(const float* in, void* out, long n, float scale, 
     return BH_EINVAL;
   }
   if (n == 0) return 0;
-  hipLaunchKernelGGL(bh::quantize_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, in, (uint8_t*)out,
+  BH_LAUNCH(bh::quantize_f32_kernel, dim3(bh::blocks(n)), dim3(256), 0, (hipStream_t)s, in, (uint8_t*)out,
                      n, scale, zp, out_signed ? -128 : 0, out_signed ? 127 : 255);
   return bh_check_launch("quantize_f32_kernel");
 }
@@ -290,7 +290,7 @@ extern "C" int bh_concat(const bh_concat_params* pp, bh_stream_t s) {
   }
   if (maxbytes == 0) return 0;
   const dim3 grid(bh::blocks(maxbytes), (unsigned)p.n_inputs);
-  hipLaunchKernelGGL(bh::concat_kernel, grid, dim3(256), 0, (hipStream_t)s, p, dv);
+  BH_LAUNCH(bh::concat_kernel, grid, dim3(256), 0, (hipStream_t)s, p, dv);
   return bh_check_launch("concat_kernel");
 }
 
@@ -318,9 +318,9 @@ extern "C" int bh_pad(const bh_pad_params* pp, bh_stream_t s) {
   dv.w = bh::FastDiv(dv.os[2]);
   dv.h = bh::FastDiv(dv.os[1]);
   if (p.elem_bytes == 1)
-    hipLaunchKernelGGL(bh::pad_kernel<uint8_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::pad_kernel<uint8_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   else
-    hipLaunchKernelGGL(bh::pad_kernel<uint32_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::pad_kernel<uint32_t>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   return bh_check_launch("pad_kernel");
 }
 
@@ -344,9 +344,9 @@ extern "C" int bh_resize_nearest(const bh_resize_nearest_params* pp, bh_stream_t
   dv.ow = bh::FastDiv(p.out_w);
   dv.oh = bh::FastDiv(p.out_h);
   if (v4)
-    hipLaunchKernelGGL(bh::resize_nearest_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::resize_nearest_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   else
-    hipLaunchKernelGGL(bh::resize_nearest_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::resize_nearest_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   return bh_check_launch("resize_nearest_kernel");
 }
 
@@ -366,7 +366,7 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
   dv.units = bh::FastDiv(p.channels);
   dv.ow = bh::FastDiv(p.out_w);
   dv.oh = bh::FastDiv(p.out_h);
-  hipLaunchKernelGGL(bh::resize_bilinear_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+  BH_LAUNCH(bh::resize_bilinear_kernel, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   return bh_check_launch("resize_bilinear_kernel");
 }
 
@@ -376,7 +376,7 @@ extern "C" int bh_softmax_i8(const bh_softmax_params* pp, bh_stream_t s) {
     return BH_EINVAL;
   }
   if (pp->rows == 0) return 0;
-  hipLaunchKernelGGL(bh::softmax_kernel, dim3(bh::blocks(pp->rows)), dim3(256), 0, (hipStream_t)s, *pp);
+  BH_LAUNCH(bh::softmax_kernel, dim3(bh::blocks(pp->rows)), dim3(256), 0, (hipStream_t)s, *pp);
   return bh_check_launch("softmax_kernel");
 }
 
@@ -402,8 +402,8 @@ extern "C" int bh_zero_insert(const bh_zero_insert_params* pp, bh_stream_t s) {
   dv.sw = bh::FastDiv(p.stride_w);
   const long total = pixels * dv.units.d;
   if (v4)
-    hipLaunchKernelGGL(bh::zero_insert_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::zero_insert_kernel<4>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   else
-    hipLaunchKernelGGL(bh::zero_insert_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
+    BH_LAUNCH(bh::zero_insert_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   return bh_check_launch("zero_insert_kernel");
 }

@@ -42,11 +42,12 @@ their engines and wait at the barrier).  `--single-engine` makes that the
 headline.  The GPU is driven exclusively through libband_hip.so.
 
 Roofline: every launch of the profiled passes (the same models at the job
-batch) is timed with HIP events in program order (HipModelExecutor::
-ProfileSubgraph); an equal chain of empty launches gives the per-launch
-floor (dispatch + gap) that is subtracted for a kernel-only duration, the
-quantity rocprofv3 reports.  The dominant kernel (largest total time) and
-the next two are reported with their algorithmic bytes and ops per launch.
+batch) is timed in program order on the executor's stream
+(HipModelExecutor::ProfileSubgraph): each kernel carries HIP events that
+hold its own dispatch begin / end timestamps (hipExtLaunchKernel), the
+kernel-only duration rocprofv3's kernel trace reports.  The dominant kernel
+(largest total time) and the next two are reported with their algorithmic
+bytes and ops per launch.
 
 Prints ONE JSON line on rank 0.  `--profile-only` runs just the profiled
 passes (for rocprofv3 kernel traces / PMC passes of exactly those launches).
@@ -331,15 +332,13 @@ def profile_roofline(args, D, models, paths):
     M = len(models)
     by_k, floors = {}, []
     for ex, key in execs:
-        rows, floor_us = ex.ProfileSubgraph(key, iters=args.profile_iters, with_floor=True)
-        floors.append(floor_us)
+        rows, empty_us = ex.ProfileSubgraph(key, iters=args.profile_iters, with_floor=True)
+        floors.append(empty_us)
         for r in rows:
             # group by kernel symbol ("conv_mfma_kernel+add" is conv_mfma_kernel
             # with its residual epilogue), as rocprofv3 reports them
-            k = by_k.setdefault(r["kernel"].split("+")[0], dict(us=0.0, event_us=0.0, bytes=0.0, ops=0.0,
-                                                                launches=0))
-            k["event_us"] += r["ms"] * 1e3
-            k["us"] += max(r["ms"] * 1e3 - floor_us, 0.0)
+            k = by_k.setdefault(r["kernel"].split("+")[0], dict(us=0.0, bytes=0.0, ops=0.0, launches=0))
+            k["us"] += r["ms"] * 1e3
             k["bytes"] += r["alg_bytes"]
             k["ops"] += r["alg_ops"]
             k["launches"] += 1
@@ -373,14 +372,13 @@ def profile_roofline(args, D, models, paths):
                 "traffic_source": pmc.get("_file") if t else
                 "null: no PMC file measured on this kernel tree (tag %s) at pass batch %d" % (tag, B),
                 "alg_bytes_per_launch": b, "alg_ops_per_launch": o, "avg_launch_us": us,
-                "avg_launch_us_event": k["event_us"] / k["launches"],
                 "launches_per_pass": k["launches"] / M, "share_of_kernel_time": k["us"] / total_us,
                 "mfma_i8_tops": o / (us * 1e-6) / 1e12, "mfma_i8_frac": o / (us * 1e-6) / 5.0e15}
 
     top = [roof(n, k) for n, k in ranked[:3]]
     dom = dict(top[0])
-    dom.update(profiled_pass_batch=B, launch_floor_us=float(np.mean(floors)), kernel_source_tag=tag,
-               next_kernels=top[1:])
+    dom.update(profiled_pass_batch=B, timing="per-dispatch begin/end timestamps (hipExtLaunchKernel events)",
+               empty_kernel_us=float(np.mean(floors)), kernel_source_tag=tag, next_kernels=top[1:])
     return dom, dict(gpu_us_per_inference=total_us / M / B, device_us=device_us), execs
 
 
@@ -388,11 +386,9 @@ def profile_only(args, D, models, paths):
     """only the profiled passes (graph replays of the batch-B variants),
     for rocprofv3: its per-kernel averages then describe exactly the launches
     the roofline line reports"""
-    execs, B = profile_executors(args, D, models, paths)
-    for ex, key in execs:
-        ex.TimeSubgraph(key, iters=max(10, args.profile_iters))
     dom, dev, _ = profile_roofline(args, D, models, paths)
-    print(json.dumps({"profile_only": True, "pass_batch": B, "roofline": dom, "device": dev}), flush=True)
+    print(json.dumps({"profile_only": True, "pass_batch": profiled_batch(args), "roofline": dom, "device": dev}),
+          flush=True)
 
 
 def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch, seed_offset=0):

@@ -110,12 +110,13 @@ int bhx_run_jobs(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mas
 /* --- extensions (measurement / tuning; not part of Band's interface) --- */
 int bhx_executor_set_graph(bhx_executor* e, int enabled);
 int bhx_executor_device(bhx_executor* e, int* ordinal);
-/* per-launch HIP-event timing of a prepared subgraph: the launch sequence is
- * queued behind a spin kernel and runs once in program order with an event
- * between consecutive launches (each kernel sees a real pass's cache state);
- * averaged over iters.  *floor_us (may be NULL) = per-launch time of the same
- * chain of empty launches: subtract it from a launch's figure for a
- * kernel-only duration comparable with rocprofv3's. */
+/* per-launch timing of a prepared subgraph: the launch sequence is queued
+ * behind a spin kernel and runs once in program order (each kernel sees a
+ * real pass's cache state); every kernel carries its dispatch begin / end
+ * timestamps (hipExtLaunchKernel events), i.e. the kernel-only duration
+ * rocprofv3's kernel trace reports; averaged over iters.  *floor_us (may be
+ * NULL) = the same figure for an empty single-wave kernel: the fixed
+ * dispatch cost inside every duration. */
 int bhx_profile_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters,
                          bhx_op_timing* out, int cap, int* n, double* floor_us);
 /* A Band GPU worker serving a mixed request stream (BASELINE C3): worker

@@ -94,6 +94,11 @@ int bh_spin_us(bh_stream_t s, int us);
 /* one empty single-wave launch (profilers time chains of them to measure
  * the dispatch + gap an event pair adds around a real launch) */
 int bh_empty_launch(bh_stream_t s);
+/* this thread's next kernel launches carry dispatch timestamps: the first
+ * kernel records `start` at its begin, every kernel records `stop` at its end
+ * (hipExtLaunchKernel); bh_profile_events(NULL, NULL) turns it off.
+ * Returns the number of kernels the previous setting timed. */
+int bh_profile_events(bh_event_t start, bh_event_t stop);
 
 /* ---- op parameter blocks ------------------------------------------------ */
 
@@ -139,7 +144,13 @@ typedef struct bh_conv_params {
    * the kernels may then evaluate TFLite's two-step requantisation with one
    * 64-bit multiply-add and shifts (same results, fewer instructions) */
   int32_t requant_fast;
+  /* kernel choice: BH_CONV_AUTO (by shape), or force one form where the
+   * layer allows it (parity tests cover every form; A-B timing) */
+  int32_t kernel_hint;
 } bh_conv_params;
+#define BH_CONV_AUTO 0
+#define BH_CONV_MFMA 1 /* conv_mfma_kernel: per-wave fragments from L2, split-K deep layers */
+#define BH_CONV_GEMM 2 /* conv_gemm_kernel: LDS-staged GEMM (1x1 s1, int8 in, symmetric filters) */
 
 /* DEPTHWISE_CONV_2D.  weights: int8-domain [k_h][k_w][out_c] (TFLite layout
  * [1,kh,kw,oc] with XOR applied for uint8 filters).  Exact int32 math

@@ -30,7 +30,7 @@ class ConvCase:
                  taps=True, kernel_hint=0):
         self.dtype = dtype
         self.taps = taps
-        self.kernel_hint = kernel_hint  # depthwise: BH_DW_* (0 = the shape's own route)
+        self.kernel_hint = kernel_hint  # BH_DW_* / BH_CONV_* (0 = the shape's own route)
         self.requant_fast = requant_fast
         self.depthwise = depthwise
         self.dm = dm
@@ -157,6 +157,7 @@ class ConvCase:
                                                int(np.abs(self.bias.astype(np.int64)).max()))
             # requant_fast: None = what the executor would choose, else forced
             p.requant_fast = fast if self.requant_fast is None else int(self.requant_fast and fast)
+            p.kernel_hint = self.kernel_hint
         return p
 
 

@@ -39,6 +39,25 @@ def test_conv1x1_rows_batched(gpu_lib, b, spatial, ic, oc, dtype):
     np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
 
 
+# the LDS-staged GEMM (conv_gemm_kernel, forced with BH_CONV_GEMM = 2) beside
+# conv_mfma_kernel (BH_CONV_MFMA = 1) on the batched deep / wide 1x1 layers:
+# both configurations (128x128 over 8 waves, 64x64 over 8 waves), M / N / K tails (K < 64, K % 64 != 0,
+# N not a tile multiple, N % 4 != 0), both requantisation paths
+@pytest.mark.parametrize("b,spatial,ic,oc", [
+    (6, 14, 512, 1024), (24, 14, 960, 160), (8, 7, 1280, 546), (6, 14, 576, 273), (1, 14, 16, 24),
+    (3, 9, 48, 20), (6, 14, 1024, 17), (2, 7, 160, 960), (24, 7, 320, 1280), (5, 13, 96, 64),
+    (24, 14, 512, 1024), (24, 14, 192, 1000)])
+def test_conv1x1_gemm_vs_mfma(gpu_lib, b, spatial, ic, oc):
+    rng = np.random.default_rng(6000 + b + spatial + ic + oc)
+    c = ConvCase(rng, b, spatial, spatial, ic, oc, 1, 1, act=3)
+    ref = c.oracle()
+    for hint in (2, 1):  # BH_CONV_GEMM, BH_CONV_MFMA
+        c.kernel_hint = hint
+        for fast in (None, False):
+            c.requant_fast = fast
+            np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="hint %d fast %s" % (hint, fast))
+
+
 # the RGB stem kernel (conv_stem_kernel: aligned row gathers + byte path at
 # the image's left / right edge and the tensor's end): SAME / VALID padding,
 # stride 1 / 2, odd widths, batch, uint8 (filter zero point), both

@@ -6,7 +6,7 @@ Usage: python tools/mix_breakdown.py [--batch 24] [--iters 20] [--top 40]
 Prepares each C3 model (MobileNetV2, SSD-MobileNetV2, DeepLabV3,
 PoseNet; 224x224 int8, the bench's synthetic weights) with a leading batch
 of B, times every launch with HIP events in program order
-(HipModelExecutor::ProfileSubgraph, the launch floor subtracted) and prints
+(HipModelExecutor::ProfileSubgraph: per-dispatch begin / end timestamps) and prints
 the launches sorted by time with their layer shape, kernel and the
 algorithmic rates they imply; then a per-kernel summary.  This is where the
 next kernel work is chosen.
@@ -49,8 +49,7 @@ def main():
         ex.SetUseGraph(False)
         eager_us = ex.TimeSubgraph(key, iters=20)
         ex.SetUseGraph(True)
-        ev_sum = sum(r["ms"] for r in prof) * 1e3
-        ko_sum = sum(max(r["ms"] * 1e3 - floor, 0.0) for r in prof)
+        ko_sum = sum(r["ms"] for r in prof) * 1e3
         for r in prof:
             op = desc["ops"][r["op_index"]]
             ins = desc["tensors"][op["inputs"][0]]["shape"] if op["inputs"] else []
@@ -59,12 +58,12 @@ def main():
             if op["builtin"] in (3, 4) and len(op["inputs"]) > 1:
                 w = desc["tensors"][op["inputs"][1]]["shape"]
                 extra = "k%dx%d" % (w[1], w[2])
-            us = max(r["ms"] * 1e3 - floor, 1e-3)
+            us = max(r["ms"] * 1e3, 1e-3)
             rows.append(dict(model=name, op=r["op_index"], kernel=r["kernel"], ins=ins, outs=outs, extra=extra,
                              us=us, bytes=r["alg_bytes"], ops=r["alg_ops"]))
-        print("%-28s graph replay %.1f us per pass (%.2f per inference), eager %.1f; %d launches; event sum %.1f, "
-              "floor %.2f us/launch, kernel-only sum %.1f" % (name, dev_us, dev_us / a.batch, eager_us, len(prof),
-                                                             ev_sum, floor, ko_sum), flush=True)
+        print("%-28s graph replay %.1f us per pass (%.2f per inference), eager %.1f; %d launches; "
+              "empty kernel %.2f us, kernel-only sum %.1f" % (name, dev_us, dev_us / a.batch, eager_us, len(prof),
+                                                             floor, ko_sum), flush=True)
         keep.append((m, ex))
     tot = sum(r["us"] for r in rows)
     print("\nsum of kernel-only launch times: %.1f us for one pass of every model (batch %d)" % (tot, a.batch))

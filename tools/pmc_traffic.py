@@ -9,7 +9,10 @@ WRITE_SIZE, each with --kernel-trace --output-format csv), as
     global loads; other widths are uncalibrated, so this is an estimate);
   * Infinity-Cache hits are counted, not excluded.
 
-usage: tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <out.json>
+usage: tools/pmc_traffic.py <fetch_pass_dir> <write_pass_dir> <out.json> [--batch B] [--config TEXT]
+The output carries a _meta record: the kernel-source tag of this tree
+(bench.kernel_source_tag) and the pass batch, so bench.py only reports the
+traffic for the kernels and batch it was measured on.
 Groups dispatches by kernel symbol (bh::<name><...>(...) -> <name>) and
 writes per-kernel means per dispatch.
 """
@@ -40,9 +43,11 @@ def load(d, counter):
     return {k: (len(v), sum(v.values()) / max(len(v), 1)) for k, v in per.items()}
 
 
-def main(fd, wd, out):
+def main(fd, wd, out, batch=24, config=""):
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import kernel_source_tag
     fetch = load(fd, "FETCH_SIZE")
-    write = load(wd, "WRITE_SIZE")
+    write = load(wd, "WRITE_SIZE") if wd != "-" else {}  # "-": a FETCH_SIZE pass only
     res = {}
     for k in sorted(set(fetch) | set(write)):
         nf, f = fetch.get(k, (0, 0.0))
@@ -51,9 +56,19 @@ def main(fd, wd, out):
                       traffic_bytes_per_launch=2.0 * f * 1024.0 + w * 1024.0)
         print("%-28s fetch %9.1f KB  write %9.1f KB  -> %10.0f B/launch (x2 fetch)  [%d/%d dispatches]"
               % (k, f, w, res[k]["traffic_bytes_per_launch"], nf, nw))
+    res["_meta"] = dict(kernel_source_tag=kernel_source_tag(), pass_batch=batch, config=config,
+                        fetch_correction="FETCH_SIZE x2 (gfx950, MI355X_MICROARCH.md HBM section)")
     with open(out, "w") as fo:
         json.dump(res, fo, indent=1, sort_keys=True)
 
 
 if __name__ == "__main__":
-    main(*sys.argv[1:4])
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("fetch_dir")
+    ap.add_argument("write_dir")
+    ap.add_argument("out")
+    ap.add_argument("--batch", type=int, default=24)
+    ap.add_argument("--config", default="")
+    a = ap.parse_args()
+    main(a.fetch_dir, a.write_dir, a.out, a.batch, a.config)

@@ -166,6 +166,67 @@ __global__ __launch_bounds__(256) void resize_bilinear_kernel(bh_resize_bilinear
   ((int8_t*)p.output)[i] = (int8_t)((s + rnd) / (1 << 20));
 }
 
+// Row form (DeepLab's 14x14 -> 224x224 logits upsample: 25 MB out per
+// batch-24 pass, which the byte-per-thread kernel spread over ~400k waves).
+// One workgroup per output row (image n, row y): the two input rows it
+// blends (y0, y1) and the column table are staged in LDS once; each thread
+// then produces 16 consecutive bytes of the row (x, channel advanced
+// incrementally, no division in the loop) and stores them as one 16-byte
+// store.  The blend is TFLite's four-term sum, factored exactly (integer
+// arithmetic) as (1-fy)(v00(1-fx) + v01 fx) + fy(v10(1-fx) + v11 fx).
+constexpr int kRzRow = 8192;   // staged input row bytes (in_w * channels)
+constexpr int kRzCols = 1024;  // staged output columns
+
+__global__ __launch_bounds__(256) void resize_bilinear_rows_kernel(bh_resize_bilinear_params p, FastDiv chans,
+                                                                   int vec_ok) {
+  __shared__ __attribute__((aligned(16))) int8_t rows[2][kRzRow];
+  __shared__ int xt[3 * kRzCols];
+  const int y = blockIdx.x % p.out_h;
+  const int n = blockIdx.x / p.out_h;
+  const int C = p.channels;
+  const int in_row = p.in_w * C;
+  const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1], iy = p.y_tab[3 * y + 2];
+  const int8_t* src0 = (const int8_t*)p.input + ((long)n * p.in_h + y0) * in_row;
+  const int8_t* src1 = (const int8_t*)p.input + ((long)n * p.in_h + y1) * in_row;
+  for (int i = threadIdx.x; i < in_row; i += 256) {
+    rows[0][i] = src0[i];
+    rows[1][i] = src1[i];
+  }
+  for (int i = threadIdx.x; i < 3 * p.out_w; i += 256) xt[i] = p.x_tab[i];
+  __syncthreads();
+  constexpr int32_t one = 1 << 10;
+  const int32_t fy = iy - one * y0;
+  const int row_bytes = p.out_w * C;
+  int8_t* dst = (int8_t*)p.output + ((long)n * p.out_h + y) * row_bytes;
+  for (int f0 = threadIdx.x * 16; f0 < row_bytes; f0 += 256 * 16) {
+    int x = (int)chans.div((uint32_t)f0);
+    int ch = f0 - x * C;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      if (f0 + b < row_bytes) {
+        const int x0 = xt[3 * x], x1 = xt[3 * x + 1];
+        const int32_t fx = xt[3 * x + 2] - one * x0;
+        const int32_t h0 = (int32_t)rows[0][x0 * C + ch] * (one - fx) + (int32_t)rows[0][x1 * C + ch] * fx;
+        const int32_t h1 = (int32_t)rows[1][x0 * C + ch] * (one - fx) + (int32_t)rows[1][x1 * C + ch] * fx;
+        const int32_t s = h0 * (one - fy) + h1 * fy;
+        const int32_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
+        const uint32_t v = (uint32_t)(uint8_t)(int8_t)((s + rnd) / (1 << 20));
+        w[b >> 2] |= v << (8 * (b & 3));
+      }
+      if (++ch == C) {
+        ch = 0;
+        ++x;
+      }
+    }
+    if (vec_ok && f0 + 16 <= row_bytes) {
+      *(v4i*)(dst + f0) = (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    } else {
+      for (int b = 0; b < 16 && f0 + b < row_bytes; ++b) dst[f0 + b] = (int8_t)(w[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
 // ---- softmax ----------------------------------------------------------------
 // One thread per row; the float operations are issued exactly as the
 // reference's loop runs them (no contraction: explicit _rn intrinsics).
@@ -361,6 +422,14 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
   if (total >= INT32_MAX || (long)p.batch * p.in_h * p.in_w * p.channels >= INT32_MAX) {
     bh_set_last_error("bh_resize_bilinear_i8: tensor too large for 32-bit indexing");
     return BH_EINVAL;
+  }
+  if ((long)p.in_w * p.channels <= bh::kRzRow && p.out_w <= bh::kRzCols &&
+      (long)p.batch * p.out_h < INT32_MAX) {
+    // 16-byte stores when every output row starts 16-byte aligned
+    const int vec_ok = ((p.out_w * p.channels) % 16 == 0 && ((uintptr_t)p.output & 15) == 0) ? 1 : 0;
+    BH_LAUNCH(bh::resize_bilinear_rows_kernel, dim3(p.batch * p.out_h), dim3(256), 0, (hipStream_t)s, p,
+              bh::FastDiv(p.channels), vec_ok);
+    return bh_check_launch("resize_bilinear_rows_kernel");
   }
   bh::ResizeDivs dv;
   dv.units = bh::FastDiv(p.channels);

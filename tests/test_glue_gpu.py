@@ -129,6 +129,7 @@ def test_pad(gpu_lib, shape, pads, elem):
 
 @pytest.mark.parametrize("ih,iw,oh,ow,c,ac,hp", [
     (5, 5, 10, 10, 8, 0, 0), (10, 10, 20, 20, 3, 0, 1), (7, 9, 13, 4, 4, 1, 0), (6, 6, 3, 3, 5, 0, 1),
+    (14, 14, 224, 224, 21, 0, 0), (14, 14, 224, 224, 16, 1, 0), (3, 5, 37, 41, 7, 0, 1), (2, 515, 3, 1030, 1, 0, 0),
 ])
 def test_resize(gpu_lib, ih, iw, oh, ow, c, ac, hp):
     from band_amd import _abi

@@ -85,7 +85,8 @@ class ConcatParams(ctypes.Structure):
 
 class PadParams(ctypes.Structure):
     _fields_ = [("elem_bytes", c_int), ("in_shape", c_int * 4), ("pad_before", c_int * 4),
-                ("pad_after", c_int * 4), ("value", ctypes.c_uint32), ("input", c_void_p), ("output", c_void_p)]
+                ("pad_after", c_int * 4), ("value", ctypes.c_uint32), ("input", c_void_p), ("output", c_void_p),
+                ("mode", c_int32)]
 
 
 class ResizeNearestParams(ctypes.Structure):

@@ -1,5 +1,7 @@
 #include "backend/hip/cpu_kernels.h"
 
+#include "backend/hip/quant.h"
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -365,6 +367,25 @@ void CpuConcat(const bh_concat_params& p) {
   }
 }
 
+namespace {
+// MIRROR_PAD source index (TFLite 2.9.2 mirror_pad.cc GetInputDimension;
+// mode 1 REFLECT skips the edge element, 2 SYMMETRIC repeats it)
+int MirrorIndex(int i, int before, int n, int mode) {
+  const int offset = mode == 1 ? 1 : 0;
+  if (i < before) {
+    const int orig = before + offset - 1;
+    return orig - std::min(i, orig - offset);
+  }
+  i -= before;
+  if (i >= n) {
+    i -= n;
+    const int orig = n - (1 + offset);
+    return orig - std::min(i, orig);
+  }
+  return i;
+}
+}  // namespace
+
 void CpuPad(const bh_pad_params& p) {
   int os[4];
   for (int d = 0; d < 4; ++d) os[d] = p.in_shape[d] + p.pad_before[d] + p.pad_after[d];
@@ -382,7 +403,16 @@ void CpuPad(const bh_pad_params& p) {
                     ic = c - p.pad_before[3];
           const bool inside = ib >= 0 && ib < p.in_shape[0] && iy >= 0 && iy < p.in_shape[1] && ix >= 0 &&
                               ix < p.in_shape[2] && ic >= 0 && ic < p.in_shape[3];
-          if (inside) {
+          if (p.mode) {
+            const long src = ((static_cast<long>(MirrorIndex(b, p.pad_before[0], p.in_shape[0], p.mode)) *
+                                   p.in_shape[1] +
+                               MirrorIndex(y, p.pad_before[1], p.in_shape[1], p.mode)) *
+                                  p.in_shape[2] +
+                              MirrorIndex(x, p.pad_before[2], p.in_shape[2], p.mode)) *
+                                 p.in_shape[3] +
+                             MirrorIndex(c, p.pad_before[3], p.in_shape[3], p.mode);
+            std::memcpy(out + i * eb, in + src * eb, eb);
+          } else if (inside) {
             const long src = ((static_cast<long>(ib) * p.in_shape[1] + iy) * p.in_shape[2] + ix) * p.in_shape[3] + ic;
             std::memcpy(out + i * eb, in + src * eb, eb);
           } else {
@@ -536,7 +566,10 @@ void CpuEltwiseF32(const bh_eltwise_f32_params& p) {
     const long i1 = t2 % so[1], i0 = t2 / so[1];
     const float a = p.a[index(p.shape_a, i0, i1, i2, i3)];
     const float b = p.b[index(p.shape_b, i0, i1, i2, i3)];
-    const float v = p.kind == BH_ELTF_ADD ? a + b : (p.kind == BH_ELTF_SUB ? a - b : a * b);
+    const float v = p.kind == BH_ELTF_ADD   ? a + b
+                    : p.kind == BH_ELTF_SUB ? a - b
+                    : p.kind == BH_ELTF_MUL ? a * b
+                                            : (a - b) * (a - b);  // SQUARED_DIFFERENCE
     p.out[i] = ClampF(v, p.act_min, p.act_max);
   }
 }
@@ -566,7 +599,9 @@ void CpuPoolF32(const bh_pool_f32_params& p) {
 
 void CpuUnaryF32(int kind, const float* in, float* out, long n, float lo, float hi) {
   for (long i = 0; i < n; ++i)
-    out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + std::exp(-in[i])) : ClampF(in[i], lo, hi);
+    out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + std::exp(-in[i]))
+             : kind == BH_UNARY_RSQRT  ? 1.0f / std::sqrt(in[i])
+                                       : ClampF(in[i], lo, hi);
 }
 
 void CpuSoftmaxF32(const float* in, float* out, long rows, int depth, float beta) {
@@ -660,6 +695,33 @@ void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool) {
     p.out_scores[k] = max_score[selected[k]];
   }
   p.out_num[0] = static_cast<float>(selected.size());
+}
+
+void CpuMean(const CpuMeanParams& p, CpuPool& pool) {
+  pool.ParallelFor(p.outer * p.inner, [&](long lo, long hi) {
+    for (long o = lo; o < hi; ++o) {
+      const long a = o / p.inner, c = o % p.inner;
+      const long base = a * p.reduce * p.inner + c;
+      if (p.type == 0) {
+        const float* x = static_cast<const float*>(p.input);
+        float s = 0.f;
+        for (long r = 0; r < p.reduce; ++r) s += x[base + r * p.inner];
+        static_cast<float*>(p.output)[o] = s / static_cast<float>(p.reduce);
+        continue;
+      }
+      int32_t acc = 0;
+      if (p.type == 1) {
+        const int8_t* x = static_cast<const int8_t*>(p.input);
+        for (long r = 0; r < p.reduce; ++r) acc += x[base + r * p.inner];
+      } else {
+        const uint8_t* x = static_cast<const uint8_t*>(p.input);
+        for (long r = 0; r < p.reduce; ++r) acc += x[base + r * p.inner];
+      }
+      acc = MultiplyByQuantizedMultiplier(acc, p.multiplier, p.shift) + p.bias;
+      if (p.type == 1) static_cast<int8_t*>(p.output)[o] = static_cast<int8_t>(std::min(std::max(acc, -128), 127));
+      else static_cast<uint8_t*>(p.output)[o] = static_cast<uint8_t>(std::min(std::max(acc, 0), 255));
+    }
+  });
 }
 
 }  // namespace hip

@@ -86,5 +86,19 @@ struct CpuDetectionParams {
 };
 void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool);
 
+// MEAN over a contiguous run of axes: the input viewed as [outer][reduce]
+// [inner] and reduced over the middle.  Quantized (8-bit): TFLite 2.9.2
+// optimized_integer_ops::Mean / optimized_ops::Mean (4-D, keep_dims, axes
+// {1, 2}): acc = sum; MultiplyByQuantizedMultiplier(acc, multiplier, shift)
+// + bias, clamped to the type's range.  Float: sum / count.
+struct CpuMeanParams {
+  long outer, reduce, inner;
+  int type;  // 0 float32, 1 int8, 2 uint8
+  int32_t multiplier, shift, bias;
+  const void* input;
+  void* output;
+};
+void CpuMean(const CpuMeanParams& p, CpuPool& pool);
+
 }  // namespace hip
 }  // namespace band

@@ -167,7 +167,7 @@ bool IsFloatOp(const TflModel& m, const TflOperator& op) {
   switch (op.builtin) {
     case kTflConv2D: case kTflDepthwiseConv2D: case kTflFullyConnected: case kTflAdd: case kTflSub: case kTflMul:
     case kTflAveragePool2D: case kTflMaxPool2D: case kTflRelu: case kTflRelu6: case kTflReluN1To1:
-    case kTflLogistic: case kTflSoftmax:
+    case kTflLogistic: case kTflSoftmax: case kTflSquaredDifference: case kTflRsqrt:
       return t == DataType::kFloat32;
     case kTflDequantize:
       return t == DataType::kFloat16;
@@ -205,7 +205,8 @@ bool FloatSupports(const TflModel& m, const TflOperator& op, std::string* why) {
     }
     case kTflAdd:
     case kTflSub:
-    case kTflMul: {
+    case kTflMul:
+    case kTflSquaredDifference: {
       if (op.inputs.size() != 2 || op.inputs[1] < 0) return no("binary op needs 2 inputs");
       const TflTensor& b = m.tensors[op.inputs[1]];
       if (b.type != DataType::kFloat32 || in.shape.size() > 4 || b.shape.size() > 4 || out.shape.size() > 4)
@@ -224,8 +225,72 @@ bool FloatSupports(const TflModel& m, const TflOperator& op, std::string* why) {
     case kTflSoftmax:
       return !in.shape.empty() ? true : no("rank >= 1");
     default:
-      return true;  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC
+      return true;  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC / RSQRT
   }
+}
+
+// MIRROR_PAD paddings (constant [rank][2] int32 / int64) and mode
+// (MirrorPadOptions.mode: 0 REFLECT, 1 SYMMETRIC -> bh_pad_params.mode 1 / 2)
+bool MirrorPadArgs(const TflModel& m, const TflOperator& op, std::vector<int64_t>* pads, int* mode) {
+  if (op.inputs.size() < 2 || op.inputs[1] < 0) return false;
+  const TflTensor& in = m.tensors[op.inputs[0]];
+  const TflTensor& pt = m.tensors[op.inputs[1]];
+  if (!pt.is_const() || (pt.type != DataType::kInt32 && pt.type != DataType::kInt64)) return false;
+  const int rank = static_cast<int>(in.shape.size());
+  const size_t eb = pt.type == DataType::kInt64 ? 8 : 4;
+  if (rank < 1 || rank > 4 || pt.data_size < 2 * rank * eb) return false;
+  pads->assign(2 * static_cast<size_t>(rank), 0);
+  for (int i = 0; i < 2 * rank; ++i) {
+    if (eb == 8) {
+      int64_t v;
+      std::memcpy(&v, pt.data + 8 * i, 8);
+      (*pads)[i] = v;
+    } else {
+      int32_t v;
+      std::memcpy(&v, pt.data + 4 * i, 4);
+      (*pads)[i] = v;
+    }
+  }
+  *mode = op.options.valid() && op.options.Int8(0, 0) == 1 ? 2 : 1;
+  for (int dd = 0; dd < rank; ++dd) {
+    const int64_t lim = in.shape[dd] - (*mode == 1 ? 1 : 0);
+    if ((*pads)[2 * dd] < 0 || (*pads)[2 * dd + 1] < 0 || (*pads)[2 * dd] > lim || (*pads)[2 * dd + 1] > lim)
+      return false;
+  }
+  return true;
+}
+
+// MEAN: the reduced axes (constant int32, negatives resolved) must be one
+// contiguous run; 8-bit tensors only in the form TFLite 2.9.2 runs through
+// optimized_integer_ops::Mean / optimized_ops::Mean (4-D, keep_dims, axes
+// {1, 2}), the one restated by CpuMean.
+bool MeanArgs(const TflModel& m, const TflOperator& op, long* outer, long* reduce, long* inner) {
+  if (op.builtin != kTflMean || op.inputs.size() < 2 || op.inputs[1] < 0 || op.outputs.empty()) return false;
+  const TflTensor& in = m.tensors[op.inputs[0]];
+  const TflTensor& out = m.tensors[op.outputs[0]];
+  const TflTensor& ax = m.tensors[op.inputs[1]];
+  if (!ax.is_const() || ax.type != DataType::kInt32 || out.type != in.type) return false;
+  const int rank = static_cast<int>(in.shape.size());
+  std::set<int> axes;
+  for (size_t i = 0; i * 4 < ax.data_size; ++i) {
+    int32_t v;
+    std::memcpy(&v, ax.data + 4 * i, 4);
+    if (v < 0) v += rank;
+    if (v < 0 || v >= rank) return false;
+    axes.insert(v);
+  }
+  if (axes.empty() || *axes.rbegin() - *axes.begin() + 1 != static_cast<int>(axes.size())) return false;
+  if (in.type != DataType::kFloat32) {
+    const bool keep = op.options.valid() && op.options.Int8(0, 0) != 0;
+    if (!IsQ8(in.type) || !HasQ(in) || !HasQ(out) || rank != 4 || !keep || axes != std::set<int>{1, 2}) return false;
+  }
+  *outer = *reduce = *inner = 1;
+  for (int dd = 0; dd < rank; ++dd) {
+    if (dd < *axes.begin()) *outer *= in.shape[dd];
+    else if (dd > *axes.rbegin()) *inner *= in.shape[dd];
+    else *reduce *= in.shape[dd];
+  }
+  return *reduce > 0 && out.num_elements() == static_cast<size_t>(*outer * *inner);
 }
 }  // namespace
 
@@ -336,6 +401,14 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
       if (in.shape.size() != 4 || out.shape.size() != 4 || out.type != in.type || eb == 0) return no("4-D only");
       return true;
     }
+    case kTflMirrorPad: {
+      const size_t eb = GetDataTypeBytes(in.type);
+      std::vector<int64_t> pads;
+      int mode = 0;
+      if ((eb != 1 && eb != 4) || out.type != in.type) return no("1/4-byte types");
+      if (!MirrorPadArgs(m, op, &pads, &mode)) return no("constant paddings within the input, rank <= 4");
+      return true;
+    }
     case kTflTransposeConv: {
       // inputs: output_shape (const int32 [4]), weights OHWI, input, [bias]
       if (op.inputs.size() < 3 || op.inputs[1] < 0 || op.inputs[2] < 0) return no("missing operands");
@@ -405,6 +478,8 @@ bool DetectionSupported(const TflModel& m, const TflOperator& op, CpuDetectionPa
 bool HipModelExecutor::CpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   if (GpuSupports(m, op, nullptr)) return true;
   if (DetectionSupported(m, op, nullptr)) return true;
+  long o, r, i;
+  if (MeanArgs(m, op, &o, &r, &i)) return true;
   return GpuSupports(m, op, why);
 }
 
@@ -725,11 +800,16 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
       return absl::OkStatus();
     }
     case kTflPad:
-    case kTflPadV2: {
+    case kTflPadV2:
+    case kTflMirrorPad: {
       const TflTensor& pt = T(op.inputs[1]);
       const int rank = static_cast<int>(in.shape.size());
       std::vector<int64_t> pads(2 * static_cast<size_t>(rank), 0);
-      for (size_t i = 0; i < pads.size() && i * (pt.type == DataType::kInt64 ? 8 : 4) < pt.data_size; ++i) {
+      int mirror = 0;
+      if (op.builtin == kTflMirrorPad && !MirrorPadArgs(d, op, &pads, &mirror))
+        return absl::InternalError("MIRROR_PAD arguments");
+      for (size_t i = 0; !mirror && i < pads.size() && i * (pt.type == DataType::kInt64 ? 8 : 4) < pt.data_size;
+           ++i) {
         if (pt.type == DataType::kInt64) {
           int64_t v;
           std::memcpy(&v, pt.data + 8 * i, 8);
@@ -757,6 +837,7 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
         value = static_cast<uint32_t>(Zp(out)) & 0xffu;  // quantized PAD pads with the output zero point
       }
       p.value = value;
+      p.mode = mirror;
       p.input = in_ptr;
       p.output = out_ptr;
       L->kind = Launch::kPad;
@@ -1353,13 +1434,17 @@ absl::Status HipModelExecutor::LowerFloat(const HipModel& model, int oi, void* i
     }
     case kTflAdd:
     case kTflSub:
-    case kTflMul: {
+    case kTflMul:
+    case kTflSquaredDifference: {
       const TflTensor& bt = T(op.inputs[1]);
       void* b_ptr = nullptr;
       RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
       bh_eltwise_f32_params& p = L->eltf;
       p = bh_eltwise_f32_params{};
-      p.kind = op.builtin == kTflAdd ? BH_ELTF_ADD : (op.builtin == kTflSub ? BH_ELTF_SUB : BH_ELTF_MUL);
+      p.kind = op.builtin == kTflAdd   ? BH_ELTF_ADD
+               : op.builtin == kTflSub ? BH_ELTF_SUB
+               : op.builtin == kTflMul ? BH_ELTF_MUL
+                                       : BH_ELTF_SQDIFF;
       Shape4(in.shape, p.shape_a);
       Shape4(bt.shape, p.shape_b);
       Shape4(out.shape, p.shape_o);
@@ -1402,10 +1487,12 @@ absl::Status HipModelExecutor::LowerFloat(const HipModel& model, int oi, void* i
       L->src = in_ptr;
       L->dst = out_ptr;
       return absl::OkStatus();
-    default: {  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC
+    default: {  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC / RSQRT
       L->kind = Launch::kUnaryF32;
       L->kernel = "unary_f32_kernel";
-      L->unary_kind = op.builtin == kTflLogistic ? BH_UNARY_LOGISTIC : BH_UNARY_CLAMP;
+      L->unary_kind = op.builtin == kTflLogistic ? BH_UNARY_LOGISTIC
+                      : op.builtin == kTflRsqrt  ? BH_UNARY_RSQRT
+                                                 : BH_UNARY_CLAMP;
       L->lo = op.builtin == kTflReluN1To1 ? -1.f : 0.f;
       L->hi = op.builtin == kTflRelu6 ? 6.f : (op.builtin == kTflReluN1To1 ? 1.f : std::numeric_limits<float>::infinity());
       L->count = static_cast<long>(in.num_elements());
@@ -1670,6 +1757,28 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     p.out_num = static_cast<float*>(outs[3]);
     L.kind = Launch::kDetectionPost;
     L.kernel = "detection_postprocess_host";
+  } else if (op.builtin == kTflMean) {
+    // MEAN (CPU worker only: CpuSupports)
+    CpuMeanParams& p = L.mean;
+    p = CpuMeanParams{};
+    if (!MeanArgs(d, op, &p.outer, &p.reduce, &p.inner)) return absl::InternalError("unsupported MEAN");
+    p.type = in.type == DataType::kFloat32 ? 0 : (in.type == DataType::kInt8 ? 1 : 2);
+    if (p.type) {
+      // optimized_integer_ops::Mean (TFLite 2.9.2): the float products as
+      // written there, then QuantizeMultiplier of the float scale
+      const float in_scale = Scale(in), out_scale = Scale(out);
+      const float n = static_cast<float>(p.reduce);
+      p.bias = Zp(out) - static_cast<int32_t>(Zp(in) * in_scale / out_scale);
+      const float real_scale = in_scale / (n * out_scale);
+      int shift = 0;
+      QuantizeMultiplier(static_cast<double>(real_scale), &p.multiplier, &shift);
+      p.shift = shift;
+    }
+    p.input = in_ptr;
+    p.output = out_ptr;
+    L.kind = Launch::kMean;
+    L.kernel = "mean_host";
+    L.alg_bytes = static_cast<double>(meta_[op.inputs[0]]->bytes + meta_[op.outputs[0]]->bytes);
   } else if (op.builtin == kTflTransposeConv) {
     RETURN_STATUS_IF(LowerTransposeConv(model, oi, out_ptr, ckey, sg, &L));
   } else if (op.builtin != kTflReshape && op.builtin != kTflSqueeze) {
@@ -1912,7 +2021,8 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
       rc = bh_softmax_f32(static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.depth, l.beta,
                           stream_);
       break;
-    case Launch::kDetectionPost: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
+    case Launch::kDetectionPost:
+    case Launch::kMean: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }
@@ -1974,6 +2084,7 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
         CpuSoftmaxF32(static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.depth, l.beta);
         break;
       case Launch::kDetectionPost: CpuDetectionPostprocess(l.det, pool); break;
+      case Launch::kMean: CpuMean(l.mean, pool); break;
       default: return absl::InternalError(std::string("no host implementation of ") + l.kernel);
     }
   }

@@ -40,7 +40,8 @@ struct Launch {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
     kConvF32, kFcF32, kEltwiseF32, kPoolF32, kUnaryF32, kSoftmaxF32,  // float32 graphs
-    kDetectionPost   // CPU-only TFLite_Detection_PostProcess
+    kDetectionPost,  // CPU-only TFLite_Detection_PostProcess
+    kMean            // CPU-only MEAN
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
@@ -64,6 +65,7 @@ struct Launch {
   float lo = 0.f, hi = 0.f, beta = 1.f;
   int depth = 0;
   CpuDetectionParams det{};
+  CpuMeanParams mean{};
   const void* table = nullptr;  // kLutU8 / kLutF32: 256-entry device table
   long count = 0;               // kLut* / kQuantF32: elements
   float q_scale = 0.f;          // kQuantF32

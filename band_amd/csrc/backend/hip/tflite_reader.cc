@@ -37,6 +37,9 @@ const char* TflBuiltinName(int c) {
     case kTflPad: return "PAD";
     case kTflMean: return "MEAN";
     case kTflSub: return "SUB";
+    case kTflRsqrt: return "RSQRT";
+    case kTflSquaredDifference: return "SQUARED_DIFFERENCE";
+    case kTflMirrorPad: return "MIRROR_PAD";
     case kTflSqueeze: return "SQUEEZE";
     case kTflTransposeConv: return "TRANSPOSE_CONV";
     case kTflResizeNearestNeighbor: return "RESIZE_NEAREST_NEIGHBOR";

@@ -24,7 +24,7 @@ enum TflBuiltin : int {
   kTflDepthwiseConv2D = 4, kTflDequantize = 6, kTflFullyConnected = 9, kTflLogistic = 14,
   kTflMaxPool2D = 17, kTflMul = 18, kTflRelu = 19, kTflReluN1To1 = 20, kTflRelu6 = 21, kTflReshape = 22,
   kTflResizeBilinear = 23, kTflSoftmax = 25, kTflCustom = 32, kTflPad = 34, kTflMean = 40,
-  kTflSub = 41, kTflSqueeze = 43, kTflPadV2 = 60, kTflTransposeConv = 67, kTflResizeNearestNeighbor = 97,
+  kTflSub = 41, kTflRsqrt = 76, kTflSquaredDifference = 99, kTflMirrorPad = 100, kTflSqueeze = 43, kTflPadV2 = 60, kTflTransposeConv = 67, kTflResizeNearestNeighbor = 97,
   kTflQuantize = 114, kTflHardSwish = 117,
 };
 

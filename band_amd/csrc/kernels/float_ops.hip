@@ -158,7 +158,10 @@ __global__ __launch_bounds__(256) void eltwise_f32_kernel(bh_eltwise_f32_params 
   const long ib = (((sb[0] == 1 ? 0 : i0) * sb[1] + (sb[1] == 1 ? 0 : i1)) * sb[2] + (sb[2] == 1 ? 0 : i2)) * sb[3] +
                   (sb[3] == 1 ? 0 : i3);
   const float a = p.a[ia], b = p.b[ib];
-  const float v = p.kind == BH_ELTF_ADD ? a + b : (p.kind == BH_ELTF_SUB ? a - b : a * b);
+  const float v = p.kind == BH_ELTF_ADD ? a + b
+                  : p.kind == BH_ELTF_SUB ? a - b
+                  : p.kind == BH_ELTF_MUL ? a * b
+                                          : (a - b) * (a - b);
   p.out[i] = clampf(v, p.act_min, p.act_max);
 }
 
@@ -191,7 +194,8 @@ __global__ __launch_bounds__(256) void unary_f32_kernel(int kind, const float* i
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const float x = in[i];
-  out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + expf(-x)) : clampf(x, lo, hi);
+  out[i] = kind == BH_UNARY_LOGISTIC ? 1.0f / (1.0f + expf(-x)) : kind == BH_UNARY_RSQRT ? 1.0f / sqrtf(x)
+                                                                                      : clampf(x, lo, hi);
 }
 
 // one wave per row: max, sum of exp, normalise
@@ -257,7 +261,7 @@ extern "C" int bh_fc_f32(const bh_fc_f32_params* pp, bh_stream_t s) {
 }
 
 extern "C" int bh_eltwise_f32(const bh_eltwise_f32_params* pp, bh_stream_t s) {
-  if (!pp || !pp->a || !pp->b || !pp->out) {
+  if (!pp || !pp->a || !pp->b || !pp->out || pp->kind < BH_ELTF_ADD || pp->kind > BH_ELTF_SQDIFF) {
     bh_set_last_error("bh_eltwise_f32: invalid parameters");
     return BH_EINVAL;
   }
@@ -280,7 +284,7 @@ extern "C" int bh_pool_f32(const bh_pool_f32_params* pp, bh_stream_t s) {
 }
 
 extern "C" int bh_unary_f32(int kind, const float* in, float* out, long n, float lo, float hi, bh_stream_t s) {
-  if (!in || !out || n < 0 || (kind != BH_UNARY_CLAMP && kind != BH_UNARY_LOGISTIC)) {
+  if (!in || !out || n < 0 || (kind != BH_UNARY_CLAMP && kind != BH_UNARY_LOGISTIC && kind != BH_UNARY_RSQRT)) {
     bh_set_last_error("bh_unary_f32: invalid parameters");
     return BH_EINVAL;
   }

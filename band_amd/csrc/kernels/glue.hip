@@ -97,6 +97,24 @@ struct PadDivs {
   int os[4];
 };
 
+// MIRROR_PAD source index of padded position i along a dimension of n
+// elements with `before` leading pads (TFLite 2.9.2 mirror_pad.cc
+// GetInputDimension; offset 1 = REFLECT skips the edge, 0 = SYMMETRIC)
+__host__ __device__ inline int mirror_index(int i, int before, int n, int mode) {
+  const int offset = mode == 1 ? 1 : 0;
+  if (i < before) {
+    const int orig = before + offset - 1;
+    return orig - min(i, orig - offset);
+  }
+  i -= before;
+  if (i >= n) {
+    i -= n;
+    const int orig = n - (1 + offset);
+    return orig - min(i, orig);
+  }
+  return i;
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void pad_kernel(bh_pad_params p, PadDivs dv, long total) {
   const long i = (long)blockIdx.x * 256 + threadIdx.x;
@@ -110,9 +128,16 @@ __global__ __launch_bounds__(256) void pad_kernel(bh_pad_params p, PadDivs dv, l
   const int ib = (int)b - p.pad_before[0], iy = y - p.pad_before[1], ix = x - p.pad_before[2],
             ic = c - p.pad_before[3];
   T v = (T)p.value;
-  if (ib >= 0 && ib < p.in_shape[0] && iy >= 0 && iy < p.in_shape[1] && ix >= 0 && ix < p.in_shape[2] && ic >= 0 &&
-      ic < p.in_shape[3])
+  if (p.mode) {
+    const int jb = mirror_index((int)b, p.pad_before[0], p.in_shape[0], p.mode);
+    const int jy = mirror_index(y, p.pad_before[1], p.in_shape[1], p.mode);
+    const int jx = mirror_index(x, p.pad_before[2], p.in_shape[2], p.mode);
+    const int jc = mirror_index(c, p.pad_before[3], p.in_shape[3], p.mode);
+    v = ((const T*)p.input)[(((long)jb * p.in_shape[1] + jy) * p.in_shape[2] + jx) * p.in_shape[3] + jc];
+  } else if (ib >= 0 && ib < p.in_shape[0] && iy >= 0 && iy < p.in_shape[1] && ix >= 0 && ix < p.in_shape[2] &&
+             ic >= 0 && ic < p.in_shape[3]) {
     v = ((const T*)p.input)[(((long)ib * p.in_shape[1] + iy) * p.in_shape[2] + ix) * p.in_shape[3] + ic];
+  }
   ((T*)p.output)[i] = v;
 }
 
@@ -366,6 +391,12 @@ extern "C" int bh_pad(const bh_pad_params* pp, bh_stream_t s) {
   for (int d = 0; d < 4; ++d) {
     if (p.in_shape[d] <= 0 || p.pad_before[d] < 0 || p.pad_after[d] < 0) {
       bh_set_last_error("bh_pad: bad shape");
+      return BH_EINVAL;
+    }
+    // mirror pads index inside the input: REFLECT < dim, SYMMETRIC <= dim
+    const int lim = p.in_shape[d] - (p.mode == 1 ? 1 : 0);
+    if ((p.mode < 0 || p.mode > 2) || (p.mode && (p.pad_before[d] > lim || p.pad_after[d] > lim))) {
+      bh_set_last_error("bh_pad: mirror pad wider than the input");
       return BH_EINVAL;
     }
     dv.os[d] = p.in_shape[d] + p.pad_before[d] + p.pad_after[d];

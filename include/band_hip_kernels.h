@@ -380,6 +380,7 @@ int bh_fc_f32(const bh_fc_f32_params* p, bh_stream_t s);
 #define BH_ELTF_ADD 0
 #define BH_ELTF_SUB 1
 #define BH_ELTF_MUL 2
+#define BH_ELTF_SQDIFF 3 /* SQUARED_DIFFERENCE: (a - b)^2 */
 typedef struct {
   int kind;
   int shape_a[4], shape_b[4], shape_o[4]; /* 4-D, broadcast dims are 1 */
@@ -401,6 +402,7 @@ int bh_pool_f32(const bh_pool_f32_params* p, bh_stream_t s);
 
 #define BH_UNARY_CLAMP 0    /* RELU / RELU6 / RELU_N1_TO_1: min(max(x, lo), hi) */
 #define BH_UNARY_LOGISTIC 1 /* 1 / (1 + exp(-x)) */
+#define BH_UNARY_RSQRT 2    /* RSQRT: 1 / sqrt(x) */
 int bh_unary_f32(int kind, const float* in, float* out, long n, float lo, float hi, bh_stream_t s);
 
 /* reference_ops::Softmax (float): per row exp((x - max) * beta) / sum */
@@ -425,6 +427,9 @@ typedef struct {
   uint32_t value;                 /* bit pattern of the pad element */
   const void* input;
   void* output;
+  /* 0: constant fill (PAD / PADV2); MIRROR_PAD: 1 REFLECT, 2 SYMMETRIC
+   * (mirror_pad.cc GetInputDimension; pads < dim for REFLECT, <= dim) */
+  int32_t mode;
 } bh_pad_params;
 int bh_pad(const bh_pad_params* p, bh_stream_t s);
 

@@ -353,6 +353,44 @@ def pad(x, pads, value):
     return out
 
 
+def mirror_pad(x, pads, mode):
+    """MIRROR_PAD (TFLite 2.9.2 kernels/mirror_pad.cc: GetInputDimension maps a
+    padded index back into the input, REFLECT skipping the edge element,
+    SYMMETRIC repeating it) - for pads within the input, the same map as
+    numpy's 'reflect' / 'symmetric' pad modes.  mode: "REFLECT" / "SYMMETRIC"."""
+    return np.pad(x, [tuple(int(v) for v in p) for p in pads], mode=mode.lower())
+
+
+def mean_q8_hw(x, *, in_scale, in_zp, out_scale, out_zp):
+    """quantized MEAN over axes {1, 2} with keep_dims (TFLite 2.9.2 reduce.cc
+    EvalMean -> optimized_integer_ops::Mean for int8, optimized_ops::Mean for
+    uint8): int32 sum, then MultiplyByQuantizedMultiplier(sum, M, shift) +
+    bias, clamped to the type; M / shift = QuantizeMultiplier of the float
+    in_scale / (H*W * out_scale), bias = out_zp - int(float(in_zp * in_scale
+    / out_scale)) with every product in float32 as written there.
+    Parity unpinned: no reference fixture holds MEAN outputs."""
+    n = np.float32(x.shape[1] * x.shape[2])
+    fin, fout = np.float32(in_scale), np.float32(out_scale)
+    bias = int(out_zp) - int(np.float32(np.float32(np.float32(in_zp) * fin) / fout))
+    real = np.float32(fin / np.float32(n * fout))
+    m, sh = quantize_multiplier(float(real))
+    acc = x.astype(np.int32).sum(axis=(1, 2), keepdims=True)
+    out = np.array([lib().tfl_mbqm(int(a), m, sh) for a in acc.reshape(-1)], np.int64).reshape(acc.shape) + bias
+    lo, hi = (-128, 127) if x.dtype == np.int8 else (0, 255)
+    return np.clip(out, lo, hi).astype(x.dtype)
+
+
+def squared_difference_f32(a, b):
+    """SQUARED_DIFFERENCE (float32, broadcast): (a - b)^2 in float32"""
+    d = (a.astype(np.float32) - b.astype(np.float32)).astype(np.float32)
+    return (d * d).astype(np.float32)
+
+
+def rsqrt_f32(x):
+    """RSQRT (float32): 1 / sqrt(x)"""
+    return (np.float32(1.0) / np.sqrt(x.astype(np.float32))).astype(np.float32)
+
+
 def nearest_index(v, in_size, out_size, align_corners, half_pixel_centers):
     return lib().tfl_nearest_index(v, in_size, out_size, int(align_corners), int(half_pixel_centers))
 

@@ -2,7 +2,7 @@
 between real conv layers (test fixtures, built with band_amd.tflite_synth)."""
 import numpy as np
 
-from band_amd.tflite_synth import QGraph
+from band_amd.tflite_synth import OPT, ModelBuilder, QGraph, Table
 
 
 def glue_zoo(dtype, seed=3):
@@ -102,3 +102,46 @@ def float_zoo(seed=13):
     g.output(g.softmax(g.fully_connected(v, 9), beta=0.8))
     g.output(e)
     return g.build()
+
+
+def norm_zoo(with_mean=True):
+    """The instance-norm / padding ops of the reference's magenta
+    style-transfer model (band/test/data/magenta_...tflite): MIRROR_PAD
+    (REFLECT and SYMMETRIC), QUANTIZE, int8 MEAN over H, W with keep_dims,
+    DEQUANTIZE, SQUARED_DIFFERENCE, ADD, RSQRT (float32 unless noted).
+    with_mean=False drops the MEAN (the GPU set has no MEAN)."""
+    mb = ModelBuilder("norm_zoo")
+    f32 = np.float32
+    x = mb.tensor("x", [1, 9, 11, 4], f32)
+    mb.inputs = [x]
+    p1 = mb.tensor("pads_reflect", [4, 2], np.int32, data=[[0, 0], [2, 1], [1, 2], [0, 0]])
+    xr = mb.tensor("x_reflect", [1, 12, 14, 4], f32)
+    mb.op(100, [x, p1], [xr], OPT_MIRROR_PAD, Table().set(0, "b", 0))  # REFLECT
+    p2 = mb.tensor("pads_symmetric", [4, 2], np.int32, data=[[0, 0], [3, 0], [0, 11], [1, 0]])
+    xs = mb.tensor("x_symmetric", [1, 12, 22, 5], f32)
+    mb.op(100, [x, p2], [xs], OPT_MIRROR_PAD, Table().set(0, "b", 1))  # SYMMETRIC
+    outs = [xr, xs]
+    if with_mean:
+        q = mb.tensor("q", [1, 12, 14, 4], np.int8, scale=0.02, zero_point=-3)
+        mb.op("QUANTIZE", [xr], [q], OPT["QuantizeOptions"], Table())
+        ax = mb.tensor("axes", [2], np.int32, data=[1, 2])
+        m = mb.tensor("mean", [1, 1, 1, 4], np.int8, scale=0.011, zero_point=2)
+        mb.op(40, [q, ax], [m], OPT_REDUCER, Table().set(0, "b", 1))  # keep_dims
+        c = mb.tensor("mean_f32", [1, 1, 1, 4], f32)
+        mb.op("DEQUANTIZE", [m], [c], OPT["DequantizeOptions"], Table())
+        outs.append(m)
+    else:
+        c = mb.tensor("centre", [1, 1, 1, 4], f32, data=np.linspace(-0.3, 0.4, 4))
+    sd = mb.tensor("sqdiff", [1, 12, 14, 4], f32)
+    mb.op(99, [xr, c], [sd], OPT_SQDIFF, Table())
+    one = mb.tensor("eps", [1], f32, data=[1e-3])
+    v = mb.tensor("var_eps", [1, 12, 14, 4], f32)
+    mb.op("ADD", [sd, one], [v], OPT["AddOptions"], Table().set(0, "b", 0))
+    r = mb.tensor("rsqrt", [1, 12, 14, 4], f32)
+    mb.op(76, [v], [r])
+    mb.outputs = outs + [sd, r]
+    return mb.build()
+
+
+# BuiltinOptions union indices of the ops above (schema.fbs)
+OPT_REDUCER, OPT_SQDIFF, OPT_MIRROR_PAD = 27, 76, 77

@@ -297,5 +297,6 @@ def test_poisson_latency_counts_submission_delay(golden_dir):
     # ~all 200 arrivals are due within the first ~0.2 ms, so the last job's
     # latency is close to the whole run, not to one job's service time
     assert lat[-1] > 0.5 * wall * 1e6
-    assert np.median(lat[100:]) > 10 * lat[:5].min()
+    # latency grows with the submission index (each job waits for all before it)
+    assert np.corrcoef(np.arange(len(lat)), lat)[0, 1] > 0.8
     e.close()

@@ -471,7 +471,10 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
         def max(self, v):
             return v
 
-    e, bm, ins = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * n_workers, 0, n_workers, args.job_batch)
+    # --device cpu: Band CPU workers stand in for the GPUs (CPU tests of this
+    # path); the worker -> device mapping is the same
+    flag = DeviceFlag.kGPU if args.device == "gpu" else DeviceFlag.kCPU
+    e, bm, ins = make_engine(args, D, paths, sched, [flag] * n_workers, 0, n_workers, args.job_batch)
     inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
     el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
     e.close()

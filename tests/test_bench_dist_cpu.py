@@ -71,3 +71,32 @@ def test_bench_c1_cpu_worker_line():
     # both CPU modes through the Band harness, host facts recorded
     assert [m["workers"] for m in cb["modes"]] == [1, 1] and cb["host"]["nproc"] >= 1
     assert cb["oracle_scalar_port_1core"]["value"] > 0
+
+
+def test_bench_single_engine_cpu_stand_ins():
+    """--single-engine: ONE Band engine (one planner thread) whose workers are
+    spread over N devices, worker w on device w % N (band/engine.cc:681-713);
+    CPU workers stand in for the GPUs"""
+    cmd = [sys.executable, "bench.py", "--single-engine", "--gpus", "2", "--device", "cpu", "--model", "mix_c3",
+           "--size", "64", "--workers-per-gpu", "2", "--cpu-threads", "1", "--steps", "6", "--warmup", "2",
+           "--jobs-per-step", "8", "--job-batch", "1", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = _json_line(r.stdout)
+    se = line["single_engine"]
+    assert line["n_gpus"] == 2 and se["n_gpus"] == 2 and se["workers"] == 4 and se["worker_to_gpu"] == "w % 2"
+    assert se["jobs"] == 6 * 8 and sum(se["jobs_per_gpu"]) == 6 * 8 and min(se["jobs_per_gpu"]) > 0
+    assert line["value"] == se["value"] and "single planner" in line["config"]["harness"]
+
+
+def test_worker_device_mapping():
+    """DeviceRegistry (backend/hip/device.cc): an explicit worker -> ordinal
+    mapping is returned as set and can be changed (bench.py remaps workers for
+    its single-engine line); without a device an unmapped worker reads 0"""
+    import band_amd
+    band_amd.SetWorkerDevice(7001, 3)
+    band_amd.SetWorkerDevice(7002, 5)
+    assert band_amd.WorkerDevice(7001) == 3 and band_amd.WorkerDevice(7002) == 5
+    band_amd.SetWorkerDevice(7001, 1)
+    assert band_amd.WorkerDevice(7001) == 1
+    assert band_amd.WorkerDevice(7999) == 0

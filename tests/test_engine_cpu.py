@@ -8,6 +8,7 @@ latency_estimator_test.cc), driven through the C API (include/band_c_api.h).
 """
 import json
 import os
+import time
 
 import numpy as np
 import pytest
@@ -49,6 +50,12 @@ def test_engine_simple_async_invoke_with_callback(golden_dir):
     assert h >= 0
     assert e.Wait(h, [o]) == kBandOk
     _check_add(o)
+    # The planner records the job (waking Wait) before it runs the callbacks,
+    # with the lock released in between (band/planner.cc:184-210), so the
+    # callback may land just after Wait returns.
+    deadline = time.monotonic() + 5.0
+    while (h, 0) not in done and time.monotonic() < deadline:
+        time.sleep(0.001)
     assert (h, 0) in done
     assert e.UnsetOnEndRequest(cb) == kBandOk
     assert e.UnsetOnEndRequest(cb) != kBandOk  # unknown handle

@@ -508,6 +508,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && f[0] == '0') allow_fusion_ = false;
   if (f && std::strcmp(f, "noirb") == 0) allow_irb_ = false;   // diagnostics: one fusion kind at a time
   if (f && std::strcmp(f, "noadd") == 0) allow_add_ = false;
+  if (f && std::strcmp(f, "nochain") == 0) allow_chain_ = false;
+  if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
@@ -899,7 +901,9 @@ absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubg
     if (sg->fused_ops.count(i)) continue;
     RETURN_STATUS_IF(Lower(model, i, sg));
   }
-  // fused blocks are GPU kernels picked by on-device timing
+  // fused chains / blocks are GPU kernels picked by on-device timing; chains
+  // first (they cut more launches), blocks over what the chains left
+  if (allow_fusion_ && allow_chain_ && device_flag_ == DeviceFlag::kGPU) FuseChains(model, sg);
   if (allow_fusion_ && allow_irb_ && device_flag_ == DeviceFlag::kGPU) FuseBlocks(model, sg);
   if (allow_fusion_) FuseGlue(model, sg);
   return absl::OkStatus();
@@ -1157,9 +1161,145 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
   sg->launches.swap(out);
 }
 
+// Rewrites dw3x3 -> conv1x1 [+fused ADD] [-> conv1x1] launch runs into one
+// bh_chain_i8 launch (a block's depthwise + project and the next block's
+// expand) when the depthwise output is private to the first conv.  The
+// first conv's output is stored only when something besides the second conv
+// reads it (the next block's residual, a subgraph output).  Taken per run
+// geometry by on-device timing against the unfused launches, as FuseBlocks.
+void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
+  const TflModel& d = model.desc();
+  auto private_tensor = [&](int t, int only_consumer) {
+    if (t < 0 || consumers_[t].size() != 1 || consumers_[t][0] != only_consumer) return false;
+    if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
+    if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
+    return std::find(d.outputs.begin(), d.outputs.end(), t) == d.outputs.end();
+  };
+  std::vector<Launch> out;
+  const auto& L = sg->launches;
+  for (size_t i = 0; i < L.size(); ++i) {
+    const bool head = L[i].kind == Launch::kDwConv && i + 1 < L.size() && L[i + 1].kind == Launch::kConv &&
+                      L[i + 1].conv.input == L[i].dw.output && !L[i].dw.out_table &&
+                      private_tensor(L[i].out_tensor, L[i + 1].op_index);
+    if (!head) {
+      out.push_back(L[i]);
+      continue;
+    }
+    const Launch& D = L[i];
+    const Launch& P1 = L[i + 1];
+    const Launch* P2 = nullptr;
+    if (i + 2 < L.size() && L[i + 2].kind == Launch::kConv && L[i + 2].conv.input == P1.conv.output &&
+        Is1x1S1(L[i + 2].conv) && !L[i + 2].conv.residual)
+      P2 = &L[i + 2];
+    bh_chain_params c{};
+    c.dw = D.dw;
+    c.pw1 = P1.conv;
+    c.px_blocks = 4;
+    // the two candidate forms: with the second conv, and without it
+    bh_chain_params c3 = c, c2 = c;
+    bool ok3 = false;
+    if (P2) {
+      c3.has_pw2 = 1;
+      c3.pw2 = P2->conv;
+      if (private_tensor(P1.out_tensor, P2->op_index)) c3.pw1.output = nullptr;
+      ok3 = bh_chain_lds_bytes(&c3) > 0;
+    }
+    const bool ok2 = bh_chain_lds_bytes(&c2) > 0;
+    if (!ok2 && !ok3) {
+      out.push_back(L[i]);
+      continue;
+    }
+    // choice: 0 = unfused, 1/2/4 = px_blocks of the 3-launch form, 11/12/14
+    // = px_blocks of the 2-launch form (the second conv stays a launch),
+    // +100 = 16 waves per workgroup
+    char key[256];
+    std::snprintf(key, sizeof(key), "ch:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", ordinal_, D.dw.batch, D.dw.in_h,
+                  D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
+                  ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0);
+    int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
+    if (autotune_ && choice < 0) {
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      LoadTuneFileLocked();
+      auto it = g_tune.find(key);
+      if (it != g_tune.end()) choice = it->second;
+    }
+    if (choice < 0) {
+      choice = 0;
+      bool measured = autotune_;
+      if (measured) {
+        std::vector<const Launch*> base = {&D, &P1};
+        if (ok3) base.push_back(P2);
+        const double u = TimeLaunches(base, 10);
+        const double u_p2 = ok3 ? TimeLaunches({P2}, 10) : 0.0;
+        measured = u > 0 && u_p2 >= 0;
+        double best = u * 0.98;  // fusion must win by > 2% to be taken
+        // (px_blocks, waves): 64 / 32 / 16 pixels per 4-wave workgroup, or
+        // 16 pixels over 16 waves (few-pixel, many-channel layers)
+        const int forms[4][2] = {{4, 4}, {2, 4}, {1, 4}, {1, 16}};
+        for (const auto& pw : forms) {
+          for (int form = 0; form < 2 && measured; ++form) {
+            bh_chain_params q = form == 0 ? c3 : c2;
+            if (form == 0 ? !ok3 : !ok2) continue;
+            q.px_blocks = pw[0];
+            q.waves = pw[1];
+            if (bh_chain_lds_bytes(&q) == 0) continue;
+            Launch F;
+            F.kind = Launch::kChain;
+            F.chain = q;
+            const double us = TimeLaunches({&F}, 10);
+            const double total = us + (form == 1 && ok3 ? u_p2 : 0.0);
+            if (us > 0 && total < best) {
+              best = total;
+              choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0);
+            }
+          }
+        }
+      }
+      if (!measured) choice = ok3 ? 4 : 14;  // no device timing: the 3-launch form when it applies
+      if (autotune_ && measured) {
+        std::lock_guard<std::mutex> lk(g_tune_mu);
+        if (!g_tune.count(key)) AppendTuneFileLocked(key, choice);
+        g_tune[key] = choice;
+      }
+    }
+    // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves
+    const bool three = choice > 0 && choice % 100 < 10;
+    if (choice == 0 || (three && !ok3) || (!three && !ok2)) {
+      out.push_back(L[i]);
+      continue;
+    }
+    Launch F;
+    F.kind = Launch::kChain;
+    F.op_index = D.op_index;
+    F.chain = three ? c3 : c2;
+    F.chain.px_blocks = choice % 10;
+    F.chain.waves = choice >= 100 ? 16 : 4;
+    F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
+    F.kernel = "chain_kernel";
+    const bh_dwconv_params& dw = F.chain.dw;
+    const bh_conv_params& a = F.chain.pw1;
+    const double px = static_cast<double>(dw.batch) * dw.out_h * dw.out_w;
+    F.alg_bytes = static_cast<double>(dw.batch) * dw.in_h * dw.in_w * dw.in_c + 9.0 * dw.out_c + 28.0 * dw.out_c +
+                  (a.residual ? px * a.out_c : 0.0) + (a.output ? px * a.out_c : 0.0) +
+                  static_cast<double>(a.out_c) * a.in_c + 12.0 * a.out_c;
+    F.alg_ops = D.alg_ops + P1.alg_ops;
+    if (three) {
+      const bh_conv_params& b = F.chain.pw2;
+      F.alg_bytes += px * b.out_c + static_cast<double>(b.out_c) * b.in_c + 12.0 * b.out_c;
+      F.alg_ops += P2->alg_ops;
+      if (!a.output) sg->fused_tensors.insert(P1.out_tensor);
+    }
+    out.push_back(F);
+    sg->fused_tensors.insert(D.out_tensor);
+    i += three ? 2 : 1;
+  }
+  sg->launches.swap(out);
+}
+
 namespace {
 void** OutSlot(Launch& l) {
   switch (l.kind) {
+    case Launch::kChain: return l.chain.has_pw2 ? &l.chain.pw2.output : &l.chain.pw1.output;
     case Launch::kConv: return &l.conv.output;
     case Launch::kDwConv: return &l.dw.output;
     case Launch::kFc: return &l.fc.output;
@@ -1995,6 +2135,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kEltwise: rc = bh_eltwise_i8(&l.elt, stream_); break;
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
+    case Launch::kChain: rc = bh_chain_i8(&l.chain, stream_); break;
     case Launch::kCopy: rc = l.src == l.dst ? 0 : bh_memcpy_d2d_async(l.dst, l.src, l.bytes, stream_); break;
     case Launch::kLutU8: rc = bh_lut_u8(l.src, l.dst, l.count, l.table, stream_); break;
     case Launch::kLutF32:

@@ -37,7 +37,7 @@ namespace hip {
 
 struct Launch {
   enum Kind {
-    kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb,
+    kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb, kChain,
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
     kConvF32, kFcF32, kEltwiseF32, kPoolF32, kUnaryF32, kSoftmaxF32,  // float32 graphs
     kDetectionPost,  // CPU-only TFLite_Detection_PostProcess
@@ -51,6 +51,7 @@ struct Launch {
   bh_eltwise_params elt{};
   bh_pool_params pool{};
   bh_irb_params irb{};
+  bh_chain_params chain{};
   bh_concat_params concat{};
   bh_pad_params pad{};
   bh_resize_nearest_params rnear{};
@@ -161,6 +162,8 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   absl::Status BuildLaunches(const HipModel& model, PreparedSubgraph* sg);
   bool TryFuseResidualAdd(const HipModel& model, int conv_op, PreparedSubgraph* sg, Launch* l);
   void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
+  // dw3x3 -> conv1x1 [+ADD] [-> conv1x1] runs into one bh_chain_i8 launch
+  void FuseChains(const HipModel& model, PreparedSubgraph* sg);
   // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
   // CONCATENATION with outer size 1 elided (producers write their slices)
   void FuseGlue(const HipModel& model, PreparedSubgraph* sg);
@@ -198,6 +201,8 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bool allow_fusion_ = true;
   bool allow_irb_ = true;  // BAND_HIP_FUSION=noirb / noadd: diagnostics
   bool allow_add_ = true;
+  bool allow_chain_ = true;   // BAND_HIP_FUSION=nochain
+  bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;

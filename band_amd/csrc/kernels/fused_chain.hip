@@ -1,0 +1,433 @@
+// Fused pointwise chain for gfx950 (int8 per-channel):
+//   DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 [-> ADD residual] [-> CONV_2D 1x1]
+//
+// Stands in for 2-3 consecutive TFLite 2.9.2 builtin kernels on Band's hot
+// path (band/backend/tfl/model_executor.cc:249-255 -> Interpreter::Invoke):
+// reference_integer_ops::DepthwiseConvPerChannel, ConvPerChannel (a
+// MobileNetV2 block's project, with the block's residual ADD folded into its
+// epilogue, or a MobileNetV1 pointwise layer) and ConvPerChannel again (the
+// NEXT block's expand).  Every intermediate is requantised to its own 8-bit
+// tensor exactly as TFLite stores it, so the result is bit-identical to the
+// unfused launches.
+//
+// Why this cut and not the inverted-residual block (irb_kernel): the two 1x1
+// layers map output pixel m to pixel m, so fusing across the block boundary
+// (project -> next expand) needs no halo and no recompute.  Only the
+// depthwise layer reads a 3x3 neighbourhood, and it reads it straight from
+// HBM / L2 (neighbouring pixel blocks of a workgroup share an XCD).  Per
+// MobileNet block that is one launch instead of three, and the depthwise
+// output - 6x the block's channels - never leaves the CU.
+//
+// A workgroup (4 waves) owns RB x 16 consecutive output pixels:
+//   phase A  depthwise on the matrix cores (block-diagonal 16x16x64 tiles,
+//            as dwconv3x3_mfma_kernel): one 16-channel group per item,
+//            requantised, 4 channels of one pixel per lane -> LDS [pix][C]
+//   phase B  first 1x1 GEMM, D^T = W1 x X^T with X from LDS, K = C; requant
+//            [+ residual ADD]; the 8-bit result -> HBM (when it has other
+//            readers) and -> LDS [pix][N1]
+//   phase C  second 1x1 GEMM from that LDS tile, K = N1; requant -> HBM
+// Waves: wave w works on pixel block w % RB and on every (4/RB)-th channel
+// tile from w / RB, so every phase keeps all four waves busy.
+#include <algorithm>
+
+#include "common.hpp"
+
+namespace bh {
+
+struct ChainDivs {
+  FastDiv out_w, out_h;
+};
+
+__device__ __forceinline__ uint32_t pack4(const int32_t v[4]) {
+  // bytes 0 of v0..v3 -> one dword (v_perm_b32 selectors as in conv_xs_kernel)
+  const uint32_t lo = __builtin_amdgcn_perm((uint32_t)v[1], (uint32_t)v[0], 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm((uint32_t)v[3], (uint32_t)v[2], 0x04000c0cu);
+  return lo | hi;
+}
+
+// One 16-channel tile t of the 1x1 layer `c` for this lane's pixel row:
+// `xrow` = the row's K bytes in LDS at this lane's 16-byte K offset.  The
+// accumulator starts at the folded bias of the lane's 4 channels.  Four
+// K-steps' weight fragments (global, L1/L2-resident) and pixel fragments
+// (LDS) are issued before their MFMAs.
+__device__ __forceinline__ v4i gemm_tile(const bh_conv_params& c, const unsigned char* xrow, int t, int KS, int r16,
+                                         int g) {
+  const int8_t* wrow = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
+  const int nb = t * 16 + 4 * g;
+  const int nl = nb < c.out_c ? nb : 0;
+  v4i acc = *(const v4i*)(c.bias_eff + nl);
+  int k = 0;
+  for (; k + 8 <= KS; k += 8) {
+    v4i w[8], x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      w[u] = *(const v4i*)(wrow + (k + u) * 64);
+      x[u] = *(const v4i*)(xrow + (k + u) * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(w[u], x[u], acc, 0, 0, 0);
+  }
+  for (; k + 4 <= KS; k += 4) {
+    v4i w[4], x[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      w[u] = *(const v4i*)(wrow + (k + u) * 64);
+      x[u] = *(const v4i*)(xrow + (k + u) * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(w[u], x[u], acc, 0, 0, 0);
+  }
+  for (; k < KS; ++k) {
+    const v4i w = *(const v4i*)(wrow + k * 64);
+    const v4i x = *(const v4i*)(xrow + k * 64);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(w, x, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void requant4(const bh_conv_params& c, int nb, v4i acc, int32_t v[4]) {
+  const v4i vm = *(const v4i*)(c.mult + nb);
+  const v4i vs = *(const v4i*)(c.shift + nb);
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    v[r] = requant_out<FAST>(acc[r], chan_q(vm[r], vs[r], c.out_zp), c.out_zp, c.act_min, c.act_max);
+}
+
+// x-stationary 1x1 GEMM for K <= 64 * KMAX: this lane's KS pixel fragments
+// are read from LDS once; the wave then walks its channel tiles t0, t0 +
+// tstep, ... two at a time, with both tiles' weight fragments and epilogue
+// operands (folded bias, multipliers, shifts) issued before their MFMAs, so
+// each pair costs one memory round trip.  epi(t, nb, acc, mult4, shift4)
+// finishes a tile (nb = the lane's first channel; may be >= out_c).
+template <int KMAX, typename Epi>
+__device__ __forceinline__ void gemm_xs(const bh_conv_params& c, const unsigned char* xrow, int KS, int t0, int tstep,
+                                        int r16, int g, Epi&& epi) {
+  v4i x[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) x[k] = k < KS ? *(const v4i*)(xrow + k * 64) : (v4i){0, 0, 0, 0};
+  const int T = (c.out_c + 15) >> 4;
+  for (int t = t0; t < T; t += 2 * tstep) {
+    const int tb = t + tstep < T ? t + tstep : t;
+    const int8_t* ra = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
+    const int8_t* rb = c.weights + (long)(tb * 16 + r16) * c.k_pad + g * 16;
+    v4i wa[KMAX], wb[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) {
+        wa[k] = *(const v4i*)(ra + k * 64);
+        wb[k] = *(const v4i*)(rb + k * 64);
+      }
+    const int na = t * 16 + 4 * g, nb = tb * 16 + 4 * g;
+    const int la = na < c.out_c ? na : 0, lb = nb < c.out_c ? nb : 0;
+    v4i acca = *(const v4i*)(c.bias_eff + la);
+    v4i accb = *(const v4i*)(c.bias_eff + lb);
+    const v4i ma = *(const v4i*)(c.mult + la), sa = *(const v4i*)(c.shift + la);
+    const v4i mb = *(const v4i*)(c.mult + lb), sb = *(const v4i*)(c.shift + lb);
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) {
+        acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(wa[k], x[k], acca, 0, 0, 0);
+        accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(wb[k], x[k], accb, 0, 0, 0);
+      }
+    epi(t, na, acca, ma, sa);
+    if (tb != t) epi(tb, nb, accb, mb, sb);
+  }
+}
+
+template <bool FAST>
+__device__ __forceinline__ void requant4m(const bh_conv_params& c, v4i acc, v4i vm, v4i vs, int32_t v[4]) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    v[r] = requant_out<FAST>(acc[r], chan_q(vm[r], vs[r], c.out_zp), c.out_zp, c.act_min, c.act_max);
+}
+
+constexpr int kXsMax = 5;  // x-stationary GEMMs up to K = 320
+
+// Workgroup-contiguous output: the tile's rows are consecutive pixels, so
+// its bytes are one contiguous run of HBM; staged in LDS and written with
+// 16-byte stores of consecutive addresses (a wave writes 1 KB per
+// instruction instead of 16 separate 16-byte row pieces).
+__device__ __forceinline__ void copy_out(const unsigned char* src, uint8_t* dst, int bytes) {
+  const int n16 = bytes >> 4;
+  for (int i = threadIdx.x; i < n16; i += blockDim.x) *(v4i*)(dst + i * 16) = *(const v4i*)(src + i * 16);
+  const int rem = (bytes - (n16 << 4)) >> 2;  // bytes % 4 == 0
+  if ((int)threadIdx.x < rem)
+    *(uint32_t*)(dst + n16 * 16 + threadIdx.x * 4) = *(const uint32_t*)(src + n16 * 16 + threadIdx.x * 4);
+}
+
+template <int RB, bool FAST, int KX, int NW>
+__global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
+                                                    ChainDivs dv) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int WPB = NW / RB;  // waves per pixel block
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  const int pb = wave % RB;
+  const int wsub = wave / RB;
+  const int blk = xcd_block(blockIdx.x, gridDim.x);
+  const int m = (blk * RB + pb) * 16 + r16;  // this lane's pixel (B operand column)
+  const bool mval = m < P;
+  unsigned char* dl = smem;           // [RB*16][S1] depthwise output; then [RB*16][N2] second 1x1 output
+  unsigned char* pl = smem + off_pl;  // [RB*16][S2] first 1x1 output (second 1x1's operand)
+  unsigned char* o1 = smem + off_o1;  // [RB*16][N1] first 1x1 output staged for HBM
+  const int m0 = blk * RB * 16;
+  const int rows = min(RB * 16, P - m0);
+  const int prow = pb * 16 + r16;
+
+  // ---- phase A: depthwise 3x3 -> LDS -------------------------------------
+  {
+    const bh_dwconv_params& d = cp.dw;
+    const int C = d.out_c;
+    const int mm = mval ? m : 0;
+    const int t = dv.out_w.div(mm);
+    const int ox = mm - t * d.out_w;
+    const int n = dv.out_h.div(t);
+    const int oy = t - n * d.out_h;
+    const int iy = oy * d.stride_h, ix = ox * d.stride_w, row0 = n * d.in_h;
+    // this lane's tap of each K-step (taps 4s..4s+3; lane group g = tap % 4)
+    int off[3];
+    bool ok[3];
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int tap = 4 * s + g;
+      const int fy = (tap * 11) >> 5;  // tap / 3 for tap < 12
+      const int fx = tap - 3 * fy;
+      const int y = iy + fy * d.dil_h - d.pad_h, x = ix + fx * d.dil_w - d.pad_w;
+      ok[s] = mval && tap < 9 && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
+      off[s] = ok[s] ? ((row0 + y) * d.in_w + x) * C : 0;
+    }
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)d.input, (short)0, d.batch * d.in_h * d.in_w * C, 0x00020000);
+    const int zfill = (int)splat_byte(d.in_zp);
+    const int dsel = r16 >> 2;
+    const int bsh = 8 * (r16 & 3);
+    // two channel groups per iteration: both items' loads (input taps,
+    // filter bytes, epilogue operands) are issued before either's MFMAs
+    struct DwItem {
+      v4i xf[3];
+      uint32_t wb[3];
+      v4i mm4, ss4;
+      int32_t be[4];
+    };
+    auto dw_load = [&](int cg, DwItem& it) {
+      const int c0 = cg * 16;
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[s] + c0, 0, 0);
+        it.xf[s] = (v4i){ok[s] ? (int)v.x : zfill, ok[s] ? (int)v.y : zfill, ok[s] ? (int)v.z : zfill,
+                         ok[s] ? (int)v.w : zfill};
+        const int tap = 4 * s + g;
+        it.wb[s] = tap < 9 ? (uint32_t)(uint8_t)d.weights[tap * C + c0 + r16] : 0u;
+      }
+      const int co = c0 + 4 * g;
+      it.mm4 = *(const v4i*)(d.mult + co);
+      it.ss4 = *(const v4i*)(d.shift + co);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) it.be[r] = d.taps[4 * (co + r) + 3];
+    };
+    auto dw_finish = [&](int cg, const DwItem& it) {
+      v4i acc = (v4i){0, 0, 0, 0};
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int w = (int)(it.wb[s] << bsh);
+        const v4i wf = (v4i){dsel == 0 ? w : 0, dsel == 1 ? w : 0, dsel == 2 ? w : 0, dsel == 3 ? w : 0};
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, it.xf[s], acc, 0, 0, 0);
+      }
+      int32_t v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        v[r] = requant_out<FAST>(acc[r] + it.be[r], chan_q(it.mm4[r], it.ss4[r], d.out_zp), d.out_zp, d.act_min,
+                                 d.act_max);
+      *(uint32_t*)(dl + prow * S1 + cg * 16 + 4 * g) = pack4(v);
+    };
+    const int G = C >> 4;
+    for (int cg = wsub; cg < G; cg += 2 * WPB) {
+      const int cgb = cg + WPB < G ? cg + WPB : cg;
+      DwItem ia, ib;
+      dw_load(cg, ia);
+      dw_load(cgb, ib);
+      dw_finish(cg, ia);
+      if (cgb != cg) dw_finish(cgb, ib);
+    }
+  }
+  __syncthreads();
+
+  // ---- phase B: first 1x1 (+ residual ADD) -> HBM and / or LDS ----------
+  {
+    const bh_conv_params& a = cp.pw1;
+    const int N1 = a.out_c;
+    const int T1 = (N1 + 15) >> 4;
+    const int KS1 = a.k_pad >> 6;
+    const unsigned char* xrow = dl + prow * S1 + g * 16;
+    const uint8_t* res = (const uint8_t*)a.residual;
+    uint8_t* out1 = (uint8_t*)a.output;
+    auto epi = [&](int t, int nb, v4i acc, v4i vm, v4i vs) {
+      if (nb >= N1) return;  // N1 % 4 == 0: all 4 channels valid
+      int32_t v[4];
+      requant4m<FAST>(a, acc, vm, vs, v);
+      if (res && mval) {
+        const uint32_t rq = *(const uint32_t*)(res + (long)m * N1 + nb);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int32_t qv = sbyte(rq, r);
+          const int32_t sy = requant_lt1((v[r] + a.add_y_off) * (1 << a.add_left_shift), a.add_y_mult, a.add_y_shift);
+          const int32_t sr = requant_lt1((qv + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
+          v[r] = clamp_i32(requant_lt1(sy + sr, a.add_o_mult, a.add_o_shift) + a.add_o_off, a.add_act_min,
+                           a.add_act_max);
+        }
+      }
+      const uint32_t pk = pack4(v);
+      if (out1) *(uint32_t*)(o1 + prow * N1 + nb) = pk;
+      if (cp.has_pw2) *(uint32_t*)(pl + prow * S2 + nb) = pk;
+    };
+    if (KS1 <= KX) {
+      gemm_xs<KX>(a, xrow, KS1, wsub, WPB, r16, g, epi);
+    } else {
+      for (int t = wsub; t < T1; t += WPB) {
+        const v4i acc = gemm_tile(a, xrow, t, KS1, r16, g);
+        const int nb = t * 16 + 4 * g;
+        const int nl = nb < N1 ? nb : 0;
+        epi(t, nb, acc, *(const v4i*)(a.mult + nl), *(const v4i*)(a.shift + nl));
+      }
+    }
+  }
+  __syncthreads();
+  if (cp.pw1.output) copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
+  if (!cp.has_pw2) return;
+
+  // ---- phase C: second 1x1 -> HBM -----------------------------------------
+  {
+    const bh_conv_params& b = cp.pw2;
+    const int N2 = b.out_c;
+    const int KS2 = b.k_pad >> 6;
+    const unsigned char* xrow = pl + prow * S2 + g * 16;
+    gemm_xs<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int nb, v4i acc, v4i vm, v4i vs) {
+      if (nb >= N2) return;
+      int32_t v[4];
+      requant4m<FAST>(b, acc, vm, vs, v);
+      *(uint32_t*)(dl + prow * N2 + nb) = pack4(v);
+    });
+  }
+  __syncthreads();
+  copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
+}
+
+// LDS regions of one workgroup: dl (depthwise output, later the second
+// 1x1's output), pl (the second 1x1's operand), o1 (the first 1x1's output
+// for HBM); all 16-byte aligned
+struct ChainLds {
+  int S1, S2, off_pl, off_o1;
+  size_t bytes;
+};
+static ChainLds chain_lds(const bh_chain_params& p) {
+  ChainLds L;
+  const int rows = p.px_blocks * 16;
+  L.S1 = p.pw1.k_pad + 16;
+  L.S2 = p.has_pw2 ? p.pw2.k_pad + 16 : 0;
+  const int dl_row = std::max(L.S1, p.has_pw2 ? (p.pw2.out_c + 15) / 16 * 16 : 0);
+  L.off_pl = rows * dl_row;
+  L.off_o1 = L.off_pl + rows * L.S2;
+  L.bytes = (size_t)L.off_o1 + (p.pw1.output ? (size_t)rows * ((p.pw1.out_c + 15) / 16 * 16) : 0);
+  return L;
+}
+
+template <int RB, bool FAST, int KX, int NW = 4>
+static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
+  if (lds > 64 * 1024) {
+    // opt in to the CU's full 160 KiB of LDS for this instantiation (once per device)
+    static thread_local int opted_device = -1;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (opted_device != dev) {
+      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
+      opted_device = dev;
+    }
+  }
+  ChainDivs dv;
+  dv.out_w = FastDiv(p.dw.out_w);
+  dv.out_h = FastDiv(p.dw.out_h);
+  const int blocks = (P + RB * 16 - 1) / (RB * 16);
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1, dv);
+}
+
+static bool conv1x1_ok(const bh_conv_params& c, int in_c) {
+  return c.k_h == 1 && c.k_w == 1 && c.stride_h == 1 && c.stride_w == 1 && c.pad_h == 0 && c.pad_w == 0 &&
+         c.in_c == in_c && c.k_pad == (in_c + 63) / 64 * 64 && c.n_pad >= (c.out_c + 15) / 16 * 16 &&
+         c.in_xor == 0 && c.w_zp == 0 && !c.out_table && c.out_c > 0 && c.out_c % 4 == 0 && c.weights &&
+         c.bias_eff && c.mult && c.shift;
+}
+
+}  // namespace bh
+
+extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
+  if (!pp) return 0;
+  const bh_chain_params& p = *pp;
+  const bh_dwconv_params& d = p.dw;
+  if (p.px_blocks != 1 && p.px_blocks != 2 && p.px_blocks != 4) return 0;
+  if (p.waves != 0 && p.waves != 4 && !(p.waves == 16 && p.px_blocks == 1)) return 0;
+  if (d.k_h != 3 || d.k_w != 3 || d.depth_multiplier != 1 || d.in_c != d.out_c || d.out_c % 16 || !d.taps ||
+      d.in_xor != 0 || d.w_zp != 0 || d.out_table || !d.input || !d.weights || !d.mult || !d.shift ||
+      d.batch <= 0 || d.out_h <= 0 || d.out_w <= 0 || d.stride_h <= 0 || d.stride_w <= 0)
+    return 0;
+  if (!bh::conv1x1_ok(p.pw1, d.out_c)) return 0;
+  const long P = (long)d.batch * d.out_h * d.out_w;
+  if (p.pw1.batch * p.pw1.out_h * p.pw1.out_w != P) return 0;
+  if (p.has_pw2) {
+    if (!bh::conv1x1_ok(p.pw2, p.pw1.out_c) || p.pw2.residual || !p.pw2.output ||
+        p.pw2.k_pad > 64 * bh::kXsMax)
+      return 0;
+    if ((long)p.pw2.batch * p.pw2.out_h * p.pw2.out_w != P) return 0;
+  } else if (!p.pw1.output) {
+    return 0;
+  }
+  const long widest = std::max<long>(std::max(d.out_c, p.pw1.out_c), p.has_pw2 ? p.pw2.out_c : 0);
+  if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
+  bh::ChainLds L = bh::chain_lds(p);
+  return L.bytes <= 160 * 1024 ? L.bytes : 0;
+}
+
+extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
+  const size_t lds = bh_chain_lds_bytes(pp);
+  if (lds == 0) {
+    bh_set_last_error("bh_chain_i8: invalid or unsupported parameters");
+    return BH_EINVAL;
+  }
+  const bh_chain_params& p = *pp;
+  const int P = p.dw.batch * p.dw.out_h * p.dw.out_w;
+  const bh::ChainLds L = bh::chain_lds(p);
+  const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast);
+  hipStream_t s = (hipStream_t)stream;
+  // K-steps of the register-resident (x-stationary) GEMMs: 2 when the
+  // second 1x1 has K <= 128 (fewer VGPRs, higher occupancy), else 5
+  const bool k2 = !p.has_pw2 || p.pw2.k_pad <= 128;
+#define BH_CHAIN_CASE(RB)                                                          \
+  if (k2) {                                                                        \
+    if (fast) bh::launch_chain<RB, true, 2>(p, P, L, lds, s);                     \
+    else bh::launch_chain<RB, false, 2>(p, P, L, lds, s);                         \
+  } else {                                                                         \
+    if (fast) bh::launch_chain<RB, true, bh::kXsMax>(p, P, L, lds, s);            \
+    else bh::launch_chain<RB, false, bh::kXsMax>(p, P, L, lds, s);                \
+  }
+  if (p.waves == 16) {  // one 16-pixel block, 16 waves (few-pixel layers)
+    if (k2) {
+      if (fast) bh::launch_chain<1, true, 2, 16>(p, P, L, lds, s);
+      else bh::launch_chain<1, false, 2, 16>(p, P, L, lds, s);
+    } else {
+      if (fast) bh::launch_chain<1, true, bh::kXsMax, 16>(p, P, L, lds, s);
+      else bh::launch_chain<1, false, bh::kXsMax, 16>(p, P, L, lds, s);
+    }
+    return bh_check_launch("chain_kernel");
+  }
+  switch (p.px_blocks) {
+    case 1: BH_CHAIN_CASE(1) break;
+    case 2: BH_CHAIN_CASE(2) break;
+    default: BH_CHAIN_CASE(4) break;
+  }
+#undef BH_CHAIN_CASE
+  return bh_check_launch("chain_kernel");
+}

@@ -19,6 +19,7 @@
  *   bh_eltwise_i8     <- ADD / SUB / MUL    (reference_integer_ops::Add / Mul, sub.cc)
  *   bh_pool_i8        <- AVERAGE_POOL_2D / MAX_POOL_2D (reference_integer_ops::{Average,Max}Pool)
  *   bh_irb_i8         <- [CONV_2D 1x1 ->] DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 [-> ADD], fused
+ *   bh_chain_i8       <- DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 [-> ADD] [-> CONV_2D 1x1], fused
  *   bh_lut_u8         <- QUANTIZE (8-bit -> 8-bit), RELU / RELU6 / RELU_N1_TO_1, LOGISTIC
  *   bh_lut_f32        <- DEQUANTIZE (8-bit -> float32)
  *   bh_quantize_f32   <- QUANTIZE (float32 -> 8-bit, reference_ops::AffineQuantize)
@@ -290,6 +291,38 @@ typedef struct bh_irb_params {
 /* LDS bytes one workgroup of bh_irb_i8 needs for a tile (0 if unsupported) */
 size_t bh_irb_lds_bytes(const bh_irb_params* p);
 int bh_irb_i8(const bh_irb_params* p, bh_stream_t s);
+
+/* Fused pointwise chain across a block boundary (int8 per-channel models):
+ *   DEPTHWISE_CONV_2D 3x3 -> CONV_2D 1x1 [-> ADD residual] [-> CONV_2D 1x1]
+ * i.e. a MobileNetV2 block's depthwise + project (+ its residual ADD) and the
+ * NEXT block's expand, or a MobileNetV1 depthwise + pointwise pair, exactly
+ * as the 2-3 TFLite ops compute them (every intermediate requantised to its
+ * own 8-bit tensor), in one launch.  No halo recompute: the 1x1 layers map
+ * pixel m to pixel m, so a workgroup owns px_blocks x 16 consecutive output
+ * pixels, computes their depthwise output for every channel into LDS
+ * (block-diagonal MFMA), the first 1x1 GEMM from LDS (MFMA) with its
+ * residual epilogue, and the second 1x1 GEMM from that result in LDS.
+ * Parameter blocks are the unfused launches' own (same packed operands):
+ *   dw.output and pw1.input are ignored (the depthwise result stays in LDS);
+ *   pw1.output may be NULL (the block output is private to pw2) or the
+ *   tensor to store; pw2 is read only when has_pw2.
+ * Supported: dw 3x3, depth multiplier 1, tap table, out_c % 16 == 0, any
+ * stride / dilation; all stages int8 in / symmetric filters (in_xor == 0,
+ * w_zp == 0), no out_table; pw1 / pw2 1x1 stride 1 with out_c % 4 == 0;
+ * pw2 without residual and with K = pw1.out_c <= 320.  px_blocks in {1, 2, 4};
+ * 16 waves (px_blocks 1) spread few-pixel layers' channel work wider. */
+typedef struct bh_chain_params {
+  bh_dwconv_params dw;
+  bh_conv_params pw1;
+  bh_conv_params pw2;
+  int has_pw2;
+  int px_blocks;
+  int waves;  /* waves per workgroup: 4 (0 = 4), or 16 with px_blocks == 1 */
+} bh_chain_params;
+
+/* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */
+size_t bh_chain_lds_bytes(const bh_chain_params* p);
+int bh_chain_i8(const bh_chain_params* p, bh_stream_t s);
 
 /* ---- host-side operand packing (pure CPU, no device calls) -------------- */
 

@@ -1,0 +1,124 @@
+"""Parity of the fused depthwise -> 1x1 [-> ADD] [-> 1x1] chain (bh_chain_i8)
+against the oracle running the TFLite ops one by one.  Bit-exact:
+
+* kernel level: every MobileNetV2 chain shape (a block's depthwise + project
+  [+ residual ADD] and the next block's expand), MobileNetV1 depthwise +
+  pointwise pairs, DeepLab's dilated chains, ragged pixel tails, every
+  px_blocks form, single-step and two-step requantisation;
+* executor level: the C3 mix models at 224x224 with every feasible chain
+  forced (BAND_HIP_FUSION=forcechain), one-job and job-batched passes.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey, tflite_synth as S
+from oracle.runner import OracleInterpreter
+from oracle.tflite_fb import Model as OModel
+from tests.chain_harness import MNV2_CHAINS, ChainCase
+
+pytestmark = pytest.mark.gpu
+
+
+def _check(c, lib, px, waves=4):
+    y_ref, f_ref = c.oracle()
+    y, f = c.gpu(lib, px, waves)
+    if c.store_pw1:
+        np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
+    if c.ce2:
+        np.testing.assert_array_equal(f, f_ref, err_msg="second conv, px_blocks %d" % px)
+
+
+@pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)
+def test_chain_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
+    rng = np.random.default_rng(h * 1000 + ce + cout + s)
+    c = ChainCase(rng, 1, h, h, ce, s, cout, res, ce2)
+    for px in (4, 2, 1):
+        _check(c, gpu_lib, px)
+    _check(c, gpu_lib, 1, waves=16)
+    c.fast = False  # TFLite's two-step requantisation in every stage
+    _check(c, gpu_lib, 4)
+
+
+@pytest.mark.parametrize("args", [
+    dict(b=2, h=112, w=112, ce=32, stride=1, cout=64, residual=False, ce2=0),      # MobileNetV1 pairs
+    dict(b=1, h=56, w=56, ce=128, stride=2, cout=256, residual=False, ce2=0),
+    dict(b=1, h=14, w=14, ce=512, stride=1, cout=512, residual=False, ce2=0),
+    dict(b=3, h=7, w=7, ce=1024, stride=1, cout=1024, residual=False, ce2=0),
+    dict(b=2, h=14, w=14, ce=576, stride=1, cout=96, residual=True, ce2=576, dil=2),  # DeepLab atrous
+    dict(b=1, h=14, w=14, ce=960, stride=1, cout=160, residual=True, ce2=960, dil=2),
+    dict(b=3, h=9, w=13, ce=48, stride=1, cout=24, residual=True, ce2=96),          # ragged pixel tail
+    dict(b=1, h=11, w=10, ce=64, stride=2, cout=40, residual=False, ce2=128),
+    dict(b=2, h=5, w=7, ce=16, stride=1, cout=8, residual=True, ce2=48),
+    dict(b=1, h=28, w=28, ce=144, stride=1, cout=24, residual=False, ce2=144, store_pw1=True),
+    dict(b=24, h=56, w=56, ce=144, stride=1, cout=24, residual=True, ce2=144),       # a batch-24 pass
+])
+def test_chain_general(gpu_lib, args):
+    rng = np.random.default_rng(sum(v for v in args.values() if isinstance(v, int)))
+    c = ChainCase(rng, **args)
+    for px in (4, 1):
+        _check(c, gpu_lib, px)
+    _check(c, gpu_lib, 1, waves=16)
+
+
+def test_chain_rejects_unsupported(gpu_lib):
+    import ctypes
+    rng = np.random.default_rng(5)
+    keep = []
+    c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep)
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
+    for field, bad in (("px_blocks", 3), ("waves", 8)):
+        old = getattr(c, field)
+        setattr(c, field, bad)
+        assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+        assert gpu_lib.bh_chain_i8(ctypes.byref(c), None) != 0
+        setattr(c, field, old)
+    c.dw.w_zp = 3  # asymmetric depthwise filter: not this kernel's
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+    c.dw.w_zp = 0
+    c.pw2.residual = c.pw1.weights  # the second conv never takes a residual
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+
+
+@pytest.fixture
+def forcechain():
+    old = os.environ.get("BAND_HIP_FUSION")
+    os.environ["BAND_HIP_FUSION"] = "forcechain"
+    yield
+    if old is None:
+        del os.environ["BAND_HIP_FUSION"]
+    else:
+        os.environ["BAND_HIP_FUSION"] = old
+
+
+@pytest.mark.parametrize("arch", list(S.MIX_C3))
+def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
+    buf = getattr(S, arch)(np.int8, size=224)
+    om = OModel(buf)
+    t = om.tensors[om.inputs[0]]
+    rng = np.random.default_rng(77 + len(arch))
+    xs = [rng.integers(-128, 128, t.shape).astype(np.int8) for _ in range(5)]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x}) for x in xs]
+    m = HipModel(41)
+    assert m.FromBuffer(buf).ok()
+    ex = HipModelExecutor(41, 1, DeviceFlag.kGPU)
+    assert ex.PrepareSubgraph(m).ok()
+    key = SubgraphKey(41, 1)
+    kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
+    assert "chain_kernel" in kernels, kernels
+    for rep in range(2):  # eager, then graph replay
+        ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
+        assert ex.ExecuteSubgraph(key).ok()
+        for o in om.outputs:
+            got = ex.GetTensorView(key, o).GetData()
+            np.testing.assert_array_equal(got, refs[0][o].reshape(got.shape), err_msg="%s run %d" % (arch, rep))
+    assert ex.PrepareJobBatches(m, key, 5).ok()
+    for s, x in enumerate(xs):
+        ex.GetJobSlotView(key, om.inputs[0], 5, s).GetData()[...] = x
+    assert ex.ExecuteJobBatch(key, 5).ok()
+    for s in range(5):
+        for o in om.outputs:
+            got = ex.GetJobSlotView(key, o, 5, s).GetData()
+            np.testing.assert_array_equal(got, refs[s][o].reshape(got.shape), err_msg="%s slot %d" % (arch, s))
+    ex._model_ref = m

@@ -73,6 +73,11 @@ class IrbParams(ctypes.Structure):
         ("input", c_void_p), ("output", c_void_p), ("debug_stamps", c_void_p), ("requant_fast", c_int32)]
 
 
+class MeanParams(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_long) for n in ("outer", "reduce", "inner")] + [("type", c_int)] + [
+        (n, c_int32) for n in ("multiplier", "shift", "bias")] + [("input", c_void_p), ("output", c_void_p)]
+
+
 class ChainParams(ctypes.Structure):
     _fields_ = [("dw", DwConvParams), ("pw1", ConvParams), ("pw2", ConvParams), ("has_pw2", c_int),
                 ("px_blocks", c_int), ("waves", c_int)]
@@ -200,6 +205,7 @@ KERNEL_SYMBOLS = {
     "bh_irb_i8": (c_int, [ctypes.POINTER(IrbParams), c_void_p]),
     "bh_irb_lds_bytes": (c_size_t, [ctypes.POINTER(IrbParams)]),
     "bh_chain_i8": (c_int, [ctypes.POINTER(ChainParams), c_void_p]),
+    "bh_mean": (c_int, [ctypes.POINTER(MeanParams), c_void_p]),
     "bh_chain_lds_bytes": (c_size_t, [ctypes.POINTER(ChainParams)]),
     "bh_last_error": (ctypes.c_char_p, []),
 }

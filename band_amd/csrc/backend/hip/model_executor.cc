@@ -364,8 +364,19 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
     case kTflRelu6:
     case kTflReluN1To1:
     case kTflLogistic:
+    case kTflHardSwish:
       if (!IsQ8(in.type) || out.type != in.type || !HasQ(in) || !HasQ(out)) return no("only 8-bit quantized");
+      if (op.builtin == kTflHardSwish) {
+        uint8_t t[256];
+        if (!HardSwishTable(in.type == DataType::kInt8, Scale(in), Zp(in), Scale(out), Zp(out), t))
+          return no("output multiplier exponent > 0 (TFLite HardSwishPrepare refuses it)");
+      }
       return true;
+    case kTflMean: {
+      long o, r, i;
+      if (!MeanArgs(m, op, &o, &r, &i)) return no("MEAN over one contiguous run of axes, 4-D keep_dims");
+      return true;
+    }
     case kTflSoftmax:
       if (!IsQ8(in.type) || out.type != in.type || !HasQ(in) || !HasQ(out) || in.shape.empty())
         return no("only 8-bit quantized in and out");
@@ -710,7 +721,8 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
     case kTflRelu:
     case kTflRelu6:
     case kTflReluN1To1:
-    case kTflLogistic: {
+    case kTflLogistic:
+    case kTflHardSwish: {
       L->src = in_ptr;
       L->dst = out_ptr;
       L->count = static_cast<long>(out.num_elements());
@@ -727,6 +739,9 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
         RequantizeTable(i8, Scale(in), Zp(in), out.type == DataType::kInt8, Scale(out), Zp(out), table);
       } else if (op.builtin == kTflLogistic) {
         LogisticTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), table);
+      } else if (op.builtin == kTflHardSwish) {
+        if (!HardSwishTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), table))
+          return absl::InternalError("HARD_SWISH: output multiplier exponent > 0");
       } else {
         const float lo = op.builtin == kTflReluN1To1 ? -1.0f : 0.0f;
         const float hi = op.builtin == kTflRelu6 ? 6.0f : 1.0f;
@@ -1898,7 +1913,7 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     L.kind = Launch::kDetectionPost;
     L.kernel = "detection_postprocess_host";
   } else if (op.builtin == kTflMean) {
-    // MEAN (CPU worker only: CpuSupports)
+    // MEAN: host kernel on a CPU worker, mean_kernel on the GPU
     CpuMeanParams& p = L.mean;
     p = CpuMeanParams{};
     if (!MeanArgs(d, op, &p.outer, &p.reduce, &p.inner)) return absl::InternalError("unsupported MEAN");
@@ -1917,7 +1932,7 @@ absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubg
     p.input = in_ptr;
     p.output = out_ptr;
     L.kind = Launch::kMean;
-    L.kernel = "mean_host";
+    L.kernel = device_flag_ == DeviceFlag::kGPU ? "mean_kernel" : "mean_host";
     L.alg_bytes = static_cast<double>(meta_[op.inputs[0]]->bytes + meta_[op.outputs[0]]->bytes);
   } else if (op.builtin == kTflTransposeConv) {
     RETURN_STATUS_IF(LowerTransposeConv(model, oi, out_ptr, ckey, sg, &L));
@@ -2162,8 +2177,21 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
       rc = bh_softmax_f32(static_cast<const float*>(l.src), static_cast<float*>(l.dst), l.count, l.depth, l.beta,
                           stream_);
       break;
-    case Launch::kDetectionPost:
-    case Launch::kMean: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
+    case Launch::kDetectionPost: return absl::InternalError(std::string(l.kernel) + " is a CPU-worker op");
+    case Launch::kMean: {
+      bh_mean_params q{};
+      q.outer = l.mean.outer;
+      q.reduce = l.mean.reduce;
+      q.inner = l.mean.inner;
+      q.type = l.mean.type;
+      q.multiplier = l.mean.multiplier;
+      q.shift = l.mean.shift;
+      q.bias = l.mean.bias;
+      q.input = l.mean.input;
+      q.output = l.mean.output;
+      rc = bh_mean(&q, stream_);
+      break;
+    }
   }
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }

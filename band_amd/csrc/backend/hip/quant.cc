@@ -3,6 +3,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <limits>
 
 namespace band {
 namespace hip {
@@ -181,6 +182,67 @@ void LogisticTable(bool is_signed, float in_scale, int32_t in_zp, float out_scal
     const int32_t quantized = static_cast<int32_t>(rescaled + static_cast<float>(out_zp));
     table[static_cast<uint8_t>(val)] = static_cast<uint8_t>(Clamp(quantized, minval, maxval));
   }
+}
+
+namespace {
+// int16 fixed-point primitives of reference_ops::HardSwish (TFLite 2.9.2
+// kernels/internal/reference/hard_swish.h and gemmlowp fixedpoint.h)
+int16_t SatRoundDoublingHighMul16(int16_t a, int16_t b) {
+  if (a == b && a == std::numeric_limits<int16_t>::min()) return std::numeric_limits<int16_t>::max();
+  const int32_t ab = static_cast<int32_t>(a) * static_cast<int32_t>(b);
+  const int32_t nudge = ab >= 0 ? (1 << 14) : (1 - (1 << 14));
+  return static_cast<int16_t>((ab + nudge) / (1 << 15));
+}
+int16_t SatDoublingHighMul16(int16_t a, int16_t b) {  // no rounding nudge
+  if (a == b && a == std::numeric_limits<int16_t>::min()) return std::numeric_limits<int16_t>::max();
+  return static_cast<int16_t>((static_cast<int32_t>(a) * static_cast<int32_t>(b)) / (1 << 15));
+}
+int16_t SatLeftShift16(int16_t v, int amount) {
+  const int64_t r = static_cast<int64_t>(v) * (int64_t{1} << amount);
+  return static_cast<int16_t>(std::min<int64_t>(std::max<int64_t>(r, -32768), 32767));
+}
+int16_t RoundDivPot16(int16_t x, int e) {
+  const int32_t mask = (1 << e) - 1;
+  const int32_t rem = x & mask;
+  const int32_t thr = (mask >> 1) + (x < 0 ? 1 : 0);
+  return static_cast<int16_t>((x >> e) + (rem > thr ? 1 : 0));
+}
+// quantization_util.h DownScaleInt32ToInt16Multiplier
+int16_t DownScaleMultiplier16(int32_t m) {
+  if (m >= std::numeric_limits<int32_t>::max() - (1 << 15)) return std::numeric_limits<int16_t>::max();
+  return static_cast<int16_t>((m + (1 << 15)) >> 16);
+}
+}  // namespace
+
+bool HardSwishTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp,
+                    uint8_t table[256]) {
+  const float hires_input_scale = (1.0f / 128.0f) * in_scale;
+  const float reluish_scale = 3.0f / 32768.0f;
+  const float output_multiplier = hires_input_scale / out_scale;
+  const float reluish_multiplier = hires_input_scale / reluish_scale;
+  int32_t om = 0, rm = 0;
+  int oexp = 0, rexp = 0;
+  QuantizeMultiplier(output_multiplier, &om, &oexp);
+  QuantizeMultiplier(reluish_multiplier, &rm, &rexp);
+  if (oexp > 0) return false;  // TF_LITE_ENSURE(output_multiplier_exponent <= 0)
+  const int16_t om16 = DownScaleMultiplier16(om), rm16 = DownScaleMultiplier16(rm);
+  const int32_t minval = is_signed ? -128 : 0, maxval = is_signed ? 127 : 255;
+  for (int32_t val = minval; val <= maxval; ++val) {
+    const int16_t x = static_cast<int16_t>(val - in_zp);
+    const int16_t hires = static_cast<int16_t>(x * (1 << 7));
+    const int16_t pre_out = SatRoundDoublingHighMul16(hires, om16);
+    int16_t reluish = hires;
+    if (rexp > 0) reluish = SatLeftShift16(reluish, rexp - 1);
+    reluish = SatRoundDoublingHighMul16(reluish, rm16);
+    if (rexp > 0) reluish = SatLeftShift16(reluish, 1);
+    if (rexp < 0) reluish = RoundDivPot16(reluish, -rexp);
+    reluish = static_cast<int16_t>((static_cast<int32_t>(reluish) + (1 << 15)) >> 1);
+    const int16_t pre = SatDoublingHighMul16(reluish, pre_out);
+    int16_t y = RoundDivPot16(pre, -oexp);
+    y = static_cast<int16_t>(y + out_zp);
+    table[static_cast<uint8_t>(val)] = static_cast<uint8_t>(Clamp(static_cast<int32_t>(y), minval, maxval));
+  }
+  return true;
 }
 
 void DequantizeTable(bool is_signed, float scale, int32_t zp, float table[256]) {

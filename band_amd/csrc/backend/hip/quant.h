@@ -62,6 +62,11 @@ void ReluTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, i
 // activations.cc PopulateLookupTable<T> with 1 / (1 + exp(-x))
 void LogisticTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp,
                    uint8_t table[256]);
+// activations.cc HardSwishPrepare (16-bit fixed-point multipliers) +
+// reference_ops::HardSwish<T> evaluated for every input byte; false when
+// TFLite's Prepare would refuse the scales (output exponent > 0)
+bool HardSwishTable(bool is_signed, float in_scale, int32_t in_zp, float out_scale, int32_t out_zp,
+                    uint8_t table[256]);
 // reference_ops::Dequantize: float(double(scale) * (q - zp))
 void DequantizeTable(bool is_signed, float scale, int32_t zp, float table[256]);
 // concatenation.cc ConcatenationWithScaling (uint8): round(q*s + b) + zp_out

@@ -507,3 +507,49 @@ extern "C" int bh_zero_insert(const bh_zero_insert_params* pp, bh_stream_t s) {
     BH_LAUNCH(bh::zero_insert_kernel<1>, dim3(bh::blocks(total)), dim3(256), 0, (hipStream_t)s, p, dv, total);
   return bh_check_launch("zero_insert_kernel");
 }
+
+// ---- MEAN ---------------------------------------------------------------
+// reduce.cc EvalMean (TFLite 2.9.2): optimized_integer_ops::Mean (int8) /
+// optimized_ops::Mean (uint8) sum the reduced window in int32, then
+// MultiplyByQuantizedMultiplier + the float-derived bias, clamped to the
+// type; float32 sums in order and divides by the count.  A thread owns one
+// output; neighbouring threads are neighbouring `inner` (channel) indices,
+// so every step of the reduction loop is one coalesced row read.
+namespace bh {
+__global__ __launch_bounds__(256) void mean_kernel(bh_mean_params p, long total) {
+  const long o = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (o >= total) return;
+  const long a = o / p.inner;
+  const long c = o - a * p.inner;
+  const long base = a * p.reduce * p.inner + c;
+  if (p.type == 0) {
+    const float* x = (const float*)p.input;
+    float s = 0.f;
+    for (long r = 0; r < p.reduce; ++r) s = __fadd_rn(s, x[base + r * p.inner]);
+    ((float*)p.output)[o] = __fdiv_rn(s, (float)p.reduce);
+    return;
+  }
+  int32_t acc = 0;
+  if (p.type == 1) {
+    const int8_t* x = (const int8_t*)p.input;
+    for (long r = 0; r < p.reduce; ++r) acc += x[base + r * p.inner];
+  } else {
+    const uint8_t* x = (const uint8_t*)p.input;
+    for (long r = 0; r < p.reduce; ++r) acc += x[base + r * p.inner];
+  }
+  acc = requant(acc, p.multiplier, p.shift) + p.bias;
+  if (p.type == 1) ((int8_t*)p.output)[o] = (int8_t)clamp_i32(acc, -128, 127);
+  else ((uint8_t*)p.output)[o] = (uint8_t)clamp_i32(acc, 0, 255);
+}
+}  // namespace bh
+
+extern "C" int bh_mean(const bh_mean_params* pp, bh_stream_t stream) {
+  if (!pp || pp->outer <= 0 || pp->reduce <= 0 || pp->inner <= 0 || pp->type < 0 || pp->type > 2 || !pp->input ||
+      !pp->output || pp->reduce * 255 >= (1l << 31)) {
+    bh_set_last_error("bh_mean: invalid parameters");
+    return BH_EINVAL;
+  }
+  const long total = pp->outer * pp->inner;
+  BH_LAUNCH(bh::mean_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *pp, total);
+  return bh_check_launch("mean_kernel");
+}

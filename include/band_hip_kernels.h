@@ -28,6 +28,8 @@
  *   bh_resize_nearest <- RESIZE_NEAREST_NEIGHBOR (reference_ops::ResizeNearestNeighbor)
  *   bh_resize_bilinear_i8 <- RESIZE_BILINEAR int8 (reference_ops::ResizeBilinearInteger)
  *   bh_softmax_i8     <- SOFTMAX 8-bit      (optimized_ops::Softmax, lookup-table path)
+ *   bh_mean           <- MEAN               (optimized_integer_ops::Mean / optimized_ops::Mean)
+ *   (HARD_SWISH 8-bit runs as a bh_lut_u8 table of reference_ops::HardSwish)
  *   bh_zero_insert + bh_conv2d_i8 <- TRANSPOSE_CONV int8 (reference_integer_ops::TransposeConv)
  *   bh_conv2d_f32 / bh_fc_f32 / bh_eltwise_f32 / bh_pool_f32 / bh_unary_f32 / bh_softmax_f32
  *                     <- the float32 forms of CONV_2D, DEPTHWISE_CONV_2D, FULLY_CONNECTED,
@@ -323,6 +325,20 @@ typedef struct bh_chain_params {
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */
 size_t bh_chain_lds_bytes(const bh_chain_params* p);
 int bh_chain_i8(const bh_chain_params* p, bh_stream_t s);
+
+/* MEAN over one contiguous run of axes (TFLite 2.9.2 reduce.cc EvalMean ->
+ * optimized_integer_ops::Mean int8 / optimized_ops::Mean uint8 / float):
+ * the input viewed as [outer][reduce][inner]; out[o][i] = for 8-bit types
+ * clamp(MultiplyByQuantizedMultiplier(sum_r x, multiplier, shift) + bias),
+ * for float32 (sum_r x in order) / reduce.  One thread per output. */
+typedef struct bh_mean_params {
+  long outer, reduce, inner;
+  int type;                       /* 0 float32, 1 int8, 2 uint8 */
+  int32_t multiplier, shift, bias;
+  const void* input;
+  void* output;
+} bh_mean_params;
+int bh_mean(const bh_mean_params* p, bh_stream_t s);
 
 /* ---- host-side operand packing (pure CPU, no device calls) -------------- */
 

@@ -62,6 +62,8 @@ def lib():
         L.tfl_relu_x.argtypes = [vp, c_i, c_l, c_i32, c_i32, c_i32, c_i, c_i32, c_i32, vp]
         L.tfl_logistic_table.argtypes = [c_f, c_i32, c_f, c_i32, c_i, vp]
         L.tfl_lookup.argtypes = [vp, c_l, vp, vp]
+        L.tfl_hard_swish.restype = c_i
+        L.tfl_hard_swish.argtypes = [vp, c_i, c_l, c_f, c_i32, c_f, c_i32, vp]
         L.tfl_softmax.argtypes = [vp, c_i, c_l, c_i, c_f, c_f, c_f, c_i32, vp]
         L.tfl_softmax_table.argtypes = [c_f, c_f, vp]
         L.tfl_transpose_conv_i8.argtypes = [vp, c_i, c_i, c_i, c_i, vp, c_i, c_i, c_i, vp, vp, c_i, c_i, c_i, c_i,
@@ -378,6 +380,19 @@ def mean_q8_hw(x, *, in_scale, in_zp, out_scale, out_zp):
     out = np.array([lib().tfl_mbqm(int(a), m, sh) for a in acc.reshape(-1)], np.int64).reshape(acc.shape) + bias
     lo, hi = (-128, 127) if x.dtype == np.int8 else (0, 255)
     return np.clip(out, lo, hi).astype(x.dtype)
+
+
+def hard_swish_q8(x, *, in_scale, in_zp, out_scale, out_zp):
+    """HARD_SWISH 8-bit (TFLite 2.9.2 activations.cc HardSwishPrepare +
+    reference_ops::HardSwish): oracle/tflite_ref.c tfl_hard_swish.
+    Parity unpinned: no reference fixture holds HARD_SWISH outputs."""
+    x = np.ascontiguousarray(x)
+    out = np.zeros_like(x)
+    rc = lib().tfl_hard_swish(_vp(x), int(x.dtype == np.int8), x.size, float(in_scale), int(in_zp),
+                              float(out_scale), int(out_zp), _vp(out))
+    if rc != 0:
+        raise ValueError("HARD_SWISH: output multiplier exponent > 0")
+    return out
 
 
 def squared_difference_f32(a, b):

@@ -434,6 +434,53 @@ void tfl_logistic_table(float in_scale, int32_t in_zp, float out_scale, int32_t 
     table[(uint8_t)val] = (uint8_t)clampi(quantized, minval, maxval);
   }
 }
+/* HARD_SWISH, 8-bit (TFLite 2.9.2 activations.cc HardSwishPrepare +
+ * reference/hard_swish.h HardSwish<T>): int16 fixed point throughout.
+ * Prepare: hires_input_scale = in_scale / 128, reluish_scale = 3 / 32768,
+ * QuantizeMultiplier of hires/out and hires/reluish, each multiplier then
+ * DownScaleInt32ToInt16Multiplier'd ((m + 2^15) >> 16, saturating). */
+static int16_t hs_sat16(int64_t v) { return (int16_t)(v < -32768 ? -32768 : (v > 32767 ? 32767 : v)); }
+static int16_t hs_srdhm16(int16_t a, int16_t b) { /* gemmlowp SaturatingRoundingDoublingHighMul<int16> */
+  if (a == -32768 && b == -32768) return 32767;
+  int32_t ab = (int32_t)a * b;
+  return (int16_t)((ab + (ab >= 0 ? 16384 : -16383)) / 32768);
+}
+static int16_t hs_sdhm16(int16_t a, int16_t b) { /* SaturatingDoublingHighMul: truncating */
+  if (a == -32768 && b == -32768) return 32767;
+  return (int16_t)(((int32_t)a * b) / 32768);
+}
+static int16_t hs_rdbypot16(int16_t x, int e) {
+  int32_t mask = (1 << e) - 1, rem = x & mask, thr = (mask >> 1) + (x < 0);
+  return (int16_t)((x >> e) + (rem > thr));
+}
+static int16_t hs_down16(int32_t m) { return m >= 2147483647 - 32768 ? 32767 : (int16_t)((m + 32768) >> 16); }
+
+int tfl_hard_swish(const uint8_t* in, int is_signed, long n, float in_scale, int32_t in_zp, float out_scale,
+                   int32_t out_zp, uint8_t* out) {
+  const float hires = (1.0f / 128.0f) * in_scale;
+  int32_t om32, rm32;
+  int oe, re;
+  tfl_quantize_multiplier((double)(hires / out_scale), &om32, &oe);
+  tfl_quantize_multiplier((double)(hires / (3.0f / 32768.0f)), &rm32, &re);
+  if (oe > 0) return -1; /* TF_LITE_ENSURE(output_multiplier_exponent <= 0) */
+  const int16_t om = hs_down16(om32), rm = hs_down16(rm32);
+  const int lo = is_signed ? -128 : 0, hi = is_signed ? 127 : 255;
+  for (long i = 0; i < n; ++i) {
+    const int16_t v = (int16_t)((int16_t)(ld(in, i, is_signed) - in_zp) * 128);
+    const int16_t on_out = hs_srdhm16(v, om);
+    int16_t r = v;
+    if (re > 0) r = hs_sat16((int64_t)r << (re - 1));
+    r = hs_srdhm16(r, rm);
+    if (re > 0) r = hs_sat16((int64_t)r * 2);
+    else if (re < 0) r = hs_rdbypot16(r, -re);
+    r = (int16_t)(((int32_t)r + 32768) >> 1);
+    int16_t y = hs_rdbypot16(hs_sdhm16(r, on_out), -oe);
+    y = (int16_t)(y + out_zp);
+    out[i] = (uint8_t)clampi(y, lo, hi);
+  }
+  return 0;
+}
+
 void tfl_lookup(const uint8_t* in, long n, const uint8_t* table, uint8_t* out) {
   for (long i = 0; i < n; ++i) out[i] = table[in[i]];
 }

@@ -145,3 +145,25 @@ def norm_zoo(with_mean=True):
 
 # BuiltinOptions union indices of the ops above (schema.fbs)
 OPT_REDUCER, OPT_SQDIFF, OPT_MIRROR_PAD = 27, 76, 77
+
+
+def hard_swish_model(dtype, in_scale=0.05, in_zp=3, out_scale=0.03, out_zp=-10):
+    """x [1, 4, 8, 8] 8-bit -> HARD_SWISH -> y (every input byte appears once)"""
+    mb = ModelBuilder("hard_swish")
+    x = mb.tensor("x", [1, 4, 8, 8], dtype, scale=in_scale, zero_point=in_zp)
+    y = mb.tensor("y", [1, 4, 8, 8], dtype, scale=out_scale, zero_point=out_zp)
+    mb.inputs = [x]
+    mb.op(117, [x], [y])
+    mb.outputs = [y]
+    return mb.build()
+
+
+def all_bytes(dtype):
+    lo = -128 if np.dtype(dtype) == np.int8 else 0
+    return np.arange(lo, lo + 256).astype(dtype).reshape(1, 4, 8, 8)
+
+
+HARD_SWISH_CASES = [  # (dtype, in_scale, in_zp, out_scale, out_zp)
+    (np.int8, 0.05, 3, 0.03, -10), (np.int8, 0.02, -128, 0.02, -100), (np.int8, 0.2, 0, 0.1, 0),
+    (np.uint8, 0.1, 128, 0.05, 20), (np.uint8, 0.03, 60, 0.04, 10),
+]

@@ -60,3 +60,24 @@ def test_mean_requant_edges():
     # RoundingDivideByPOT(-44, 3) = -6, bias 7: 1, not 2)
     assert orc.mean_q8_hw(np.full((1, 4, 4, 1), -3, np.int8), in_scale=0.02, in_zp=-3, out_scale=0.011,
                           out_zp=2).item() == 1
+
+
+import pytest  # noqa: E402
+
+from tests.glue_models import HARD_SWISH_CASES, all_bytes, hard_swish_model  # noqa: E402
+
+
+@pytest.mark.parametrize("dtype,s_in,zp_in,s_out,zp_out", HARD_SWISH_CASES)
+def test_hard_swish_cpu_executor(dtype, s_in, zp_in, s_out, zp_out):
+    """HARD_SWISH as the executor's 256-entry table (kCPU worker) vs the
+    oracle's element-wise restatement, every input byte.  Parity unpinned (no
+    reference fixture holds HARD_SWISH outputs); the fixed-point result stays
+    within 1 of the float formula x * relu6(x + 3) / 6."""
+    x = all_bytes(dtype)
+    got = run_executor(hard_swish_model(dtype, s_in, zp_in, s_out, zp_out), x, DeviceFlag.kCPU)[0]
+    ref = orc.hard_swish_q8(x, in_scale=s_in, in_zp=zp_in, out_scale=s_out, out_zp=zp_out)
+    np.testing.assert_array_equal(got.reshape(ref.shape), ref)
+    xf = np.float32(s_in) * (x.astype(np.float32) - zp_in)
+    lo, hi = (-128, 127) if np.dtype(dtype) == np.int8 else (0, 255)
+    fl = np.clip(np.round(xf * np.clip(xf + 3, 0, 6) / 6 / s_out) + zp_out, lo, hi)
+    assert np.abs(ref.astype(np.int32) - fl).max() <= 1

@@ -1,8 +1,8 @@
-"""MIRROR_PAD / SQUARED_DIFFERENCE / RSQRT on the GPU (pad_kernel's mirror
-mode, eltwise_f32_kernel, unary_f32_kernel) vs the oracle restatements, and
-the reference's magenta style-transfer fixture through a Band engine over
-[CPU, GPU] workers (MEAN stays on the CPU worker; the analyzer splits the
-model around it) against the CPU-only engine.  Float tolerance as the other
+"""MIRROR_PAD / SQUARED_DIFFERENCE / RSQRT / MEAN / HARD_SWISH on the GPU
+(pad_kernel's mirror mode, eltwise_f32_kernel, unary_f32_kernel,
+mean_kernel, the HARD_SWISH byte table) vs the oracle restatements, and the
+reference's magenta style-transfer fixture through a Band engine over
+[CPU, GPU] workers against the CPU-only engine.  Float tolerance as the other
 float tests: |got - ref| <= 1e-3 |ref| + 1e-4 max(1, max |ref|)."""
 import ctypes
 import os
@@ -82,3 +82,59 @@ def test_magenta_cpu_gpu_engine(golden_dir, tmp_path):
         outs[label] = o.data().copy()
         e.close()
     _close(outs["cpu+gpu"], outs["cpu"])
+
+
+from oracle import runner as orc  # noqa: E402
+from tests.glue_models import HARD_SWISH_CASES, all_bytes, hard_swish_model  # noqa: E402
+
+
+@pytest.mark.parametrize("dtype,s_in,zp_in,s_out,zp_out", HARD_SWISH_CASES)
+def test_hard_swish_gpu_executor(gpu_lib, dtype, s_in, zp_in, s_out, zp_out):
+    x = all_bytes(dtype)
+    got = run_executor(hard_swish_model(dtype, s_in, zp_in, s_out, zp_out), x, DeviceFlag.kGPU, worker=1)[0]
+    ref = orc.hard_swish_q8(x, in_scale=s_in, in_zp=zp_in, out_scale=s_out, out_zp=zp_out)
+    np.testing.assert_array_equal(got.reshape(ref.shape), ref)
+
+
+def test_norm_zoo_gpu_executor_with_mean(gpu_lib):
+    """the whole norm zoo, int8 MEAN included, on one GPU executor"""
+    x = np.random.default_rng(3).uniform(-1, 1, (1, 9, 11, 4)).astype(np.float32)
+    got = run_executor(norm_zoo(), x, DeviceFlag.kGPU, worker=1)
+    ref = norm_zoo_oracle(x)
+    for g, r in zip(got[:3], ref[:3]):  # mirror pads, int8 MEAN: exact
+        np.testing.assert_array_equal(g.reshape(r.shape), r)
+    for g, r in zip(got[3:], ref[3:]):
+        _close(g.reshape(r.shape), r)
+
+
+@pytest.mark.parametrize("dtype,shape", [(np.int8, (2, 7, 7, 1280)), (np.uint8, (3, 14, 9, 40)),
+                                         (np.int8, (1, 56, 56, 24)), (np.float32, (2, 7, 7, 96))])
+def test_mean_launcher(gpu_lib, dtype, shape):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(sum(shape))
+    if dtype == np.float32:
+        x = rng.standard_normal(shape).astype(np.float32)
+        ref = x.mean(axis=(1, 2), keepdims=True, dtype=np.float64)
+        m, sh, bias = 0, 0, 0
+    else:
+        lo, hi = (-128, 128) if dtype == np.int8 else (0, 256)
+        x = rng.integers(lo, hi, shape).astype(dtype)
+        s_in, zp_in, s_out, zp_out = 0.02, int(rng.integers(lo, hi)), 0.013, int(rng.integers(lo // 4, hi // 4))
+        ref = orc.mean_q8_hw(x, in_scale=s_in, in_zp=zp_in, out_scale=s_out, out_zp=zp_out)
+        n = np.float32(shape[1] * shape[2])
+        bias = zp_out - int(np.float32(np.float32(np.float32(zp_in) * np.float32(s_in)) / np.float32(s_out)))
+        m, sh = orc.quantize_multiplier(float(np.float32(np.float32(s_in) / np.float32(n * np.float32(s_out)))))
+    dx = DeviceBuffer.from_array(x)
+    dy = DeviceBuffer(ref.size * np.dtype(dtype).itemsize)
+    p = _abi.MeanParams(outer=shape[0], reduce=shape[1] * shape[2], inner=shape[3],
+                        type={np.float32: 0, np.int8: 1, np.uint8: 2}[dtype], multiplier=m, shift=sh, bias=bias,
+                        input=dx.value, output=dy.value)
+    _abi.check(gpu_lib.bh_mean(ctypes.byref(p), None), "bh_mean")
+    got = dy.download(dtype, ref.shape)
+    if dtype == np.float32:
+        _close(got, ref)
+    else:
+        np.testing.assert_array_equal(got, ref)
+    p.reduce = 0
+    assert gpu_lib.bh_mean(ctypes.byref(p), None) != 0

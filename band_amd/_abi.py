@@ -80,7 +80,7 @@ class MeanParams(ctypes.Structure):
 
 class ChainParams(ctypes.Structure):
     _fields_ = [("dw", DwConvParams), ("pw1", ConvParams), ("pw2", ConvParams), ("has_pw2", c_int),
-                ("px_blocks", c_int), ("waves", c_int)]
+                ("px_blocks", c_int), ("waves", c_int), ("persist", c_int)]
 
 
 # symbol -> (restype, argtypes)

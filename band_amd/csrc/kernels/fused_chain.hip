@@ -335,6 +335,293 @@ static ChainLds chain_lds(const bh_chain_params& p) {
   return L;
 }
 
+
+// ---- persistent form -------------------------------------------------------
+// For chains whose filters fit in LDS (the 112x112 .. 28x28 MobileNet blocks
+// and the 14x14 ones with narrow projections): a workgroup loads both 1x1
+// filters, the depthwise filter and every epilogue table into LDS ONCE, then
+// walks a contiguous range of 64-pixel blocks (ranges of one XCD adjacent,
+// so depthwise halo rows stay in one L2).  Per block the only global round
+// trips are the depthwise input loads - 12 per wave in flight (4 pixel
+// blocks x 3 taps of one 16-channel group, as dwconv3x3_mfma_kernel) - and
+// the residual reads; both 1x1 GEMMs run from LDS.  Outputs leave through
+// the contiguous LDS-staged copy.
+struct PersistLds {
+  int ws1, ws2, S1, S2;
+  int off_w2, off_t1, off_t2, off_dwt, off_dww, off_dl, off_pl, off_o1;
+  size_t bytes;
+};
+
+__host__ __device__ inline PersistLds persist_lds(const bh_chain_params& p) {
+  PersistLds L;
+  const int T1 = (p.pw1.out_c + 15) / 16;
+  const int T2 = p.has_pw2 ? (p.pw2.out_c + 15) / 16 : 0;
+  const int C = p.dw.out_c;
+  L.ws1 = p.pw1.k_pad + 16;
+  L.ws2 = p.has_pw2 ? p.pw2.k_pad + 16 : 0;
+  L.S1 = L.ws1;
+  L.S2 = L.ws2;
+  size_t o = (size_t)T1 * 16 * L.ws1;  // W1 at 0
+  L.off_w2 = (int)o;
+  o += (size_t)T2 * 16 * L.ws2;
+  L.off_t1 = (int)o;
+  o += 12 * (size_t)T1 * 16;
+  L.off_t2 = (int)o;
+  o += 12 * (size_t)T2 * 16;
+  L.off_dwt = (int)o;
+  o += 12 * (size_t)C;
+  L.off_dww = (int)o;
+  o += (9 * (size_t)C + 15) / 16 * 16;
+  const int dl_row = L.S1 > (T2 * 16) ? L.S1 : T2 * 16;
+  L.off_dl = (int)o;
+  o += 64 * (size_t)dl_row;
+  L.off_pl = (int)o;
+  o += 64 * (size_t)L.S2;
+  L.off_o1 = (int)o;
+  o += p.pw1.output ? 64 * (size_t)T1 * 16 : 0;
+  L.bytes = o;
+  return L;
+}
+
+template <bool FAST, int KX>
+__global__ __launch_bounds__(256) void chain_persist_kernel(bh_chain_params cp, int P, PersistLds L, ChainDivs dv) {
+  typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r16 = lane & 15;
+  const int g = lane >> 4;
+  const bh_dwconv_params& d = cp.dw;
+  const bh_conv_params& a = cp.pw1;
+  const bh_conv_params& b = cp.pw2;
+  const int C = d.out_c, G = C >> 4;
+  const int N1 = a.out_c, T1 = (N1 + 15) >> 4, KS1 = a.k_pad >> 6;
+  const int N2 = cp.has_pw2 ? b.out_c : 0, T2 = (N2 + 15) >> 4, KS2 = cp.has_pw2 ? b.k_pad >> 6 : 0;
+  unsigned char* W1 = smem;
+  unsigned char* W2 = smem + L.off_w2;
+  int* t1 = (int*)(smem + L.off_t1);   // bias_eff | mult | shift, T1*16 each (zero past N1)
+  int* t2 = (int*)(smem + L.off_t2);
+  int* dwt = (int*)(smem + L.off_dwt); // folded bias | mult | shift, C each
+  unsigned char* dww = smem + L.off_dww;
+  unsigned char* dl = smem + L.off_dl;
+  unsigned char* pl = smem + L.off_pl;
+  unsigned char* o1 = smem + L.off_o1;
+
+  // ---- prologue: filters and tables -> LDS (once per workgroup) ----------
+  {
+    const int cpr1 = a.k_pad >> 4;
+    for (int i = tid; i < T1 * 16 * cpr1; i += 256) {
+      const int r = i / cpr1, c = i - r * cpr1;
+      *(v4i*)(W1 + r * L.ws1 + c * 16) = *(const v4i*)(a.weights + (long)r * a.k_pad + c * 16);
+    }
+    if (cp.has_pw2) {
+      const int cpr2 = b.k_pad >> 4;
+      for (int i = tid; i < T2 * 16 * cpr2; i += 256) {
+        const int r = i / cpr2, c = i - r * cpr2;
+        *(v4i*)(W2 + r * L.ws2 + c * 16) = *(const v4i*)(b.weights + (long)r * b.k_pad + c * 16);
+      }
+    }
+    for (int i = tid; i < T1 * 16; i += 256) {
+      const bool v = i < N1;
+      t1[i] = v ? a.bias_eff[i] : 0;
+      t1[T1 * 16 + i] = v ? a.mult[i] : 0;
+      t1[2 * T1 * 16 + i] = v ? a.shift[i] : 0;
+    }
+    for (int i = tid; i < T2 * 16; i += 256) {
+      const bool v = i < N2;
+      t2[i] = v ? b.bias_eff[i] : 0;
+      t2[T2 * 16 + i] = v ? b.mult[i] : 0;
+      t2[2 * T2 * 16 + i] = v ? b.shift[i] : 0;
+    }
+    for (int i = tid; i < C; i += 256) {
+      dwt[i] = d.taps[4 * i + 3];
+      dwt[C + i] = d.mult[i];
+      dwt[2 * C + i] = d.shift[i];
+    }
+    for (int i = tid; i < 9 * C / 4; i += 256) ((uint32_t*)dww)[i] = ((const uint32_t*)d.weights)[i];
+  }
+  __syncthreads();
+
+  const int nblocks = (P + 63) >> 6;
+  const int logical = xcd_block(blockIdx.x, gridDim.x);
+  const int per = (nblocks + gridDim.x - 1) / gridDim.x;
+  const int kb0 = logical * per;
+  const int kb1 = min(nblocks, kb0 + per);
+  const __amdgpu_buffer_rsrc_t rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)d.input, (short)0, d.batch * d.in_h * d.in_w * C, 0x00020000);
+  const int zfill = (int)splat_byte(d.in_zp);
+  const int dsel = r16 >> 2;
+  const int bsh = 8 * (r16 & 3);
+  const int prow = wave * 16 + r16;  // phases B / C: this wave's 16 pixels
+  const uint8_t* res = (const uint8_t*)a.residual;
+  uint8_t* out1 = (uint8_t*)a.output;
+
+  for (int kb = kb0; kb < kb1; ++kb) {
+    const int m0 = kb * 64;
+    const int rows = min(64, P - m0);
+    // ---- phase A: wave w takes channel groups w, w+4, ... of all 64 pixels
+    {
+      int off[4][3];
+      bool ok[4][3];
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        const int m = m0 + pb * 16 + r16;
+        const bool mv = m < P;
+        const int mm = mv ? m : 0;
+        const int t = dv.out_w.div(mm);
+        const int ox = mm - t * d.out_w;
+        const int n = dv.out_h.div(t);
+        const int oy = t - n * d.out_h;
+        const int iy = oy * d.stride_h, ix = ox * d.stride_w, row0 = n * d.in_h;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int tap = 4 * s + g;
+          const int fy = (tap * 11) >> 5;
+          const int fx = tap - 3 * fy;
+          const int y = iy + fy * d.dil_h - d.pad_h, x = ix + fx * d.dil_w - d.pad_w;
+          ok[pb][s] = mv && tap < 9 && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
+          off[pb][s] = ok[pb][s] ? ((row0 + y) * d.in_w + x) * C : 0;
+        }
+      }
+      for (int cg = wave; cg < G; cg += 4) {
+        const int c0 = cg * 16;
+        v4i xf[4][3];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+          for (int s = 0; s < 3; ++s) {
+            const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[pb][s] + c0, 0, 0);
+            xf[pb][s] = (v4i){ok[pb][s] ? (int)v.x : zfill, ok[pb][s] ? (int)v.y : zfill,
+                              ok[pb][s] ? (int)v.z : zfill, ok[pb][s] ? (int)v.w : zfill};
+          }
+        v4i wf[3];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const int tap = 4 * s + g;
+          const uint32_t wb = tap < 9 ? (uint32_t)dww[tap * C + c0 + r16] : 0u;
+          const int w = (int)(wb << bsh);
+          wf[s] = (v4i){dsel == 0 ? w : 0, dsel == 1 ? w : 0, dsel == 2 ? w : 0, dsel == 3 ? w : 0};
+        }
+        const int co = c0 + 4 * g;
+        const v4i be = *(const v4i*)(dwt + co);
+        const v4i mm4 = *(const v4i*)(dwt + C + co);
+        const v4i ss4 = *(const v4i*)(dwt + 2 * C + co);
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          v4i acc = be;
+#pragma unroll
+          for (int s = 0; s < 3; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[s], xf[pb][s], acc, 0, 0, 0);
+          int32_t v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            v[r] = requant_out<FAST>(acc[r], chan_q(mm4[r], ss4[r], d.out_zp), d.out_zp, d.act_min, d.act_max);
+          *(uint32_t*)(dl + (pb * 16 + r16) * L.S1 + co) = pack4(v);
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- phase B: first 1x1 from LDS; wave w takes channel tiles w, w+4,
+    // ... for all 64 pixels, so each tile's channel constants (ChanQ) are
+    // derived once for 16 values per lane and its filter fragments read once
+    {
+      int mp[4];
+      bool mv[4];
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb) {
+        mp[pb] = m0 + pb * 16 + r16;
+        mv[pb] = mp[pb] < P;
+      }
+      for (int t = wave; t < T1; t += 4) {
+        const unsigned char* wrow = W1 + (t * 16 + r16) * L.ws1 + g * 16;
+        const int nb = t * 16 + 4 * g;
+        const v4i be = *(const v4i*)(t1 + nb);
+        v4i acc[4] = {be, be, be, be};
+        for (int k = 0; k < KS1; ++k) {
+          const v4i w = *(const v4i*)(wrow + k * 64);
+#pragma unroll
+          for (int pb = 0; pb < 4; ++pb)
+            acc[pb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(
+                w, *(const v4i*)(dl + (pb * 16 + r16) * L.S1 + g * 16 + k * 64), acc[pb], 0, 0, 0);
+        }
+        if (nb >= N1) continue;
+        const v4i vm = *(const v4i*)(t1 + T1 * 16 + nb);
+        const v4i vs = *(const v4i*)(t1 + 2 * T1 * 16 + nb);
+        ChanQ q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = chan_q(vm[r], vs[r], a.out_zp);
+        uint32_t rq[4];
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) rq[pb] = res && mv[pb] ? *(const uint32_t*)(res + (long)mp[pb] * N1 + nb) : 0u;
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          int32_t v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb][r], q[r], a.out_zp, a.act_min, a.act_max);
+          if (res) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int32_t qv = sbyte(rq[pb], r);
+              const int32_t sy =
+                  requant_lt1((v[r] + a.add_y_off) * (1 << a.add_left_shift), a.add_y_mult, a.add_y_shift);
+              const int32_t sr =
+                  requant_lt1((qv + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
+              v[r] = clamp_i32(requant_lt1(sy + sr, a.add_o_mult, a.add_o_shift) + a.add_o_off, a.add_act_min,
+                               a.add_act_max);
+            }
+          }
+          const uint32_t pk = pack4(v);
+          const int row = pb * 16 + r16;
+          if (out1) *(uint32_t*)(o1 + row * N1 + nb) = pk;
+          if (cp.has_pw2) *(uint32_t*)(pl + row * L.S2 + nb) = pk;
+        }
+      }
+    }
+    __syncthreads();
+    if (out1) copy_out(o1, out1 + (long)m0 * N1, rows * N1);
+    if (cp.has_pw2) {
+      // ---- phase C: second 1x1 from LDS -> dl (row stride N2); the 64
+      // pixels' K fragments stay in registers (K <= 64 * KX)
+      v4i x[4][KX];
+#pragma unroll
+      for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+        for (int k = 0; k < KX; ++k)
+          x[pb][k] = k < KS2 ? *(const v4i*)(pl + (pb * 16 + r16) * L.S2 + g * 16 + k * 64) : (v4i){0, 0, 0, 0};
+      for (int t = wave; t < T2; t += 4) {
+        const unsigned char* wrow = W2 + (t * 16 + r16) * L.ws2 + g * 16;
+        const int nb = t * 16 + 4 * g;
+        const v4i be = *(const v4i*)(t2 + nb);
+        v4i acc[4] = {be, be, be, be};
+#pragma unroll
+        for (int k = 0; k < KX; ++k)
+          if (k < KS2) {
+            const v4i w = *(const v4i*)(wrow + k * 64);
+#pragma unroll
+            for (int pb = 0; pb < 4; ++pb) acc[pb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(w, x[pb][k], acc[pb], 0, 0, 0);
+          }
+        if (nb >= N2) continue;
+        const v4i vm = *(const v4i*)(t2 + T2 * 16 + nb);
+        const v4i vs = *(const v4i*)(t2 + 2 * T2 * 16 + nb);
+        ChanQ q[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) q[r] = chan_q(vm[r], vs[r], b.out_zp);
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) {
+          int32_t v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb][r], q[r], b.out_zp, b.act_min, b.act_max);
+          *(uint32_t*)(dl + (pb * 16 + r16) * N2 + nb) = pack4(v);
+        }
+      }
+      __syncthreads();
+      copy_out(dl, (uint8_t*)b.output + (long)m0 * N2, rows * N2);
+    }
+    __syncthreads();  // dl / o1 are rewritten by the next block
+  }
+}
+
 template <int RB, bool FAST, int KX, int NW = 4>
 static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024) {
@@ -353,6 +640,36 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_h = FastDiv(p.dw.out_h);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
   BH_LAUNCH((chain_kernel<RB, FAST, KX, NW>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1, dv);
+}
+
+template <bool FAST, int KX>
+static void launch_persist(const bh_chain_params& p, int P, size_t lds, hipStream_t s) {
+  static thread_local int opted_device = -1;
+  int dev = 0;
+  (void)hipGetDevice(&dev);
+  if (opted_device != dev) {
+    (void)hipFuncSetAttribute((const void*)chain_persist_kernel<FAST, KX>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
+    opted_device = dev;
+  }
+  ChainDivs dv;
+  dv.out_w = FastDiv(p.dw.out_w);
+  dv.out_h = FastDiv(p.dw.out_h);
+  const int nblocks = (P + 63) / 64;
+  // workgroups resident per CU (registers and LDS, <= 4), 256 CUs: one
+  // wave of workgroups, each taking a contiguous range of pixel blocks
+  static thread_local size_t cached_lds = 0;
+  static thread_local int cached_per_cu = 1;
+  if (cached_lds != lds) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, chain_persist_kernel<FAST, KX>, 256, lds) != hipSuccess)
+      n = 1;
+    cached_per_cu = std::max(1, std::min(4, n));
+    cached_lds = lds;
+  }
+  const int per_cu = cached_per_cu;
+  const int grid = std::min(nblocks, 256 * per_cu);
+  BH_LAUNCH((chain_persist_kernel<FAST, KX>), dim3(grid), dim3(256), lds, s, p, P, persist_lds(p), dv);
 }
 
 static bool conv1x1_ok(const bh_conv_params& c, int in_c) {
@@ -387,6 +704,11 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   }
   const long widest = std::max<long>(std::max(d.out_c, p.pw1.out_c), p.has_pw2 ? p.pw2.out_c : 0);
   if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
+  if (p.persist) {
+    if (p.px_blocks != 4 || (p.waves != 0 && p.waves != 4)) return 0;
+    const size_t bytes = bh::persist_lds(p).bytes;
+    return bytes <= 160 * 1024 ? bytes : 0;
+  }
   bh::ChainLds L = bh::chain_lds(p);
   return L.bytes <= 160 * 1024 ? L.bytes : 0;
 }
@@ -412,6 +734,16 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
   } else {                                                                         \
     if (fast) bh::launch_chain<RB, true, bh::kXsMax>(p, P, L, lds, s);            \
     else bh::launch_chain<RB, false, bh::kXsMax>(p, P, L, lds, s);                \
+  }
+  if (p.persist) {
+    if (k2) {
+      if (fast) bh::launch_persist<true, 2>(p, P, lds, s);
+      else bh::launch_persist<false, 2>(p, P, lds, s);
+    } else {
+      if (fast) bh::launch_persist<true, bh::kXsMax>(p, P, lds, s);
+      else bh::launch_persist<false, bh::kXsMax>(p, P, lds, s);
+    }
+    return bh_check_launch("chain_persist_kernel");
   }
   if (p.waves == 16) {  // one 16-pixel block, 16 waves (few-pixel layers)
     if (k2) {

@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4):
+def _check(c, lib, px, waves=4, persist=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves)
+    y, f = c.gpu(lib, px, waves, persist)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -37,8 +37,12 @@ def test_chain_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
     for px in (4, 2, 1):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
+    if _persist_fits(c, gpu_lib):
+        _check(c, gpu_lib, 4, persist=1)
     c.fast = False  # TFLite's two-step requantisation in every stage
     _check(c, gpu_lib, 4)
+    if _persist_fits(c, gpu_lib):
+        _check(c, gpu_lib, 4, persist=1)
 
 
 @pytest.mark.parametrize("args", [
@@ -60,6 +64,14 @@ def test_chain_general(gpu_lib, args):
     for px in (4, 1):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
+    if _persist_fits(c, gpu_lib):
+        _check(c, gpu_lib, 4, persist=1)
+
+
+def _persist_fits(c, lib):
+    import ctypes
+    keep = []
+    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, 4, keep, 4, 1))) > 0
 
 
 def test_chain_rejects_unsupported(gpu_lib):

@@ -21,7 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--px", default="1,2,4,1w16")
+    ap.add_argument("--px", default="1,2,4,1w16,4p")
+    ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
     from tests.chain_harness import MNV2_CHAINS, ChainCase
@@ -32,13 +33,16 @@ def main():
     lib.bh_event_create(ctypes.byref(e0))
     lib.bh_event_create(ctypes.byref(e1))
     total = {}
-    for (h, ce, s, cout, res, ce2) in MNV2_CHAINS:
+    only = [int(v) for v in a.only.split(",")] if a.only else list(range(len(MNV2_CHAINS)))
+    for (h, ce, s, cout, res, ce2) in [MNV2_CHAINS[i] for i in only]:
         c = ChainCase(np.random.default_rng(1), a.batch, h, h, ce, s, cout, res, ce2)
         row = []
         for form in a.px.split(","):
-            px, waves = (int(form.split("w")[0]), int(form.split("w")[1])) if "w" in form else (int(form), 4)
+            persist = int(form.endswith("p"))
+            f = form.rstrip("p")
+            px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves)
+            q = c.params(lib, px, keep, waves, persist)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue

@@ -156,6 +156,76 @@ __device__ __forceinline__ void copy_out(const unsigned char* src, uint8_t* dst,
     *(uint32_t*)(dst + n16 * 16 + threadIdx.x * 4) = *(const uint32_t*)(src + n16 * 16 + threadIdx.x * 4);
 }
 
+// The non-persistent chain computes every GEMM UNtransposed, D = X W^T:
+// lane (r16, g) of v_mfma_i32_16x16x64_i8 ends with D[4g + r][r16], i.e.
+// FOUR PIXELS of ONE channel.  The channel's requantisation constants
+// (ChanQ: a 64-bit rounding constant, shifts, masks) are then derived once
+// for 4 values instead of once per value, and the results go to the LDS
+// staging tiles as bytes (no packing); the HBM stores stay the contiguous
+// 16-byte copy_out.  The operand fragments are the same bytes as the
+// transposed form's: only the MFMA operand order changes.
+__device__ __forceinline__ v4i gemm_tile_nt(const bh_conv_params& c, const unsigned char* xrow, int t, int KS,
+                                            int r16, int g) {
+  const int8_t* wrow = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
+  const int n = t * 16 + r16;
+  const int be = c.bias_eff[n < c.out_c ? n : 0];
+  v4i acc = (v4i){be, be, be, be};
+  int k = 0;
+  for (; k + 8 <= KS; k += 8) {
+    v4i w[8], x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      w[u] = *(const v4i*)(wrow + (k + u) * 64);
+      x[u] = *(const v4i*)(xrow + (k + u) * 64);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[u], w[u], acc, 0, 0, 0);
+  }
+  for (; k < KS; ++k) {
+    const v4i w = *(const v4i*)(wrow + k * 64);
+    const v4i x = *(const v4i*)(xrow + k * 64);
+    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, w, acc, 0, 0, 0);
+  }
+  return acc;
+}
+
+// x-stationary form of gemm_tile_nt for K <= 64 * KMAX, two channel tiles
+// per memory round trip; epi(t, n, acc, mult, shift) finishes a tile for
+// this lane's channel n (may be >= out_c).
+template <int KMAX, typename Epi>
+__device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsigned char* xrow, int KS, int t0,
+                                           int tstep, int r16, int g, Epi&& epi) {
+  v4i x[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k) x[k] = k < KS ? *(const v4i*)(xrow + k * 64) : (v4i){0, 0, 0, 0};
+  const int T = (c.out_c + 15) >> 4;
+  for (int t = t0; t < T; t += 2 * tstep) {
+    const int tb = t + tstep < T ? t + tstep : t;
+    const int8_t* ra = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
+    const int8_t* rb = c.weights + (long)(tb * 16 + r16) * c.k_pad + g * 16;
+    v4i wa[KMAX], wb[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) {
+        wa[k] = *(const v4i*)(ra + k * 64);
+        wb[k] = *(const v4i*)(rb + k * 64);
+      }
+    const int na = t * 16 + r16, nb = tb * 16 + r16;
+    const int la = na < c.out_c ? na : 0, lb = nb < c.out_c ? nb : 0;
+    const int ba = c.bias_eff[la], bb = c.bias_eff[lb];
+    const int ma = c.mult[la], sa = c.shift[la], mb = c.mult[lb], sb = c.shift[lb];
+    v4i acca = (v4i){ba, ba, ba, ba}, accb = (v4i){bb, bb, bb, bb};
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) {
+        acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], wa[k], acca, 0, 0, 0);
+        accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], wb[k], accb, 0, 0, 0);
+      }
+    epi(t, na, acca, ma, sa);
+    if (tb != t) epi(tb, nb, accb, mb, sb);
+  }
+}
+
 template <int RB, bool FAST, int KX, int NW>
 __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     ChainDivs dv) {
@@ -169,14 +239,15 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
   const int pb = wave % RB;
   const int wsub = wave / RB;
   const int blk = xcd_block(blockIdx.x, gridDim.x);
-  const int m = (blk * RB + pb) * 16 + r16;  // this lane's pixel (B operand column)
+  const int m0 = blk * RB * 16;
+  const int rows = min(RB * 16, P - m0);
+  const int m = m0 + pb * 16 + r16;  // this lane's pixel as an A-operand row
   const bool mval = m < P;
   unsigned char* dl = smem;           // [RB*16][S1] depthwise output; then [RB*16][N2] second 1x1 output
   unsigned char* pl = smem + off_pl;  // [RB*16][S2] first 1x1 output (second 1x1's operand)
   unsigned char* o1 = smem + off_o1;  // [RB*16][N1] first 1x1 output staged for HBM
-  const int m0 = blk * RB * 16;
-  const int rows = min(RB * 16, P - m0);
-  const int prow = pb * 16 + r16;
+  const int prow = pb * 16 + r16;     // this lane's operand row
+  const int orow = pb * 16 + 4 * g;   // first of this lane's 4 result rows
 
   // ---- phase A: depthwise 3x3 -> LDS -------------------------------------
   {
@@ -210,8 +281,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     struct DwItem {
       v4i xf[3];
       uint32_t wb[3];
-      v4i mm4, ss4;
-      int32_t be[4];
+      int32_t be, mu, sh;
     };
     auto dw_load = [&](int cg, DwItem& it) {
       const int c0 = cg * 16;
@@ -223,26 +293,24 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
         const int tap = 4 * s + g;
         it.wb[s] = tap < 9 ? (uint32_t)(uint8_t)d.weights[tap * C + c0 + r16] : 0u;
       }
-      const int co = c0 + 4 * g;
-      it.mm4 = *(const v4i*)(d.mult + co);
-      it.ss4 = *(const v4i*)(d.shift + co);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) it.be[r] = d.taps[4 * (co + r) + 3];
+      const int c = c0 + r16;  // this lane's result channel
+      it.be = d.taps[4 * c + 3];
+      it.mu = d.mult[c];
+      it.sh = d.shift[c];
     };
     auto dw_finish = [&](int cg, const DwItem& it) {
-      v4i acc = (v4i){0, 0, 0, 0};
+      v4i acc = (v4i){it.be, it.be, it.be, it.be};
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
         const int w = (int)(it.wb[s] << bsh);
         const v4i wf = (v4i){dsel == 0 ? w : 0, dsel == 1 ? w : 0, dsel == 2 ? w : 0, dsel == 3 ? w : 0};
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf, it.xf[s], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(it.xf[s], wf, acc, 0, 0, 0);
       }
-      int32_t v[4];
+      const ChanQ q = chan_q(it.mu, it.sh, d.out_zp);
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        v[r] = requant_out<FAST>(acc[r] + it.be[r], chan_q(it.mm4[r], it.ss4[r], d.out_zp), d.out_zp, d.act_min,
-                                 d.act_max);
-      *(uint32_t*)(dl + prow * S1 + cg * 16 + 4 * g) = pack4(v);
+        dl[(orow + r) * S1 + cg * 16 + r16] =
+            (unsigned char)requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
     };
     const int G = C >> 4;
     for (int cg = wsub; cg < G; cg += 2 * WPB) {
@@ -256,7 +324,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
   }
   __syncthreads();
 
-  // ---- phase B: first 1x1 (+ residual ADD) -> HBM and / or LDS ----------
+  // ---- phase B: first 1x1 (+ residual ADD) -> LDS (operand) / LDS (staged) -
   {
     const bh_conv_params& a = cp.pw1;
     const int N1 = a.out_c;
@@ -264,34 +332,42 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     const int KS1 = a.k_pad >> 6;
     const unsigned char* xrow = dl + prow * S1 + g * 16;
     const uint8_t* res = (const uint8_t*)a.residual;
-    uint8_t* out1 = (uint8_t*)a.output;
-    auto epi = [&](int t, int nb, v4i acc, v4i vm, v4i vs) {
-      if (nb >= N1) return;  // N1 % 4 == 0: all 4 channels valid
+    const bool out1 = a.output != nullptr;
+    auto epi = [&](int t, int n, v4i acc, int mu, int sh) {
+      if (n >= N1) return;
+      const ChanQ q = chan_q(mu, sh, a.out_zp);
       int32_t v[4];
-      requant4m<FAST>(a, acc, vm, vs, v);
-      if (res && mval) {
-        const uint32_t rq = *(const uint32_t*)(res + (long)m * N1 + nb);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, a.out_zp, a.act_min, a.act_max);
+      if (res) {
+        int32_t rq[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int32_t qv = sbyte(rq, r);
+          const int mr = m0 + orow + r;
+          rq[r] = mr < P ? (int32_t)(int8_t)res[(long)mr * N1 + n] : 0;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
           const int32_t sy = requant_lt1((v[r] + a.add_y_off) * (1 << a.add_left_shift), a.add_y_mult, a.add_y_shift);
-          const int32_t sr = requant_lt1((qv + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
+          const int32_t sr = requant_lt1((rq[r] + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
           v[r] = clamp_i32(requant_lt1(sy + sr, a.add_o_mult, a.add_o_shift) + a.add_o_off, a.add_act_min,
                            a.add_act_max);
         }
       }
-      const uint32_t pk = pack4(v);
-      if (out1) *(uint32_t*)(o1 + prow * N1 + nb) = pk;
-      if (cp.has_pw2) *(uint32_t*)(pl + prow * S2 + nb) = pk;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        if (out1) o1[(orow + r) * N1 + n] = (unsigned char)v[r];
+        if (cp.has_pw2) pl[(orow + r) * S2 + n] = (unsigned char)v[r];
+      }
     };
     if (KS1 <= KX) {
-      gemm_xs<KX>(a, xrow, KS1, wsub, WPB, r16, g, epi);
+      gemm_xs_nt<KX>(a, xrow, KS1, wsub, WPB, r16, g, epi);
     } else {
       for (int t = wsub; t < T1; t += WPB) {
-        const v4i acc = gemm_tile(a, xrow, t, KS1, r16, g);
-        const int nb = t * 16 + 4 * g;
-        const int nl = nb < N1 ? nb : 0;
-        epi(t, nb, acc, *(const v4i*)(a.mult + nl), *(const v4i*)(a.shift + nl));
+        const v4i acc = gemm_tile_nt(a, xrow, t, KS1, r16, g);
+        const int n = t * 16 + r16;
+        const int nl = n < N1 ? n : 0;
+        epi(t, n, acc, a.mult[nl], a.shift[nl]);
       }
     }
   }
@@ -299,17 +375,18 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
   if (cp.pw1.output) copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
   if (!cp.has_pw2) return;
 
-  // ---- phase C: second 1x1 -> HBM -----------------------------------------
+  // ---- phase C: second 1x1 -> LDS staging (dl, row stride N2) -> HBM ------
   {
     const bh_conv_params& b = cp.pw2;
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
     const unsigned char* xrow = pl + prow * S2 + g * 16;
-    gemm_xs<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int nb, v4i acc, v4i vm, v4i vs) {
-      if (nb >= N2) return;
-      int32_t v[4];
-      requant4m<FAST>(b, acc, vm, vs, v);
-      *(uint32_t*)(dl + prow * N2 + nb) = pack4(v);
+    gemm_xs_nt<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
+      if (n >= N2) return;
+      const ChanQ q = chan_q(mu, sh, b.out_zp);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        dl[(orow + r) * N2 + n] = (unsigned char)requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
     });
   }
   __syncthreads();
@@ -453,7 +530,6 @@ __global__ __launch_bounds__(256) void chain_persist_kernel(bh_chain_params cp, 
   const int zfill = (int)splat_byte(d.in_zp);
   const int dsel = r16 >> 2;
   const int bsh = 8 * (r16 & 3);
-  const int prow = wave * 16 + r16;  // phases B / C: this wave's 16 pixels
   const uint8_t* res = (const uint8_t*)a.residual;
   uint8_t* out1 = (uint8_t*)a.output;
 

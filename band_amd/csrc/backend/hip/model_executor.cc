@@ -1226,7 +1226,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     }
     // choice: 0 = unfused, 1/2/4 = px_blocks of the 3-launch form, 11/12/14
     // = px_blocks of the 2-launch form (the second conv stays a launch),
-    // +100 = 16 waves per workgroup, +200 = persistent form
+    // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
     std::snprintf(key, sizeof(key), "ch:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", ordinal_, D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
@@ -1252,7 +1252,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // 16 pixels over 16 waves (few-pixel, many-channel layers)
         // {px_blocks, waves, persist}: the last is the persistent form
         // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
-        const int forms[5][3] = {{4, 4, 0}, {2, 4, 0}, {1, 4, 0}, {1, 16, 0}, {4, 4, 1}};
+        const int forms[6][3] = {{4, 4, 0}, {2, 4, 0}, {1, 4, 0}, {1, 8, 0}, {1, 16, 0}, {4, 4, 1}};
         for (const auto& pw : forms) {
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
@@ -1268,7 +1268,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             const double total = us + (form == 1 && ok3 ? u_p2 : 0.0);
             if (us > 0 && total < best) {
               best = total;
-              choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[2] ? 200 : 0);
+              choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
+                       (pw[2] ? 200 : 0);
             }
           }
         }
@@ -1281,7 +1282,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       }
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
-    // +200 for the persistent form
+    // +200 for the persistent form, +300 for 8 waves
     const bool three = choice > 0 && choice % 100 < 10;
     if (choice == 0 || (three && !ok3) || (!three && !ok2)) {
       out.push_back(L[i]);
@@ -1292,8 +1293,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.op_index = D.op_index;
     F.chain = three ? c3 : c2;
     F.chain.px_blocks = choice % 10;
-    F.chain.waves = choice >= 100 && choice < 200 ? 16 : 4;
-    F.chain.persist = choice >= 200 ? 1 : 0;
+    F.chain.waves = choice >= 300 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
+    F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
     F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
     F.kernel = "chain_kernel";
     const bh_dwconv_params& dw = F.chain.dw;

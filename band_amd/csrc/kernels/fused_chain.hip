@@ -762,7 +762,7 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   const bh_chain_params& p = *pp;
   const bh_dwconv_params& d = p.dw;
   if (p.px_blocks != 1 && p.px_blocks != 2 && p.px_blocks != 4) return 0;
-  if (p.waves != 0 && p.waves != 4 && !(p.waves == 16 && p.px_blocks == 1)) return 0;
+  if (p.waves != 0 && p.waves != 4 && !((p.waves == 8 || p.waves == 16) && p.px_blocks == 1)) return 0;
   if (d.k_h != 3 || d.k_w != 3 || d.depth_multiplier != 1 || d.in_c != d.out_c || d.out_c % 16 || !d.taps ||
       d.in_xor != 0 || d.w_zp != 0 || d.out_table || !d.input || !d.weights || !d.mult || !d.shift ||
       d.batch <= 0 || d.out_h <= 0 || d.out_w <= 0 || d.stride_h <= 0 || d.stride_w <= 0)
@@ -828,6 +828,16 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
     } else {
       if (fast) bh::launch_chain<1, true, bh::kXsMax, 16>(p, P, L, lds, s);
       else bh::launch_chain<1, false, bh::kXsMax, 16>(p, P, L, lds, s);
+    }
+    return bh_check_launch("chain_kernel");
+  }
+  if (p.waves == 8) {  // one 16-pixel block, 8 waves (mid-size layers)
+    if (k2) {
+      if (fast) bh::launch_chain<1, true, 2, 8>(p, P, L, lds, s);
+      else bh::launch_chain<1, false, 2, 8>(p, P, L, lds, s);
+    } else {
+      if (fast) bh::launch_chain<1, true, bh::kXsMax, 8>(p, P, L, lds, s);
+      else bh::launch_chain<1, false, bh::kXsMax, 8>(p, P, L, lds, s);
     }
     return bh_check_launch("chain_kernel");
   }

@@ -319,7 +319,7 @@ typedef struct bh_chain_params {
   bh_conv_params pw2;
   int has_pw2;
   int px_blocks;
-  int waves;  /* waves per workgroup: 4 (0 = 4), or 16 with px_blocks == 1 */
+  int waves;  /* waves per workgroup: 4 (0 = 4), or 8 / 16 with px_blocks == 1 */
   /* 1: persistent form - both 1x1 filters, the depthwise filter and all
    * tables staged in LDS once per workgroup, which then walks a contiguous
    * range of 64-pixel blocks (px_blocks 4, 4 waves; filters must fit LDS) */

@@ -37,6 +37,7 @@ def test_chain_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
     for px in (4, 2, 1):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
+    _check(c, gpu_lib, 1, waves=8)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
     c.fast = False  # TFLite's two-step requantisation in every stage
@@ -64,6 +65,7 @@ def test_chain_general(gpu_lib, args):
     for px in (4, 1):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
+    _check(c, gpu_lib, 1, waves=8)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
 
@@ -80,7 +82,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     keep = []
     c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
-    for field, bad in (("px_blocks", 3), ("waves", 8)):
+    for field, bad in (("px_blocks", 3), ("waves", 12)):
         old = getattr(c, field)
         setattr(c, field, bad)
         assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0

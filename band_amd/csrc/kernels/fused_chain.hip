@@ -228,7 +228,7 @@ __device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsign
 
 template <int RB, bool FAST, int KX, int NW>
 __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
-                                                    ChainDivs dv) {
+                                                    int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int WPB = NW / RB;  // waves per pixel block
@@ -246,6 +246,18 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
   unsigned char* dl = smem;           // [RB*16][S1] depthwise output; then [RB*16][N2] second 1x1 output
   unsigned char* pl = smem + off_pl;  // [RB*16][S2] first 1x1 output (second 1x1's operand)
   unsigned char* o1 = smem + off_o1;  // [RB*16][N1] first 1x1 output staged for HBM
+  // residual ADD: add.cc rescales each 8-bit operand on its own
+  // (MultiplyByQuantizedMultiplierSmallerThanOneExp of (q + offset) << 20),
+  // so both rescalings are 256-entry tables, built once per workgroup
+  int* add_tab = (int*)(smem + off_add);  // [0, 256): first conv's output, [256, 512): residual
+  if (cp.pw1.residual) {
+    const bh_conv_params& a = cp.pw1;
+    for (int i = threadIdx.x; i < 512; i += NW * 64) {
+      const int q = (i & 255) - 128;
+      add_tab[i] = i < 256 ? requant_lt1((q + a.add_y_off) * (1 << a.add_left_shift), a.add_y_mult, a.add_y_shift)
+                           : requant_lt1((q + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
+    }
+  }
   const int prow = pb * 16 + r16;     // this lane's operand row
   const int orow = pb * 16 + 4 * g;   // first of this lane's 4 result rows
 
@@ -348,8 +360,8 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int32_t sy = requant_lt1((v[r] + a.add_y_off) * (1 << a.add_left_shift), a.add_y_mult, a.add_y_shift);
-          const int32_t sr = requant_lt1((rq[r] + a.add_r_off) * (1 << a.add_left_shift), a.add_r_mult, a.add_r_shift);
+          const int32_t sy = add_tab[v[r] + 128];
+          const int32_t sr = add_tab[256 + rq[r] + 128];
           v[r] = clamp_i32(requant_lt1(sy + sr, a.add_o_mult, a.add_o_shift) + a.add_o_off, a.add_act_min,
                            a.add_act_max);
         }
@@ -397,7 +409,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
 // 1x1's output), pl (the second 1x1's operand), o1 (the first 1x1's output
 // for HBM); all 16-byte aligned
 struct ChainLds {
-  int S1, S2, off_pl, off_o1;
+  int S1, S2, off_pl, off_o1, off_add;
   size_t bytes;
 };
 static ChainLds chain_lds(const bh_chain_params& p) {
@@ -408,7 +420,8 @@ static ChainLds chain_lds(const bh_chain_params& p) {
   const int dl_row = std::max(L.S1, p.has_pw2 ? (p.pw2.out_c + 15) / 16 * 16 : 0);
   L.off_pl = rows * dl_row;
   L.off_o1 = L.off_pl + rows * L.S2;
-  L.bytes = (size_t)L.off_o1 + (p.pw1.output ? (size_t)rows * ((p.pw1.out_c + 15) / 16 * 16) : 0);
+  L.off_add = L.off_o1 + (p.pw1.output ? rows * ((p.pw1.out_c + 15) / 16 * 16) : 0);
+  L.bytes = (size_t)L.off_add + (p.pw1.residual ? 512 * sizeof(int) : 0);
   return L;
 }
 
@@ -715,7 +728,8 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_w = FastDiv(p.dw.out_w);
   dv.out_h = FastDiv(p.dw.out_h);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
-  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1, dv);
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
+            L.off_add, dv);
 }
 
 template <bool FAST, int KX>

@@ -373,7 +373,12 @@ def profile_roofline(args, D, models, paths):
                 "null: no PMC file measured on this kernel tree (tag %s) at pass batch %d" % (tag, B),
                 "alg_bytes_per_launch": b, "alg_ops_per_launch": o, "avg_launch_us": us,
                 "launches_per_pass": k["launches"] / M, "share_of_kernel_time": k["us"] / total_us,
-                "mfma_i8_tops": o / (us * 1e-6) / 1e12, "mfma_i8_frac": o / (us * 1e-6) / 5.0e15}
+                "mfma_i8_tops": o / (us * 1e-6) / 1e12, "mfma_i8_frac": o / (us * 1e-6) / 5.0e15,
+                # achieved / min(P_mfma, AI x BW_hbm), the attainable
+                # rate at this kernel's arithmetic intensity (algorithmic ops / bytes)
+                "arith_intensity_op_per_byte": o / b if b else None,
+                "attainable_tops": min(5.0e15, (o / b) * 8.0e12) / 1e12 if b else None,
+                "attainable_frac": (o / (us * 1e-6)) / min(5.0e15, (o / b) * 8.0e12) if b and o else None}
 
     top = [roof(n, k) for n, k in ranked[:3]]
     dom = dict(top[0])

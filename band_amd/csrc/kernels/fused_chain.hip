@@ -226,7 +226,44 @@ __device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsign
   }
 }
 
-template <int RB, bool FAST, int KX, int NW>
+// RB == 4 form of gemm_xs_nt: wave w takes channel tiles w, w+4, ... for
+// ALL 64 pixels of the workgroup (4 pixel blocks), so a tile's filter
+// fragments, folded bias and requantisation constants serve 16 values per
+// lane instead of 4 (the conv_xs_kernel amortisation).  epi(n, acc[4], mult,
+// shift) finishes channel n for the 4 pixel blocks.
+template <int KMAX, typename Epi>
+__device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsigned char* base, int stride, int KS,
+                                            int wave, int r16, int g, Epi&& epi) {
+  v4i x[4][KMAX];
+#pragma unroll
+  for (int pb = 0; pb < 4; ++pb)
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      x[pb][k] = k < KS ? *(const v4i*)(base + (pb * 16 + r16) * stride + g * 16 + k * 64) : (v4i){0, 0, 0, 0};
+  const int T = (c.out_c + 15) >> 4;
+  for (int t = wave; t < T; t += 4) {
+    const int n = t * 16 + r16;
+    const int nl = n < c.out_c ? n : 0;
+    const int8_t* wrow = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
+    v4i w[KMAX];
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) w[k] = *(const v4i*)(wrow + k * 64);
+    const int be = c.bias_eff[nl], mu = c.mult[nl], sh = c.shift[nl];
+    v4i acc[4];
+#pragma unroll
+    for (int pb = 0; pb < 4; ++pb) acc[pb] = (v4i){be, be, be, be};
+#pragma unroll
+    for (int k = 0; k < KMAX; ++k)
+      if (k < KS) {
+#pragma unroll
+        for (int pb = 0; pb < 4; ++pb) acc[pb] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[pb][k], w[k], acc[pb], 0, 0, 0);
+      }
+    epi(n, acc, mu, sh);
+  }
+}
+
+template <int RB, bool FAST, int KX, int NW, bool AM>
 __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -372,7 +409,34 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
         if (cp.has_pw2) pl[(orow + r) * S2 + n] = (unsigned char)v[r];
       }
     };
-    if (KS1 <= KX) {
+    if (AM && KS1 <= KX) {
+      gemm_xs4_nt<KX>(a, dl, S1, KS1, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
+        if (n >= N1) return;
+        const ChanQ q = chan_q(mu, sh, a.out_zp);
+#pragma unroll
+        for (int pb4 = 0; pb4 < 4; ++pb4) {
+          const int rb = pb4 * 16 + 4 * g;
+          int32_t v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, a.out_zp, a.act_min, a.act_max);
+          if (res) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int mr = m0 + rb + r;
+              const int32_t rq = mr < P ? (int32_t)(int8_t)res[(long)mr * N1 + n] : 0;
+              v[r] = clamp_i32(requant_lt1(add_tab[v[r] + 128] + add_tab[256 + rq + 128], a.add_o_mult, a.add_o_shift) +
+                                   a.add_o_off,
+                               a.add_act_min, a.add_act_max);
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if (out1) o1[(rb + r) * N1 + n] = (unsigned char)v[r];
+            if (cp.has_pw2) pl[(rb + r) * S2 + n] = (unsigned char)v[r];
+          }
+        }
+      });
+    } else if (KS1 <= KX) {
       gemm_xs_nt<KX>(a, xrow, KS1, wsub, WPB, r16, g, epi);
     } else {
       for (int t = wsub; t < T1; t += WPB) {
@@ -393,13 +457,26 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
     const unsigned char* xrow = pl + prow * S2 + g * 16;
-    gemm_xs_nt<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
-      if (n >= N2) return;
-      const ChanQ q = chan_q(mu, sh, b.out_zp);
+    if (AM) {
+      gemm_xs4_nt<KX>(b, pl, S2, KS2, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
+        if (n >= N2) return;
+        const ChanQ q = chan_q(mu, sh, b.out_zp);
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        dl[(orow + r) * N2 + n] = (unsigned char)requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
-    });
+        for (int pb4 = 0; pb4 < 4; ++pb4)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            dl[(pb4 * 16 + 4 * g + r) * N2 + n] =
+                (unsigned char)requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
+      });
+    } else {
+      gemm_xs_nt<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
+        if (n >= N2) return;
+        const ChanQ q = chan_q(mu, sh, b.out_zp);
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          dl[(orow + r) * N2 + n] = (unsigned char)requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+      });
+    }
   }
   __syncthreads();
   copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
@@ -711,7 +788,7 @@ __global__ __launch_bounds__(256) void chain_persist_kernel(bh_chain_params cp, 
   }
 }
 
-template <int RB, bool FAST, int KX, int NW = 4>
+template <int RB, bool FAST, int KX, int NW = 4, bool AM = false>
 static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024) {
     // opt in to the CU's full 160 KiB of LDS for this instantiation (once per device)
@@ -719,7 +796,7 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (opted_device != dev) {
-      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW, AM>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       opted_device = dev;
     }
@@ -728,7 +805,7 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_w = FastDiv(p.dw.out_w);
   dv.out_h = FastDiv(p.dw.out_h);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
-  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
             L.off_add, dv);
 }
 
@@ -853,6 +930,15 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
       if (fast) bh::launch_chain<1, true, bh::kXsMax, 8>(p, P, L, lds, s);
       else bh::launch_chain<1, false, bh::kXsMax, 8>(p, P, L, lds, s);
     }
+    return bh_check_launch("chain_kernel");
+  }
+  // 64-pixel workgroups whose 1x1 layers have enough channel tiles to keep
+  // all four waves busy take the amortised form (a wave's channel tile over
+  // all 64 pixels; more registers, so only where it pays)
+  const int t_main = p.has_pw2 ? (p.pw2.out_c + 15) / 16 : (p.pw1.out_c + 15) / 16;
+  if (p.px_blocks == 4 && k2 && t_main >= 8) {
+    if (fast) bh::launch_chain<4, true, 2, 4, true>(p, P, L, lds, s);
+    else bh::launch_chain<4, false, 2, 4, true>(p, P, L, lds, s);
     return bh_check_launch("chain_kernel");
   }
   switch (p.px_blocks) {

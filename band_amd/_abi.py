@@ -109,6 +109,11 @@ class ResizeBilinearParams(ctypes.Structure):
         (n, c_void_p) for n in ("y_tab", "x_tab", "input", "output")]
 
 
+class ResizeBilinearU8Params(ctypes.Structure):
+    _fields_ = [(n, c_int) for n in ("batch", "in_h", "in_w", "channels", "out_h", "out_w")] + [
+        (n, c_void_p) for n in ("y_idx", "x_idx", "y_frac", "x_frac", "input", "output")]
+
+
 class SoftmaxParams(ctypes.Structure):
     _fields_ = [("rows", ctypes.c_long), ("depth", c_int), ("is_signed", c_int), ("table", c_void_p),
                 ("out_scale", ctypes.c_float), ("out_zp", c_int32), ("input", c_void_p), ("output", c_void_p)]
@@ -190,6 +195,7 @@ KERNEL_SYMBOLS = {
     "bh_pad": (c_int, [ctypes.POINTER(PadParams), c_void_p]),
     "bh_resize_nearest": (c_int, [ctypes.POINTER(ResizeNearestParams), c_void_p]),
     "bh_resize_bilinear_i8": (c_int, [ctypes.POINTER(ResizeBilinearParams), c_void_p]),
+    "bh_resize_bilinear_u8": (c_int, [ctypes.POINTER(ResizeBilinearU8Params), c_void_p]),
     "bh_softmax_i8": (c_int, [ctypes.POINTER(SoftmaxParams), c_void_p]),
     "bh_zero_insert": (c_int, [ctypes.POINTER(ZeroInsertParams), c_void_p]),
     "bh_conv2d_f32": (c_int, [ctypes.POINTER(ConvF32Params), c_void_p]),

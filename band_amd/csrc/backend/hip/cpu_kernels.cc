@@ -458,6 +458,33 @@ void CpuResizeBilinear(const bh_resize_bilinear_params& p) {
     }
 }
 
+// optimized_ops::ResizeBilinear<uint8> (float weights, + 0.5f, truncation);
+// this file is built with -ffp-contract=off, so every product and sum is
+// rounded separately as in the reference's x86 build
+void CpuResizeBilinearU8(const bh_resize_bilinear_u8_params& p) {
+  const uint8_t* in = static_cast<const uint8_t*>(p.input);
+  uint8_t* out = static_cast<uint8_t*>(p.output);
+  long i = 0;
+  for (int n = 0; n < p.batch; ++n)
+    for (int y = 0; y < p.out_h; ++y) {
+      const int y0 = p.y_idx[2 * y], y1 = p.y_idx[2 * y + 1];
+      const float dy = p.y_frac[y];
+      for (int x = 0; x < p.out_w; ++x) {
+        const int x0 = p.x_idx[2 * x], x1 = p.x_idx[2 * x + 1];
+        const float dx = p.x_frac[x];
+        const float s0 = (1.0f - dy) * (1.0f - dx), s1 = (1.0f - dy) * dx, s2 = dy * (1.0f - dx), s3 = dy * dx;
+        const uint8_t* b = in + static_cast<long>(n) * p.in_h * p.in_w * p.channels;
+        for (int c = 0; c < p.channels; ++c, ++i) {
+          const float v = static_cast<float>(b[(static_cast<long>(y0) * p.in_w + x0) * p.channels + c]) * s0 +
+                          static_cast<float>(b[(static_cast<long>(y0) * p.in_w + x1) * p.channels + c]) * s1 +
+                          static_cast<float>(b[(static_cast<long>(y1) * p.in_w + x0) * p.channels + c]) * s2 +
+                          static_cast<float>(b[(static_cast<long>(y1) * p.in_w + x1) * p.channels + c]) * s3 + 0.5f;
+          out[i] = static_cast<uint8_t>(static_cast<int>(v));
+        }
+      }
+    }
+}
+
 // optimized_ops::Softmax (8-bit) with the exp table built on the host
 void CpuSoftmax(const bh_softmax_params& p) {
   const bool sg = p.is_signed != 0;

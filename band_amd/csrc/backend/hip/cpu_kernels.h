@@ -59,6 +59,7 @@ void CpuConcat(const bh_concat_params& p);
 void CpuPad(const bh_pad_params& p);
 void CpuResizeNearest(const bh_resize_nearest_params& p);
 void CpuResizeBilinear(const bh_resize_bilinear_params& p);
+void CpuResizeBilinearU8(const bh_resize_bilinear_u8_params& p);
 void CpuSoftmax(const bh_softmax_params& p);
 void CpuZeroInsert(const bh_zero_insert_params& p);
 

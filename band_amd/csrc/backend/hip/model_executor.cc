@@ -439,8 +439,9 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
       return true;
     }
     case kTflResizeBilinear:
-      if (in.type != DataType::kInt8 || out.type != in.type || in.shape.size() != 4 || out.shape.size() != 4)
-        return no("int8 4-D only (ResizeBilinearInteger)");
+      if ((in.type != DataType::kInt8 && in.type != DataType::kUInt8) || out.type != in.type || in.shape.size() != 4 ||
+          out.shape.size() != 4)
+        return no("int8 / uint8 4-D only (ResizeBilinearInteger / the uint8 float path)");
       return true;
     default:
       return no("op not in the HIP kernel set");
@@ -884,6 +885,32 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
         p.output = out_ptr;
         L->kind = Launch::kResizeNearest;
         L->kernel = "resize_nearest_kernel";
+      } else if (in.type == DataType::kUInt8) {
+        // uint8: optimized_ops::ResizeBilinear's float path
+        std::vector<int32_t> iy, ix;
+        std::vector<float> fy, fx;
+        BilinearFloatTable(ih, oh, ac, hp, &iy, &fy);
+        BilinearFloatTable(iw, ow, ac, hp, &ix, &fx);
+        // one upload: {y_idx, x_idx} int32 then {y_frac, x_frac} float
+        std::vector<int32_t> blob(iy);
+        blob.insert(blob.end(), ix.begin(), ix.end());
+        blob.resize(blob.size() + fy.size() + fx.size());
+        std::memcpy(blob.data() + iy.size() + ix.size(), fy.data(), fy.size() * 4);
+        std::memcpy(blob.data() + iy.size() + ix.size() + fy.size(), fx.data(), fx.size() * 4);
+        const void* dt = nullptr;
+        RETURN_STATUS_IF(UploadConst(ckey + "/tab8", blob.data(), blob.size() * 4, sg, &dt));
+        const int32_t* t32 = static_cast<const int32_t*>(dt);
+        bh_resize_bilinear_u8_params& p = L->rbil8;
+        p = bh_resize_bilinear_u8_params{};
+        p.batch = b; p.in_h = ih; p.in_w = iw; p.channels = c; p.out_h = oh; p.out_w = ow;
+        p.y_idx = t32;
+        p.x_idx = t32 + 2 * oh;
+        p.y_frac = reinterpret_cast<const float*>(t32 + 2 * oh + 2 * ow);
+        p.x_frac = reinterpret_cast<const float*>(t32 + 3 * oh + 2 * ow);
+        p.input = in_ptr;
+        p.output = out_ptr;
+        L->kind = Launch::kResizeBilinearU8;
+        L->kernel = "resize_bilinear_u8_kernel";
       } else {
         std::vector<int32_t> ty, tx;
         BilinearIntegerTable(ih, oh, ac, hp, &ty);
@@ -2169,6 +2196,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kPad: rc = bh_pad(&l.pad, stream_); break;
     case Launch::kResizeNearest: rc = bh_resize_nearest(&l.rnear, stream_); break;
     case Launch::kResizeBilinear: rc = bh_resize_bilinear_i8(&l.rbil, stream_); break;
+    case Launch::kResizeBilinearU8: rc = bh_resize_bilinear_u8(&l.rbil8, stream_); break;
     case Launch::kSoftmax: rc = bh_softmax_i8(&l.softmax, stream_); break;
     case Launch::kZeroInsert: rc = bh_zero_insert(&l.zi, stream_); break;
     case Launch::kConvF32: rc = bh_conv2d_f32(&l.convf, stream_); break;
@@ -2246,6 +2274,7 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
       case Launch::kPad: CpuPad(l.pad); break;
       case Launch::kResizeNearest: CpuResizeNearest(l.rnear); break;
       case Launch::kResizeBilinear: CpuResizeBilinear(l.rbil); break;
+      case Launch::kResizeBilinearU8: CpuResizeBilinearU8(l.rbil8); break;
       case Launch::kSoftmax: CpuSoftmax(l.softmax); break;
       case Launch::kZeroInsert: CpuZeroInsert(l.zi); break;
       case Launch::kConvF32: CpuConvF32(l.convf, pool); break;

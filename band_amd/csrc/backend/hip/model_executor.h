@@ -40,6 +40,7 @@ struct Launch {
     kConv, kDwConv, kFc, kEltwise, kPool, kCopy, kIrb, kChain,
     kLutU8, kLutF32, kQuantF32, kConcat, kPad, kResizeNearest, kResizeBilinear, kSoftmax, kZeroInsert,
     kConvF32, kFcF32, kEltwiseF32, kPoolF32, kUnaryF32, kSoftmaxF32,  // float32 graphs
+    kResizeBilinearU8,
     kDetectionPost,  // CPU-only TFLite_Detection_PostProcess
     kMean            // CPU-only MEAN
   } kind;
@@ -56,6 +57,7 @@ struct Launch {
   bh_pad_params pad{};
   bh_resize_nearest_params rnear{};
   bh_resize_bilinear_params rbil{};
+  bh_resize_bilinear_u8_params rbil8{};
   bh_softmax_params softmax{};
   bh_zero_insert_params zi{};
   bh_conv_f32_params convf{};

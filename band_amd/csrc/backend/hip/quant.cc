@@ -277,6 +277,23 @@ int NearestNeighborIndex(int v, int in_size, int out_size, bool align_corners, b
   return o;
 }
 
+void BilinearFloatTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
+                        std::vector<int32_t>* idx, std::vector<float>* frac) {
+  float scale = static_cast<float>(in_size) / static_cast<float>(out_size);
+  if (align_corners && out_size > 1) scale = static_cast<float>(in_size - 1) / static_cast<float>(out_size - 1);
+  idx->assign(2 * static_cast<size_t>(out_size), 0);
+  frac->assign(static_cast<size_t>(out_size), 0.f);
+  for (int v = 0; v < out_size; ++v) {
+    const float fv = static_cast<float>(v);
+    const float scaled = half_pixel_centers ? (fv + 0.5f) * scale - 0.5f : fv * scale;
+    const int32_t lo = std::max(static_cast<int32_t>(std::floor(scaled)), 0);
+    const int32_t hi = std::min(static_cast<int32_t>(std::ceil(scaled)), in_size - 1);
+    (*idx)[2 * v] = lo;
+    (*idx)[2 * v + 1] = hi;
+    (*frac)[v] = scaled - static_cast<float>(lo);
+  }
+}
+
 void BilinearIntegerTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
                           std::vector<int32_t>* tab) {
   int32_t scale_10 = ((1 << 10) * in_size + out_size / 2) / out_size;

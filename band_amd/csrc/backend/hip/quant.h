@@ -77,6 +77,10 @@ void SoftmaxExpTable(float in_scale, float beta, float table[256]);
 int NearestNeighborIndex(int v, int in_size, int out_size, bool align_corners, bool half_pixel_centers);
 // reference_ops::ResizeBilinearInteger: per output row / column
 // {lower, upper, 10-bit scaled coordinate}
+// resize_bilinear.h ComputeInterpolationValues in float (the uint8 / float
+// path): idx = {lower, upper} per output coordinate, frac = scaled - lower
+void BilinearFloatTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
+                        std::vector<int32_t>* idx, std::vector<float>* frac);
 void BilinearIntegerTable(int in_size, int out_size, bool align_corners, bool half_pixel_centers,
                           std::vector<int32_t>* tab);
 

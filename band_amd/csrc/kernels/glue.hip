@@ -553,3 +553,61 @@ extern "C" int bh_mean(const bh_mean_params* pp, bh_stream_t stream) {
   BH_LAUNCH(bh::mean_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, *pp, total);
   return bh_check_launch("mean_kernel");
 }
+
+// ---- RESIZE_BILINEAR uint8 ----------------------------------------------------
+// optimized_ops::ResizeBilinear<uint8> (TFLite 2.9.2) -> ResizeBilinear-
+// GenericSmallChannel: the four weights and the weighted sum in float, in
+// the reference's operation order (explicit _rn intrinsics: no contraction),
+// + 0.5f, truncated to uint8.  One thread per output byte; the float
+// interpolation coordinates come from host tables (ComputeInterpolationValues).
+namespace bh {
+__global__ __launch_bounds__(256) void resize_bilinear_u8_kernel(bh_resize_bilinear_u8_params p, ResizeDivs dv,
+                                                                 long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int pix = (int)dv.units.div((uint32_t)i);
+  const int c = (int)(i - (long)pix * p.channels);
+  const int t = (int)dv.ow.div((uint32_t)pix);
+  const int x = pix - t * p.out_w;
+  const int n = (int)dv.oh.div((uint32_t)t);
+  const int y = t - n * p.out_h;
+  const int y0 = p.y_idx[2 * y], y1 = p.y_idx[2 * y + 1];
+  const int x0 = p.x_idx[2 * x], x1 = p.x_idx[2 * x + 1];
+  const float dy = p.y_frac[y], dx = p.x_frac[x];
+  const float s0 = __fmul_rn(__fsub_rn(1.0f, dy), __fsub_rn(1.0f, dx));
+  const float s1 = __fmul_rn(__fsub_rn(1.0f, dy), dx);
+  const float s2 = __fmul_rn(dy, __fsub_rn(1.0f, dx));
+  const float s3 = __fmul_rn(dy, dx);
+  const uint8_t* b = (const uint8_t*)p.input + (long)n * p.in_h * p.in_w * p.channels;
+  const float a0 = (float)b[((long)y0 * p.in_w + x0) * p.channels + c];
+  const float a1 = (float)b[((long)y0 * p.in_w + x1) * p.channels + c];
+  const float a2 = (float)b[((long)y1 * p.in_w + x0) * p.channels + c];
+  const float a3 = (float)b[((long)y1 * p.in_w + x1) * p.channels + c];
+  float v = __fadd_rn(__fmul_rn(a0, s0), __fmul_rn(a1, s1));
+  v = __fadd_rn(v, __fmul_rn(a2, s2));
+  v = __fadd_rn(v, __fmul_rn(a3, s3));
+  v = __fadd_rn(v, 0.5f);
+  ((uint8_t*)p.output)[i] = (uint8_t)(int)v;
+}
+}  // namespace bh
+
+extern "C" int bh_resize_bilinear_u8(const bh_resize_bilinear_u8_params* pp, bh_stream_t s) {
+  if (!pp || !pp->input || !pp->output || !pp->y_idx || !pp->x_idx || !pp->y_frac || !pp->x_frac || pp->batch <= 0 ||
+      pp->in_h <= 0 || pp->in_w <= 0 || pp->channels <= 0 || pp->out_h <= 0 || pp->out_w <= 0) {
+    bh_set_last_error("bh_resize_bilinear_u8: invalid parameters");
+    return BH_EINVAL;
+  }
+  const bh_resize_bilinear_u8_params& p = *pp;
+  const long total = (long)p.batch * p.out_h * p.out_w * p.channels;
+  if (total >= INT32_MAX) {
+    bh_set_last_error("bh_resize_bilinear_u8: tensor too large for 32-bit indexing");
+    return BH_EINVAL;
+  }
+  bh::ResizeDivs dv;
+  dv.units = bh::FastDiv(p.channels);
+  dv.ow = bh::FastDiv(p.out_w);
+  dv.oh = bh::FastDiv(p.out_h);
+  BH_LAUNCH(bh::resize_bilinear_u8_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)s, p, dv,
+            total);
+  return bh_check_launch("resize_bilinear_u8_kernel");
+}

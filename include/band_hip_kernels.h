@@ -27,6 +27,7 @@
  *   bh_pad            <- PAD / PADV2        (reference_ops::Pad)
  *   bh_resize_nearest <- RESIZE_NEAREST_NEIGHBOR (reference_ops::ResizeNearestNeighbor)
  *   bh_resize_bilinear_i8 <- RESIZE_BILINEAR int8 (reference_ops::ResizeBilinearInteger)
+ *   bh_resize_bilinear_u8 <- RESIZE_BILINEAR uint8 (optimized_ops::ResizeBilinear, float path)
  *   bh_softmax_i8     <- SOFTMAX 8-bit      (optimized_ops::Softmax, lookup-table path)
  *   bh_mean           <- MEAN               (optimized_integer_ops::Mean / optimized_ops::Mean)
  *   (HARD_SWISH 8-bit runs as a bh_lut_u8 table of reference_ops::HardSwish)
@@ -504,6 +505,24 @@ typedef struct {
   void* output;
 } bh_resize_bilinear_params;
 int bh_resize_bilinear_i8(const bh_resize_bilinear_params* p, bh_stream_t s);
+
+/* RESIZE_BILINEAR uint8 (TFLite 2.9.2 optimized_ops::ResizeBilinear for
+ * uint8 -> ResizeBilinearGenericSmallChannel<uint8>): float interpolation.
+ * Host tables from ComputeInterpolationValues (float scale, floor / ceil):
+ * y_idx [2*out_h] = {y0, y1}, y_frac [out_h] = input_y - y0 (float), same
+ * for x.  Per output byte, in float with no contraction:
+ *   (uint8)(v00*(1-dy)(1-dx) + v01*(1-dy)dx + v10*dy(1-dx) + v11*dy*dx + 0.5f)
+ * summed left to right as the reference's expression. */
+typedef struct {
+  int batch, in_h, in_w, channels, out_h, out_w;
+  const int32_t* y_idx;
+  const int32_t* x_idx;
+  const float* y_frac;
+  const float* x_frac;
+  const void* input;
+  void* output;
+} bh_resize_bilinear_u8_params;
+int bh_resize_bilinear_u8(const bh_resize_bilinear_u8_params* p, bh_stream_t s);
 
 typedef struct {
   long rows;

@@ -74,6 +74,7 @@ def lib():
         L.tfl_nearest_index.argtypes = [c_i, c_i, c_i, c_i, c_i]
         L.tfl_resize_nearest.argtypes = [vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, vp]
         L.tfl_resize_bilinear_i8.argtypes = [vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, vp]
+        L.tfl_resize_bilinear_u8.argtypes = [vp, c_i, c_i, c_i, c_i, c_i, c_i, c_i, c_i, vp]
         _LIB = L
     return _LIB
 
@@ -428,6 +429,16 @@ def resize_bilinear_i8(x, out_hw, align_corners=False, half_pixel_centers=False)
     return out
 
 
+def resize_bilinear_u8(x, out_hw, align_corners=False, half_pixel_centers=False):
+    """optimized_ops::ResizeBilinear<uint8> float path (parity unpinned)."""
+    x = np.ascontiguousarray(x, np.uint8)
+    b, ih, iw, c = x.shape
+    out = np.zeros((b, out_hw[0], out_hw[1], c), np.uint8)
+    lib().tfl_resize_bilinear_u8(_vp(x), b, ih, iw, c, out_hw[0], out_hw[1], int(align_corners),
+                                 int(half_pixel_centers), _vp(out))
+    return out
+
+
 # ---------------------------------------------------------------------------
 # whole-model runner
 # ---------------------------------------------------------------------------
@@ -698,8 +709,10 @@ class OracleInterpreter:
                 ac, hp = opt.scalar(0, "b", 0) if opt else 0, opt.scalar(1, "b", 0) if opt else 0
                 return [resize_nearest(x, (oh, ow), ac, hp)]
             ac, hp = opt.scalar(2, "b", 0) if opt else 0, opt.scalar(3, "b", 0) if opt else 0
+            if ti.np_dtype == np.uint8:
+                return [resize_bilinear_u8(x, (oh, ow), ac, hp)]
             if ti.np_dtype != np.int8:
-                raise NotImplementedError("oracle: RESIZE_BILINEAR restated for int8 only")
+                raise NotImplementedError("oracle: RESIZE_BILINEAR restated for int8 / uint8 only")
             return [resize_bilinear_i8(x, (oh, ow), ac, hp)]
         if code == OP["CUSTOM"] and o.custom == "TFLite_Detection_PostProcess":
             from .detection_postprocess import detection_postprocess, read_flexbuffer_map

@@ -621,6 +621,43 @@ void tfl_resize_bilinear_i8(const int8_t* in, int b, int ih, int iw, int c, int 
     }
 }
 
+/* optimized_ops::ResizeBilinear for uint8 (TFLite 2.9.2; TFLite is a
+ * third-party dependency of Band, not vendored under /root/reference):
+ * ResizeBilinearGenericSmallChannel<uint8> with float scales and
+ * reference_ops::ComputeInterpolationValues; four float weights, the
+ * weighted sum left to right, + 0.5f, truncated.  Parity unpinned: no
+ * reference fixture covers this op. */
+static void interp_float(int value, float scale, int half_pixel_centers, int input_size, float* scaled, int* lo,
+                         int* hi) {
+  *scaled = half_pixel_centers ? ((float)value + 0.5f) * scale - 0.5f : (float)value * scale;
+  *lo = imax((int)floorf(*scaled), 0);
+  *hi = imin((int)ceilf(*scaled), input_size - 1);
+}
+void tfl_resize_bilinear_u8(const uint8_t* in, int b, int ih, int iw, int c, int oh, int ow, int align_corners,
+                            int half_pixel_centers, uint8_t* out) {
+  const float hs = (align_corners && oh > 1) ? (float)(ih - 1) / (float)(oh - 1) : (float)ih / (float)oh;
+  const float ws = (align_corners && ow > 1) ? (float)(iw - 1) / (float)(ow - 1) : (float)iw / (float)ow;
+  for (int n = 0; n < b; ++n)
+    for (int y = 0; y < oh; ++y) {
+      float iy;
+      int y0, y1;
+      interp_float(y, hs, half_pixel_centers, ih, &iy, &y0, &y1);
+      for (int x = 0; x < ow; ++x) {
+        float ix;
+        int x0, x1;
+        interp_float(x, ws, half_pixel_centers, iw, &ix, &x0, &x1);
+        const float w00 = (1 - (iy - y0)) * (1 - (ix - x0)), w01 = (1 - (iy - y0)) * (ix - x0);
+        const float w10 = (iy - y0) * (1 - (ix - x0)), w11 = (iy - y0) * (ix - x0);
+        for (int ch = 0; ch < c; ++ch) {
+#define AT(yy, xx) in[(((long)n * ih + (yy)) * iw + (xx)) * c + ch]
+          const float v = AT(y0, x0) * w00 + AT(y0, x1) * w01 + AT(y1, x0) * w10 + AT(y1, x1) * w11 + 0.5f;
+#undef AT
+          out[(((long)n * oh + y) * ow + x) * c + ch] = (uint8_t)(int)v;
+        }
+      }
+    }
+}
+
 /* optimized_ops::PopulateSoftmaxLookupTable alone (the table tfl_softmax uses) */
 void tfl_softmax_table(float in_scale, float beta, float* table) {
   const float scale = -in_scale * beta;

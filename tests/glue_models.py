@@ -13,8 +13,7 @@ def glue_zoo(dtype, seed=3):
     c = g.concat([a, b, g.relu(a, "RELU")])
     d = g.pad(c, [[0, 0], [1, 2], [2, 1], [0, 0]])
     e = g.resize(d, (20, 26))
-    f = g.resize(g.conv(e, 8, k=1, act="NONE"), (9, 7), bilinear=(np.dtype(dtype) == np.int8),
-                 half_pixel_centers=True)
+    f = g.resize(g.conv(e, 8, k=1, act="NONE"), (9, 7), bilinear=True, half_pixel_centers=True)
     h = g.logistic(f)
     k = g.softmax(g.relu(g.quantize(f, 0.1, 3 if np.dtype(dtype) == np.int8 else 130), "RELU_N1_TO_1"), beta=0.7)
     g.output(h)
@@ -167,3 +166,40 @@ HARD_SWISH_CASES = [  # (dtype, in_scale, in_zp, out_scale, out_zp)
     (np.int8, 0.05, 3, 0.03, -10), (np.int8, 0.02, -128, 0.02, -100), (np.int8, 0.2, 0, 0.1, 0),
     (np.uint8, 0.1, 128, 0.05, 20), (np.uint8, 0.03, 60, 0.04, 10),
 ]
+
+
+def bilinear_model(dtype, in_hw, out_hw, c, align_corners=False, half_pixel_centers=False):
+    """x [2, ih, iw, c] -> RESIZE_BILINEAR -> y [2, oh, ow, c]"""
+    g = QGraph(dtype, seed=17, name="bilinear")
+    x = g.input([2, in_hw[0], in_hw[1], c], scale=0.05)
+    g.output(g.resize(x, out_hw, bilinear=True, align_corners=align_corners, half_pixel_centers=half_pixel_centers))
+    return g.build()
+
+
+BILINEAR_CASES = [  # (in_hw, out_hw, c, align_corners, half_pixel_centers)
+    ((5, 5), (10, 10), 8, 0, 0), ((10, 10), (20, 20), 3, 0, 1), ((7, 9), (13, 4), 4, 1, 0), ((6, 6), (3, 3), 5, 0, 1),
+    ((3, 5), (37, 41), 7, 0, 1), ((4, 4), (4, 4), 2, 1, 1), ((1, 1), (3, 5), 3, 0, 0),
+]
+
+
+def bilinear_u8_numpy(x, out_hw, ac, hp):
+    """A second, numpy float32 restatement of the uint8 float path (checks
+    the C oracle): ComputeInterpolationValues + four weights + 0.5f"""
+    f32 = np.float32
+    _, ih, iw, _ = x.shape
+
+    def coords(n_in, n_out):
+        s = f32(n_in - 1) / f32(n_out - 1) if ac and n_out > 1 else f32(n_in) / f32(n_out)
+        v = np.arange(n_out, dtype=f32)
+        sc = (v + f32(0.5)) * s - f32(0.5) if hp else v * s
+        lo = np.maximum(np.floor(sc).astype(np.int64), 0)
+        hi = np.minimum(np.ceil(sc).astype(np.int64), n_in - 1)
+        return lo, hi, (sc - lo.astype(f32)).astype(f32)
+    y0, y1, dy = coords(ih, out_hw[0])
+    x0, x1, dx = coords(iw, out_hw[1])
+    dy, dx = dy[None, :, None, None], dx[None, None, :, None]
+    one = f32(1)
+    a = x.astype(f32)
+    v = (a[:, y0][:, :, x0] * ((one - dy) * (one - dx)) + a[:, y0][:, :, x1] * ((one - dy) * dx)
+         + a[:, y1][:, :, x0] * (dy * (one - dx)) + a[:, y1][:, :, x1] * (dy * dx) + f32(0.5))
+    return v.astype(np.int32).astype(np.uint8)

@@ -166,6 +166,38 @@ def test_resize(gpu_lib, ih, iw, oh, ow, c, ac, hp):
     np.testing.assert_array_equal(dy2.download(np.int8, ref.shape), ref)
 
 
+@pytest.mark.parametrize("ih,iw,oh,ow,c,ac,hp", [
+    (5, 5, 10, 10, 8, 0, 0), (10, 10, 20, 20, 3, 0, 1), (7, 9, 13, 4, 4, 1, 0), (14, 14, 224, 224, 21, 0, 0),
+    (2, 515, 3, 1030, 1, 0, 1),
+])
+def test_resize_bilinear_u8(gpu_lib, ih, iw, oh, ow, c, ac, hp):
+    """uint8 bilinear launcher with host float tables (the executor's
+    BilinearFloatTable restated in numpy float32) vs the oracle"""
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(ih * 7 + ow)
+    x = rng.integers(0, 256, (2, ih, iw, c)).astype(np.uint8)
+    ref = orc.resize_bilinear_u8(x, (oh, ow), ac, hp)
+    f32 = np.float32
+
+    def tab(n_in, n_out):
+        s = f32(n_in - 1) / f32(n_out - 1) if ac and n_out > 1 else f32(n_in) / f32(n_out)
+        v = np.arange(n_out, dtype=f32)
+        sc = (v + f32(0.5)) * s - f32(0.5) if hp else v * s
+        lo = np.maximum(np.floor(sc).astype(np.int32), 0)
+        hi = np.minimum(np.ceil(sc).astype(np.int32), n_in - 1)
+        return np.stack([lo, hi], 1).astype(np.int32).reshape(-1), (sc - lo.astype(f32)).astype(f32)
+    yi, yf = tab(ih, oh)
+    xi, xf = tab(iw, ow)
+    keep = [_dev(a) for a in (x, yi, xi, yf, xf)]
+    dy = DeviceBuffer(ref.nbytes)
+    q = _abi.ResizeBilinearU8Params(batch=2, in_h=ih, in_w=iw, channels=c, out_h=oh, out_w=ow, y_idx=keep[1].value,
+                                    x_idx=keep[2].value, y_frac=keep[3].value, x_frac=keep[4].value,
+                                    input=keep[0].value, output=dy.value)
+    _check(gpu_lib.bh_resize_bilinear_u8(ctypes.byref(q), None), "bilinear_u8")
+    np.testing.assert_array_equal(dy.download(np.uint8, ref.shape), ref)
+
+
 @pytest.mark.parametrize("dtype,depth", [(np.int8, 2), (np.int8, 91), (np.uint8, 10)])
 def test_softmax(gpu_lib, dtype, depth):
     from band_amd import _abi

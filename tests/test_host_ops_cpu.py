@@ -81,3 +81,21 @@ def test_hard_swish_cpu_executor(dtype, s_in, zp_in, s_out, zp_out):
     lo, hi = (-128, 127) if np.dtype(dtype) == np.int8 else (0, 255)
     fl = np.clip(np.round(xf * np.clip(xf + 3, 0, 6) / 6 / s_out) + zp_out, lo, hi)
     assert np.abs(ref.astype(np.int32) - fl).max() <= 1
+
+
+from tests.glue_models import BILINEAR_CASES, bilinear_model, bilinear_u8_numpy  # noqa: E402
+
+
+@pytest.mark.parametrize("in_hw,out_hw,c,ac,hp", BILINEAR_CASES)
+def test_resize_bilinear_u8_cpu_executor(in_hw, out_hw, c, ac, hp):
+    """uint8 RESIZE_BILINEAR (optimized_ops::ResizeBilinear float path) on the
+    kCPU worker vs the C oracle, and the C oracle vs a numpy float32
+    restatement.  Parity unpinned: no reference fixture holds uint8 bilinear
+    outputs."""
+    rng = np.random.default_rng(in_hw[0] * 31 + out_hw[1])
+    x = rng.integers(0, 256, (2, in_hw[0], in_hw[1], c)).astype(np.uint8)
+    x.flat[:4] = [0, 255, 255, 0]
+    ref = orc.resize_bilinear_u8(x, out_hw, ac, hp)
+    np.testing.assert_array_equal(ref, bilinear_u8_numpy(x, out_hw, ac, hp))
+    got = run_executor(bilinear_model(np.uint8, in_hw, out_hw, c, ac, hp), x, DeviceFlag.kCPU)[0]
+    np.testing.assert_array_equal(got.reshape(ref.shape), ref)

@@ -138,3 +138,16 @@ def test_mean_launcher(gpu_lib, dtype, shape):
         np.testing.assert_array_equal(got, ref)
     p.reduce = 0
     assert gpu_lib.bh_mean(ctypes.byref(p), None) != 0
+
+
+from tests.glue_models import BILINEAR_CASES, bilinear_model  # noqa: E402
+
+
+@pytest.mark.parametrize("in_hw,out_hw,c,ac,hp", BILINEAR_CASES + [((14, 14), (224, 224), 21, 0, 0)])
+def test_resize_bilinear_u8_gpu_executor(gpu_lib, in_hw, out_hw, c, ac, hp):
+    """uint8 RESIZE_BILINEAR through resize_bilinear_u8_kernel vs the oracle"""
+    rng = np.random.default_rng(in_hw[0] * 31 + out_hw[1])
+    x = rng.integers(0, 256, (2, in_hw[0], in_hw[1], c)).astype(np.uint8)
+    got = run_executor(bilinear_model(np.uint8, in_hw, out_hw, c, ac, hp), x, DeviceFlag.kGPU, worker=1)[0]
+    ref = orc.resize_bilinear_u8(x, out_hw, ac, hp)
+    np.testing.assert_array_equal(got.reshape(ref.shape), ref)

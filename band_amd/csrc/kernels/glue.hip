@@ -10,6 +10,9 @@
 //     10-bit fixed point (RESIZE_BILINEAR int8) -> host-built per-row and
 //     per-column tables; the device only gathers and (bilinear) does the
 //     integer 4-tap blend.
+//   * float sequences (softmax, mean, uint8 bilinear) keep TFLite's operation
+//     order; the Makefile builds this file with -ffp-contract=off, since HIP's
+//     _rn intrinsics are plain operators that would otherwise fuse to FMA.
 //   * SOFTMAX (8-bit, lookup-table path) -> host-built float exp table; the
 //     per-row sum runs sequentially in TFLite's order, so the float result is
 //     the same.

@@ -58,7 +58,9 @@ import hashlib
 import json
 import os
 import platform
+import sys
 import tempfile
+import threading
 import time
 
 import numpy as np
@@ -664,5 +666,18 @@ def main():
     D.close()
 
 
+def heartbeat(period_s=60.0):
+    """one stderr line a minute while the (GIL-free) native engine runs, so
+    long configurations (C4 / C5 at many steps) never look hung"""
+    t0 = time.time()
+
+    def run():
+        while True:
+            time.sleep(period_s)
+            print("bench: running, %.0f s" % (time.time() - t0), file=sys.stderr, flush=True)
+    threading.Thread(target=run, daemon=True).start()
+
+
 if __name__ == "__main__":
+    heartbeat()
     main()

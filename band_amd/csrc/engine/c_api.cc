@@ -510,4 +510,25 @@ void BandxEngineWaitAll(BandEngine* engine) {
   if (engine) engine->impl->WaitAll();
 }
 
+BandStatus BandxEngineRequestsAsync(BandEngine* engine, BandModel** models, int n, BandTensor*** inputs,
+                                    BandRequestHandle* handles) {
+  if (!engine || !models || n <= 0 || !inputs || !handles) return kBandErr;
+  std::vector<band::ModelId> ids;
+  std::vector<band::RequestOption> opts;
+  std::vector<band::Tensors> ins;
+  for (int i = 0; i < n; ++i) {
+    if (!models[i]) return kBandErr;
+    ids.push_back(models[i]->impl->GetId());
+    opts.push_back(band::RequestOption::GetDefaultOption());
+    ins.push_back(ToVec(inputs[i], BandEngineGetNumInputTensors(engine, models[i])));
+  }
+  auto r = engine->impl->RequestAsync(ids, opts, ins);
+  if (!r.ok()) {
+    BAND_LOG(LogSeverity::kError, "RequestsAsync: %s", r.status().message().c_str());
+    return kBandErr;
+  }
+  for (int i = 0; i < n; ++i) handles[i] = r.value()[i];
+  return kBandOk;
+}
+
 }  // extern "C"

@@ -292,18 +292,49 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
       return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
     jobs.push_back(std::move(job));
   }
-  for (size_t i = 0; i < jobs.size() && i < inputs.size(); ++i) {
-    TensorRingBuffer* in_ring = model_input_buffer_.at(model_ids[i]).get();
-    // blocks while the model has a full ring of unfinished requests
-    const int handle = in_ring->AllocBlocking();
-    if (!in_ring->PutTensorsToHandle(inputs[i], handle).ok()) {
-      for (size_t k = 0; k <= i; ++k) model_input_buffer_.at(model_ids[k])->Release();
-      return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
-    }
-    jobs[i].input_handle = handle;
-    jobs[i].output_handle = model_output_buffer_.at(model_ids[i])->Alloc();
+  // Ring slots are taken per run of consecutive same-model requests, all of
+  // a run's slots in one step (AllocBlockingN), and the run is enqueued at
+  // once: a call never holds slots of jobs it has not enqueued, so neither a
+  // call larger than the ring nor two concurrent calls sharing a model can
+  // wait on each other forever.  A run larger than the ring is refused
+  // before anything is taken.
+  const size_t n_in = std::min(jobs.size(), inputs.size());
+  for (size_t i = 0; i < n_in;) {
+    size_t j = i;
+    while (j < n_in && model_ids[j] == model_ids[i]) ++j;
+    const int ring = model_input_buffer_.at(model_ids[i])->size();
+    if (static_cast<int>(j - i) > ring)
+      return absl::InternalError("RequestAsync: " + std::to_string(j - i) + " consecutive requests of model " +
+                                 std::to_string(model_ids[i]) + " exceed its request ring (" + std::to_string(ring) +
+                                 " slots)");
+    i = j;
   }
-  return EnqueueBatch(std::move(jobs));
+  std::vector<JobId> ids;
+  ids.reserve(jobs.size());
+  for (size_t i = 0; i < jobs.size();) {
+    size_t j = i;
+    if (i < n_in) {
+      while (j < n_in && model_ids[j] == model_ids[i]) ++j;
+      TensorRingBuffer* in_ring = model_input_buffer_.at(model_ids[i]).get();
+      // blocks while the model's ring has fewer than j - i free slots
+      const int first = in_ring->AllocBlockingN(static_cast<int>(j - i));
+      for (size_t k = i; k < j; ++k) {
+        const int handle = first + static_cast<int>(k - i);
+        if (!in_ring->PutTensorsToHandle(inputs[k], handle).ok()) {
+          for (size_t r = i; r < j; ++r) in_ring->Release();
+          return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[k]));
+        }
+        jobs[k].input_handle = handle;
+        jobs[k].output_handle = model_output_buffer_.at(model_ids[k])->Alloc();
+      }
+    } else {
+      j = jobs.size();  // requests without inputs (no ring slot)
+    }
+    std::vector<Job> run(std::make_move_iterator(jobs.begin() + i), std::make_move_iterator(jobs.begin() + j));
+    for (JobId id : EnqueueBatch(std::move(run))) ids.push_back(id);
+    i = j;
+  }
+  return ids;
 }
 
 void Engine::ReleaseRequest(const Job& job) {

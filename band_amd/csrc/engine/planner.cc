@@ -136,12 +136,14 @@ void Planner::EnqueueFinishedJob(Job& job) {
     end_invoke_.notify_all();
   }
   lock.unlock();  // callbacks may re-enter the engine
+  // the request's input slot was consumed when the job started: free it
+  // before the callbacks, which may submit into this model's full ring
+  if (finished) engine_.ReleaseRequest(job);
   if (job.require_callback && finished) {
     std::lock_guard<std::mutex> cb_lock(on_end_request_mtx_);
     const absl::Status s = job.status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
     for (auto& cb : on_end_request_callbacks_) cb.second(job.job_id, s);
   }
-  if (finished) engine_.ReleaseRequest(job);
 }
 
 void Planner::PrepareReenqueue(Job& job) {

@@ -102,12 +102,21 @@ int TensorRingBuffer::AllocBlocking() {
   return head_++;
 }
 
+int TensorRingBuffer::AllocBlockingN(int n) {
+  std::unique_lock<std::mutex> lock(head_mtx_);
+  slot_cv_.wait(lock, [this, n] { return outstanding_ + n <= size_; });
+  outstanding_ += n;
+  const int first = head_;
+  head_ += n;
+  return first;
+}
+
 void TensorRingBuffer::Release() {
   {
     std::lock_guard<std::mutex> lock(head_mtx_);
     if (outstanding_ > 0) --outstanding_;
   }
-  slot_cv_.notify_one();
+  slot_cv_.notify_all();  // waiters may need different slot counts
 }
 
 int TensorRingBuffer::Outstanding() const {

@@ -54,7 +54,8 @@ class Tensor : public interface::ITensor {
 // that has not run yet and that job later fails its input or output copy.
 // AllocBlocking() waits until fewer than `size` requests taken with it are
 // unfinished; Release() is called once per such request when its job is
-// finished (Planner::EnqueueFinishedJob, after the end-request callbacks).
+// finished (Planner::EnqueueFinishedJob, before the end-request callbacks,
+// so a callback may submit into a full ring).
 class TensorRingBuffer {
  public:
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
@@ -62,6 +63,9 @@ class TensorRingBuffer {
   int Alloc();
   // Alloc() once fewer than size() AllocBlocking()-ed requests are unfinished
   int AllocBlocking();
+  // n consecutive handles at once (the first is returned), once n slots are
+  // free; n must not exceed size()
+  int AllocBlockingN(int n);
   void Release();
   int size() const { return size_; }
   int Outstanding() const;

@@ -133,6 +133,7 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineGetSubgraphs": (c_int, [c_void_p, c_void_p, POINTER(c_int), POINTER(c_uint64), c_int]),
     "BandxEngineGetExpectedLatency": (c_int64, [c_void_p, c_void_p, c_int, c_uint64]),
     "BandxEngineWaitAll": (None, [c_void_p]),
+    "BandxEngineRequestsAsync": (c_int, [c_void_p, POINTER(c_void_p), c_int, POINTER(c_void_p), POINTER(c_int)]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
                                          POINTER(c_double), POINTER(c_int), POINTER(c_double)]),
@@ -334,6 +335,18 @@ class Engine:
         if option is None:
             return int(self.lib.BandEngineRequestAsync(self.handle, model.handle, _ptrs(inputs)))
         return int(self.lib.BandEngineRequestAsyncOptions(self.handle, model.handle, option, _ptrs(inputs)))
+
+    def RequestsAsync(self, models, inputs):
+        """One batched RequestAsync (Band's vector overload) of len(models)
+        requests; returns the job handles, or None when the call is refused"""
+        n = len(models)
+        ms = (c_void_p * n)(*[m.handle.value for m in models])
+        keep = [_ptrs(x) for x in inputs]
+        ins = (c_void_p * n)(*[ctypes.cast(k, c_void_p) for k in keep])
+        hs = (c_int * n)()
+        if self.lib.BandxEngineRequestsAsync(self.handle, ms, n, ins, hs) != kBandOk:
+            return None
+        return list(hs)
 
     def Wait(self, handle, outputs):
         return self.lib.BandEngineWait(self.handle, handle, _ptrs(outputs), len(outputs))

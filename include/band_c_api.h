@@ -210,6 +210,13 @@ BAND_CAPI_EXPORT int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandM
                                                        uint64_t unit_mask);
 /* blocks until every submitted job finished */
 BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
+/* One RequestAsync call for n requests (band/engine.cc:455-529, the batched
+ * overload Band's own benchmark tool uses): request i runs models[i] on the
+ * input tensors inputs[i] (that model's inputs, in order).  handles[i]
+ * receives each job id.  A run of consecutive same-model requests larger
+ * than that model's request ring is refused (kBandErr, nothing submitted). */
+BAND_CAPI_EXPORT BandStatus BandxEngineRequestsAsync(BandEngine* engine, BandModel** models, int n,
+                                                     BandTensor*** inputs, BandRequestHandle* handles);
 
 /* Closed-loop request driver: submits exactly n_jobs requests, round-robin
  * over the n_models models (model j % n_models), with at most max_inflight

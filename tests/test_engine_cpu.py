@@ -291,6 +291,89 @@ def test_closed_loop_beyond_ring_capacity(tmp_path):
     e.close()
 
 
+def test_batched_request_larger_than_ring_is_refused(tmp_path):
+    """one RequestAsync of 129 same-model jobs (ring 128) used to
+    take slots one by one and wait forever for the 129th; it is refused with
+    nothing held, and a 128-job batch and a later single request still run"""
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], num_threads=[1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    t = e.CreateInputTensor(m, 0)
+    assert e.RequestsAsync([m] * 129, [[t]] * 129) is None
+    hs = e.RequestsAsync([m] * 128, [[t]] * 128)
+    assert hs is not None and len(hs) == 128 and len(set(hs)) == 128
+    h = e.RequestAsync(m, [t])  # waits for a slot of the batch above, then runs
+    assert h >= 0
+    e.WaitAll()
+    assert all(e.GetJobRecord(j).status == JobStatus.kSuccess for j in hs + [h])
+    e.close()
+
+
+def test_concurrent_batched_requests_share_a_ring(tmp_path):
+    """two threads each submitting 100-job batches of one model (ring 128):
+    slots are taken per batch in one step and each batch is enqueued at once,
+    so the callers cannot each hold part of the ring and wait on each other"""
+    import threading
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU, DeviceFlag.kCPU], num_threads=[1, 1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    t = e.CreateInputTensor(m, 0)
+    got = [[], []]
+
+    def submit(k):
+        for _ in range(3):
+            got[k].append(e.RequestsAsync([m] * 100, [[t]] * 100))
+
+    th = [threading.Thread(target=submit, args=(k,)) for k in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "batched submitters deadlocked"
+    hs = [h for k in range(2) for b in got[k] for h in b]
+    assert len(hs) == 600
+    e.WaitAll()
+    assert all(e.GetJobRecord(h).status == JobStatus.kSuccess for h in hs)
+    e.close()
+
+
+def test_callback_resubmits_into_full_ring(tmp_path):
+    """an end-request callback that resubmits into its model's
+    full ring (closed-loop resubmission through BandEngineSetOnEndRequest)
+    with a single worker: the finished job's slot is released before the
+    callbacks run, so the resubmission does not wait on its own worker"""
+    import threading
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], num_threads=[1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    t = e.CreateInputTensor(m, 0)
+    ring = 128
+    extra = []
+    done = threading.Event()
+    opt = RequestOptionGetDefault()
+    opt.require_callback = True
+
+    def on_end(job, status):
+        if len(extra) < 20:
+            extra.append(e.RequestAsync(m, [t], opt))
+        elif not done.is_set():
+            done.set()
+
+    e.SetOnEndRequest(on_end)
+    hs = [e.RequestAsync(m, [t], opt) for _ in range(ring)]
+    assert all(h >= 0 for h in hs)
+    assert done.wait(timeout=120), "resubmitting callback deadlocked the worker"
+    e.WaitAll()
+    assert len(extra) == 20 and all(h >= 0 for h in extra)
+    e.close()
+
+
 def test_poisson_latency_counts_submission_delay(golden_dir):
     """open loop: latency runs from each request's scheduled arrival, so an
     arrival held back by the in-flight bound still shows its wait (no

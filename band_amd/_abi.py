@@ -155,6 +155,7 @@ KERNEL_SYMBOLS = {
     "bh_set_device": (c_int, [c_int]),
     "bh_get_device": (c_int, [ctypes.POINTER(c_int)]),
     "bh_device_arch": (c_int, [c_int, ctypes.c_char_p, c_size_t]),
+    "bh_device_pci_bus_id": (c_int, [c_int, ctypes.c_char_p, c_int]),
     "bh_stream_create": (c_int, [ctypes.POINTER(c_void_p)]),
     "bh_stream_destroy": (c_int, [c_void_p]),
     "bh_stream_sync": (c_int, [c_void_p]),

@@ -43,7 +43,11 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_model_get_id": (c_int, [c_void_p]),
     "bhx_model_destroy": (None, [c_void_p]),
     "bhx_executor_create": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "bhx_executor_create_masked": (c_int, [c_int, c_int, c_int, c_int, ctypes.POINTER(c_int), c_int,
+                                           ctypes.POINTER(c_void_p)]),
     "bhx_executor_destroy": (None, [c_void_p]),
+    "bhx_gpu_numa_node": (c_int, [c_int]),
+    "bhx_gpu_numa_cpus": (c_int, [c_int, ctypes.POINTER(c_int), c_int]),
     "bhx_investigate_model_spec": (c_int, [c_void_p, c_void_p, ctypes.c_char_p, c_size_t,
                                            ctypes.POINTER(c_size_t)]),
     "bhx_prepare_subgraph": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int), c_int,
@@ -321,11 +325,19 @@ class HipTensorView:
 class HipModelExecutor:
     """IModelExecutor (band/interface/model_executor.h:30-180) of the HIP backend."""
 
-    def __init__(self, model_id, worker_id, device_flag, num_threads=-1):
+    def __init__(self, model_id, worker_id, device_flag, num_threads=-1, cpus=None):
+        """cpus: the executor's CpuSet (CPU ids); a kCPU executor pins its host
+        thread pool to it (band/backend/tfl/model_executor.cc:356-359)"""
         self.lib = _abi.load()
         h = c_void_p()
-        _abi.check(self.lib.bhx_executor_create(int(model_id), int(worker_id), int(device_flag),
-                                                int(num_threads), ctypes.byref(h)), "CreateModelExecutor")
+        if cpus:
+            arr = (c_int * len(cpus))(*[int(c) for c in cpus])
+            _abi.check(self.lib.bhx_executor_create_masked(int(model_id), int(worker_id), int(device_flag),
+                                                           int(num_threads), arr, len(cpus), ctypes.byref(h)),
+                       "CreateModelExecutor")
+        else:
+            _abi.check(self.lib.bhx_executor_create(int(model_id), int(worker_id), int(device_flag),
+                                                    int(num_threads), ctypes.byref(h)), "CreateModelExecutor")
         self.handle = h
         self.model_id, self.worker_id, self.device_flag = int(model_id), int(worker_id), DeviceFlag(device_flag)
 
@@ -491,3 +503,14 @@ def RunMixedJobs(executors, keys, requests, n_jobs, first_model=0):
     if not st.ok():
         raise _abi.BandHipError("bhx_run_mixed_jobs: " + st.message())
     return lat[:n_jobs], mo[:n_jobs]
+
+
+def GpuNumaCpus(ordinal):
+    """(NUMA node, CPUs of that node the process may use) of GPU `ordinal`:
+    where a kGPU executor pins its worker thread (backend/hip/affinity.h)"""
+    lib = _abi.load()
+    node = int(lib.bhx_gpu_numa_node(int(ordinal)))
+    cap = 4096
+    arr = (c_int * cap)()
+    n = int(lib.bhx_gpu_numa_cpus(int(ordinal), arr, cap))
+    return node, [arr[i] for i in range(min(n, cap))]

@@ -1,0 +1,43 @@
+// Host thread placement for the HIP backend's workers.
+//
+// kCPU executors honour the CpuSet Band hands every executor
+// (band/interface/model_executor.h:41-50): the reference passes it to the
+// TFLite interpreter's thread pool (band/backend/tfl/model_executor.cc:356-359,
+// InterpreterBuilder::SetCpuMasks), so a kCPU HipModelExecutor pins its host
+// pool to it.  An empty set (what BandCPUMaskGetSet returns on Linux,
+// band/device/cpu.cc:377-381) leaves the threads where they are.
+//
+// kGPU executors pin the calling worker thread to the CPUs of its GPU's NUMA
+// node (PCI sysfs numa_node of hipDeviceGetPCIBusId), intersected with the
+// CPUs the process may use, before the thread's first GPU call: the job's
+// host copies (request ring -> pinned input mirror -> H2D) then stay on the
+// socket the GPU hangs off.  BANDX_NUMA_PIN=0 turns this off.
+#pragma once
+
+#include <pthread.h>
+
+#include <string>
+#include <vector>
+
+namespace band {
+namespace hip {
+
+// "0-3,8,10-11" -> {0,1,2,3,8,10,11}; malformed pieces are skipped
+std::vector<int> ParseCpuList(const std::string& s);
+// CPUs the process was started with (sched_getaffinity of the process,
+// captured on first use, before any thread of ours narrowed its own)
+const std::vector<int>& ProcessCpus();
+// pins thread `t` to `cpus`; false when cpus is empty or the call fails
+bool PinThread(pthread_t t, const std::vector<int>& cpus);
+// CPUs of the calling thread's current affinity mask
+std::vector<int> CallingThreadCpus();
+// NUMA node of GPU `ordinal` (-1 when unknown: no sysfs entry, no NUMA)
+int GpuNumaNode(int ordinal);
+// CPUs of that node intersected with ProcessCpus(); empty when unknown
+std::vector<int> GpuNumaCpus(int ordinal);
+// pins the calling thread to GpuNumaCpus(ordinal), once per (thread,
+// ordinal); returns whether the thread is now pinned to that node
+bool PinCallingThreadToGpu(int ordinal);
+
+}  // namespace hip
+}  // namespace band

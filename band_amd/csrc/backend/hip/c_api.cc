@@ -8,6 +8,7 @@
 #include <memory>
 #include <string>
 
+#include "backend/hip/affinity.h"
 #include "backend/hip/backend.h"
 #include "band_hip_backend.h"
 
@@ -104,7 +105,26 @@ int bhx_executor_create(int model_id, int worker_id, int device_flag, int num_th
   *out = new bhx_executor{std::unique_ptr<band::interface::IModelExecutor>(e)};
   return 0;
 }
+int bhx_executor_create_masked(int model_id, int worker_id, int device_flag, int num_threads, const int* cpus,
+                               int n_cpus, bhx_executor** out) {
+  if (!out || device_flag < 0 || device_flag > 3 || n_cpus < 0 || (n_cpus > 0 && !cpus)) return Fail("bad arguments");
+  band::CpuSet mask = band::BandCPUMaskGetSet(band::CPUMaskFlag::kAll);
+  for (int i = 0; i < n_cpus; ++i) mask.Enable(cpus[i]);
+  auto* e = BackendFactory::CreateModelExecutor(BackendType::kTfLite, model_id, worker_id,
+                                                static_cast<DeviceFlag>(device_flag), mask, num_threads);
+  if (!e) return Fail("HIP backend not registered");
+  *out = new bhx_executor{std::unique_ptr<band::interface::IModelExecutor>(e)};
+  return 0;
+}
 void bhx_executor_destroy(bhx_executor* e) { delete e; }
+
+int bhx_gpu_numa_node(int ordinal) { return band::hip::GpuNumaNode(ordinal); }
+
+int bhx_gpu_numa_cpus(int ordinal, int* cpus, int cap) {
+  const std::vector<int> v = band::hip::GpuNumaCpus(ordinal);
+  for (int i = 0; i < cap && i < static_cast<int>(v.size()); ++i) cpus[i] = v[i];
+  return static_cast<int>(v.size());
+}
 
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed) {
   if (!e || !m) return Fail("null argument");

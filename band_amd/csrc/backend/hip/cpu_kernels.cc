@@ -1,5 +1,7 @@
 #include "backend/hip/cpu_kernels.h"
 
+#include "backend/hip/affinity.h"
+
 #include "backend/hip/quant.h"
 
 #include <algorithm>
@@ -13,8 +15,12 @@ namespace hip {
 
 // ---- pool ---------------------------------------------------------------------
 
-CpuPool::CpuPool(int num_threads) {
-  for (int i = 1; i < std::max(1, num_threads); ++i) threads_.emplace_back([this, i] { Loop(i); });
+CpuPool::CpuPool(int num_threads, const std::vector<int>& cpus) {
+  for (int i = 1; i < std::max(1, num_threads); ++i) {
+    threads_.emplace_back([this, i] { Loop(i); });
+    // the executor's CpuSet (affinity.h); pinned before the thread's first job
+    if (!cpus.empty()) PinThread(threads_.back().native_handle(), cpus);
+  }
 }
 
 CpuPool::~CpuPool() {
@@ -681,24 +687,35 @@ void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool) {
       best[i] = arg;
     }
   });
-  std::vector<int> keep;
+  // Greedy NMS in stable descending score order, as the reference's
+  // stable_sort + suppression sweep: only SELECTED boxes suppress, so a
+  // candidate is selected iff its IoU with every box selected before it is
+  // <= iou_threshold.  The candidates are therefore drawn lazily from a heap
+  // (score descending, index ascending = the stable order) and each is
+  // checked against the <= max_detections boxes selected so far; the draw
+  // stops once max_detections are selected.  Same selections, same float
+  // expressions (IoU of the selected box against the candidate), without
+  // sorting every box above the threshold or sweeping them per selection.
+  std::vector<int> heap;
   for (int i = 0; i < n; ++i)
-    if (max_score[i] >= p.score_threshold) keep.push_back(i);
-  std::stable_sort(keep.begin(), keep.end(), [&](int a, int b) { return max_score[a] > max_score[b]; });
-  const int out_size = std::min(static_cast<int>(keep.size()), p.max_detections);
-  std::vector<uint8_t> active(keep.size(), 1);
-  std::vector<int> selected;
+    if (max_score[i] >= p.score_threshold) heap.push_back(i);
+  const int out_size = std::min(static_cast<int>(heap.size()), p.max_detections);
+  auto later = [&](int a, int b) {  // heap order: a is drawn after b
+    return max_score[a] < max_score[b] || (max_score[a] == max_score[b] && a > b);
+  };
+  std::make_heap(heap.begin(), heap.end(), later);
   auto area = [&](const Box& b) { return (b.ymax - b.ymin) * (b.xmax - b.xmin); };
-  for (size_t i = 0; i < keep.size() && static_cast<int>(selected.size()) < out_size; ++i) {
-    if (!active[i]) continue;
-    selected.push_back(keep[i]);
-    active[i] = 0;
-    const Box& bi = boxes[keep[i]];
-    const float ai = area(bi);
-    for (size_t j = i + 1; j < keep.size(); ++j) {
-      if (!active[j]) continue;
-      const Box& bj = boxes[keep[j]];
-      const float aj = area(bj);
+  std::vector<int> selected;
+  while (!heap.empty() && static_cast<int>(selected.size()) < out_size) {
+    std::pop_heap(heap.begin(), heap.end(), later);
+    const int cand = heap.back();
+    heap.pop_back();
+    const Box& bj = boxes[cand];
+    const float aj = area(bj);
+    bool keep_it = true;
+    for (int s : selected) {
+      const Box& bi = boxes[s];
+      const float ai = area(bi);
       float iou = 0.0f;
       if (ai > 0.0f && aj > 0.0f) {
         const float iy0 = std::max(bi.ymin, bj.ymin), ix0 = std::max(bi.xmin, bj.xmin);
@@ -706,8 +723,12 @@ void CpuDetectionPostprocess(const CpuDetectionParams& p, CpuPool& pool) {
         const float inter = std::max(iy1 - iy0, 0.0f) * std::max(ix1 - ix0, 0.0f);
         iou = inter / (ai + aj - inter);
       }
-      if (iou > p.iou_threshold) active[j] = 0;
+      if (iou > p.iou_threshold) {
+        keep_it = false;
+        break;
+      }
     }
+    if (keep_it) selected.push_back(cand);
   }
   std::memset(p.out_boxes, 0, sizeof(float) * 4 * p.max_detections);
   std::memset(p.out_classes, 0, sizeof(float) * p.max_detections);

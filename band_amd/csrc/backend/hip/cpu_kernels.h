@@ -23,10 +23,11 @@ namespace band {
 namespace hip {
 
 // A fixed pool of worker threads (the executor's num_threads; the calling
-// thread is one of them) running ParallelFor over index ranges.
+// thread is one of them) running ParallelFor over index ranges.  A non-empty
+// `cpus` pins the pool's own threads to those CPUs (the executor's CpuSet).
 class CpuPool {
  public:
-  explicit CpuPool(int num_threads);
+  explicit CpuPool(int num_threads, const std::vector<int>& cpus = {});
   ~CpuPool();
   CpuPool(const CpuPool&) = delete;
   CpuPool& operator=(const CpuPool&) = delete;

@@ -1,5 +1,7 @@
 #include "backend/hip/model_executor.h"
 
+#include "backend/hip/affinity.h"
+
 #include <algorithm>
 #include <limits>
 #include <cmath>
@@ -62,7 +64,9 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
     stream_ = DeviceRegistry::Get().StreamForWorker(worker_id_);
   } else if (device_flag_ == DeviceFlag::kCPU) {
     // host execution of the lowered program (cpu_kernels.h)
-    cpu_pool_ = std::make_unique<CpuPool>(num_threads_ > 0 ? num_threads_ : 1);
+    // pinned to the executor's CpuSet when it names CPUs (affinity.h)
+    cpu_pool_ = std::make_unique<CpuPool>(num_threads_ > 0 ? num_threads_ : 1,
+                                          thread_affinity_mask_.GetMaskBitsVector());
   }
   const char* g = std::getenv("BAND_HIP_GRAPH");
   if (g && g[0] == '0') use_graph_ = false;
@@ -1009,6 +1013,10 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
   }
 }
 
+// bumped whenever a chain form's LDS layout or parameter rules change, so a
+// tune file written by an older kernel tree is not replayed against this one
+constexpr int kChainTuneVersion = 3;
+
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
   std::snprintf(buf, sizeof(buf), "%d:%d:%dx%dx%d:%d:%d:%dx%d:%d:%d:%d", ordinal, q.batch, q.in_h, q.in_w, q.in_c,
@@ -1255,7 +1263,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // = px_blocks of the 2-launch form (the second conv stays a launch),
     // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
-    std::snprintf(key, sizeof(key), "ch:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", ordinal_, D.dw.batch, D.dw.in_h,
+    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", kChainTuneVersion, ordinal_, D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
                   ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
@@ -1322,6 +1330,12 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.px_blocks = choice % 10;
     F.chain.waves = choice >= 300 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
+    // a choice read from a tune file written by another kernel tree may name
+    // a form these parameters do not admit: keep the unfused launches then
+    if (bh_chain_lds_bytes(&F.chain) == 0) {
+      out.push_back(L[i]);
+      continue;
+    }
     F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
     F.kernel = "chain_kernel";
     const bh_dwconv_params& dw = F.chain.dw;
@@ -2303,6 +2317,8 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (!sg) return absl::InternalError("Cannot find subgraph");
   if (device_flag_ == DeviceFlag::kCPU) return ExecuteOnHost(sg);
   if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("Unsupported device type");
+  // the worker thread goes to its GPU's NUMA node before its first GPU call
+  PinCallingThreadToGpu(ordinal_);
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) {

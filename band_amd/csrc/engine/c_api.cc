@@ -1,5 +1,6 @@
 // Band C API over the native harness (band/c/c_api.cc restated; see
 // include/band_c_api.h for the contract).
+#include <pthread.h>
 #include "band_c_api.h"
 
 #include <condition_variable>
@@ -439,6 +440,7 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   bool failed = false;
   const int64_t t0 = band::time::NowMicros();
   std::thread waiter([&] {
+    pthread_setname_np(pthread_self(), "bandx-waiter");
     for (int done = 0; done < n_jobs; ++done) {
       std::unique_lock<std::mutex> l(mu);
       cv.wait(l, [&] { return !pending.empty(); });
@@ -504,6 +506,12 @@ BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTen
         return std::make_pair(static_cast<int64_t>(t), pick(rng));
       },
       latency_us, worker_ids, model_index, wall_s);
+}
+
+int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id) {
+  if (!engine || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return -1;
+  const band::Worker* w = engine->impl->GetWorker(worker_id);
+  return w ? w->GetJobsRun() : -1;
 }
 
 void BandxEngineWaitAll(BandEngine* engine) {

@@ -321,7 +321,7 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
       for (size_t k = i; k < j; ++k) {
         const int handle = first + static_cast<int>(k - i);
         if (!in_ring->PutTensorsToHandle(inputs[k], handle).ok()) {
-          for (size_t r = i; r < j; ++r) in_ring->Release();
+          for (size_t r = i; r < j; ++r) in_ring->Release(first + static_cast<int>(r - i));
           return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[k]));
         }
         jobs[k].input_handle = handle;
@@ -340,7 +340,7 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
 void Engine::ReleaseRequest(const Job& job) {
   if (job.input_handle < 0) return;
   auto it = model_input_buffer_.find(job.model_id);
-  if (it != model_input_buffer_.end()) it->second->Release();
+  if (it != model_input_buffer_.end()) it->second->Release(job.input_handle);
 }
 
 int Engine::RequestRingSize(ModelId model_id) const {
@@ -397,6 +397,13 @@ std::set<WorkerId> Engine::GetIdleWorkers() const {
   std::set<WorkerId> idle;
   for (const auto& kv : workers_waiting_)
     if (kv.second == 0) idle.insert(kv.first);
+  return idle;
+}
+
+std::set<WorkerId> Engine::GetIdleWorkersNow() {
+  std::set<WorkerId> idle;
+  for (WorkerId w = 0; w < static_cast<WorkerId>(workers_.size()); ++w)
+    if (workers_[w]->IsIdleNow()) idle.insert(idle.end(), w);
   return idle;
 }
 

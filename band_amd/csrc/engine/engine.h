@@ -85,6 +85,7 @@ class Engine : public IEngine {
   void UpdateWorkersWaiting() const override;
   WorkerWaitingTime GetWorkerWaitingTime() const override { return workers_waiting_; }
   std::set<WorkerId> GetIdleWorkers() const override;
+  std::set<WorkerId> GetIdleWorkersNow() override;
   size_t GetNumWorkers() const override { return workers_.size(); }
   DeviceFlag GetWorkerDevice(WorkerId id) const override;
   Worker* GetWorker(WorkerId id) override;

@@ -29,6 +29,13 @@ class IEngine {
   virtual void UpdateWorkersWaiting() const = 0;
   virtual WorkerWaitingTime GetWorkerWaitingTime() const = 0;
   virtual std::set<WorkerId> GetIdleWorkers() const = 0;
+  // idle workers read directly (round_robin needs no waiting times): one
+  // lock per worker instead of pricing every queue; the default is the
+  // reference's UpdateWorkersWaiting + GetIdleWorkers
+  virtual std::set<WorkerId> GetIdleWorkersNow() {
+    UpdateWorkersWaiting();
+    return GetIdleWorkers();
+  }
   virtual size_t GetNumWorkers() const = 0;
   virtual DeviceFlag GetWorkerDevice(WorkerId id) const = 0;
   virtual Worker* GetWorker(WorkerId id) = 0;

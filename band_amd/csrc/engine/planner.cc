@@ -1,5 +1,7 @@
 #include "engine/planner.h"
 
+#include <pthread.h>
+
 #include <cstdio>
 
 #include "engine/logger.h"
@@ -35,6 +37,7 @@ bool SafeBool::wait() {
 
 Planner::Planner(IEngine& engine) : engine_(engine), jobs_finished_record_(kNumFinishedRecords) {
   planner_thread_ = std::thread([this] {
+    pthread_setname_np(pthread_self(), "band-planner");
     absl::Status s = Plan();
     if (!s.ok()) BAND_LOG(LogSeverity::kError, "planner thread failed: %s", s.message().c_str());
   });

@@ -51,8 +51,8 @@ bool FixedWorkerGlobalQueueScheduler::Schedule(JobQueue& requests) {
 
 bool RoundRobinScheduler::Schedule(JobQueue& requests) {
   bool ok = true;
-  engine_.UpdateWorkersWaiting();
-  const std::set<WorkerId> idle = engine_.GetIdleWorkers();
+  if (requests.empty()) return ok;
+  const std::set<WorkerId> idle = engine_.GetIdleWorkersNow();
   if (idle.empty() || requests.empty()) return ok;
   // idle workers in rotation order, starting at next_
   std::vector<WorkerId> order(idle.lower_bound(next_), idle.end());

@@ -84,7 +84,7 @@ absl::Status Tensor::SetQuantization(Quantization q) {
 
 TensorRingBuffer::TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors,
                                    std::vector<int> tensor_indices, int size)
-    : size_(size > 0 ? size : 1), num_tensors_(tensors.size()), slots_(size_) {
+    : size_(size > 0 ? size : 1), num_tensors_(tensors.size()), slots_(size_), busy_(size_, 0) {
   for (auto& slot : slots_)
     for (const auto& t : tensors) slot.emplace_back(new Tensor(t.get()));
   for (size_t i = 0; i < tensor_indices.size(); ++i) tensor_to_buffer_[tensor_indices[i]] = static_cast<int>(i);
@@ -95,26 +95,36 @@ int TensorRingBuffer::Alloc() {
   return head_++;
 }
 
-int TensorRingBuffer::AllocBlocking() {
-  std::unique_lock<std::mutex> lock(head_mtx_);
-  slot_cv_.wait(lock, [this] { return outstanding_ < size_; });
-  ++outstanding_;
-  return head_++;
-}
+int TensorRingBuffer::AllocBlocking() { return AllocBlockingN(1); }
 
+// Slots are handed out in handle order, so the n slots a call takes are the
+// next n of the ring; the call waits until each of them is free.  Jobs of one
+// model can finish out of order (several workers), so counting unfinished
+// requests is not enough: a slot whose request is still pending must not be
+// handed to a newer one (it would overwrite that request's input, and its
+// handle would leave the ring's valid window before its output copy).
 int TensorRingBuffer::AllocBlockingN(int n) {
   std::unique_lock<std::mutex> lock(head_mtx_);
-  slot_cv_.wait(lock, [this, n] { return outstanding_ + n <= size_; });
+  auto free_run = [this, n] {
+    if (n > size_) return false;
+    for (int k = 0; k < n; ++k)
+      if (busy_[Slot(head_ + k)]) return false;
+    return true;
+  };
+  slot_cv_.wait(lock, free_run);
+  for (int k = 0; k < n; ++k) busy_[Slot(head_ + k)] = 1;
   outstanding_ += n;
   const int first = head_;
   head_ += n;
   return first;
 }
 
-void TensorRingBuffer::Release() {
+void TensorRingBuffer::Release(int handle) {
   {
     std::lock_guard<std::mutex> lock(head_mtx_);
-    if (outstanding_ > 0) --outstanding_;
+    if (handle < 0 || !busy_[Slot(handle)]) return;
+    busy_[Slot(handle)] = 0;
+    --outstanding_;
   }
   slot_cv_.notify_all();  // waiters may need different slot counts
 }

@@ -52,21 +52,23 @@ class Tensor : public interface::ITensor {
 // Back-pressure (deviation): the reference's Alloc never waits, so a model
 // with more than `size` unfinished requests reuses the slot of a request
 // that has not run yet and that job later fails its input or output copy.
-// AllocBlocking() waits until fewer than `size` requests taken with it are
-// unfinished; Release() is called once per such request when its job is
-// finished (Planner::EnqueueFinishedJob, before the end-request callbacks,
-// so a callback may submit into a full ring).
+// AllocBlocking() waits until the next slot of the ring is free - the slot
+// itself, not a count, since jobs of one model finish out of order; Release()
+// frees a request's slot when its job is finished
+// (Planner::EnqueueFinishedJob, before the end-request callbacks, so a
+// callback may submit into a full ring).
 class TensorRingBuffer {
  public:
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
                    int size = 128);
   int Alloc();
-  // Alloc() once fewer than size() AllocBlocking()-ed requests are unfinished
+  // Alloc() once the next slot's request (if any) is finished
   int AllocBlocking();
-  // n consecutive handles at once (the first is returned), once n slots are
-  // free; n must not exceed size()
+  // n consecutive handles at once (the first is returned), once those n
+  // slots are free; n must not exceed size()
   int AllocBlockingN(int n);
-  void Release();
+  // frees the slot of a handle taken with AllocBlocking[N]
+  void Release(int handle);
   int size() const { return size_; }
   int Outstanding() const;
   bool IsTensorIndexValid(int tensor_index) const { return tensor_to_buffer_.count(tensor_index) != 0; }
@@ -85,6 +87,7 @@ class TensorRingBuffer {
   std::map<int, int> tensor_to_buffer_;
   mutable std::mutex head_mtx_;
   std::condition_variable slot_cv_;
+  std::vector<char> busy_;  // per slot: taken by AllocBlocking[N], not yet released
   int head_ = 0;
   int outstanding_ = 0;
 };

@@ -1,5 +1,8 @@
 #include "engine/worker.h"
 
+#include <pthread.h>
+#include <sched.h>
+
 #include <algorithm>
 #include <cstdio>
 
@@ -29,7 +32,24 @@ absl::Status Worker::Init(const WorkerConfig& config) {
 void Worker::Start() {
   std::call_once(start_once_, [this] {
     started_ = true;
-    thread_ = std::thread([this] { Work(); });
+    thread_ = std::thread([this] {
+      // named for per-thread profiles (tools/planner_ceiling.py); a CpuSet
+      // that names CPUs pins the worker thread (band/worker.cc:195-205 does
+      // this on mobile builds, where BandCPUMaskGetSet fills the sets)
+      char name[16];
+      std::snprintf(name, sizeof(name), "band-w%d", worker_id_);
+      pthread_setname_np(pthread_self(), name);
+      const std::vector<int> cpus = cpu_set_.GetMaskBitsVector();
+      if (!cpus.empty()) {
+        cpu_set_t m;
+        CPU_ZERO(&m);
+        for (int c : cpus)
+          if (c < CPU_SETSIZE) CPU_SET(c, &m);
+        if (pthread_setaffinity_np(pthread_self(), sizeof(m), &m) != 0)
+          BAND_LOG(LogSeverity::kWarning, "worker %d: could not set its CPU affinity", worker_id_);
+      }
+      Work();
+    });
   });
 }
 
@@ -45,12 +65,14 @@ void Worker::End() {
 void Worker::Pause() {
   std::lock_guard<std::mutex> lock(device_mtx_);
   is_paused_ = true;
+  RefreshIdle();
 }
 
 void Worker::Resume() {
   {
     std::lock_guard<std::mutex> lock(device_mtx_);
     is_paused_ = false;
+    RefreshIdle();
   }
   request_cv_.notify_one();
 }
@@ -87,6 +109,7 @@ void Worker::Work() {
         job->status = JobStatus::kInvokeFailure;
         Job failed = *job;
         EndEnqueue();
+        RefreshIdle();
         lock.unlock();
         engine_->EnqueueFinishedJob(failed);
         engine_->Trigger();
@@ -133,9 +156,11 @@ void Worker::Work() {
       BAND_LOG(LogSeverity::kError, "worker %d failed to copy input of job %d", worker_id_, job->job_id);
       job->status = JobStatus::kInputCopyFailure;
     }
+    jobs_run_.fetch_add(1, std::memory_order_relaxed);
     engine_->EnqueueFinishedJob(*job);
     lock.lock();
     EndEnqueue();
+    RefreshIdle();
     lock.unlock();
     engine_->Trigger();
   }
@@ -181,12 +206,14 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   if (!status.ok())
     BAND_LOG(LogSeverity::kError, "worker %d failed to invoke a batch of %d jobs: %s", worker_id_, n,
              status.message().c_str());
+  jobs_run_.fetch_add(n, std::memory_order_relaxed);
   for (int i = 1; i < n; ++i) engine_->EnqueueFinishedJob(*jobs[i]);
   engine_->EnqueueFinishedJob(*head);
   {
     std::lock_guard<std::mutex> lock(device_mtx_);
     partners_expected_us_ = 0;
     EndEnqueue();
+    RefreshIdle();
   }
   engine_->Trigger();
 }
@@ -215,6 +242,7 @@ void DeviceQueueWorker::TakeBatchPartners(const Job& head, int max, std::vector<
 bool DeviceQueueWorker::EnqueueJob(Job& job) {
   if (!IsEnqueueReady()) return false;
   requests_.push_back(job);
+  idle_.store(false, std::memory_order_release);
   request_cv_.notify_one();
   return true;
 }
@@ -240,6 +268,7 @@ bool GlobalQueueWorker::EnqueueJob(Job& job) {
   if (!IsEnqueueReady()) return false;
   current_job_ = job;
   is_busy_ = true;
+  idle_.store(false, std::memory_order_release);
   request_cv_.notify_one();
   return true;
 }

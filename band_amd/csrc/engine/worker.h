@@ -7,6 +7,7 @@
 //   GlobalQueueWorker - one job at a time, the planner holds the queue
 //                       (SEL / HEFT / LSF)
 #pragma once
+#include <atomic>
 #include <condition_variable>
 #include <cstdint>
 #include <mutex>
@@ -48,6 +49,12 @@ class Worker {
   virtual bool HasJob() = 0;
   virtual int GetCurrentJobId() = 0;
   virtual int64_t GetWaitingTime() = 0;
+  // no queued or running job and available: what GetWaitingTime() == 0
+  // means, read without the lock or pricing a queue (the planner's
+  // round_robin scan touches every worker on every wake-up)
+  bool IsIdleNow() const { return idle_.load(std::memory_order_acquire); }
+  // subgraph executions finished by this worker (each job of a batched pass)
+  int64_t GetJobsRun() const { return jobs_run_.load(std::memory_order_relaxed); }
 
  protected:
   virtual Job* GetCurrentJob() = 0;
@@ -78,6 +85,13 @@ class Worker {
   // GetWaitingTime keeps counting them (at their one-job latency, an upper
   // bound of their share of the batched pass)
   int64_t partners_expected_us_ = 0;
+  // IsIdleNow's flag, recomputed under device_mtx_ wherever the queue or
+  // the availability changes
+  std::atomic<bool> idle_{true};
+  std::atomic<int64_t> jobs_run_{0};
+  void RefreshIdle() {
+    idle_.store(IsAvailable() && !HasJob() && partners_expected_us_ == 0, std::memory_order_release);
+  }
 
  private:
   std::thread thread_;

@@ -62,6 +62,13 @@ extern "C" int bh_device_arch(int ordinal, char* buf, size_t cap) {
   return 0;
 }
 
+// PCI bus id of `ordinal` ("0000:75:00.0"), NUL-terminated: the host side
+// reads the device's NUMA node from /sys/bus/pci/devices/<id>/numa_node
+extern "C" int bh_device_pci_bus_id(int ordinal, char* buf, int cap) {
+  if (!buf || cap < 13) return BH_EINVAL;
+  return ck(hipDeviceGetPCIBusId(buf, cap, ordinal), "hipDeviceGetPCIBusId");
+}
+
 extern "C" int bh_stream_create(bh_stream_t* stream) {
   hipStream_t s = nullptr;
   int rc = ck(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
@@ -151,9 +158,10 @@ extern "C" int bh_spin_us(bh_stream_t s, int us) {
 __global__ void bh_empty_kernel(int) {}
 
 // One empty single-wave launch: profilers time chains of these exactly like
-// a real launch sequence to learn what an event pair measures beyond a
-// kernel's own duration (dispatch + inter-kernel gap).
+// a real launch sequence.  Through BH_LAUNCH, so under bh_profile_events it
+// carries the same dispatch begin / end timestamps as the real kernels and
+// its duration is the fixed cost inside every kernel-only duration.
 extern "C" int bh_empty_launch(bh_stream_t s) {
-  hipLaunchKernelGGL(bh_empty_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, 0);
+  BH_LAUNCH(bh_empty_kernel, dim3(1), dim3(64), 0, (hipStream_t)s, 0);
   return bh_check_launch("bh_empty_kernel");
 }

@@ -133,6 +133,7 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineGetSubgraphs": (c_int, [c_void_p, c_void_p, POINTER(c_int), POINTER(c_uint64), c_int]),
     "BandxEngineGetExpectedLatency": (c_int64, [c_void_p, c_void_p, c_int, c_uint64]),
     "BandxEngineWaitAll": (None, [c_void_p]),
+    "BandxEngineGetWorkerJobCount": (c_int64, [c_void_p, c_int]),
     "BandxEngineRequestsAsync": (c_int, [c_void_p, POINTER(c_void_p), c_int, POINTER(c_void_p), POINTER(c_int)]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
@@ -386,6 +387,11 @@ class Engine:
         ms = (c_uint64 * max(n, 1))()
         self.lib.BandxEngineGetSubgraphs(self.handle, model.handle, ws, ms, n)
         return [(ws[i], ms[i]) for i in range(n)]
+
+    def GetWorkerJobCount(self, worker_id):
+        """subgraph executions worker `worker_id` has finished (each job of a
+        batched pass counted once; a split model once per subgraph)"""
+        return int(self.lib.BandxEngineGetWorkerJobCount(self.handle, int(worker_id)))
 
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))

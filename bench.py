@@ -555,6 +555,7 @@ def main():
         single = single_engine_line(args, D, paths, sched, W, max(1, args.gpus), n_warm, n_timed)
         elapsed, lat_us, worker_ids = n_timed / single["value"], None, []
         jobs_per_worker = single["jobs_per_gpu"]
+        subgraph_jobs = None
         n_ranks = 1
     else:
         engine, band_models, inputs = make_engine(args, D, paths, sched, workers, n_cpu, W, args.job_batch,
@@ -579,6 +580,9 @@ def main():
         else:
             elapsed, lat_us, worker_ids = run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D)
         jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
+        # every subgraph execution per worker (warm-up included): a split
+        # model's GPU share is invisible in the last-subgraph counts above
+        subgraph_jobs = [engine.GetWorkerJobCount(w) for w in range(n_cpu + W)]
         engine.close()
         n_ranks = D.world
     all_lat = [x for part in D.gather((lat_us * 1e-6).tolist() if lat_us is not None else []) for x in part]
@@ -641,6 +645,7 @@ def main():
                                   ", %d requests in flight per engine" % inflight,
                        "step": "%d jobs (%d of each model), round-robin over the models" % (jps, jps // M),
                        "jobs_per_worker_rank0": jobs_per_worker,
+                       "subgraph_jobs_per_worker_rank0": subgraph_jobs,
                        "max_job_batch": args.job_batch,
                        "model": args.model, "global_batch": n_ranks * W * max(1, args.job_batch), "seq_len": None,
                        "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus)) if args.single_engine

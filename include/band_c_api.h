@@ -210,6 +210,10 @@ BAND_CAPI_EXPORT int64_t BandxEngineGetExpectedLatency(BandEngine* engine, BandM
                                                        uint64_t unit_mask);
 /* blocks until every submitted job finished */
 BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
+/* jobs (subgraph executions) worker `worker_id` has finished since the
+ * engine started, each job of a batched pass counted once; -1 for a bad id.
+ * A model split over workers counts once per subgraph on each worker. */
+BAND_CAPI_EXPORT int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id);
 /* One RequestAsync call for n requests (band/engine.cc:455-529, the batched
  * overload Band's own benchmark tool uses): request i runs models[i] on the
  * input tensors inputs[i] (that model's inputs, in order).  handles[i]

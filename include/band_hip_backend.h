@@ -72,7 +72,17 @@ void bhx_model_destroy(bhx_model* m);
 
 /* IModelExecutor (BackendFactory::CreateModelExecutor) */
 int bhx_executor_create(int model_id, int worker_id, int device_flag, int num_threads, bhx_executor** out);
+/* the same with an explicit CpuSet (band/interface/model_executor.h:41-50's
+ * thread_affinity_mask): cpus[0..n_cpus) enabled; a kCPU executor pins its
+ * host thread pool to it (band/backend/tfl/model_executor.cc:356-359) */
+int bhx_executor_create_masked(int model_id, int worker_id, int device_flag, int num_threads, const int* cpus,
+                               int n_cpus, bhx_executor** out);
 void bhx_executor_destroy(bhx_executor* e);
+/* NUMA node of GPU `ordinal` from its PCI sysfs entry (-1: unknown), and the
+ * CPUs of that node the process may use (count returned, up to cap written):
+ * where a kGPU executor pins its worker thread (affinity.h) */
+int bhx_gpu_numa_node(int ordinal);
+int bhx_gpu_numa_cpus(int ordinal, int* cpus, int cap);
 /* InvestigateModelSpec -> ModelSpec serialised as JSON into buf.
  * *needed receives the full length (+1); the call fails if cap < needed. */
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed);

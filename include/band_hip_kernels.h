@@ -66,6 +66,8 @@ int bh_set_device(int ordinal);
 int bh_get_device(int* ordinal);
 /* arch name of `ordinal` (e.g. "gfx950:sramecc+:xnack-"), NUL-terminated */
 int bh_device_arch(int ordinal, char* buf, size_t cap);
+/* PCI bus id of `ordinal` ("0000:75:00.0", hipDeviceGetPCIBusId), NUL-terminated; cap >= 13 */
+int bh_device_pci_bus_id(int ordinal, char* buf, int cap);
 int bh_stream_create(bh_stream_t* stream);
 int bh_stream_destroy(bh_stream_t stream);
 int bh_stream_sync(bh_stream_t stream);

@@ -62,7 +62,10 @@ def _postprocess_only(n, classes, background, seed, max_det=10, score_th=0.3, io
 
 
 @pytest.mark.parametrize("n,classes,background,seed,max_det,score_th", [
-    (50, 3, 1, 0, 10, 0.3), (300, 7, 0, 1, 25, 0.5), (1000, 2, 1, 2, 100, 0.0), (64, 5, 1, 3, 5, 1.1)])
+    (50, 3, 1, 0, 10, 0.3), (300, 7, 0, 1, 25, 0.5), (1000, 2, 1, 2, 100, 0.0), (64, 5, 1, 3, 5, 1.1),
+    # heavy suppression over many tied candidates (the lazy-heap NMS draws
+    # far past max_detections before it fills the output)
+    (6000, 4, 1, 4, 100, 0.0), (4000, 90, 1, 5, 25, 0.2)])
 def test_detection_postprocess_vs_oracle(tmp_path, n, classes, background, seed, max_det, score_th):
     buf, feeds = _postprocess_only(n, classes, background, seed, max_det, score_th)
     got = _run_cpu(buf, feeds, tmp_path)

@@ -80,7 +80,8 @@ class MeanParams(ctypes.Structure):
 
 class ChainParams(ctypes.Structure):
     _fields_ = [("dw", DwConvParams), ("pw1", ConvParams), ("pw2", ConvParams), ("has_pw2", c_int),
-                ("px_blocks", c_int), ("waves", c_int), ("persist", c_int)]
+                ("px_blocks", c_int), ("waves", c_int), ("persist", c_int), ("tile", c_int),
+                ("tile_blob", c_void_p), ("debug_stamps", c_void_p)]
 
 
 # symbol -> (restype, argtypes)
@@ -214,6 +215,10 @@ KERNEL_SYMBOLS = {
     "bh_chain_i8": (c_int, [ctypes.POINTER(ChainParams), c_void_p]),
     "bh_mean": (c_int, [ctypes.POINTER(MeanParams), c_void_p]),
     "bh_chain_lds_bytes": (c_size_t, [ctypes.POINTER(ChainParams)]),
+    "bh_chain_tile_lds_bytes": (c_size_t, [ctypes.POINTER(ChainParams)]),
+    "bh_chain_tile_launch": (c_int, [ctypes.POINTER(ChainParams), c_void_p]),
+    "bh_chain_tile_blob_bytes": (c_size_t, [ctypes.POINTER(ChainParams)]),
+    "bh_chain_tile_pack": (c_int, [ctypes.POINTER(ChainParams), c_void_p, c_void_p]),
     "bh_last_error": (ctypes.c_char_p, []),
 }
 

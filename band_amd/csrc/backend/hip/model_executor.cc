@@ -526,6 +526,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "noadd") == 0) allow_add_ = false;
   if (f && std::strcmp(f, "nochain") == 0) allow_chain_ = false;
   if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
+  if (f && std::strcmp(f, "forcetile") == 0) force_chain_ = force_tile_chain_ = true;  // ... in the tile form
+  if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
@@ -1217,6 +1219,18 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
 // first conv's output is stored only when something besides the second conv
 // reads it (the next block's residual, a subgraph output).  Taken per run
 // geometry by on-device timing against the unfused launches, as FuseBlocks.
+// The tile form's constant block (bh_chain_tile_pack): built on the device
+// from the chain's filter / table pointers, owned by the subgraph.
+bool HipModelExecutor::PackChainTile(bh_chain_params* q, PreparedSubgraph* sg) {
+  const size_t nb = bh_chain_tile_blob_bytes(q);
+  if (nb == 0 || ordinal_ < 0) return false;
+  auto blob = std::make_shared<DeviceBlob>(ordinal_, nb);
+  if (!blob->ok() || bh_chain_tile_pack(q, blob->ptr(), stream_) != 0 || bh_stream_sync(stream_) != 0) return false;
+  q->tile_blob = blob->ptr();
+  sg->consts.push_back(blob);
+  return true;
+}
+
 void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
   const TflModel& d = model.desc();
   auto private_tensor = [&](int t, int only_consumer) {
@@ -1267,6 +1281,11 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
                   ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
+    if (force_tile_chain_) {
+      bh_chain_params q = ok3 ? c3 : c2;
+      q.tile = 1;
+      if (bh_chain_lds_bytes(&q) > 0) choice += 400;
+    }
     if (autotune_ && choice < 0) {
       std::lock_guard<std::mutex> lk(g_tune_mu);
       LoadTuneFileLocked();
@@ -1287,15 +1306,20 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // 16 pixels over 16 waves (few-pixel, many-channel layers)
         // {px_blocks, waves, persist}: the last is the persistent form
         // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
-        const int forms[6][3] = {{4, 4, 0}, {2, 4, 0}, {1, 4, 0}, {1, 8, 0}, {1, 16, 0}, {4, 4, 1}};
+        // {.., tile}: the 2-D tile form (8 x 8 pixels, one LDS-DMA burst)
+        const int forms[7][4] = {{4, 4, 0, 0}, {2, 4, 0, 0}, {1, 4, 0, 0}, {1, 8, 0, 0},
+                                 {1, 16, 0, 0}, {4, 4, 1, 0}, {4, 4, 0, 1}};
         for (const auto& pw : forms) {
+          if (pw[3] && no_tile_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;
             q.px_blocks = pw[0];
             q.waves = pw[1];
             q.persist = pw[2];
+            q.tile = pw[3];
             if (bh_chain_lds_bytes(&q) == 0) continue;
+            if (q.tile && !PackChainTile(&q, sg)) continue;
             Launch F;
             F.kind = Launch::kChain;
             F.chain = q;
@@ -1304,7 +1328,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0);
+                       (pw[2] ? 200 : 0) + (pw[3] ? 400 : 0);
             }
           }
         }
@@ -1317,7 +1341,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       }
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
-    // +200 for the persistent form, +300 for 8 waves
+    // +200 for the persistent form, +300 for 8 waves, +400 for the tile form
     const bool three = choice > 0 && choice % 100 < 10;
     if (choice == 0 || (three && !ok3) || (!three && !ok2)) {
       out.push_back(L[i]);
@@ -1328,16 +1352,17 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.op_index = D.op_index;
     F.chain = three ? c3 : c2;
     F.chain.px_blocks = choice % 10;
-    F.chain.waves = choice >= 300 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
+    F.chain.waves = choice >= 300 && choice < 400 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
+    F.chain.tile = choice >= 400 && choice < 500 ? 1 : 0;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then
-    if (bh_chain_lds_bytes(&F.chain) == 0) {
+    if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {
       out.push_back(L[i]);
       continue;
     }
     F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
-    F.kernel = "chain_kernel";
+    F.kernel = F.chain.tile ? "chain_tile_kernel" : "chain_kernel";
     const bh_dwconv_params& dw = F.chain.dw;
     const bh_conv_params& a = F.chain.pw1;
     const double px = static_cast<double>(dw.batch) * dw.out_h * dw.out_w;

@@ -165,6 +165,7 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bool TryFuseResidualAdd(const HipModel& model, int conv_op, PreparedSubgraph* sg, Launch* l);
   void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
   // dw3x3 -> conv1x1 [+ADD] [-> conv1x1] runs into one bh_chain_i8 launch
+  bool PackChainTile(bh_chain_params* q, PreparedSubgraph* sg);
   void FuseChains(const HipModel& model, PreparedSubgraph* sg);
   // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
   // CONCATENATION with outer size 1 elided (producers write their slices)
@@ -205,6 +206,8 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bool allow_add_ = true;
   bool allow_chain_ = true;   // BAND_HIP_FUSION=nochain
   bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
+  bool force_tile_chain_ = false;  // BAND_HIP_FUSION=forcetile: every feasible chain in the tile form
+  bool no_tile_chain_ = false;     // BAND_HIP_FUSION=notile: the tuner skips the tile form
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;

@@ -268,6 +268,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
                                                     int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const unsigned long long t_entry = __builtin_amdgcn_s_memtime();  // before any kernarg load
   constexpr int WPB = NW / RB;  // waves per pixel block
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -297,6 +298,14 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
   }
   const int prow = pb * 16 + r16;     // this lane's operand row
   const int orow = pb * 16 + 4 * g;   // first of this lane's 4 result rows
+  // diagnostics (tools/tile_probe.py --raster): shader-clock stamps at the
+  // phase boundaries, debug_stamps[8 * workgroup]
+  unsigned long long* stamps =
+      cp.debug_stamps ? (unsigned long long*)cp.debug_stamps + 8 * (long)blockIdx.x : nullptr;
+#define CHAIN_STAMP(k) \
+  if (stamps && threadIdx.x == 0) stamps[k] = __builtin_amdgcn_s_memtime();
+  CHAIN_STAMP(0)
+  if (stamps && threadIdx.x == 0) stamps[7] = t_entry;
 
   // ---- phase A: depthwise 3x3 -> LDS -------------------------------------
   {
@@ -372,6 +381,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     }
   }
   __syncthreads();
+  CHAIN_STAMP(1)
 
   // ---- phase B: first 1x1 (+ residual ADD) -> LDS (operand) / LDS (staged) -
   {
@@ -448,7 +458,9 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     }
   }
   __syncthreads();
+  CHAIN_STAMP(2)
   if (cp.pw1.output) copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
+  CHAIN_STAMP(3)
   if (!cp.has_pw2) return;
 
   // ---- phase C: second 1x1 -> LDS staging (dl, row stride N2) -> HBM ------
@@ -479,7 +491,10 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
     }
   }
   __syncthreads();
+  CHAIN_STAMP(4)
   copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
+  CHAIN_STAMP(5)
+#undef CHAIN_STAMP
 }
 
 // LDS regions of one workgroup: dl (depthwise output, later the second
@@ -852,8 +867,10 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   if (!pp) return 0;
   const bh_chain_params& p = *pp;
   const bh_dwconv_params& d = p.dw;
-  if (p.px_blocks != 1 && p.px_blocks != 2 && p.px_blocks != 4) return 0;
-  if (p.waves != 0 && p.waves != 4 && !((p.waves == 8 || p.waves == 16) && p.px_blocks == 1)) return 0;
+  if (!p.tile) {
+    if (p.px_blocks != 1 && p.px_blocks != 2 && p.px_blocks != 4) return 0;
+    if (p.waves != 0 && p.waves != 4 && !((p.waves == 8 || p.waves == 16) && p.px_blocks == 1)) return 0;
+  }
   if (d.k_h != 3 || d.k_w != 3 || d.depth_multiplier != 1 || d.in_c != d.out_c || d.out_c % 16 || !d.taps ||
       d.in_xor != 0 || d.w_zp != 0 || d.out_table || !d.input || !d.weights || !d.mult || !d.shift ||
       d.batch <= 0 || d.out_h <= 0 || d.out_w <= 0 || d.stride_h <= 0 || d.stride_w <= 0)
@@ -871,6 +888,7 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   }
   const long widest = std::max<long>(std::max(d.out_c, p.pw1.out_c), p.has_pw2 ? p.pw2.out_c : 0);
   if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
+  if (p.tile) return bh_chain_tile_lds_bytes(pp);
   if (p.persist) {
     if (p.px_blocks != 4 || (p.waves != 0 && p.waves != 4)) return 0;
     const size_t bytes = bh::persist_lds(p).bytes;
@@ -887,6 +905,7 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
     return BH_EINVAL;
   }
   const bh_chain_params& p = *pp;
+  if (p.tile) return bh_chain_tile_launch(pp, stream);
   const int P = p.dw.batch * p.dw.out_h * p.dw.out_w;
   const bh::ChainLds L = bh::chain_lds(p);
   const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast);

@@ -327,10 +327,32 @@ typedef struct bh_chain_params {
    * tables staged in LDS once per workgroup, which then walks a contiguous
    * range of 64-pixel blocks (px_blocks 4, 4 waves; filters must fit LDS) */
   int persist;
+  /* 1: 2-D tile form (chain_tile_kernel) - a workgroup owns an 8 x 8 tile of
+   * output pixels and stages its depthwise input patch (tile + halo), the
+   * residual tile, both 1x1 filters and every table in LDS with one burst of
+   * LDS-DMA; stride / dilation 1 or 2, pw2 K <= 320.  px_blocks, waves and
+   * persist are ignored */
+  int tile;
+  /* tile form: the chain's constant block (both 1x1 filters swizzled for
+   * LDS, every table, the depthwise filter) built once by
+   * bh_chain_tile_pack into bh_chain_tile_blob_bytes() of device memory */
+  const void* tile_blob;
+  /* tile form, diagnostics: when non-NULL each workgroup writes 8 shader-
+   * clock stamps (s_memtime) at its phase boundaries to
+   * debug_stamps[8 * workgroup]; NULL in production */
+  void* debug_stamps;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */
 size_t bh_chain_lds_bytes(const bh_chain_params* p);
+/* the tile form's share of bh_chain_lds_bytes / bh_chain_i8 (tile != 0) */
+size_t bh_chain_tile_lds_bytes(const bh_chain_params* p);
+int bh_chain_tile_launch(const bh_chain_params* p, bh_stream_t s);
+/* the tile form's constant block: its size for these parameters (as if
+ * tile == 1; 0 if the form does not apply) and a device pass that builds it
+ * from the params' filter / table pointers into `blob` */
+size_t bh_chain_tile_blob_bytes(const bh_chain_params* p);
+int bh_chain_tile_pack(const bh_chain_params* p, void* blob, bh_stream_t s);
 int bh_chain_i8(const bh_chain_params* p, bh_stream_t s);
 
 /* MEAN over one contiguous run of axes (TFLite 2.9.2 reduce.cc EvalMean ->

@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist)
+    y, f = c.gpu(lib, px, waves, persist, tile)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -70,6 +70,65 @@ def test_chain_general(gpu_lib, args):
         _check(c, gpu_lib, 4, persist=1)
 
 
+def _tile_fits(c, lib):
+    import ctypes
+    keep = []
+    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, 4, keep, 4, 0, 1))) > 0
+
+
+@pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)
+def test_chain_tile_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
+    """the 2-D tile form (chain_tile_kernel): every MobileNetV2 chain whose
+    tile fits LDS, at batch 1 and 3 (ragged tiles at 7x7 / 14x14 / 28x28 /
+    56x56 edges are all 8-tile multiples only at 56 / 112)"""
+    for b in (1, 3):
+        rng = np.random.default_rng(h * 1000 + ce + cout + s + b)
+        c = ChainCase(rng, b, h, h, ce, s, cout, res, ce2)
+        if not _tile_fits(c, gpu_lib):
+            # LDS holds patch + both filters: the wide 14x14 / 7x7 chains
+            # stay with the raster forms
+            assert ce >= 384, "tile form should cover the %dx%dx%d chain" % (h, h, ce)
+            continue
+        _check(c, gpu_lib, 4, tile=1)
+        c.fast = False
+        _check(c, gpu_lib, 4, tile=1)
+
+
+@pytest.mark.parametrize("args", [
+    dict(b=2, h=112, w=112, ce=32, stride=1, cout=64, residual=False, ce2=0),      # MobileNetV1 pairs
+    dict(b=1, h=56, w=56, ce=128, stride=2, cout=256, residual=False, ce2=0),
+    dict(b=2, h=28, w=28, ce=256, stride=1, cout=256, residual=False, ce2=0),
+    dict(b=2, h=14, w=14, ce=192, stride=1, cout=64, residual=True, ce2=192, dil=2),  # dilated
+    dict(b=3, h=9, w=13, ce=48, stride=1, cout=24, residual=True, ce2=96),          # ragged tiles
+    dict(b=1, h=11, w=10, ce=64, stride=2, cout=40, residual=False, ce2=128),
+    dict(b=2, h=5, w=7, ce=16, stride=1, cout=8, residual=True, ce2=48),
+    dict(b=1, h=3, w=2, ce=16, stride=2, cout=4, residual=False, ce2=16),           # one partial tile
+    dict(b=1, h=28, w=28, ce=144, stride=1, cout=24, residual=False, ce2=144, store_pw1=True),
+    dict(b=1, h=20, w=20, ce=96, stride=1, cout=40, residual=True, ce2=320),         # pw2 K 320 (KX 5)
+    dict(b=24, h=56, w=56, ce=144, stride=1, cout=24, residual=True, ce2=144),       # a batch-24 pass
+    dict(b=24, h=112, w=112, ce=32, stride=1, cout=16, residual=False, ce2=96),
+])
+def test_chain_tile_general(gpu_lib, args):
+    rng = np.random.default_rng(7 + sum(v for v in args.values() if isinstance(v, int)))
+    c = ChainCase(rng, **args)
+    assert _tile_fits(c, gpu_lib)
+    _check(c, gpu_lib, 4, tile=1)
+
+
+def test_chain_tile_rejects(gpu_lib):
+    import ctypes
+    rng = np.random.default_rng(9)
+    keep = []
+    c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep, tile=1)
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
+    c.tile = 2  # no such form
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+    assert gpu_lib.bh_chain_i8(ctypes.byref(c), None) != 0
+    c.tile = 1
+    c.dw.stride_h = c.dw.stride_w = 3  # the tile's patch is sized for stride <= 2
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+
+
 def _persist_fits(c, lib):
     import ctypes
     keep = []
@@ -95,11 +154,11 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture
-def forcechain():
+@pytest.fixture(params=["forcechain", "forcetile"])
+def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
-    os.environ["BAND_HIP_FUSION"] = "forcechain"
-    yield
+    os.environ["BAND_HIP_FUSION"] = request.param
+    yield request.param
     if old is None:
         del os.environ["BAND_HIP_FUSION"]
     else:
@@ -120,7 +179,9 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
     assert ex.PrepareSubgraph(m).ok()
     key = SubgraphKey(41, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
-    assert "chain_kernel" in kernels, kernels
+    assert "chain_kernel" in kernels or "chain_tile_kernel" in kernels, kernels
+    if forcechain == "forcetile":
+        assert "chain_tile_kernel" in kernels, kernels
     for rep in range(2):  # eager, then graph replay
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
         assert ex.ExecuteSubgraph(key).ok()

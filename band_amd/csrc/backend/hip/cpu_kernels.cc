@@ -331,25 +331,40 @@ void CpuPool2D(const bh_pool_params& p, CpuPool& pool) {
 
 // ---- glue ops ---------------------------------------------------------------
 
-void CpuLutU8(const void* in, void* out, long n, const uint8_t* table) {
+// element-wise kernels split over the pool above this many elements
+constexpr long kParallelElems = 1 << 16;
+
+void CpuLutU8(const void* in, void* out, long n, const uint8_t* table, CpuPool& pool) {
   const uint8_t* s = static_cast<const uint8_t*>(in);
   uint8_t* d = static_cast<uint8_t*>(out);
-  for (long i = 0; i < n; ++i) d[i] = table[s[i]];
+  auto run = [&](long b, long e) {
+    for (long i = b; i < e; ++i) d[i] = table[s[i]];
+  };
+  if (n >= kParallelElems) pool.ParallelFor(n, run);
+  else run(0, n);
 }
 
-void CpuLutF32(const void* in, float* out, long n, const float* table) {
+void CpuLutF32(const void* in, float* out, long n, const float* table, CpuPool& pool) {
   const uint8_t* s = static_cast<const uint8_t*>(in);
-  for (long i = 0; i < n; ++i) out[i] = table[s[i]];
+  auto run = [&](long b, long e) {
+    for (long i = b; i < e; ++i) out[i] = table[s[i]];
+  };
+  if (n >= kParallelElems) pool.ParallelFor(n, run);
+  else run(0, n);
 }
 
 // quantize.cc AffineQuantize: round(x / scale) + zp, clamped
-void CpuQuantizeF32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed) {
+void CpuQuantizeF32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed, CpuPool& pool) {
   uint8_t* d = static_cast<uint8_t*>(out);
   const int32_t lo = out_signed ? -128 : 0, hi = out_signed ? 127 : 255;
-  for (long i = 0; i < n; ++i) {
-    const volatile float q = in[i] / scale;  // one IEEE division, no contraction
-    d[i] = static_cast<uint8_t>(Clamp(static_cast<int32_t>(std::round(static_cast<float>(q))) + zp, lo, hi));
-  }
+  auto run = [&](long b, long e) {
+    for (long i = b; i < e; ++i) {
+      const volatile float q = in[i] / scale;  // one IEEE division, no contraction
+      d[i] = static_cast<uint8_t>(Clamp(static_cast<int32_t>(std::round(static_cast<float>(q))) + zp, lo, hi));
+    }
+  };
+  if (n >= kParallelElems) pool.ParallelFor(n, run);
+  else run(0, n);
 }
 
 void CpuConcat(const bh_concat_params& p) {

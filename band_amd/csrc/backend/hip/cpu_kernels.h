@@ -53,9 +53,9 @@ void CpuDwConv(const bh_dwconv_params& p, CpuPool& pool);
 void CpuFc(const bh_fc_params& p, CpuPool& pool);
 void CpuEltwise(const bh_eltwise_params& p, CpuPool& pool);
 void CpuPool2D(const bh_pool_params& p, CpuPool& pool);
-void CpuLutU8(const void* in, void* out, long n, const uint8_t* table);
-void CpuLutF32(const void* in, float* out, long n, const float* table);
-void CpuQuantizeF32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed);
+void CpuLutU8(const void* in, void* out, long n, const uint8_t* table, CpuPool& pool);
+void CpuLutF32(const void* in, float* out, long n, const float* table, CpuPool& pool);
+void CpuQuantizeF32(const float* in, void* out, long n, float scale, int32_t zp, int out_signed, CpuPool& pool);
 void CpuConcat(const bh_concat_params& p);
 void CpuPad(const bh_pad_params& p);
 void CpuResizeNearest(const bh_resize_nearest_params& p);

@@ -43,7 +43,7 @@ PinnedBuffer::PinnedBuffer(size_t bytes, bool pinned) : bytes_(bytes), pinned_(p
   if (ptr_) std::memset(ptr_, 0, n / 64 * 64);
 }
 PinnedBuffer::~PinnedBuffer() {
-  if (!ptr_) return;
+  if (!ptr_ || !owned_) return;
   if (pinned_) bh_host_free(ptr_);
   else std::free(ptr_);
 }

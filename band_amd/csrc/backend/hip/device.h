@@ -51,6 +51,9 @@ class DeviceBlob {
 class PinnedBuffer {
  public:
   explicit PinnedBuffer(size_t bytes, bool pinned = true);
+  // a non-owning view of host memory someone else owns (a kCPU executor's
+  // boundary tensors alias its host arena: no copy in or out)
+  PinnedBuffer(char* external, size_t bytes) : ptr_(external), bytes_(bytes), pinned_(false), owned_(false) {}
   ~PinnedBuffer();
   PinnedBuffer(const PinnedBuffer&) = delete;
   PinnedBuffer& operator=(const PinnedBuffer&) = delete;
@@ -62,6 +65,7 @@ class PinnedBuffer {
   void* ptr_ = nullptr;
   size_t bytes_ = 0;
   bool pinned_ = true;
+  bool owned_ = true;
 };
 
 class DeviceRegistry {

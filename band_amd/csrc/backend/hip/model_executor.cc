@@ -569,6 +569,30 @@ absl::StatusOr<ModelSpec> HipModelExecutor::InvestigateModelSpec(interface::IMod
     }
     for (int i = 0; i < num_ops; ++i)
       if (!GpuSupports(d, d.ops[i], nullptr)) unsupported[flag].insert(i);
+    // Placement at a CPU-only boundary: a DEQUANTIZE whose every consumer
+    // only the CPU runs (TFLite_Detection_PostProcess's inputs) is declared
+    // unsupported here too, so the model analyzer puts it on the CPU side and
+    // the GPU -> CPU hand-off carries the 8-bit tensor instead of its float
+    // expansion (EfficientDet-Lite2's 37,629 x 90 class scores: 3.4 MB
+    // instead of 13.5 MB per job, copied four times on the way).  The
+    // outputs are the same (DEQUANTIZE is one exact table either side).
+    // BAND_HIP_CPU_BOUNDARY_DEQUANT=0 keeps every DEQUANTIZE on the GPU.
+    const char* bd = std::getenv("BAND_HIP_CPU_BOUNDARY_DEQUANT");
+    if (!(bd && bd[0] == '0')) {
+      std::vector<std::vector<int>> users(d.tensors.size());
+      for (int i = 0; i < num_ops; ++i)
+        for (int t : d.ops[i].inputs)
+          if (t >= 0) users[t].push_back(i);
+      for (int i = 0; i < num_ops; ++i) {
+        const TflOperator& op = d.ops[i];
+        if (op.builtin != kTflDequantize || op.outputs.empty() || op.outputs[0] < 0) continue;
+        const std::vector<int>& u = users[op.outputs[0]];
+        if (u.empty()) continue;
+        bool cpu_only = true;
+        for (int c : u) cpu_only &= unsupported[flag].count(c) > 0;
+        if (cpu_only && CpuSupports(d, op, nullptr)) unsupported[flag].insert(i);
+      }
+    }
   }
   for (int i = 0; i < num_ops; ++i)
     if (!CpuSupports(d, d.ops[i], nullptr)) unsupported[DeviceFlag::kCPU].insert(i);
@@ -2126,6 +2150,14 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
     for (const auto& kv : alias) sg->offset[kv.first] = sg->offset.at(kv.second);
     sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
     if (!sg->arena->ok()) return absl::InternalError("arena allocation failed");
+    if (cpu) {
+      // a host executor's boundary tensors ARE its arena slots (every tensor
+      // has its own slot): Band's copies land where the kernels read
+      char* arena = static_cast<char*>(sg->arena->ptr());
+      for (int t : sg->inputs) sg->host[t] = std::make_unique<PinnedBuffer>(arena + sg->offset.at(t), meta_[t]->bytes);
+      for (int t : sg->outputs)
+        sg->host[t] = std::make_unique<PinnedBuffer>(arena + sg->offset.at(t), meta_[t]->bytes);
+    }
     RETURN_STATUS_IF(BuildLaunches(*hm, sg.get()));
   } else {
     return absl::InternalError(std::string("Unsupported device type ") + ToString(device_flag_));
@@ -2290,7 +2322,12 @@ absl::Status HipModelExecutor::Enqueue(PreparedSubgraph* sg) {
 // kCPU worker: the same launch program over host memory (cpu_kernels.h)
 absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
   char* arena = static_cast<char*>(sg->arena->ptr());
-  for (int t : sg->inputs) std::memcpy(arena + sg->offset.at(t), sg->host.at(t)->data(), meta_[t]->bytes);
+  auto sync = [&](int t, bool in) {  // no copy when the mirror is the arena slot
+    char* slot = arena + sg->offset.at(t);
+    char* mirror = sg->host.at(t)->data();
+    if (slot != mirror) std::memcpy(in ? slot : mirror, in ? mirror : slot, meta_[t]->bytes);
+  };
+  for (int t : sg->inputs) sync(t, true);
   CpuPool& pool = *cpu_pool_;
   for (const Launch& l : sg->launches) {
     switch (l.kind) {
@@ -2302,12 +2339,12 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
       case Launch::kCopy:
         if (l.src != l.dst) std::memmove(l.dst, l.src, l.bytes);
         break;
-      case Launch::kLutU8: CpuLutU8(l.src, l.dst, l.count, static_cast<const uint8_t*>(l.table)); break;
+      case Launch::kLutU8: CpuLutU8(l.src, l.dst, l.count, static_cast<const uint8_t*>(l.table), pool); break;
       case Launch::kLutF32:
-        CpuLutF32(l.src, static_cast<float*>(l.dst), l.count, static_cast<const float*>(l.table));
+        CpuLutF32(l.src, static_cast<float*>(l.dst), l.count, static_cast<const float*>(l.table), pool);
         break;
       case Launch::kQuantF32:
-        CpuQuantizeF32(static_cast<const float*>(l.src), l.dst, l.count, l.q_scale, l.q_zp, l.q_signed);
+        CpuQuantizeF32(static_cast<const float*>(l.src), l.dst, l.count, l.q_scale, l.q_zp, l.q_signed, pool);
         break;
       case Launch::kConcat: CpuConcat(l.concat); break;
       case Launch::kPad: CpuPad(l.pad); break;
@@ -2331,8 +2368,8 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
       default: return absl::InternalError(std::string("no host implementation of ") + l.kernel);
     }
   }
-  for (int t : sg->outputs) std::memcpy(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes);
-  for (int t : sg->extra_d2h) std::memcpy(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes);
+  for (int t : sg->outputs) sync(t, false);
+  for (int t : sg->extra_d2h) sync(t, false);
   ++sg->runs;
   return absl::OkStatus();
 }

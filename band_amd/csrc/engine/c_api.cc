@@ -173,6 +173,7 @@ void BandAddConfig(BandConfigBuilder* b, int field, int count, ...) {
     case BAND_RESOURCE_MONITOR_INTERVAL_MS: (void)va_arg(vl, int); break;
     case BAND_RESOURCE_MONITOR_LOG_PATH: (void)va_arg(vl, const char*); break;
     case BANDX_WORKER_MAX_JOB_BATCH: c.worker_config.max_job_batch = va_arg(vl, int); break;
+    case BANDX_PROFILE_SHARE_IDENTICAL: c.profile_config.share_identical_workers = va_arg(vl, int) != 0; break;
     default: BAND_LOG(LogSeverity::kWarning, "unknown config field %d", field);
   }
   va_end(vl);

@@ -15,6 +15,10 @@ struct ProfileConfig {
   int num_runs = 1;
   std::string profile_data_path;
   float smoothing_factor = 0.1f;
+  // extension (BANDX_PROFILE_SHARE_IDENTICAL): workers of one device kind
+  // (same DeviceFlag, thread count and CPU mask) share their latency
+  // estimates - see LatencyEstimator::UpdateLatency
+  bool share_identical_workers = false;
 };
 
 struct PlannerConfig {

@@ -52,6 +52,7 @@ absl::Status Engine::Init(const RuntimeConfig& config) {
   }
   const bool global = planner_->GetWorkerType() == static_cast<int>(WorkerType::kGlobalQueue);
   max_job_batch_ = std::max(1, config.worker_config.max_job_batch);
+  rotate_ties_ = config.profile_config.share_identical_workers;
   for (DeviceFlag flag : config.worker_config.workers) {
     if (!valid.count(flag)) {
       BAND_LOG(LogSeverity::kWarning, "%s worker is not created (device unavailable)", ToString(flag));
@@ -590,11 +591,19 @@ std::pair<SubgraphKey, int64_t> Engine::GetShortestSubgraphKey(const std::vector
                                                                const WorkerWaitingTime& waiting) const {
   int64_t best = std::numeric_limits<int64_t>::max();
   SubgraphKey best_key;
-  for (const SubgraphKey& k : keys) {
+  // The reference keeps the LAST of equal totals (band/engine.cc:1158-1178).
+  // With shared estimates (share_identical_workers) identical idle workers
+  // tie exactly, so that rule sends every job to the highest worker id that
+  // is idle; ties then go round-robin instead (the scan starts one key later
+  // on every call and keeps the first minimum).
+  const size_t n = keys.size();
+  const size_t r0 = rotate_ties_ && n ? tie_rotation_.fetch_add(1, std::memory_order_relaxed) % n : 0;
+  for (size_t i = 0; i < n; ++i) {
+    const SubgraphKey& k = keys[(r0 + i) % n];
     auto it = waiting.find(k.GetWorkerId());
     const int64_t wait = it == waiting.end() ? 0 : it->second;
     const int64_t total = GetExpected(k) + std::max(wait, start_time);
-    if (best >= total) {
+    if (rotate_ties_ ? best > total : best >= total) {
       best = total;
       best_key = k;
     }

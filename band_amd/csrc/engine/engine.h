@@ -13,6 +13,7 @@
 //  * the model analyzer resolves op support by device flag (see
 //    model_analyzer.cc).
 #pragma once
+#include <atomic>
 #include <functional>
 #include <map>
 #include <memory>
@@ -145,6 +146,9 @@ class Engine : public IEngine {
 
   SubgraphConfig subgraph_config_;
   int max_job_batch_ = 1;
+  // share_identical_workers: equal expected latencies break round-robin
+  bool rotate_ties_ = false;
+  mutable std::atomic<size_t> tie_rotation_{0};
   using ViewFn = std::function<std::shared_ptr<interface::ITensorView>(int)>;
   absl::Status CopyInputs(const Job& job, const ViewFn& view);
   absl::Status CopyOutputs(const Job& job, const ViewFn& view);

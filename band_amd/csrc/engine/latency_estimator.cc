@@ -1,5 +1,6 @@
 #include "engine/latency_estimator.h"
 
+#include <algorithm>
 #include <cstdio>
 
 #include "engine/logger.h"
@@ -20,6 +21,7 @@ absl::Status LatencyEstimator::Init(const ProfileConfig& config) {
   profile_num_warmups_ = config.num_warmups;
   profile_num_runs_ = config.num_runs;
   profile_smoothing_factor_ = config.smoothing_factor;
+  share_identical_ = config.share_identical_workers;
   if (!profile_online_) {
     std::ifstream f(profile_data_path_);
     if (f) {
@@ -33,13 +35,45 @@ absl::Status LatencyEstimator::Init(const ProfileConfig& config) {
   return absl::OkStatus();
 }
 
-// EWMA with the configured smoothing factor (band/latency_estimator.cc:32-45)
+std::vector<WorkerId> LatencyEstimator::IdenticalWorkers(WorkerId w) const {
+  std::vector<WorkerId> out;
+  const Worker* a = engine_->GetWorker(w);
+  if (!a) return out;
+  for (WorkerId v = 0; v < static_cast<WorkerId>(engine_->GetNumWorkers()); ++v) {
+    const Worker* b = engine_->GetWorker(v);
+    if (b && b->GetDeviceFlag() == a->GetDeviceFlag() && b->GetNumThreads() == a->GetNumThreads() &&
+        b->GetWorkerThreadAffinity().GetCPUMaskFlag() == a->GetWorkerThreadAffinity().GetCPUMaskFlag())
+      out.push_back(v);
+  }
+  return out;
+}
+
+// EWMA with the configured smoothing factor (band/latency_estimator.cc:32-45).
+//
+// Extension (share_identical_workers): the reference keeps one estimate per
+// (subgraph, worker) and moves it only when that worker runs the subgraph.
+// Under shortest_expected_latency an idle worker is chosen by its estimate
+// alone, so among IDENTICAL workers the ones whose first profile happened to
+// read high are never chosen, never run, and their estimates never move:
+// they starve (r02 C5: three of eight GPU workers of one MI355X got 2, 8 and
+// 66 jobs against ~450-1150).  With sharing, a latency observed on one worker
+// updates the same subgraph on every worker of the same device kind.
 void LatencyEstimator::UpdateLatency(const SubgraphKey& key, int64_t latency) {
+  std::vector<WorkerId> peers;
+  if (share_identical_) peers = IdenticalWorkers(key.GetWorkerId());
   std::lock_guard<std::mutex> lock(mu_);
-  auto it = profile_database_.find(key);
-  if (it == profile_database_.end()) return;
-  it->second.moving_averaged = static_cast<int64_t>(profile_smoothing_factor_ * latency +
-                                                    (1 - profile_smoothing_factor_) * it->second.moving_averaged);
+  auto ewma = [&](const SubgraphKey& k) {
+    auto it = profile_database_.find(k);
+    if (it == profile_database_.end()) return;
+    it->second.moving_averaged = static_cast<int64_t>(profile_smoothing_factor_ * latency +
+                                                      (1 - profile_smoothing_factor_) * it->second.moving_averaged);
+  };
+  if (peers.empty()) {
+    ewma(key);
+    return;
+  }
+  const std::set<int> units = key.GetUnitIndicesSet();
+  for (WorkerId w : peers) ewma(SubgraphKey(key.GetModelId(), w, units));
 }
 
 // Online: pause each worker, let it drain, and time every subgraph of the
@@ -70,6 +104,27 @@ absl::Status LatencyEstimator::ProfileModel(ModelId model_id) {
       });
       profiler.join();
       worker->Resume();
+    }
+    if (share_identical_) {
+      // identical workers start from one estimate: the median of their
+      // profiles of each subgraph
+      std::lock_guard<std::mutex> lock(mu_);
+      std::map<std::pair<unsigned long long, WorkerId>, std::vector<int64_t>> groups;  // (units, first peer)
+      std::map<SubgraphKey, WorkerId> head;
+      for (const auto& kv : profile_database_) {
+        if (kv.first.GetModelId() != model_id) continue;
+        const std::vector<WorkerId> peers = IdenticalWorkers(kv.first.GetWorkerId());
+        const WorkerId h = peers.empty() ? kv.first.GetWorkerId() : peers.front();
+        head[kv.first] = h;
+        groups[{kv.first.GetUnitIndices().to_ullong(), h}].push_back(kv.second.moving_averaged);
+      }
+      for (auto& kv : groups) std::sort(kv.second.begin(), kv.second.end());
+      for (auto& kv : profile_database_) {
+        auto h = head.find(kv.first);
+        if (h == head.end()) continue;
+        const auto& v = groups[{kv.first.GetUnitIndices().to_ullong(), h->second}];
+        kv.second.moving_averaged = v[v.size() / 2];
+      }
     }
     engine_->Trigger();  // jobs bounced while the workers were paused
   } else if (const ModelSpec* spec = engine_->GetModelSpec(model_id)) {

@@ -43,6 +43,9 @@ class LatencyEstimator {
   float profile_smoothing_factor_ = 0.1f;
   std::string profile_data_path_;
   std::string profile_json_text_;
+  bool share_identical_ = false;
+  // workers of the same device kind as w (w included), for share_identical_
+  std::vector<WorkerId> IdenticalWorkers(WorkerId w) const;
 };
 
 }  // namespace band

@@ -102,9 +102,13 @@ def parse():
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
+    p.add_argument("--share-profiles", type=int, default=0, choices=[0, 1],
+                   help="BANDX_PROFILE_SHARE_IDENTICAL: identical workers share latency estimates (SEL / HEFT)")
     p.add_argument("--single-engine", action="store_true",
                    help="headline = one process, one Band engine, GPU workers over all --gpus GPUs")
     p.add_argument("--no-single-engine", action="store_true", help="N>1: skip the single-engine line")
+    p.add_argument("--single-engine-wpg", type=int, default=0,
+                   help="--single-engine: GPU workers per GPU (default --workers-per-gpu; 1 = one Worker per GPU)")
     p.add_argument("--profile-only", action="store_true",
                    help="run only the profiled batch passes (rocprofv3 traces); prints their per-kernel table")
     return p.parse_args()
@@ -191,19 +195,50 @@ class Dist:
 
 def host_cores():
     """host cores this process may use: its affinity set, capped by the
-    per-job CPU share the box grants (OMP_NUM_THREADS, 16 on the GPU box)"""
+    per-job CPU share the box grants (OMP_NUM_THREADS, 16 on the GPU box) and
+    by the container's cgroup CPU quota"""
     n = len(os.sched_getaffinity(0))
     try:
         cap = int(os.environ.get("OMP_NUM_THREADS", "0"))
     except ValueError:
         cap = 0
-    return min(n, cap) if cap > 0 else n
+    n = min(n, cap) if cap > 0 else n
+    quota, _ = cgroup_cpu_quota()
+    return max(1, min(n, int(quota))) if quota else n
+
+
+def cgroup_cpu_quota():
+    """the container's CPU quota in CPUs (cgroup v2 cpu.max, or v1
+    cpu.cfs_quota_us / cpu.cfs_period_us), None when unlimited or unknown"""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            return (None if q == "max" else round(int(q) / int(per), 2)), path
+        except (OSError, ValueError):
+            pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return (None if q < 0 else round(q / per, 2)), "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"
+    except (OSError, ValueError):
+        return None, None
+
+
+_START_AFFINITY = None
 
 
 def host_info():
     """nproc / lscpu facts of the host, read from /proc (no subprocess)"""
+    global _START_AFFINITY
+    if _START_AFFINITY is None:
+        _START_AFFINITY = os.sched_getaffinity(0)
+    quota, qsrc = cgroup_cpu_quota()
     info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)),
-            "omp_num_threads": os.environ.get("OMP_NUM_THREADS")}
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "cgroup_cpu_quota": quota, "cgroup_cpu_source": qsrc}
     try:
         with open("/proc/cpuinfo") as f:
             txt = f.read()
@@ -227,6 +262,11 @@ def cpu_baseline(args, models, paths, seconds):
     infrastructure, kept as a reference point)."""
     from band_amd import DeviceFlag
     from band_amd.engine import Engine, Model, SchedulerType, make_config
+    # the GPU path pins the threads that call it to the GPU's NUMA node
+    # (backend/hip/affinity.h); the CPU workers of this baseline are created
+    # from this thread, so it goes back to the process's starting CPU set
+    if _START_AFFINITY:
+        os.sched_setaffinity(0, _START_AFFINITY)
     T = host_cores()
     M = len(models)
     modes = []
@@ -279,7 +319,11 @@ def cpu_baseline(args, models, paths, seconds):
                 sample="Band engine kCPU workers (the product's host kernels), round_robin over %s 224x224 int8; "
                        "best of BASELINE.md modes (i) 1 worker x %d threads and (ii) %d workers x 1 thread, ~%.0f s "
                        "each; best: %s" % (names, T, T, seconds, best["mode"]),
-                modes=modes, oracle_scalar_port_1core=oracle, host=host_info())
+                modes=modes, oracle_scalar_port_1core=oracle, host=host_info(),
+                cores_reason="min(affinity, OMP_NUM_THREADS, cgroup quota): the GPU box grants each GPU job a "
+                             "16-CPU share (OMP_NUM_THREADS=16 there, and pools are to be sized to it), so BASELINE.md's "
+                             "'all physical cores' becomes the job's share; the host's own core count is reported "
+                             "beside it")
 
 
 def kernel_source_tag():
@@ -406,7 +450,8 @@ def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch, seed_offset
     engine = Engine(make_config([sched], workers,
                                 num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
                                 num_warmups=3, num_runs=5,
-                                max_job_batch=job_batch if job_batch > 1 else None))
+                                max_job_batch=job_batch if job_batch > 1 else None,
+                                share_identical=bool(args.share_profiles) if args.share_profiles else None))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + seed_offset)
     for path in paths:
@@ -552,7 +597,8 @@ def main():
     if args.single_engine:
         # headline: one process, one engine over all --gpus GPUs
         assert D.world == 1, "--single-engine runs in one process (no torchrun)"
-        single = single_engine_line(args, D, paths, sched, W, max(1, args.gpus), n_warm, n_timed)
+        single = single_engine_line(args, D, paths, sched, args.single_engine_wpg or W, max(1, args.gpus), n_warm,
+                                    n_timed)
         elapsed, lat_us, worker_ids = n_timed / single["value"], None, []
         jobs_per_worker = single["jobs_per_gpu"]
         subgraph_jobs = None
@@ -601,11 +647,16 @@ def main():
                   "p99_job_latency_ms": float(np.percentile(l1, 99))}
         e1.close()
 
-    # N > 1: the same C3 workload through ONE engine spanning every GPU
+    # N > 1: the same C3 workload through ONE engine spanning every GPU, with
+    # W workers per GPU and with one worker per GPU (north_star's "One Worker
+    # per GPU via worker_device_queue")
+    single_1wpg = None
     if D.world > 1 and not args.no_single_engine and not poisson and on_gpu:
         D.barrier()  # every rank has closed its engines
         if D.rank == 0:
             single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world)
+            if W != 1:
+                single_1wpg = single_engine_line(args, D, paths, sched, 1, D.world, n_warm, n_timed * D.world)
         D.barrier()
 
     roof, dev = None, None
@@ -647,6 +698,7 @@ def main():
                        "jobs_per_worker_rank0": jobs_per_worker,
                        "subgraph_jobs_per_worker_rank0": subgraph_jobs,
                        "max_job_batch": args.job_batch,
+                       "share_profiles": bool(args.share_profiles),
                        "model": args.model, "global_batch": n_ranks * W * max(1, args.job_batch), "seq_len": None,
                        "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus)) if args.single_engine
                        else "job-sharded x%d (no collective)" % n_ranks,
@@ -661,6 +713,7 @@ def main():
             "device_us_per_model": dev["device_us"] if dev else None,
             "band_one_job_per_pass": batch1,
             "single_engine": single,
+            "single_engine_one_worker_per_gpu": single_1wpg,
             "roofline": roof,
             "cpu_baseline": cpu,
             "host": dict(hinfo, node=platform.node()),

@@ -95,6 +95,9 @@ typedef enum BandConfigField {
   /* extension: a GPU device-queue worker runs up to this many queued
    * whole-model jobs of one model as one batched pass (default 1 = Band) */
   BANDX_WORKER_MAX_JOB_BATCH = 1000,
+  /* int: 1 = workers of one device kind (same device flag, thread count and
+   * CPU mask: e.g. several GPU workers of one node) share latency estimates */
+  BANDX_PROFILE_SHARE_IDENTICAL = 1001,
 } BandConfigField;
 
 typedef struct BandRequestOption {

@@ -125,6 +125,25 @@ def test_c4_efficientdet_lite2_448_heft(gpu_lib, tmp_path):
     e.close()
 
 
+def test_c4_boundary_dequantize_on_cpu(gpu_lib):
+    """the DEQUANTIZEs feeding TFLite_Detection_PostProcess are declared
+    unsupported on the GPU (the analyzer then keeps them on the CPU side and
+    the GPU -> CPU hand-off carries int8), every other DEQUANTIZE is not"""
+    from band_amd import HipModel, HipModelExecutor
+    buf = S.efficientdet_lite2(np.int8, size=448)
+    om = OModel(buf)
+    m = HipModel(3)
+    assert m.FromBuffer(buf).ok()
+    spec = HipModelExecutor(3, 1, DeviceFlag.kGPU).InvestigateModelSpec(m)
+    custom = [i for i, op in enumerate(om.operators) if op.builtin == 32]
+    assert custom and set(custom) <= spec.unsupported_ops[DeviceFlag.kGPU]
+    feeding = {i for i, op in enumerate(om.operators) if op.builtin == 6
+               and any(set(op.outputs) & set(om.operators[c].inputs) for c in custom)}
+    assert feeding and feeding <= spec.unsupported_ops[DeviceFlag.kGPU]
+    others = {i for i, op in enumerate(om.operators) if op.builtin == 6} - feeding
+    assert not (others & spec.unsupported_ops[DeviceFlag.kGPU])
+
+
 C5_MODELS = [("mobilenet_v1_int8", lambda: S.mobilenet_v1(np.int8)),
              ("mobilenet_v2_int8", lambda: S.mobilenet_v2(np.int8)),
              ("ssd_mobilenet_v2_int8", lambda: S.ssd_mobilenet_v2(np.int8)),

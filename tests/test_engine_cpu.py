@@ -390,3 +390,28 @@ def test_poisson_latency_counts_submission_delay(golden_dir):
     # latency grows with the submission index (each job waits for all before it)
     assert np.corrcoef(np.arange(len(lat)), lat)[0, 1] > 0.8
     e.close()
+
+
+def test_sel_shared_estimates_identical_workers(golden_dir):
+    """BANDX_PROFILE_SHARE_IDENTICAL: identical workers (same device flag,
+    thread count and CPU mask) start from one estimate (the median of their
+    profiles) and every observed latency moves all of them, so shortest
+    expected latency cannot starve a worker whose first profile read high;
+    without sharing each worker keeps its own estimate (the reference)."""
+    for share in (True, False):
+        e = Engine(make_config([SchedulerType.kShortestExpectedLatency], [DeviceFlag.kCPU] * 3,
+                               num_threads=[1, 1, 1], num_warmups=1, num_runs=3, share_identical=share))
+        m = Model()
+        assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+        assert e.RegisterModel(m)
+        t = e.CreateInputTensor(m, 0)
+        lat, wid, _ = e.RunClosedLoop([m], 600, 6, [t])
+        assert len(lat) == 600
+        subs = e.GetSubgraphs(m)
+        exp = {w: e.GetExpectedLatency(m, w, mask) for w, mask in subs}
+        if share:
+            assert len(set(exp.values())) == 1, exp  # one estimate for the three workers
+            counts = np.bincount(wid, minlength=3)
+            # equal estimates break round-robin: every worker near its share
+            assert (counts >= 0.5 * counts.mean()).all(), counts
+        e.close()

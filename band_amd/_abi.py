@@ -167,6 +167,7 @@ KERNEL_SYMBOLS = {
     "bh_memcpy_h2d_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bh_memcpy_d2h_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bh_memcpy_d2d_async": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
+    "bh_copy_d2d": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "bh_memset_async": (c_int, [c_void_p, c_int, c_size_t, c_void_p]),
     "bh_memcpy_h2d": (c_int, [c_void_p, c_void_p, c_size_t]),
     "bh_memcpy_d2h": (c_int, [c_void_p, c_void_p, c_size_t]),

@@ -4,6 +4,8 @@
 
 #include "backend/hip/quant.h"
 
+#include <pthread.h>
+
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -18,6 +20,7 @@ namespace hip {
 CpuPool::CpuPool(int num_threads, const std::vector<int>& cpus) {
   for (int i = 1; i < std::max(1, num_threads); ++i) {
     threads_.emplace_back([this, i] { Loop(i); });
+    pthread_setname_np(threads_.back().native_handle(), "band-cpupool");
     // the executor's CpuSet (affinity.h); pinned before the thread's first job
     if (!cpus.empty()) PinThread(threads_.back().native_handle(), cpus);
   }

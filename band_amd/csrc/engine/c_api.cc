@@ -1,6 +1,7 @@
 // Band C API over the native harness (band/c/c_api.cc restated; see
 // include/band_c_api.h for the contract).
 #include <pthread.h>
+#include <set>
 #include "band_c_api.h"
 
 #include <condition_variable>
@@ -427,57 +428,113 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
       out_ptrs[m].push_back(outs[m].back().get());
     }
   }
+  // Lanes: each lane is a submitter thread and a waiter thread over every
+  // lanes-th job.  One submitter copies every request into its model's ring
+  // (150 KB per 224x224 job): at ~55k jobs/s that one thread was the host
+  // ceiling of the C3 line (bench.py host_threads_timed: 0.99 of a core), as
+  // was one waiter copying DeepLab's 1 MB outputs out.  BANDX_DRIVER_LANES
+  // (default 4) sets the count; the in-flight bound and the per-model unread
+  // bound stay global.
+  int lanes = 4;
+  if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
+  lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
   std::mutex mu;
   std::condition_variable cv;
   struct Pending {
     int index, model;
     band::JobId id;
     int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
+    long seq;         // submission number within its model
   };
-  std::deque<Pending> pending;
+  std::vector<std::deque<Pending>> pending(lanes);
+  // each lane's waiter reads outputs into tensors of its own
+  std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> lane_outs(lanes);
+  std::vector<std::vector<band::Tensors>> lane_out_ptrs(lanes);
+  for (int l = 0; l < lanes; ++l) {
+    lane_outs[l].resize(n_models);
+    lane_out_ptrs[l].resize(n_models);
+    for (int m = 0; m < n_models; ++m) {
+      if (l == 0) {
+        lane_out_ptrs[l][m] = out_ptrs[m];
+        continue;
+      }
+      const band::ModelId id = models[m]->impl->GetId();
+      for (int t : e.GetOutputTensorIndices(id)) {
+        lane_outs[l][m].emplace_back(e.CreateTensor(id, t));
+        if (!lane_outs[l][m].back()) return kBandErr;
+        lane_out_ptrs[l][m].push_back(lane_outs[l][m].back().get());
+      }
+    }
+  }
+  // arrivals are drawn in job order (the open-loop schedule is one sequence)
+  std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
+  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
   int inflight = 0;
   std::vector<int> unread(n_models, 0), ring(n_models, 0);
   for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
+  // Lanes read out of submission order, so a model's unread COUNT no longer
+  // bounds how far its ring moves past its OLDEST unread request: a request
+  // of model m is submitted only while it is fewer than ring - lanes
+  // submissions ahead of that oldest one (the engine may hand concurrent
+  // submitters their ring handles in a different order, by at most lanes)
+  std::vector<long> next_seq(n_models, 0);
+  std::vector<std::set<long>> unread_seq(n_models);
   bool failed = false;
   const int64_t t0 = band::time::NowMicros();
-  std::thread waiter([&] {
-    pthread_setname_np(pthread_self(), "bandx-waiter");
-    for (int done = 0; done < n_jobs; ++done) {
-      std::unique_lock<std::mutex> l(mu);
-      cv.wait(l, [&] { return !pending.empty(); });
-      Pending item = pending.front();
-      pending.pop_front();
-      l.unlock();
-      absl::Status s = item.id >= 0 ? e.Wait(item.id, out_ptrs[item.model]) : absl::InternalError("submit");
-      band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
-      l.lock();
-      if (!s.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) failed = true;
-      if (latency_us)
-        latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
-      if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
-      if (model_index) model_index[item.index] = item.model;
-      --inflight;
-      --unread[item.model];
-      cv.notify_all();
-    }
-  });
-  for (int j = 0; j < n_jobs; ++j) {
-    const auto arrival = next_arrival(j);
-    const int64_t now = band::time::NowMicros() - t0;
-    if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
-    const int m = arrival.second;
-    {
-      std::unique_lock<std::mutex> l(mu);
-      cv.wait(l, [&] { return inflight < max_inflight && unread[m] < ring[m]; });
-      ++inflight;
-      ++unread[m];
-    }
-    auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
-    std::lock_guard<std::mutex> l(mu);
-    pending.push_back({j, m, id.ok() ? id.value() : -1, t0 + arrival.first});
-    cv.notify_all();
+  std::vector<std::thread> threads;
+  for (int l = 0; l < lanes; ++l) {
+    const int mine = n_jobs > l ? (n_jobs - 1 - l) / lanes + 1 : 0;
+    threads.emplace_back([&, l, mine] {
+      pthread_setname_np(pthread_self(), "bandx-waiter");
+      for (int done = 0; done < mine; ++done) {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !pending[l].empty(); });
+        Pending item = pending[l].front();
+        pending[l].pop_front();
+        lk.unlock();
+        absl::Status st =
+            item.id >= 0 ? e.Wait(item.id, lane_out_ptrs[l][item.model]) : absl::InternalError("submit");
+        band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
+        lk.lock();
+        if (!st.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) failed = true;
+        if (latency_us)
+          latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
+        if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
+        if (model_index) model_index[item.index] = item.model;
+        --inflight;
+        --unread[item.model];
+        unread_seq[item.model].erase(item.seq);
+        cv.notify_all();
+      }
+    });
+    threads.emplace_back([&, l] {
+      pthread_setname_np(pthread_self(), "bandx-submit");
+      for (int j = l; j < n_jobs; j += lanes) {
+        const auto& arrival = arrivals[j];
+        const int64_t now = band::time::NowMicros() - t0;
+        if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
+        const int m = arrival.second;
+        const long span = std::max(1, ring[m] - lanes);
+        long seq;
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] {
+            return inflight < max_inflight && unread[m] < ring[m] &&
+                   (unread_seq[m].empty() || next_seq[m] - *unread_seq[m].begin() < span);
+          });
+          ++inflight;
+          ++unread[m];
+          seq = next_seq[m]++;
+          unread_seq[m].insert(seq);
+        }
+        auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
+        std::lock_guard<std::mutex> lk(mu);
+        pending[l].push_back({j, m, id.ok() ? id.value() : -1, t0 + arrival.first, seq});
+        cv.notify_all();
+      }
+    });
   }
-  waiter.join();
+  for (auto& t : threads) t.join();
   if (wall_s) *wall_s = (band::time::NowMicros() - t0) * 1e-6;
   return failed ? kBandErr : kBandOk;
 }

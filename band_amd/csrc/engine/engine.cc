@@ -326,7 +326,7 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
           return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[k]));
         }
         jobs[k].input_handle = handle;
-        jobs[k].output_handle = model_output_buffer_.at(model_ids[k])->Alloc();
+        jobs[k].output_handle = model_output_buffer_.at(model_ids[k])->Claim(handle);
       }
     } else {
       j = jobs.size();  // requests without inputs (no ring slot)

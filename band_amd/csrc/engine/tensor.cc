@@ -95,6 +95,12 @@ int TensorRingBuffer::Alloc() {
   return head_++;
 }
 
+int TensorRingBuffer::Claim(int handle) {
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  if (handle + 1 > head_) head_ = handle + 1;
+  return handle;
+}
+
 int TensorRingBuffer::AllocBlocking() { return AllocBlockingN(1); }
 
 // Slots are handed out in handle order, so the n slots a call takes are the

@@ -62,6 +62,11 @@ class TensorRingBuffer {
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
                    int size = 128);
   int Alloc();
+  // takes `handle` itself (the head moves past it): a model's output slot
+  // uses its request's input handle, so the input ring's per-slot
+  // back-pressure also keeps the output handle inside this ring's window
+  // until the job has written it, whatever order concurrent callers finish in
+  int Claim(int handle);
   // Alloc() once the next slot's request (if any) is finished
   int AllocBlocking();
   // n consecutive handles at once (the first is returned), once those n

@@ -2,6 +2,7 @@
 // streams, pinned host memory, async copies, stream capture into hipGraphs
 // and events.  Every function returns 0 or the hipError_t it hit, and
 // records a message retrievable with bh_last_error().
+#include <algorithm>
 #include <stdio.h>
 #include <string.h>
 
@@ -91,6 +92,33 @@ extern "C" int bh_memcpy_h2d_async(void* d, const void* s, size_t n, bh_stream_t
 extern "C" int bh_memcpy_d2h_async(void* d, const void* s, size_t n, bh_stream_t st) {
   return n ? ck(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)st), "hipMemcpyAsync D2H") : 0;
 }
+// Device-to-device copy as an ordinary kernel: 16-byte vector copies where
+// both ends are 16-byte aligned, bytes otherwise.  The executor's in-graph
+// copies (kCopy launches) use this instead of hipMemcpyAsync D2D, whose
+// graph node is a runtime blit kernel: those blit nodes are what separated
+// the graphs rocprofv3 7.2's kernel tracer crashed on (SSD-MobileNetV2 at
+// batch 24) from the ones it traced.
+__global__ void bh_copy_kernel(unsigned char* __restrict__ d, const unsigned char* __restrict__ s, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  if ((((uintptr_t)d | (uintptr_t)s) & 15) == 0) {
+    const size_t n16 = n >> 4;
+    for (size_t k = i; k < n16; k += stride) ((uint4*)d)[k] = ((const uint4*)s)[k];
+    for (size_t k = (n16 << 4) + i; k < n; k += stride) d[k] = s[k];
+  } else {
+    for (size_t k = i; k < n; k += stride) d[k] = s[k];
+  }
+}
+
+extern "C" int bh_copy_d2d(void* d, const void* s, size_t n, bh_stream_t st) {
+  if (!n) return 0;
+  const size_t units = (n + 15) / 16;
+  const unsigned blocks = (unsigned)std::min<size_t>((units + 255) / 256, 4096);
+  BH_LAUNCH(bh_copy_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)st, (unsigned char*)d, (const unsigned char*)s,
+            n);
+  return bh_check_launch("bh_copy_kernel");
+}
+
 extern "C" int bh_memcpy_d2d_async(void* d, const void* s, size_t n, bh_stream_t st) {
   return n ? ck(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)st), "hipMemcpyAsync D2D") : 0;
 }

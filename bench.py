@@ -102,8 +102,10 @@ def parse():
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
-    p.add_argument("--share-profiles", type=int, default=0, choices=[0, 1],
-                   help="BANDX_PROFILE_SHARE_IDENTICAL: identical workers share latency estimates (SEL / HEFT)")
+    p.add_argument("--share-profiles", type=int, default=-1, choices=[-1, 0, 1],
+                   help="BANDX_PROFILE_SHARE_IDENTICAL: identical workers share latency estimates; -1 (default) = "
+                        "on for the latency-driven schedulers (SEL / HEFT: C4, C5), 0 = the reference's "
+                        "per-worker estimates")
     p.add_argument("--single-engine", action="store_true",
                    help="headline = one process, one Band engine, GPU workers over all --gpus GPUs")
     p.add_argument("--no-single-engine", action="store_true", help="N>1: skip the single-engine line")
@@ -451,7 +453,7 @@ def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch, seed_offset
                                 num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
                                 num_warmups=3, num_runs=5,
                                 max_job_batch=job_batch if job_batch > 1 else None,
-                                share_identical=bool(args.share_profiles) if args.share_profiles else None))
+                                share_identical=(args.share_profiles > 0) if args.share_profiles >= 0 else None))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + seed_offset)
     for path in paths:
@@ -495,14 +497,42 @@ def workload_label(args, models, n_cpu, W, poisson):
             % (args.model, edge, edge, args.scheduler, W))
 
 
+def thread_cpu():
+    """CPU seconds (user + system) of every thread of this process, keyed by
+    (tid, name): the engine names its threads band-planner, band-w<id> and
+    bandx-waiter; the closed-loop submitter is the calling (python) thread"""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open("/proc/self/task/%s/stat" % tid) as f:
+                raw = f.read()
+            st = raw.rsplit(")", 1)[1].split()
+            out[(tid, raw[raw.index("(") + 1:raw.rindex(")")])] = (int(st[11]) + int(st[12])) / tick
+        except (OSError, ValueError):
+            pass
+    return out
+
+
+HOST_THREADS = {}
+
+
 def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
-    """warm-up, barrier, exactly n_timed jobs, barrier; max over ranks"""
+    """warm-up, barrier, exactly n_timed jobs, barrier; max over ranks.  The
+    CPU share of each host thread over the timed loop goes to HOST_THREADS
+    (a thread near 1.0 is a host-side ceiling)"""
     engine.RunClosedLoop(band_models, n_warm, inflight, inputs)
     D.barrier()
+    c0 = thread_cpu()
     t0 = time.perf_counter()
     lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
     t1 = time.perf_counter()
+    c1 = thread_cpu()
     D.barrier()
+    busy = sorted((((c1[k] - c0.get(k, 0.0)) / (t1 - t0), k[1]) for k in c1), reverse=True)
+    HOST_THREADS.clear()
+    HOST_THREADS.update(busiest=[[n, round(b, 3)] for b, n in busy[:6]],
+                        process_cpu_cores=round(sum(b for b, _ in busy), 2))
     return D.max(t1 - t0), lat_us, worker_ids
 
 
@@ -584,6 +614,8 @@ def main():
         args.scheduler = "heterogeneous_earliest_finish_time"
     if not (on_gpu and n_cpu == 0 and args.scheduler == "round_robin"):
         args.job_batch = 1  # job batching applies to round_robin over GPU workers only
+    if args.share_profiles < 0:
+        args.share_profiles = int(args.scheduler in ("shortest_expected_latency", "heterogeneous_earliest_finish_time"))
     batching = args.job_batch > 1
     jps = max(M, args.jobs_per_step // M * M)
     args.jobs_per_step = jps
@@ -594,6 +626,7 @@ def main():
 
     poisson = None
     single = None
+    host_threads = None
     if args.single_engine:
         # headline: one process, one engine over all --gpus GPUs
         assert D.world == 1, "--single-engine runs in one process (no torchrun)"
@@ -625,6 +658,7 @@ def main():
             elapsed = D.max(t1 - t0)
         else:
             elapsed, lat_us, worker_ids = run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D)
+            host_threads = dict(HOST_THREADS)
         jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
         # every subgraph execution per worker (warm-up included): a split
         # model's GPU share is invisible in the last-subgraph counts above
@@ -717,6 +751,7 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "host": dict(hinfo, node=platform.node()),
+            "host_threads_timed": host_threads,
         }
         print(json.dumps(line), flush=True)
     for path in paths:

@@ -233,7 +233,9 @@ BAND_CAPI_EXPORT BandStatus BandxEngineRequestsAsync(BandEngine* engine, BandMod
  * (128), so no result is overwritten before it is read.
  * latency_us[j] = end - enqueue of job j (band/common.h:351-353);
  * worker_ids[j] = worker that ran its last subgraph (may be NULL);
- * *wall_s = submission of the first job to completion of the last. */
+ * *wall_s = submission of the first job to completion of the last.
+ * Jobs are submitted and read by BANDX_DRIVER_LANES (default 4) pairs of
+ * submitter / waiter threads, job j on lane j % lanes. */
 BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs,
                                                      int n_models, int n_jobs, int max_inflight, double* latency_us,
                                                      int* worker_ids, double* wall_s);

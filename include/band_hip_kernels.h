@@ -78,6 +78,8 @@ int bh_host_free(void* ptr);
 int bh_memcpy_h2d_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
 int bh_memcpy_d2h_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
 int bh_memcpy_d2d_async(void* dst, const void* src, size_t bytes, bh_stream_t s);
+/* the same copy as a kernel launch (bh_copy_kernel), not a runtime blit */
+int bh_copy_d2d(void* dst, const void* src, size_t bytes, bh_stream_t s);
 int bh_memset_async(void* dst, int value, size_t bytes, bh_stream_t s);
 int bh_memcpy_h2d(void* dst, const void* src, size_t bytes);
 int bh_memcpy_d2h(void* dst, const void* src, size_t bytes);

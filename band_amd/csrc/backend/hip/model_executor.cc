@@ -2255,7 +2255,17 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
     case Launch::kChain: rc = bh_chain_i8(&l.chain, stream_); break;
-    case Launch::kCopy: rc = l.src == l.dst ? 0 : bh_copy_d2d(l.dst, l.src, l.bytes, stream_); break;
+    case Launch::kCopy: {
+      // a kernel copy, not a blit: graphs replayed under rocprofv3's kernel
+      // trace crash on blit (memcpy) nodes; BAND_HIP_BLIT_COPY=1 restores them
+      static const bool blit = [] {
+        const char* v = std::getenv("BAND_HIP_BLIT_COPY");
+        return v && v[0] == '1';
+      }();
+      if (l.src != l.dst)
+        rc = blit ? bh_memcpy_d2d_async(l.dst, l.src, l.bytes, stream_) : bh_copy_d2d(l.dst, l.src, l.bytes, stream_);
+      break;
+    }
     case Launch::kLutU8: rc = bh_lut_u8(l.src, l.dst, l.count, l.table, stream_); break;
     case Launch::kLutF32:
       rc = bh_lut_f32(l.src, l.dst, l.count, static_cast<const float*>(l.table), stream_);

@@ -433,9 +433,11 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // (150 KB per 224x224 job): at ~55k jobs/s that one thread was the host
   // ceiling of the C3 line (bench.py host_threads_timed: 0.99 of a core), as
   // was one waiter copying DeepLab's 1 MB outputs out.  BANDX_DRIVER_LANES
-  // (default 4) sets the count; the in-flight bound and the per-model unread
-  // bound stay global.
-  int lanes = 4;
+  // sets the count (default 1: 4 and 8 lanes measured 55.7k / 55.0k against
+  // 59.7k inf/s with one, profiles/r03l_lanes*.json - the submitter was busy,
+  // not the bound); the in-flight bound and the per-model unread bound stay
+  // global.
+  int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
   lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
   std::mutex mu;
@@ -496,7 +498,12 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
             item.id >= 0 ? e.Wait(item.id, lane_out_ptrs[l][item.model]) : absl::InternalError("submit");
         band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
         lk.lock();
-        if (!st.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) failed = true;
+        if (!st.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) {
+          if (!failed)
+            BAND_LOG(band::LogSeverity::kError, "request driver: job %d (model %d, lane %d) failed: %s; record %d, status %s",
+                     item.id, item.model, l, std::string(st.message()).c_str(), j.job_id, band::ToString<band::JobStatus>(j.status));
+          failed = true;
+        }
         if (latency_us)
           latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
         if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
@@ -570,6 +577,14 @@ int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id) {
   if (!engine || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return -1;
   const band::Worker* w = engine->impl->GetWorker(worker_id);
   return w ? w->GetJobsRun() : -1;
+}
+
+int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int worker_id, int64_t out[4]) {
+  if (!engine || !out || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return -1;
+  const band::Worker* w = engine->impl->GetWorker(worker_id);
+  if (!w) return -1;
+  w->GetPhaseTimes(out);
+  return 0;
 }
 
 void BandxEngineWaitAll(BandEngine* engine) {

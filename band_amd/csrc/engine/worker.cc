@@ -131,12 +131,15 @@ void Worker::Work() {
         continue;
       }
     }
+    const int64_t t_in = time::NowMicros();
     if (engine_->TryCopyInputTensors(*job).ok()) {
       lock.lock();
       job->invoke_time = time::NowMicros();
       lock.unlock();
+      phase_us_[0].fetch_add(job->invoke_time - t_in, std::memory_order_relaxed);
       const absl::Status status = engine_->Invoke(key);
       job->end_time = time::NowMicros();
+      phase_us_[1].fetch_add(job->end_time - job->invoke_time, std::memory_order_relaxed);
       if (status.ok()) {
         engine_->UpdateLatency(key, job->end_time - job->invoke_time);
         if (!job->following_jobs.empty()) {
@@ -145,6 +148,7 @@ void Worker::Work() {
           engine_->EnqueueBatch(job->following_jobs, true);
         }
         const absl::Status out = engine_->TryCopyOutputTensors(*job);
+        phase_us_[2].fetch_add(time::NowMicros() - job->end_time, std::memory_order_relaxed);
         job->status = out.ok() ? JobStatus::kSuccess : JobStatus::kOutputCopyFailure;
         if (!out.ok()) BAND_LOG(LogSeverity::kWarning, "%s", out.message().c_str());
       } else {
@@ -157,6 +161,7 @@ void Worker::Work() {
       job->status = JobStatus::kInputCopyFailure;
     }
     jobs_run_.fetch_add(1, std::memory_order_relaxed);
+    phase_us_[3].fetch_add(1, std::memory_order_relaxed);
     engine_->EnqueueFinishedJob(*job);
     lock.lock();
     EndEnqueue();
@@ -176,6 +181,7 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   const int n = static_cast<int>(jobs.size());
   const SubgraphKey key = head->subgraph_key;
   std::vector<bool> copied(n, false);
+  const int64_t t_in = time::NowMicros();
   for (int i = 0; i < n; ++i) {
     copied[i] = engine_->TryCopyInputTensorsToSlot(*jobs[i], n, i).ok();
     if (!copied[i]) {
@@ -190,6 +196,8 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   }
   const absl::Status status = engine_->InvokeJobBatch(key, n);
   const int64_t end_time = time::NowMicros();
+  phase_us_[0].fetch_add(invoke_time - t_in, std::memory_order_relaxed);
+  phase_us_[1].fetch_add(end_time - invoke_time, std::memory_order_relaxed);
   for (int i = 0; i < n; ++i) {
     Job& j = *jobs[i];
     j.invoke_time = invoke_time;
@@ -207,6 +215,8 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
     BAND_LOG(LogSeverity::kError, "worker %d failed to invoke a batch of %d jobs: %s", worker_id_, n,
              status.message().c_str());
   jobs_run_.fetch_add(n, std::memory_order_relaxed);
+  phase_us_[2].fetch_add(time::NowMicros() - end_time, std::memory_order_relaxed);
+  phase_us_[3].fetch_add(1, std::memory_order_relaxed);
   for (int i = 1; i < n; ++i) engine_->EnqueueFinishedJob(*jobs[i]);
   engine_->EnqueueFinishedJob(*head);
   {

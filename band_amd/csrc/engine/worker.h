@@ -55,6 +55,12 @@ class Worker {
   bool IsIdleNow() const { return idle_.load(std::memory_order_acquire); }
   // subgraph executions finished by this worker (each job of a batched pass)
   int64_t GetJobsRun() const { return jobs_run_.load(std::memory_order_relaxed); }
+  // host time of the worker's job phases, microseconds since start:
+  // [0] input copies (request ring -> executor), [1] invoke (launch + sync),
+  // [2] output copies (executor -> output ring), [3] passes run
+  void GetPhaseTimes(int64_t out[4]) const {
+    for (int i = 0; i < 4; ++i) out[i] = phase_us_[i].load(std::memory_order_relaxed);
+  }
 
  protected:
   virtual Job* GetCurrentJob() = 0;
@@ -89,6 +95,7 @@ class Worker {
   // the availability changes
   std::atomic<bool> idle_{true};
   std::atomic<int64_t> jobs_run_{0};
+  std::atomic<int64_t> phase_us_[4] = {{0}, {0}, {0}, {0}};
   void RefreshIdle() {
     idle_.store(IsAvailable() && !HasJob() && partners_expected_us_ == 0, std::memory_order_release);
   }

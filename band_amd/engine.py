@@ -135,6 +135,7 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineGetExpectedLatency": (c_int64, [c_void_p, c_void_p, c_int, c_uint64]),
     "BandxEngineWaitAll": (None, [c_void_p]),
     "BandxEngineGetWorkerJobCount": (c_int64, [c_void_p, c_int]),
+    "BandxEngineGetWorkerPhaseTimes": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64)]),
     "BandxEngineRequestsAsync": (c_int, [c_void_p, POINTER(c_void_p), c_int, POINTER(c_void_p), POINTER(c_int)]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
@@ -395,6 +396,14 @@ class Engine:
         """subgraph executions worker `worker_id` has finished (each job of a
         batched pass counted once; a split model once per subgraph)"""
         return int(self.lib.BandxEngineGetWorkerJobCount(self.handle, int(worker_id)))
+
+    def GetWorkerPhaseTimes(self, worker_id):
+        """host microseconds worker `worker_id` spent copying inputs, invoking
+        (launch + sync) and copying outputs, and the passes it ran"""
+        out = (c_int64 * 4)()
+        if self.lib.BandxEngineGetWorkerPhaseTimes(self.handle, int(worker_id), out) != 0:
+            raise _abi.BandHipError("GetWorkerPhaseTimes: bad worker id %d" % worker_id)
+        return dict(copy_in_us=out[0], invoke_us=out[1], copy_out_us=out[2], passes=out[3])
 
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))

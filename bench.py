@@ -88,6 +88,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-roofline", action="store_true",
+                   help="skip the per-launch roofline / device-time profile (e.g. under a rocprofv3 trace)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=8.0, help="per CPU-baseline mode")
     p.add_argument("--profile-iters", type=int, default=20)
     p.add_argument("--scheduler", default="round_robin",
@@ -508,7 +510,10 @@ def thread_cpu():
             with open("/proc/self/task/%s/stat" % tid) as f:
                 raw = f.read()
             st = raw.rsplit(")", 1)[1].split()
-            out[(tid, raw[raw.index("(") + 1:raw.rindex(")")])] = (int(st[11]) + int(st[12])) / tick
+            name = raw[raw.index("(") + 1:raw.rindex(")")]
+            if int(tid) == os.getpid():
+                name += "(main)"  # unnamed runtime threads inherit the process name
+            out[(tid, name)] = (int(st[11]) + int(st[12])) / tick
         except (OSError, ValueError):
             pass
     return out
@@ -523,16 +528,31 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     (a thread near 1.0 is a host-side ceiling)"""
     engine.RunClosedLoop(band_models, n_warm, inflight, inputs)
     D.barrier()
+    n_workers = engine.GetNumWorkers()
+    p0 = [engine.GetWorkerPhaseTimes(w) for w in range(n_workers)]
     c0 = thread_cpu()
     t0 = time.perf_counter()
     lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
     t1 = time.perf_counter()
     c1 = thread_cpu()
+    p1 = [engine.GetWorkerPhaseTimes(w) for w in range(n_workers)]
     D.barrier()
     busy = sorted((((c1[k] - c0.get(k, 0.0)) / (t1 - t0), k[1]) for k in c1), reverse=True)
     HOST_THREADS.clear()
     HOST_THREADS.update(busiest=[[n, round(b, 3)] for b, n in busy[:6]],
                         process_cpu_cores=round(sum(b for b, _ in busy), 2))
+    # where the workers' wall time went over the timed loop (fractions of
+    # workers x wall): input copies, invoke (launch + device sync), output
+    # copies; the rest is waiting for work
+    ph = {k: sum(b[k] - a[k] for a, b in zip(p0, p1)) for k in p0[0]} if n_workers else {}
+    if ph.get("passes"):
+        wall_us = (t1 - t0) * 1e6 * n_workers
+        HOST_THREADS.update(worker_phases=dict(
+            copy_in=round(ph["copy_in_us"] / wall_us, 3), invoke=round(ph["invoke_us"] / wall_us, 3),
+            copy_out=round(ph["copy_out_us"] / wall_us, 3), passes=ph["passes"],
+            us_per_pass=dict(copy_in=round(ph["copy_in_us"] / ph["passes"], 1),
+                             invoke=round(ph["invoke_us"] / ph["passes"], 1),
+                             copy_out=round(ph["copy_out_us"] / ph["passes"], 1))))
     return D.max(t1 - t0), lat_us, worker_ids
 
 
@@ -694,7 +714,7 @@ def main():
         D.barrier()
 
     roof, dev = None, None
-    if on_gpu and D.rank == 0:
+    if on_gpu and D.rank == 0 and not args.no_roofline:
         roof, dev, _ = profile_roofline(args, D, models, paths)
 
     cpu = None

@@ -217,6 +217,12 @@ BAND_CAPI_EXPORT void BandxEngineWaitAll(BandEngine* engine);
  * engine started, each job of a batched pass counted once; -1 for a bad id.
  * A model split over workers counts once per subgraph on each worker. */
 BAND_CAPI_EXPORT int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id);
+/* host time of worker `worker_id`'s job phases since the engine started:
+ * out[0] input copies (request ring -> executor), out[1] invoke (launch +
+ * device sync), out[2] output copies (executor -> output ring), all in
+ * microseconds, and out[3] the passes run (a batched pass counts once).
+ * Returns 0, or -1 for a bad id. */
+BAND_CAPI_EXPORT int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int worker_id, int64_t out[4]);
 /* One RequestAsync call for n requests (band/engine.cc:455-529, the batched
  * overload Band's own benchmark tool uses): request i runs models[i] on the
  * input tensors inputs[i] (that model's inputs, in order).  handles[i]

@@ -70,6 +70,11 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   }
   const char* g = std::getenv("BAND_HIP_GRAPH");
   if (g && g[0] == '0') use_graph_ = false;
+  if (const char* io = std::getenv("BAND_HIP_IO")) {
+    const std::string m(io);
+    io_mode_ = m == "graph" ? 0 : m == "stream" ? 1 : 2;
+  }
+  if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
 }
 
 HipModelExecutor::~HipModelExecutor() {
@@ -2311,13 +2316,48 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
   return rc ? HipErr(rc, l.kernel) : absl::OkStatus();
 }
 
+// diagnostics only (tools/concurrency_probe.py --no-io): kernels without
+// the host copies, to separate device compute scaling from the transfers
+static bool ProbeNoIo() {
+  static const bool v = [] {
+    const char* e = std::getenv("BAND_HIP_PROBE_NO_IO");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 absl::Status HipModelExecutor::Enqueue(PreparedSubgraph* sg) {
+  RETURN_STATUS_IF(EnqueueInputs(sg));
+  RETURN_STATUS_IF(EnqueueLaunches(sg));
+  return EnqueueOutputs(sg);
+}
+
+absl::Status HipModelExecutor::EnqueueLaunches(PreparedSubgraph* sg) {
+  for (const Launch& l : sg->launches) RETURN_STATUS_IF(EnqueueLaunch(l));
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::EnqueuePass(PreparedSubgraph* sg) {
+  if (!use_graph_ || !sg->graph) return Enqueue(sg);
+  if (!sg->io_in_graph) RETURN_STATUS_IF(EnqueueInputs(sg));
+  const int rc = bh_graph_launch(sg->graph, stream_);
+  if (rc) return HipErr(rc, "graph launch");
+  return sg->io_in_graph ? absl::OkStatus() : EnqueueOutputs(sg);
+}
+
+absl::Status HipModelExecutor::EnqueueInputs(PreparedSubgraph* sg) {
+  if (ProbeNoIo()) return absl::OkStatus();
   char* arena = static_cast<char*>(sg->arena->ptr());
   for (int t : sg->inputs) {
     int rc = bh_memcpy_h2d_async(arena + sg->offset.at(t), sg->host.at(t)->data(), meta_[t]->bytes, stream_);
     if (rc) return HipErr(rc, "H2D input");
   }
-  for (const Launch& l : sg->launches) RETURN_STATUS_IF(EnqueueLaunch(l));
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::EnqueueOutputs(PreparedSubgraph* sg) {
+  if (ProbeNoIo()) return absl::OkStatus();
+  char* arena = static_cast<char*>(sg->arena->ptr());
   for (int t : sg->outputs) {
     int rc = bh_memcpy_d2h_async(sg->host.at(t)->data(), arena + sg->offset.at(t), meta_[t]->bytes, stream_);
     if (rc) return HipErr(rc, "D2H output");
@@ -2396,19 +2436,19 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (use_graph_ && !sg->graph && sg->runs > 0) {
     rc = bh_capture_begin(stream_);
     if (rc) return HipErr(rc, "capture begin");
-    absl::Status s = Enqueue(sg);
+    size_t io_bytes = 0;
+    for (int t : sg->inputs) io_bytes += meta_[t]->bytes;
+    for (int t : sg->outputs) io_bytes += meta_[t]->bytes;
+    for (int t : sg->extra_d2h) io_bytes += meta_[t]->bytes;
+    sg->io_in_graph = io_mode_ == 0 || (io_mode_ == 2 && io_bytes < io_stream_bytes_);
+    absl::Status s = sg->io_in_graph ? Enqueue(sg) : EnqueueLaunches(sg);
     bh_graph_exec_t g = nullptr;
     rc = bh_capture_end(stream_, &g);
     if (!s.ok()) return s;
     if (rc) return HipErr(rc, "capture end");
     sg->graph = g;
   }
-  if (use_graph_ && sg->graph) {
-    rc = bh_graph_launch(sg->graph, stream_);
-    if (rc) return HipErr(rc, "graph launch");
-  } else {
-    RETURN_STATUS_IF(Enqueue(sg));
-  }
+  RETURN_STATUS_IF(EnqueuePass(sg));
   rc = bh_stream_sync(stream_);
   if (rc) return HipErr(rc, "stream sync");
   ++sg->runs;
@@ -2438,6 +2478,8 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
     v.exec = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
                                                 num_threads_);
     v.exec->use_graph_ = use_graph_;
+    v.exec->io_mode_ = io_mode_;
+    v.exec->io_stream_bytes_ = io_stream_bytes_;
     // the base subgraph's op set (a whole-model key prepares all ops)
     RETURN_STATUS_IF(v.exec->PrepareSubgraph(v.model.get(), ops, units));
     PreparedSubgraph* vs = v.exec->Find(key);
@@ -2504,12 +2546,7 @@ absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, d
   for (int i = 0; i < iters && status.ok(); ++i) {
     if (i >= kDepth && bh_event_sync(ring[i % kDepth]) != 0) status = HipErr(1, "event sync");
     if (!status.ok()) break;
-    if (use_graph_ && sg->graph) {
-      const int rc = bh_graph_launch(sg->graph, stream_);
-      if (rc) status = HipErr(rc, "graph launch");
-    } else {
-      status = Enqueue(sg);
-    }
+    status = EnqueuePass(sg);
     bh_event_record(ring[i % kDepth], stream_);
   }
   bh_event_record(e1, stream_);

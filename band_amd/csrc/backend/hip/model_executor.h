@@ -103,6 +103,7 @@ struct PreparedSubgraph {
   std::vector<Launch> launches;
   std::vector<std::shared_ptr<DeviceBlob>> consts;
   bh_graph_exec_t graph = nullptr;
+  bool io_in_graph = true;  // the graph holds the host copies (set at capture)
   int runs = 0;
 };
 
@@ -185,6 +186,13 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   absl::Status LowerGlue(const HipModel& model, int op_index, void* in_ptr, void* out_ptr, const std::string& ckey,
                          PreparedSubgraph* sg, Launch* l);
   absl::Status Enqueue(PreparedSubgraph* sg);
+  // Enqueue's three parts: host->device inputs, the launches, device->host
+  // outputs (and intermediates a later subgraph reads)
+  absl::Status EnqueueInputs(PreparedSubgraph* sg);
+  absl::Status EnqueueLaunches(PreparedSubgraph* sg);
+  absl::Status EnqueueOutputs(PreparedSubgraph* sg);
+  // one pass: the graph (captured on first use) or the eager launches
+  absl::Status EnqueuePass(PreparedSubgraph* sg);
   absl::Status ExecuteOnHost(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
 
@@ -214,6 +222,14 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bh_stream_t stream_ = nullptr;
   std::unique_ptr<CpuPool> cpu_pool_;  // kCPU executors
   bool use_graph_ = true;
+  // Where a graph pass's host copies go: captured into the graph (blit
+  // kernels on the compute queue; lowest latency for small transfers) or
+  // issued on the stream around a kernels-only graph (DMA engines, leaving
+  // the CUs to the kernels of concurrent passes).  BAND_HIP_IO = graph |
+  // stream | auto (default: stream from io_stream_bytes_ of host I/O per
+  // pass, BAND_HIP_IO_STREAM_BYTES)
+  int io_mode_ = 2;  // 0 graph, 1 stream, 2 auto
+  size_t io_stream_bytes_ = 512 << 10;
   static const std::vector<int> kEmpty;
 };
 

@@ -7,6 +7,7 @@ than S = 1, the passes compete for one device resource; if it scales, the
 engine-level line is bound elsewhere (host side, copies, queue mapping).
 
 usage: python3 tools/concurrency_probe.py [--model mobilenet_v2] [--batch 24] [--streams 1,2,4,8] [--iters 100]
+       [--no-io]
        (--model mix: each stream replays the four C3 models in turn)"""
 import argparse
 import os
@@ -24,7 +25,10 @@ def main():
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--streams", default="1,2,4,8")
     ap.add_argument("--iters", type=int, default=100)
+    ap.add_argument("--no-io", action="store_true", help="kernels only: no H2D / D2H in the passes (diagnostic)")
     a = ap.parse_args()
+    if a.no_io:
+        os.environ["BAND_HIP_PROBE_NO_IO"] = "1"
     import numpy as np
     from band_amd import DeviceFlag, HipModel, HipModelExecutor, SetWorkerDevice, SubgraphKey
     from band_amd import tflite_synth as S

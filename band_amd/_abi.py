@@ -81,7 +81,7 @@ class MeanParams(ctypes.Structure):
 class ChainParams(ctypes.Structure):
     _fields_ = [("dw", DwConvParams), ("pw1", ConvParams), ("pw2", ConvParams), ("has_pw2", c_int),
                 ("px_blocks", c_int), ("waves", c_int), ("persist", c_int), ("tile", c_int),
-                ("tile_blob", c_void_p), ("debug_stamps", c_void_p)]
+                ("tile_blob", c_void_p), ("debug_stamps", c_void_p), ("deep", c_int)]
 
 
 # symbol -> (restype, argtypes)
@@ -176,6 +176,7 @@ KERNEL_SYMBOLS = {
     "bh_graph_launch": (c_int, [c_void_p, c_void_p]),
     "bh_graph_destroy": (c_int, [c_void_p]),
     "bh_event_create": (c_int, [ctypes.POINTER(c_void_p)]),
+    "bh_event_create_blocking": (c_int, [ctypes.POINTER(c_void_p)]),
     "bh_event_destroy": (c_int, [c_void_p]),
     "bh_event_record": (c_int, [c_void_p, c_void_p]),
     "bh_event_sync": (c_int, [c_void_p]),

@@ -75,6 +75,7 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
     io_mode_ = m == "graph" ? 0 : m == "stream" ? 1 : 2;
   }
   if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
+  if (const char* sy = std::getenv("BAND_HIP_SYNC")) block_sync_ = std::string(sy) == "block";
 }
 
 HipModelExecutor::~HipModelExecutor() {
@@ -83,6 +84,7 @@ HipModelExecutor::~HipModelExecutor() {
     if (stream_) bh_stream_sync(stream_);
     for (auto& kv : subgraphs_)
       if (kv.second->graph) bh_graph_destroy(kv.second->graph);
+    if (done_event_) bh_event_destroy(done_event_);
   }
   subgraphs_.clear();
 }
@@ -533,6 +535,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
   if (f && std::strcmp(f, "forcetile") == 0) force_chain_ = force_tile_chain_ = true;  // ... in the tile form
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
+  if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
+  if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
@@ -1046,7 +1050,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 3;
+constexpr int kChainTuneVersion = 4;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1315,6 +1319,12 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       q.tile = 1;
       if (bh_chain_lds_bytes(&q) > 0) choice += 400;
     }
+    if (force_deep_chain_) {
+      bh_chain_params q = ok3 ? c3 : c2;
+      q.px_blocks = 1;
+      q.deep = 1;
+      choice = bh_chain_lds_bytes(&q) > 0 ? (ok3 ? 1001 : 1011) : (ok3 ? 4 : 14);
+    }
     if (autotune_ && choice < 0) {
       std::lock_guard<std::mutex> lk(g_tune_mu);
       LoadTuneFileLocked();
@@ -1336,10 +1346,13 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // {px_blocks, waves, persist}: the last is the persistent form
         // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
         // {.., tile}: the 2-D tile form (8 x 8 pixels, one LDS-DMA burst)
-        const int forms[7][4] = {{4, 4, 0, 0}, {2, 4, 0, 0}, {1, 4, 0, 0}, {1, 8, 0, 0},
-                                 {1, 16, 0, 0}, {4, 4, 1, 0}, {4, 4, 0, 1}};
+        // {.., deep}: the deep-issue raster forms
+        const int forms[10][5] = {{4, 4, 0, 0, 0}, {2, 4, 0, 0, 0}, {1, 4, 0, 0, 0}, {1, 8, 0, 0, 0},
+                                  {1, 16, 0, 0, 0}, {4, 4, 1, 0, 0}, {4, 4, 0, 1, 0}, {2, 4, 0, 0, 1},
+                                  {1, 4, 0, 0, 1}, {1, 8, 0, 0, 1}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
+          if (pw[4] && no_deep_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;
@@ -1347,6 +1360,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             q.waves = pw[1];
             q.persist = pw[2];
             q.tile = pw[3];
+            q.deep = pw[4];
             if (bh_chain_lds_bytes(&q) == 0) continue;
             if (q.tile && !PackChainTile(&q, sg)) continue;
             Launch F;
@@ -1357,7 +1371,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0) + (pw[3] ? 400 : 0);
+                       (pw[2] ? 200 : 0) + (pw[3] ? 400 : 0) + (pw[4] ? 1000 : 0);
             }
           }
         }
@@ -1370,7 +1384,10 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       }
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
-    // +200 for the persistent form, +300 for 8 waves, +400 for the tile form
+    // +200 for the persistent form, +300 for 8 waves, +400 for the tile
+    // form, +1000 for the deep-issue form
+    const int deep = choice >= 1000 ? 1 : 0;
+    choice %= 1000;
     const bool three = choice > 0 && choice % 100 < 10;
     if (choice == 0 || (three && !ok3) || (!three && !ok2)) {
       out.push_back(L[i]);
@@ -1384,6 +1401,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.waves = choice >= 300 && choice < 400 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
     F.chain.tile = choice >= 400 && choice < 500 ? 1 : 0;
+    F.chain.deep = deep;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then
     if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {
@@ -2449,7 +2467,13 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
     sg->graph = g;
   }
   RETURN_STATUS_IF(EnqueuePass(sg));
-  rc = bh_stream_sync(stream_);
+  if (block_sync_) {
+    if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
+    rc = bh_event_record(done_event_, stream_);
+    if (!rc) rc = bh_event_sync(done_event_);
+  } else {
+    rc = bh_stream_sync(stream_);
+  }
   if (rc) return HipErr(rc, "stream sync");
   ++sg->runs;
   return absl::OkStatus();
@@ -2479,6 +2503,7 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
                                                 num_threads_);
     v.exec->use_graph_ = use_graph_;
     v.exec->io_mode_ = io_mode_;
+    v.exec->block_sync_ = block_sync_;
     v.exec->io_stream_bytes_ = io_stream_bytes_;
     // the base subgraph's op set (a whole-model key prepares all ops)
     RETURN_STATUS_IF(v.exec->PrepareSubgraph(v.model.get(), ops, units));

@@ -216,6 +216,8 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
   bool force_tile_chain_ = false;  // BAND_HIP_FUSION=forcetile: every feasible chain in the tile form
   bool no_tile_chain_ = false;     // BAND_HIP_FUSION=notile: the tuner skips the tile form
+  bool no_deep_chain_ = false;     // BAND_HIP_FUSION=nodeep: the tuner skips the deep-issue forms
+  bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;
@@ -229,6 +231,11 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   // stream | auto (default: stream from io_stream_bytes_ of host I/O per
   // pass, BAND_HIP_IO_STREAM_BYTES)
   int io_mode_ = 2;  // 0 graph, 1 stream, 2 auto
+  // BAND_HIP_SYNC=block: ExecuteSubgraph waits on a blocking-sync event
+  // (the worker thread sleeps until the GPU's interrupt) instead of spinning
+  // in hipStreamSynchronize - frees a core per GPU worker
+  bool block_sync_ = false;
+  bh_event_t done_event_ = nullptr;
   size_t io_stream_bytes_ = 512 << 10;
   static const std::vector<int> kEmpty;
 };

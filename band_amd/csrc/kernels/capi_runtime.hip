@@ -158,6 +158,14 @@ extern "C" int bh_event_create(bh_event_t* ev) {
   *ev = (bh_event_t)e;
   return rc;
 }
+// an event whose hipEventSynchronize sleeps on the completion interrupt
+// instead of spinning the calling thread (no timing)
+extern "C" int bh_event_create_blocking(bh_event_t* ev) {
+  hipEvent_t e = nullptr;
+  int rc = ck(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming), "hipEventCreateWithFlags");
+  *ev = (bh_event_t)e;
+  return rc;
+}
 extern "C" int bh_event_destroy(bh_event_t ev) { return ck(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy"); }
 extern "C" int bh_event_record(bh_event_t ev, bh_stream_t s) {
   return ck(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord");

@@ -418,9 +418,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_con
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   constexpr int ROWS = BM + BN;  // 64-byte rows staged per K-step
-  static_assert(ROWS % (16 * W) == 0, "whole staging instructions per wave");
-  constexpr int NI = ROWS / (16 * W);  // glds instructions per wave per K-step (16 rows each)
-  constexpr int STAGE = ROWS * 64;
+  // glds instructions per wave per K-step (16 rows each); when ROWS is not a
+  // multiple of 16 * W the last instruction of some waves stages padding rows
+  // (a valid filter row into LDS nobody reads), so every wave issues NI and
+  // the counted vmcnt waits stay uniform
+  constexpr int NI = (ROWS + 16 * W - 1) / (16 * W);
+  constexpr int STAGE = NI * 16 * W * 64;
   constexpr int D = NB - 1;  // K-steps staged ahead of the one computed
   __shared__ __attribute__((aligned(16))) uint8_t lds[NB * STAGE];
   const int lane = threadIdx.x & 63;
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_con
       src[j] = (const uint8_t*)p.input + (long)m * K + 16 * g;
       kval[j] = K - 16 * g;
     } else {
-      const int n = min(tn0 + row - BM, p.n_pad - 1);
+      const int n = min(min(tn0 + row - BM, tn0 + BN - 1), p.n_pad - 1);  // padding rows: the tile's last
       src[j] = (const uint8_t*)p.weights + (long)n * p.k_pad + 16 * g;
       kval[j] = 0x7fffffff;
     }
@@ -549,7 +552,10 @@ static int launch_shape(const bh_conv_params& p, int M, int K, int N, hipStream_
 // still give one workgroup per CU - PoseNet's 512/1024-channel layers, 1.6-2.7x
 // conv_mfma_kernel; otherwise 64x64 tiles over 8 waves (16x32 each, 3 LDS
 // buffers), which keep ~4 waves per SIMD on the mid-size layers.
-// BH_GEMM_CFG=1 selects the first 4-wave form (128x128 ... 64x64, 4 buffers).
+// BH_GEMM_CFG=1 selects the first 4-wave form (128x128 ... 64x64, 4 buffers);
+// 5: the two-tile rule without the 160-row tile.  Deeper LDS rings (3-4
+// K-steps ahead) and 4-wave 128x64 tiles measured no faster
+// (profiles/r03y_gemm.txt).
 static int launch_gemm_shape(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const int N = p.out_c;
   static const int cfg = [] {
@@ -562,7 +568,15 @@ static int launch_gemm_shape(const bh_conv_params& p, int M, int K, hipStream_t 
     if (wgs(M, N, 64, 128) >= 256) return launch_gemm<2, 4, 2, 2, 4>(p, M, K, s);
     return launch_gemm<2, 2, 2, 2, 4>(p, M, K, s);
   }
-  if (wgs(M, N, 128, 128) >= 256) return launch_gemm<4, 2, 2, 4, 2>(p, M, K, s);
+  // 128 x 128 tiles over 8 waves once they give a workgroup per CU; when
+  // they give more than one round of workgroups but 160 x 128 tiles fit in
+  // one, those (8 waves, 64 B of padding rows per wave staged per K-step).
+  // BH_GEMM_CFG=5: without the 160-row tile.  (4-wave 160 x 128 / 80 x 128
+  // tiles measured slower than two rounds of 8-wave ones:
+  // profiles/r03z_gemm.txt.)
+  const long w128 = wgs(M, N, 128, 128);
+  if (cfg != 5 && w128 > 256 && wgs(M, N, 160, 128) <= 256) return launch_gemm<5, 2, 2, 4, 2>(p, M, K, s);
+  if (w128 >= 256) return launch_gemm<4, 2, 2, 4, 2>(p, M, K, s);
   return launch_gemm<1, 2, 4, 2, 3>(p, M, K, s);
 }
 

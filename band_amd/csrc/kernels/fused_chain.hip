@@ -164,65 +164,68 @@ __device__ __forceinline__ void copy_out(const unsigned char* src, uint8_t* dst,
 // staging tiles as bytes (no packing); the HBM stores stay the contiguous
 // 16-byte copy_out.  The operand fragments are the same bytes as the
 // transposed form's: only the MFMA operand order changes.
+template <int KB = 4>
 __device__ __forceinline__ v4i gemm_tile_nt(const bh_conv_params& c, const unsigned char* xrow, int t, int KS,
                                             int r16, int g) {
   const int8_t* wrow = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
   const int n = t * 16 + r16;
   const int be = c.bias_eff[n < c.out_c ? n : 0];
   v4i acc = (v4i){be, be, be, be};
-  int k = 0;
-  for (; k + 8 <= KS; k += 8) {
-    v4i w[8], x[8];
+  // KB K-steps' filter fragments are issued before any of their MFMAs (a
+  // ragged last batch included): K <= 64 * KB costs one L2 round trip
+  // instead of one per K-step
+  for (int k = 0; k < KS; k += KB) {
+    v4i w[KB], x[KB];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      w[u] = *(const v4i*)(wrow + (k + u) * 64);
-      x[u] = *(const v4i*)(xrow + (k + u) * 64);
-    }
+    for (int u = 0; u < KB; ++u)
+      if (k + u < KS) {
+        w[u] = *(const v4i*)(wrow + (k + u) * 64);
+        x[u] = *(const v4i*)(xrow + (k + u) * 64);
+      }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[u], w[u], acc, 0, 0, 0);
-  }
-  for (; k < KS; ++k) {
-    const v4i w = *(const v4i*)(wrow + k * 64);
-    const v4i x = *(const v4i*)(xrow + k * 64);
-    acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(x, w, acc, 0, 0, 0);
+    for (int u = 0; u < KB; ++u)
+      if (k + u < KS) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[u], w[u], acc, 0, 0, 0);
   }
   return acc;
 }
 
-// x-stationary form of gemm_tile_nt for K <= 64 * KMAX, two channel tiles
-// per memory round trip; epi(t, n, acc, mult, shift) finishes a tile for
-// this lane's channel n (may be >= out_c).
-template <int KMAX, typename Epi>
+// x-stationary form of gemm_tile_nt for K <= 64 * KMAX: TT channel tiles
+// per memory round trip (every tile's filter fragments and epilogue
+// operands issued before their MFMAs); epi(t, n, acc, mult, shift)
+// finishes a tile for this lane's channel n (may be >= out_c).
+template <int KMAX, int TT = 2, typename Epi>
 __device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsigned char* xrow, int KS, int t0,
                                            int tstep, int r16, int g, Epi&& epi) {
   v4i x[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) x[k] = k < KS ? *(const v4i*)(xrow + k * 64) : (v4i){0, 0, 0, 0};
   const int T = (c.out_c + 15) >> 4;
-  for (int t = t0; t < T; t += 2 * tstep) {
-    const int tb = t + tstep < T ? t + tstep : t;
-    const int8_t* ra = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
-    const int8_t* rb = c.weights + (long)(tb * 16 + r16) * c.k_pad + g * 16;
-    v4i wa[KMAX], wb[KMAX];
+  for (int t = t0; t < T; t += TT * tstep) {
+    int tt[TT], nn[TT], mu[TT], sh[TT];
+    v4i w[TT][KMAX], acc[TT];
+#pragma unroll
+    for (int u = 0; u < TT; ++u) {
+      tt[u] = t + u * tstep < T ? t + u * tstep : t;  // past the end: a duplicate, not finished
+      const int8_t* r = c.weights + (long)(tt[u] * 16 + r16) * c.k_pad + g * 16;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k)
+        if (k < KS) w[u][k] = *(const v4i*)(r + k * 64);
+      nn[u] = tt[u] * 16 + r16;
+      const int l = nn[u] < c.out_c ? nn[u] : 0;
+      const int b = c.bias_eff[l];
+      mu[u] = c.mult[l];
+      sh[u] = c.shift[l];
+      acc[u] = (v4i){b, b, b, b};
+    }
 #pragma unroll
     for (int k = 0; k < KMAX; ++k)
       if (k < KS) {
-        wa[k] = *(const v4i*)(ra + k * 64);
-        wb[k] = *(const v4i*)(rb + k * 64);
-      }
-    const int na = t * 16 + r16, nb = tb * 16 + r16;
-    const int la = na < c.out_c ? na : 0, lb = nb < c.out_c ? nb : 0;
-    const int ba = c.bias_eff[la], bb = c.bias_eff[lb];
-    const int ma = c.mult[la], sa = c.shift[la], mb = c.mult[lb], sb = c.shift[lb];
-    v4i acca = (v4i){ba, ba, ba, ba}, accb = (v4i){bb, bb, bb, bb};
 #pragma unroll
-    for (int k = 0; k < KMAX; ++k)
-      if (k < KS) {
-        acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], wa[k], acca, 0, 0, 0);
-        accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], wb[k], accb, 0, 0, 0);
+        for (int u = 0; u < TT; ++u) acc[u] = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], w[u][k], acc[u], 0, 0, 0);
       }
-    epi(t, na, acca, ma, sa);
-    if (tb != t) epi(tb, nb, accb, mb, sb);
+#pragma unroll
+    for (int u = 0; u < TT; ++u)
+      if (u == 0 || tt[u] != t) epi(tt[u], nn[u], acc[u], mu[u], sh[u]);
   }
 }
 
@@ -263,13 +266,16 @@ __device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsig
   }
 }
 
-template <int RB, bool FAST, int KX, int NW, bool AM>
+template <int RB, bool FAST, int KX, int NW, bool AM, int DA = 2>
 __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_entry = __builtin_amdgcn_s_memtime();  // before any kernarg load
   constexpr int WPB = NW / RB;  // waves per pixel block
+  // channel tiles per round of the x-stationary 1x1 GEMMs (more when the
+  // K fragments are few); the deep form (DA > 2) takes more as well
+  constexpr int TTC = DA > 2 ? (KX <= 2 ? 6 : 3) : 2;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int r16 = lane & 15;
@@ -370,14 +376,17 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
         dl[(orow + r) * S1 + cg * 16 + r16] =
             (unsigned char)requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
     };
+    // DA channel groups per round: every item's loads (input taps, filter
+    // bytes, epilogue operands) are issued before any item's MFMAs, so a
+    // wave pays one global round trip per DA groups
     const int G = C >> 4;
-    for (int cg = wsub; cg < G; cg += 2 * WPB) {
-      const int cgb = cg + WPB < G ? cg + WPB : cg;
-      DwItem ia, ib;
-      dw_load(cg, ia);
-      dw_load(cgb, ib);
-      dw_finish(cg, ia);
-      if (cgb != cg) dw_finish(cgb, ib);
+    for (int cg = wsub; cg < G; cg += DA * WPB) {
+      DwItem it[DA];
+#pragma unroll
+      for (int u = 0; u < DA; ++u) dw_load(cg + u * WPB < G ? cg + u * WPB : cg, it[u]);
+#pragma unroll
+      for (int u = 0; u < DA; ++u)
+        if (u == 0 || cg + u * WPB < G) dw_finish(cg + u * WPB, it[u]);
     }
   }
   __syncthreads();
@@ -447,10 +456,10 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
         }
       });
     } else if (KS1 <= KX) {
-      gemm_xs_nt<KX>(a, xrow, KS1, wsub, WPB, r16, g, epi);
+      gemm_xs_nt<KX, TTC>(a, xrow, KS1, wsub, WPB, r16, g, epi);
     } else {
       for (int t = wsub; t < T1; t += WPB) {
-        const v4i acc = gemm_tile_nt(a, xrow, t, KS1, r16, g);
+        const v4i acc = gemm_tile_nt<(DA > 2 ? 8 : 4)>(a, xrow, t, KS1, r16, g);
         const int n = t * 16 + r16;
         const int nl = n < N1 ? n : 0;
         epi(t, n, acc, a.mult[nl], a.shift[nl]);
@@ -481,7 +490,7 @@ __global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int 
                 (unsigned char)requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
       });
     } else {
-      gemm_xs_nt<KX>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
+      gemm_xs_nt<KX, TTC>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
         if (n >= N2) return;
         const ChanQ q = chan_q(mu, sh, b.out_zp);
 #pragma unroll
@@ -803,7 +812,7 @@ __global__ __launch_bounds__(256) void chain_persist_kernel(bh_chain_params cp, 
   }
 }
 
-template <int RB, bool FAST, int KX, int NW = 4, bool AM = false>
+template <int RB, bool FAST, int KX, int NW = 4, bool AM = false, int DA = 2>
 static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024) {
     // opt in to the CU's full 160 KiB of LDS for this instantiation (once per device)
@@ -811,7 +820,7 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (opted_device != dev) {
-      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW, AM>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW, AM, DA>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       opted_device = dev;
     }
@@ -820,7 +829,7 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_w = FastDiv(p.dw.out_w);
   dv.out_h = FastDiv(p.dw.out_h);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
-  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
             L.off_add, dv);
 }
 
@@ -889,6 +898,9 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   const long widest = std::max<long>(std::max(d.out_c, p.pw1.out_c), p.has_pw2 ? p.pw2.out_c : 0);
   if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
   if (p.tile) return bh_chain_tile_lds_bytes(pp);
+  if (p.deep && (p.persist || !((p.px_blocks == 1 && (p.waves == 0 || p.waves == 4 || p.waves == 8)) ||
+                                (p.px_blocks == 2 && (p.waves == 0 || p.waves == 4)))))
+    return 0;
   if (p.persist) {
     if (p.px_blocks != 4 || (p.waves != 0 && p.waves != 4)) return 0;
     const size_t bytes = bh::persist_lds(p).bytes;
@@ -930,6 +942,25 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
       else bh::launch_persist<false, bh::kXsMax>(p, P, lds, s);
     }
     return bh_check_launch("chain_persist_kernel");
+  }
+  if (p.deep) {  // deep-issue forms (DA = 6): px_blocks 1 with 4 or 8 waves, px_blocks 2 with 4
+#define BH_DEEP(RB, NW)                                                                      \
+  if (k2) {                                                                                  \
+    if (fast) bh::launch_chain<RB, true, 2, NW, false, 6>(p, P, L, lds, s);                  \
+    else bh::launch_chain<RB, false, 2, NW, false, 6>(p, P, L, lds, s);                      \
+  } else {                                                                                   \
+    if (fast) bh::launch_chain<RB, true, bh::kXsMax, NW, false, 6>(p, P, L, lds, s);         \
+    else bh::launch_chain<RB, false, bh::kXsMax, NW, false, 6>(p, P, L, lds, s);             \
+  }
+    if (p.px_blocks == 2) {
+      BH_DEEP(2, 4)
+    } else if (p.waves == 8) {
+      BH_DEEP(1, 8)
+    } else {
+      BH_DEEP(1, 4)
+    }
+#undef BH_DEEP
+    return bh_check_launch("chain_kernel");
   }
   if (p.waves == 16) {  // one 16-pixel block, 16 waves (few-pixel layers)
     if (k2) {

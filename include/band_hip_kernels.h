@@ -92,6 +92,9 @@ int bh_graph_destroy(bh_graph_exec_t exec);
 
 /* ---- events (timing) ---------------------------------------------------- */
 int bh_event_create(bh_event_t* ev);
+/* an event whose bh_event_sync sleeps until the GPU signals it (no
+ * timing); replaces bh_stream_sync's spin-wait */
+int bh_event_create_blocking(bh_event_t* ev);
 int bh_event_destroy(bh_event_t ev);
 int bh_event_record(bh_event_t ev, bh_stream_t s);
 int bh_event_sync(bh_event_t ev);
@@ -343,6 +346,10 @@ typedef struct bh_chain_params {
    * clock stamps (s_memtime) at its phase boundaries to
    * debug_stamps[8 * workgroup]; NULL in production */
   void* debug_stamps;
+  /* 1: deep-issue form - each wave issues the loads of 6 depthwise channel
+   * groups per round (instead of 2) and the x-stationary 1x1 GEMMs take 3-6
+   * channel tiles per round; px_blocks 1 (4 or 8 waves) or 2 (4 waves) */
+  int deep;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */

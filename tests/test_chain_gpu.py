@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0, tile=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist, tile)
+    y, f = c.gpu(lib, px, waves, persist, tile, deep)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -38,10 +38,13 @@ def test_chain_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
     _check(c, gpu_lib, 1, waves=8)
+    for px, w in ((1, 4), (1, 8), (2, 4)):  # the deep-issue forms
+        _check(c, gpu_lib, px, waves=w, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
     c.fast = False  # TFLite's two-step requantisation in every stage
     _check(c, gpu_lib, 4)
+    _check(c, gpu_lib, 1, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
 
@@ -66,6 +69,8 @@ def test_chain_general(gpu_lib, args):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
     _check(c, gpu_lib, 1, waves=8)
+    for px, w in ((1, 4), (1, 8), (2, 4)):
+        _check(c, gpu_lib, px, waves=w, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
 
@@ -141,6 +146,10 @@ def test_chain_rejects_unsupported(gpu_lib):
     keep = []
     c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
+    c.deep = 1
+    c.px_blocks = 4  # the deep forms take 16 or 32 pixels per workgroup
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
+    c.deep, c.px_blocks = 0, 4
     for field, bad in (("px_blocks", 3), ("waves", 12)):
         old = getattr(c, field)
         setattr(c, field, bad)
@@ -154,7 +163,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcedeep"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param

@@ -21,8 +21,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t",
-                    help="forms: px_blocks [wN waves] [p persistent]; t = the 2-D tile form")
+    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,1d,1w8d,2d",
+                    help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
@@ -41,10 +41,11 @@ def main():
         for form in a.px.split(","):
             tile = int(form == "t")
             persist = int(form.endswith("p"))
-            f = "4" if tile else form.rstrip("p")
+            deep = int(form.endswith("d"))
+            f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves, persist, tile)
+            q = c.params(lib, px, keep, waves, persist, tile, deep)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue

@@ -2,6 +2,7 @@
 // include/band_c_api.h for the contract).
 #include <pthread.h>
 #include <set>
+#include <unordered_map>
 #include "band_c_api.h"
 
 #include <condition_variable>
@@ -396,9 +397,15 @@ namespace {
 // end - the job's SCHEDULED arrival, so time a request waited to be submitted
 // (in-flight bound, ring back-pressure) counts as the queueing it is rather
 // than vanishing from the percentiles (no coordinated omission).
-// Outputs are read in submission order; a model never has more unread
-// requests than its request ring has slots, so no result is overwritten
-// before it is read (the engine's own back-pressure covers unfinished ones).
+// Outputs are read in COMPLETION order: an end-of-request callback queues
+// each finished request and reader threads copy its outputs out, so one slow
+// request does not hold the finished ones behind it (read in submission
+// order, a request of a slow batched pass kept every later one counted as in
+// flight and starved the closed loop).  Per model, a request is submitted
+// only while it is fewer than ring - submitters submissions ahead of that
+// model's oldest unread request, so no result is overwritten in the output
+// ring before it is read (the engine may hand concurrent submitters their
+// ring handles in a different order, by at most the submitter count).
 BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models, int n_jobs,
                          int max_inflight, bool open_loop,
                          const std::function<std::pair<int64_t, int>(int)>& next_arrival, double* latency_us,
@@ -406,9 +413,8 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   if (!engine || !models || n_models <= 0 || n_jobs < 0 || max_inflight <= 0) return kBandErr;
   band::Engine& e = *engine->impl;
   // per model: one input tensor (copied into the request ring at submit)
-  // and one output tensor per waiter use
-  std::vector<std::vector<std::unique_ptr<band::Tensor>>> own_in(n_models), outs(n_models);
-  std::vector<band::Tensors> in_ptrs(n_models), out_ptrs(n_models);
+  std::vector<std::vector<std::unique_ptr<band::Tensor>>> own_in(n_models);
+  std::vector<band::Tensors> in_ptrs(n_models);
   for (int m = 0; m < n_models; ++m) {
     const band::ModelId id = models[m]->impl->GetId();
     const auto in_idx = e.GetInputTensorIndices(id);
@@ -422,98 +428,98 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         in_ptrs[m].push_back(own_in[m].back().get());
       }
     }
-    for (int t : e.GetOutputTensorIndices(id)) {
-      outs[m].emplace_back(e.CreateTensor(id, t));
-      if (!outs[m].back()) return kBandErr;
-      out_ptrs[m].push_back(outs[m].back().get());
-    }
   }
-  // Lanes: each lane is a submitter thread and a waiter thread over every
-  // lanes-th job.  One submitter copies every request into its model's ring
-  // (150 KB per 224x224 job): at ~55k jobs/s that one thread was the host
-  // ceiling of the C3 line (bench.py host_threads_timed: 0.99 of a core), as
-  // was one waiter copying DeepLab's 1 MB outputs out.  BANDX_DRIVER_LANES
-  // sets the count (default 1: 4 and 8 lanes measured 55.7k / 55.0k against
-  // 59.7k inf/s with one, profiles/r03l_lanes*.json - the submitter was busy,
-  // not the bound); the in-flight bound and the per-model unread bound stay
-  // global.
+  // Submitters (BANDX_DRIVER_LANES, default 1) copy requests into the rings
+  // (150 KB per 224x224 job); readers (BANDX_DRIVER_READERS, default 2) copy
+  // results out (DeepLab's are 1 MB), each into output tensors of its own.
   int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
   lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
-  std::mutex mu;
-  std::condition_variable cv;
-  struct Pending {
-    int index, model;
-    band::JobId id;
-    int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
-    long seq;         // submission number within its model
-  };
-  std::vector<std::deque<Pending>> pending(lanes);
-  // each lane's waiter reads outputs into tensors of its own
-  std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> lane_outs(lanes);
-  std::vector<std::vector<band::Tensors>> lane_out_ptrs(lanes);
-  for (int l = 0; l < lanes; ++l) {
-    lane_outs[l].resize(n_models);
-    lane_out_ptrs[l].resize(n_models);
+  int readers = 2;
+  if (const char* rv = std::getenv("BANDX_DRIVER_READERS")) readers = std::max(1, std::atoi(rv));
+  readers = std::max(1, std::min(readers, n_jobs > 0 ? n_jobs : 1));
+  std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> reader_outs(readers);
+  std::vector<std::vector<band::Tensors>> reader_out_ptrs(readers);
+  for (int r = 0; r < readers; ++r) {
+    reader_outs[r].resize(n_models);
+    reader_out_ptrs[r].resize(n_models);
     for (int m = 0; m < n_models; ++m) {
-      if (l == 0) {
-        lane_out_ptrs[l][m] = out_ptrs[m];
-        continue;
-      }
       const band::ModelId id = models[m]->impl->GetId();
       for (int t : e.GetOutputTensorIndices(id)) {
-        lane_outs[l][m].emplace_back(e.CreateTensor(id, t));
-        if (!lane_outs[l][m].back()) return kBandErr;
-        lane_out_ptrs[l][m].push_back(lane_outs[l][m].back().get());
+        reader_outs[r][m].emplace_back(e.CreateTensor(id, t));
+        if (!reader_outs[r][m].back()) return kBandErr;
+        reader_out_ptrs[r][m].push_back(reader_outs[r][m].back().get());
       }
     }
   }
-  // arrivals are drawn in job order (the open-loop schedule is one sequence)
-  std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
-  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
-  int inflight = 0;
+  struct Pending {
+    int index, model;
+    int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
+    long seq;         // submission number within its model
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::unordered_map<band::JobId, Pending> pending;  // submitted, not yet read
+  std::deque<band::JobId> done;                      // finished, ready to read
+  std::set<band::JobId> early;  // finished before its submitter recorded it
+  int inflight = 0, retired = 0, taken = 0;
   std::vector<int> unread(n_models, 0), ring(n_models, 0);
   for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
-  // Lanes read out of submission order, so a model's unread COUNT no longer
-  // bounds how far its ring moves past its OLDEST unread request: a request
-  // of model m is submitted only while it is fewer than ring - lanes
-  // submissions ahead of that oldest one (the engine may hand concurrent
-  // submitters their ring handles in a different order, by at most lanes)
   std::vector<long> next_seq(n_models, 0);
   std::vector<std::set<long>> unread_seq(n_models);
   bool failed = false;
+  // arrivals are drawn in job order (the open-loop schedule is one sequence)
+  std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
+  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
+  const band::CallbackId cb = e.SetOnEndRequest([&](int id, absl::Status) {
+    std::lock_guard<std::mutex> lk(mu);
+    if (pending.count(id))
+      done.push_back(id);
+    else
+      early.insert(id);
+    cv.notify_all();
+  });
+  auto retire = [&](const Pending& item, bool ok) {  // under mu
+    if (!ok && !failed) failed = true;
+    --inflight;
+    --unread[item.model];
+    unread_seq[item.model].erase(item.seq);
+    ++retired;
+  };
   const int64_t t0 = band::time::NowMicros();
   std::vector<std::thread> threads;
-  for (int l = 0; l < lanes; ++l) {
-    const int mine = n_jobs > l ? (n_jobs - 1 - l) / lanes + 1 : 0;
-    threads.emplace_back([&, l, mine] {
-      pthread_setname_np(pthread_self(), "bandx-waiter");
-      for (int done = 0; done < mine; ++done) {
+  for (int r = 0; r < readers; ++r) {
+    threads.emplace_back([&, r] {
+      pthread_setname_np(pthread_self(), "bandx-reader");
+      while (true) {
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return !pending[l].empty(); });
-        Pending item = pending[l].front();
-        pending[l].pop_front();
+        cv.wait(lk, [&] { return !done.empty() || taken >= n_jobs; });
+        if (done.empty()) break;
+        const band::JobId id = done.front();
+        done.pop_front();
+        ++taken;
+        const Pending item = pending.at(id);
+        pending.erase(id);
         lk.unlock();
-        absl::Status st =
-            item.id >= 0 ? e.Wait(item.id, lane_out_ptrs[l][item.model]) : absl::InternalError("submit");
-        band::Job j = item.id >= 0 ? e.GetFinishedJob(item.id) : band::Job();
-        lk.lock();
-        if (!st.ok() || j.job_id != item.id || j.status != band::JobStatus::kSuccess) {
-          if (!failed)
-            BAND_LOG(band::LogSeverity::kError, "request driver: job %d (model %d, lane %d) failed: %s; record %d, status %s",
-                     item.id, item.model, l, std::string(st.message()).c_str(), j.job_id, band::ToString<band::JobStatus>(j.status));
-          failed = true;
-        }
+        band::Job j = e.GetFinishedJob(id);
+        absl::Status st = j.job_id == id ? e.GetOutputTensors(id, reader_out_ptrs[r][item.model])
+                                         : absl::InternalError("no finished record");
+        const bool ok = st.ok() && j.status == band::JobStatus::kSuccess;
+        if (!ok)
+          BAND_LOG(band::LogSeverity::kError, "request driver: job %d (model %d) failed: %s; record %d, status %s",
+                   id, item.model, std::string(st.message()).c_str(), j.job_id,
+                   band::ToString<band::JobStatus>(j.status));
         if (latency_us)
           latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
         if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
         if (model_index) model_index[item.index] = item.model;
-        --inflight;
-        --unread[item.model];
-        unread_seq[item.model].erase(item.seq);
+        lk.lock();
+        retire(item, ok);
         cv.notify_all();
       }
     });
+  }
+  for (int l = 0; l < lanes; ++l) {
     threads.emplace_back([&, l] {
       pthread_setname_np(pthread_self(), "bandx-submit");
       for (int j = l; j < n_jobs; j += lanes) {
@@ -536,12 +542,22 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         }
         auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
         std::lock_guard<std::mutex> lk(mu);
-        pending[l].push_back({j, m, id.ok() ? id.value() : -1, t0 + arrival.first, seq});
+        const Pending item{j, m, t0 + arrival.first, seq};
+        if (!id.ok()) {
+          BAND_LOG(band::LogSeverity::kError, "request driver: submit of job %d failed: %s", j,
+                   std::string(id.status().message()).c_str());
+          ++taken;
+          retire(item, false);
+        } else {
+          pending[id.value()] = item;
+          if (early.erase(id.value())) done.push_back(id.value());
+        }
         cv.notify_all();
       }
     });
   }
   for (auto& t : threads) t.join();
+  (void)e.UnsetOnEndRequest(cb);
   if (wall_s) *wall_s = (band::time::NowMicros() - t0) * 1e-6;
   return failed ? kBandErr : kBandOk;
 }

@@ -1,5 +1,7 @@
 #include "engine/engine.h"
 
+#include <cstdlib>
+
 #include "band/interface/job_batching.h"
 
 #include <algorithm>
@@ -195,10 +197,17 @@ absl::Status Engine::RegisterModel(Model* model) {
     }
     if (in_views.size() != spec.input_tensors.size() || out_views.size() != spec.output_tensors.size())
       return absl::InternalError("no worker exposes the model's input/output tensors");
+    // request slots per model: the reference's 128, or BANDX_REQUEST_RING_SLOTS
+    // (a slot is held from RequestAsync until the job finishes, and slots
+    // are taken in order, so one slow job stalls new requests of its model
+    // once 128 younger ones are outstanding - deep closed loops over
+    // several workers want more)
+    int slots = 128;
+    if (const char* rs = std::getenv("BANDX_REQUEST_RING_SLOTS")) slots = std::max(1, std::atoi(rs));
     model_input_buffer_[model_id].reset(new TensorRingBuffer(
-        in_views, std::vector<int>(spec.input_tensors.begin(), spec.input_tensors.end())));
+        in_views, std::vector<int>(spec.input_tensors.begin(), spec.input_tensors.end()), slots));
     model_output_buffer_[model_id].reset(new TensorRingBuffer(
-        out_views, std::vector<int>(spec.output_tensors.begin(), spec.output_tensors.end())));
+        out_views, std::vector<int>(spec.output_tensors.begin(), spec.output_tensors.end()), slots));
 
     absl::Status ls = latency_estimator_->ProfileModel(model_id);
     if (!ls.ok()) return ls;

@@ -1,6 +1,10 @@
 // Scheduler policies; each cites the reference policy it restates.
 #include "engine/scheduler.h"
 
+#include <cstdlib>
+#include <map>
+#include <string>
+
 #include <algorithm>
 #include <limits>
 #include <unordered_set>
@@ -57,12 +61,31 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
   // idle workers in rotation order, starting at next_
   std::vector<WorkerId> order(idle.lower_bound(next_), idle.end());
   order.insert(order.end(), idle.begin(), idle.lower_bound(next_));
+  if (group_largest_ < 0) {
+    const char* g = std::getenv("BANDX_BATCH_GROUP");
+    group_largest_ = g && std::string(g) == "largest" ? 1 : 0;
+  }
   for (WorkerId w : order) {
     if (requests.empty()) break;
     auto it = std::find_if(requests.begin(), requests.end(), [&](const Job& j) {
       return engine_.GetLargestSubgraphKey(j.model_id, w).IsValid();
     });
     if (it == requests.end()) continue;
+    if (group_largest_ && requests.size() > 1) {
+      // the model with the most queued requests this worker can run; its
+      // oldest request leads the pass (ties: the older group)
+      std::map<ModelId, int> count;
+      for (const Job& j : requests) ++count[j.model_id];
+      int most = 0;
+      for (auto j = requests.begin(); j != requests.end(); ++j) {
+        const int c = count[j->model_id];
+        if (c > most && engine_.GetLargestSubgraphKey(j->model_id, w).IsValid()) {
+          most = c;
+          it = j;
+        }
+        count[j->model_id] = 0;  // later requests of a model are not its oldest
+      }
+    }
     Job job = std::move(*it);
     it = requests.erase(it);
     const SubgraphKey key = engine_.GetLargestSubgraphKey(job.model_id, w);

@@ -62,6 +62,10 @@ class RoundRobinScheduler : public IScheduler {
 
  private:
   WorkerId next_ = 0;  // scan starts here
+  // job batching, BANDX_BATCH_GROUP=largest: an idle worker's pass takes the
+  // model with the most queued requests (its oldest first) instead of the
+  // queue head's model, so passes are fuller (deviation; off by default)
+  int group_largest_ = -1;  // -1: read the environment on first use
 };
 
 // repeatedly place the job whose best plan finishes last ("largest shortest

@@ -76,6 +76,7 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   }
   if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
   if (const char* sy = std::getenv("BAND_HIP_SYNC")) block_sync_ = std::string(sy) == "block";
+  if (const char* d = std::getenv("BAND_HIP_DIRECT_IO")) direct_io_ = d[0] != '0';
 }
 
 HipModelExecutor::~HipModelExecutor() {
@@ -2502,7 +2503,9 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
     v.exec = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
                                                 num_threads_);
     v.exec->use_graph_ = use_graph_;
-    v.exec->io_mode_ = io_mode_;
+    // direct job I/O captures the variants' graphs without host copies
+    v.exec->io_mode_ = direct_io_ ? 1 : io_mode_;
+    v.exec->direct_io_ = direct_io_;
     v.exec->block_sync_ = block_sync_;
     v.exec->io_stream_bytes_ = io_stream_bytes_;
     // the base subgraph's op set (a whole-model key prepares all ops)
@@ -2546,6 +2549,96 @@ absl::Status HipModelExecutor::ExecuteJobBatch(const SubgraphKey& key, int n) {
   const JobBatchVariant* v = VariantFor(key, n);
   if (!v || n < 1) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
   return v->exec->ExecuteSubgraph(key);
+}
+
+absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int n,
+                                                     const std::vector<const interface::ITensor*>& in,
+                                                     const std::vector<interface::ITensor*>& out) {
+  if (device_flag_ != DeviceFlag::kGPU || n < 2 || !direct_io_) return absl::UnimplementedError("direct job batch I/O");
+  PreparedSubgraph* base = Find(key);
+  const JobBatchVariant* v = VariantFor(key, n);
+  if (!base || !v) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
+  if (in.size() != base->inputs.size() * n || out.size() != base->outputs.size() * n)
+    return absl::InternalError("direct job batch I/O: tensor count mismatch");
+  std::vector<size_t> per_job;
+  for (int t : base->inputs) per_job.push_back(meta_[t]->bytes);
+  for (int t : base->outputs) per_job.push_back(meta_[t]->bytes);
+  PreparedSubgraph* vs = v->exec->Find(key);
+  if (!vs) return absl::InternalError("job batch variant lost its subgraph");
+  return v->exec->RunDirect(vs, n, per_job, in, out);
+}
+
+absl::Status HipModelExecutor::RunDirect(PreparedSubgraph* sg, int n, const std::vector<size_t>& per_job,
+                                         const std::vector<const interface::ITensor*>& in,
+                                         const std::vector<interface::ITensor*>& out) {
+  // a graph that already holds its host copies, or intermediates a later
+  // subgraph reads back, take the staged path
+  if (!sg->extra_d2h.empty() || (use_graph_ && sg->graph && sg->io_in_graph))
+    return absl::UnimplementedError("direct job batch I/O");
+  const size_t ni = sg->inputs.size();
+  for (size_t i = 0; i < in.size(); ++i)
+    if (!in[i] || in[i]->GetBytes() != per_job[i / n]) return absl::InternalError("direct job batch I/O: input size");
+  for (size_t i = 0; i < out.size(); ++i)
+    if (out[i] && out[i]->GetBytes() != per_job[ni + i / n]) return absl::InternalError("direct job batch I/O: output size");
+  PinCallingThreadToGpu(ordinal_);
+  int rc = bh_set_device(ordinal_);
+  if (rc) return HipErr(rc, "hipSetDevice");
+  if (use_graph_ && !sg->graph && sg->runs > 0) {  // kernels-only graph
+    rc = bh_capture_begin(stream_);
+    if (rc) return HipErr(rc, "capture begin");
+    absl::Status s = EnqueueLaunches(sg);
+    bh_graph_exec_t g = nullptr;
+    rc = bh_capture_end(stream_, &g);
+    if (!s.ok()) return s;
+    if (rc) return HipErr(rc, "capture end");
+    sg->graph = g;
+    sg->io_in_graph = false;
+  }
+  char* arena = static_cast<char*>(sg->arena->ptr());
+  // jobs whose host tensors are adjacent (consecutive ring slots of one
+  // page-locked block) go in one DMA: a run of slots s0..s1 of tensor k
+  for (size_t k = 0; k < ni; ++k)
+    for (int s0 = 0; s0 < n;) {
+      const char* h0 = in[k * n + s0]->GetData();
+      int s1 = s0 + 1;
+      while (s1 < n && in[k * n + s1]->GetData() == h0 + (s1 - s0) * per_job[k]) ++s1;
+      rc = bh_memcpy_h2d_async(arena + sg->offset.at(sg->inputs[k]) + s0 * per_job[k], h0, (s1 - s0) * per_job[k],
+                               stream_);
+      if (rc) return HipErr(rc, "H2D input");
+      s0 = s1;
+    }
+  if (use_graph_ && sg->graph) {
+    rc = bh_graph_launch(sg->graph, stream_);
+    if (rc) return HipErr(rc, "graph launch");
+  } else {
+    RETURN_STATUS_IF(EnqueueLaunches(sg));
+  }
+  for (size_t k = 0; k < sg->outputs.size(); ++k) {
+    const size_t pb = per_job[ni + k];
+    for (int s0 = 0; s0 < n;) {
+      interface::ITensor* o = out[k * n + s0];
+      if (!o) {
+        ++s0;
+        continue;
+      }
+      char* h0 = o->GetData();
+      int s1 = s0 + 1;
+      while (s1 < n && out[k * n + s1] && out[k * n + s1]->GetData() == h0 + (s1 - s0) * pb) ++s1;
+      rc = bh_memcpy_d2h_async(h0, arena + sg->offset.at(sg->outputs[k]) + s0 * pb, (s1 - s0) * pb, stream_);
+      if (rc) return HipErr(rc, "D2H output");
+      s0 = s1;
+    }
+  }
+  if (block_sync_) {
+    if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
+    rc = bh_event_record(done_event_, stream_);
+    if (!rc) rc = bh_event_sync(done_event_);
+  } else {
+    rc = bh_stream_sync(stream_);
+  }
+  if (rc) return HipErr(rc, "stream sync");
+  ++sg->runs;
+  return absl::OkStatus();
 }
 
 absl::Status HipModelExecutor::TimeSubgraph(const SubgraphKey& key, int iters, double* us) {

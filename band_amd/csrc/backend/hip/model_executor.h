@@ -138,6 +138,8 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   std::shared_ptr<interface::ITensorView> GetJobSlotView(const SubgraphKey& key, int index, int n,
                                                          int slot) override;
   absl::Status ExecuteJobBatch(const SubgraphKey& key, int n) override;
+  absl::Status ExecuteJobBatchDirect(const SubgraphKey& key, int n, const std::vector<const interface::ITensor*>& in,
+                                     const std::vector<interface::ITensor*>& out) override;
 
   // --- extensions used by the C ABI / bench (not part of Band's interface) ---
   void SetUseGraph(bool on) { use_graph_ = on; }
@@ -193,6 +195,11 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   absl::Status EnqueueOutputs(PreparedSubgraph* sg);
   // one pass: the graph (captured on first use) or the eager launches
   absl::Status EnqueuePass(PreparedSubgraph* sg);
+  // a job-batch variant's pass with each job's I/O copied straight between
+  // host tensors and its slot of the boundary tensors (per_job: the
+  // batch-1 bytes of each input, then of each output)
+  absl::Status RunDirect(PreparedSubgraph* sg, int n, const std::vector<size_t>& per_job,
+                         const std::vector<const interface::ITensor*>& in, const std::vector<interface::ITensor*>& out);
   absl::Status ExecuteOnHost(PreparedSubgraph* sg);
   absl::Status EnqueueLaunch(const Launch& l);
 
@@ -235,6 +242,10 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   // (the worker thread sleeps until the GPU's interrupt) instead of spinning
   // in hipStreamSynchronize - frees a core per GPU worker
   bool block_sync_ = false;
+  // batched passes copy each job's I/O straight between the request rings'
+  // page-locked slots and the device (ExecuteJobBatchDirect);
+  // BAND_HIP_DIRECT_IO=0 stages them through the slot views instead
+  bool direct_io_ = true;
   bh_event_t done_event_ = nullptr;
   size_t io_stream_bytes_ = 512 << 10;
   static const std::vector<int> kEmpty;

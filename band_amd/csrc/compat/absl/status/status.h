@@ -35,4 +35,6 @@ inline Status InvalidArgumentError(std::string m) { return Status(StatusCode::kI
 inline Status DeadlineExceededError(std::string m) { return Status(StatusCode::kDeadlineExceeded, std::move(m)); }
 inline Status NotFoundError(std::string m) { return Status(StatusCode::kNotFound, std::move(m)); }
 inline Status UnavailableError(std::string m) { return Status(StatusCode::kUnavailable, std::move(m)); }
+inline Status UnimplementedError(std::string m) { return Status(StatusCode::kUnimplemented, std::move(m)); }
+inline bool IsUnimplemented(const Status& s) { return s.code() == StatusCode::kUnimplemented; }
 }  // namespace absl

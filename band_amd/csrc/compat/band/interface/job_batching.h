@@ -14,10 +14,12 @@
 #pragma once
 
 #include <memory>
+#include <vector>
 
 #include "absl/status/status.h"
 #include "band/common.h"
 #include "band/interface/model.h"
+#include "band/interface/tensor.h"
 #include "band/interface/tensor_view.h"
 
 namespace band {
@@ -37,6 +39,16 @@ class IJobBatching {
   // Runs n (1 <= n <= MaxJobBatch) jobs whose inputs were written through
   // the slot views; synchronous like ExecuteSubgraph.
   virtual absl::Status ExecuteJobBatch(const SubgraphKey& key, int n) = 0;
+  // Optional: runs n (>= 2) jobs reading job s's input tensor k (the order
+  // of GetInputs(key)) from in[k * n + s] and writing its output tensor k
+  // (GetOutputs(key) order) into out[k * n + s] (nullptr: not wanted) - host
+  // tensors, typically the request rings' slots in page-locked memory - with
+  // no staging through the slot views; synchronous.  Unimplemented: the
+  // caller uses the slot views and ExecuteJobBatch instead.
+  virtual absl::Status ExecuteJobBatchDirect(const SubgraphKey& key, int n, const std::vector<const ITensor*>& in,
+                                             const std::vector<ITensor*>& out) {
+    return absl::UnimplementedError("direct job batch I/O");
+  }
 };
 
 }  // namespace interface

@@ -742,6 +742,39 @@ absl::Status Engine::InvokeJobBatch(const SubgraphKey& key, int n) {
   return jb->ExecuteJobBatch(key, n);
 }
 
+absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vector<Job*>& jobs) {
+  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  interface::IModelExecutor* exec = GetModelExecutor(key);
+  const int n = static_cast<int>(jobs.size());
+  if (!jb || !exec || n < 2) return absl::UnimplementedError("direct job batch I/O");
+  const ModelId model = jobs[0]->model_id;
+  auto in_it = model_input_buffer_.find(model);
+  auto out_it = model_output_buffer_.find(model);
+  if (in_it == model_input_buffer_.end() || out_it == model_output_buffer_.end())
+    return absl::UnimplementedError("no request rings");
+  const std::vector<int>& ins = exec->GetInputs(key);
+  const std::vector<int>& outs = exec->GetOutputs(key);
+  std::vector<const interface::ITensor*> in(ins.size() * n, nullptr);
+  std::vector<interface::ITensor*> out(outs.size() * n, nullptr);
+  for (int s = 0; s < n; ++s) {
+    const Job& j = *jobs[s];
+    if (j.model_id != model || j.input_handle < 0 || j.output_handle < 0)
+      return absl::UnimplementedError("job without request slots");
+    for (size_t k = 0; k < ins.size(); ++k) {
+      Tensor* t = in_it->second->SlotTensor(ins[k], j.input_handle);
+      if (!t || !t->IsRingMemory()) return absl::UnimplementedError("input slot not page-locked");
+      in[k * n + s] = t;
+    }
+    for (size_t k = 0; k < outs.size(); ++k) {
+      if (!out_it->second->IsTensorIndexValid(outs[k])) continue;
+      Tensor* t = out_it->second->SlotTensor(outs[k], j.output_handle);
+      if (!t || !t->IsRingMemory()) return absl::UnimplementedError("output slot not page-locked");
+      out[k * n + s] = t;
+    }
+  }
+  return jb->ExecuteJobBatchDirect(key, n, in, out);
+}
+
 absl::Status Engine::TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) {
   if (job.output_handle < 0) return absl::OkStatus();
   const SubgraphKey& key = job.subgraph_key;

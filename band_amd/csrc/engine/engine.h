@@ -109,6 +109,7 @@ class Engine : public IEngine {
   int MaxJobBatch(const SubgraphKey& key) const override;
   absl::Status TryCopyInputTensorsToSlot(const Job& job, int n, int slot) override;
   absl::Status InvokeJobBatch(const SubgraphKey& key, int n) override;
+  absl::Status InvokeJobBatchDirect(const SubgraphKey& key, const std::vector<Job*>& jobs) override;
   absl::Status TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) override;
   void UpdateLatency(const SubgraphKey& key, int64_t latency) override { latency_estimator_->UpdateLatency(key, latency); }
   int64_t GetProfiled(const SubgraphKey& key) const override { return latency_estimator_->GetProfiled(key); }

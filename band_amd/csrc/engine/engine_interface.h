@@ -71,6 +71,12 @@ class IEngine {
     return absl::InternalError("job batching unsupported");
   }
   virtual absl::Status InvokeJobBatch(const SubgraphKey& key, int n) { return absl::InternalError("job batching unsupported"); }
+  // one batched pass whose I/O goes straight between the request rings'
+  // slots and the device (IJobBatching::ExecuteJobBatchDirect);
+  // Unimplemented: use the slot copies + InvokeJobBatch
+  virtual absl::Status InvokeJobBatchDirect(const SubgraphKey& key, const std::vector<Job*>& jobs) {
+    return absl::UnimplementedError("direct job batch I/O");
+  }
   virtual absl::Status TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) {
     return absl::InternalError("job batching unsupported");
   }

@@ -2,6 +2,7 @@
 
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 
 namespace band {
 
@@ -41,20 +42,58 @@ Affine* CloneAffine(const Affine* src) {
 }
 }  // namespace
 
-Tensor::Tensor(const interface::ITensor* view, bool copy_data)
+namespace {
+std::mutex g_ring_alloc_mu;
+RingHostAllocator g_ring_alloc;
+}  // namespace
+
+void SetRingHostAllocator(RingHostAllocator a) {
+  std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
+  g_ring_alloc = a;
+}
+
+Tensor::Tensor(const interface::ITensor* view, bool copy_data, bool ring_memory)
     : type_(view->GetType()),
       dims_(view->GetDims(), view->GetDims() + view->GetNumDims()),
-      data_(view->GetBytes()),
+      name_(view->GetName() ? view->GetName() : "") {
+  const size_t bytes = view->GetBytes();
+  if (ring_memory && bytes > 0) {
+    RingHostAllocator a;
+    {
+      std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
+      a = g_ring_alloc;
+    }
+    if (a.alloc && a.free && (ext_ = static_cast<char*>(a.alloc(bytes))) != nullptr) {
+      ext_bytes_ = bytes;
+      ext_free_ = a.free;
+    }
+  }
+  if (!ext_) data_.resize(bytes);
+  Quantization q = view->GetQuantization();
+  if (q.GetType() == QuantizationType::kAffineQuantization && q.GetParams()) {
+    qtype_ = QuantizationType::kAffineQuantization;
+    qparams_ = CloneAffine(static_cast<const Affine*>(q.GetParams()));
+  }
+  if (copy_data && bytes) std::memcpy(GetData(), view->GetData(), bytes);
+}
+
+Tensor::Tensor(const interface::ITensor* view, char* external)
+    : type_(view->GetType()),
+      dims_(view->GetDims(), view->GetDims() + view->GetNumDims()),
+      ext_(external),
+      ext_bytes_(view->GetBytes()),
       name_(view->GetName() ? view->GetName() : "") {
   Quantization q = view->GetQuantization();
   if (q.GetType() == QuantizationType::kAffineQuantization && q.GetParams()) {
     qtype_ = QuantizationType::kAffineQuantization;
     qparams_ = CloneAffine(static_cast<const Affine*>(q.GetParams()));
   }
-  if (copy_data && !data_.empty()) std::memcpy(data_.data(), view->GetData(), data_.size());
 }
 
-Tensor::~Tensor() { FreeQuant(); }
+Tensor::~Tensor() {
+  FreeQuant();
+  if (ext_ && ext_free_) ext_free_(ext_);
+}
 
 void Tensor::FreeQuant() {
   if (!qparams_) return;
@@ -69,7 +108,13 @@ void Tensor::SetDims(const std::vector<int>& dims) {
   dims_ = dims;
   size_t n = GetDataTypeBytes(type_);
   for (int d : dims_) n *= static_cast<size_t>(d);
-  data_.resize(n);
+  if (ext_ && n != ext_bytes_) {  // a resized ring slot falls back to heap memory
+    if (ext_free_) ext_free_(ext_);
+    ext_ = nullptr;
+    ext_bytes_ = 0;
+    ext_free_ = nullptr;
+  }
+  if (!ext_) data_.resize(n);
 }
 
 Quantization Tensor::GetQuantization() const { return Quantization(qtype_, qparams_); }
@@ -85,9 +130,33 @@ absl::Status Tensor::SetQuantization(Quantization q) {
 TensorRingBuffer::TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors,
                                    std::vector<int> tensor_indices, int size)
     : size_(size > 0 ? size : 1), num_tensors_(tensors.size()), slots_(size_), busy_(size_, 0) {
-  for (auto& slot : slots_)
-    for (const auto& t : tensors) slot.emplace_back(new Tensor(t.get()));
+  RingHostAllocator a;
+  {
+    std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
+    a = g_ring_alloc;
+  }
+  std::vector<size_t> stride(tensors.size(), 0);
+  if (a.alloc && a.free) {
+    block_free_ = a.free;
+    for (size_t i = 0; i < tensors.size(); ++i) {
+      // slots back to back: consecutive handles form one contiguous run
+      stride[i] = tensors[i]->GetBytes();
+      char* b = stride[i] ? static_cast<char*>(a.alloc(stride[i] * size_)) : nullptr;
+      blocks_.push_back(b);
+    }
+  }
+  for (int s = 0; s < size_; ++s)
+    for (size_t i = 0; i < tensors.size(); ++i) {
+      char* b = i < blocks_.size() ? blocks_[i] : nullptr;
+      slots_[s].emplace_back(b ? new Tensor(tensors[i].get(), b + s * stride[i]) : new Tensor(tensors[i].get()));
+    }
   for (size_t i = 0; i < tensor_indices.size(); ++i) tensor_to_buffer_[tensor_indices[i]] = static_cast<int>(i);
+}
+
+TensorRingBuffer::~TensorRingBuffer() {
+  slots_.clear();  // the slot tensors view the blocks
+  for (char* b : blocks_)
+    if (b) block_free_(b);
 }
 
 int TensorRingBuffer::Alloc() {
@@ -143,6 +212,12 @@ int TensorRingBuffer::Outstanding() const {
 bool TensorRingBuffer::IsHandleValid(int handle) const {
   std::lock_guard<std::mutex> lock(head_mtx_);
   return handle >= 0 && head_ - size_ <= handle && handle < head_;
+}
+
+Tensor* TensorRingBuffer::SlotTensor(int tensor_index, int handle) {
+  auto it = tensor_to_buffer_.find(tensor_index);
+  if (it == tensor_to_buffer_.end() || !IsHandleValid(handle)) return nullptr;
+  return slots_[Slot(handle)][it->second].get();
 }
 
 absl::Status TensorRingBuffer::GetTensorFromHandle(interface::ITensor* dst, int tensor_index, int handle) const {

@@ -14,21 +14,38 @@
 
 namespace band {
 
+// Host memory for the request rings' slots.  A backend may install an
+// allocator of page-locked memory (the HIP backend does), so a batched pass
+// can DMA a request's input from its ring slot and its outputs into its
+// output slot with no staging copy; `alloc` may return nullptr, and then
+// plain heap memory is used.
+struct RingHostAllocator {
+  void* (*alloc)(size_t bytes) = nullptr;
+  void (*free)(void* p) = nullptr;
+};
+void SetRingHostAllocator(RingHostAllocator a);
+
 class Tensor : public interface::ITensor {
  public:
-  explicit Tensor(const interface::ITensor* view, bool copy_data = false);
+  // ring_memory: the bytes come from the ring host allocator, if one is set
+  explicit Tensor(const interface::ITensor* view, bool copy_data = false, bool ring_memory = false);
+  // a slot of a request ring's page-locked block: `external` holds
+  // view->GetBytes() bytes, owned by the ring
+  Tensor(const interface::ITensor* view, char* external);
   ~Tensor() override;
   Tensor(const Tensor&) = delete;
   Tensor& operator=(const Tensor&) = delete;
 
   DataType GetType() const override { return type_; }
   void SetType(DataType type) override { type_ = type; }
-  const char* GetData() const override { return data_.data(); }
-  char* GetData() override { return data_.data(); }
+  const char* GetData() const override { return ext_ ? ext_ : data_.data(); }
+  char* GetData() override { return ext_ ? ext_ : data_.data(); }
   const int* GetDims() const override { return dims_.data(); }
   size_t GetNumDims() const override { return dims_.size(); }
   void SetDims(const std::vector<int>& dims) override;
-  size_t GetBytes() const override { return data_.size(); }
+  size_t GetBytes() const override { return ext_ ? ext_bytes_ : data_.size(); }
+  // the bytes came from the ring host allocator (page-locked)
+  bool IsRingMemory() const { return ext_ != nullptr; }
   const char* GetName() const override { return name_.c_str(); }
   Quantization GetQuantization() const override;
   absl::Status SetQuantization(Quantization quantization) override;
@@ -38,6 +55,9 @@ class Tensor : public interface::ITensor {
   DataType type_;
   std::vector<int> dims_;
   std::vector<char> data_;
+  char* ext_ = nullptr;  // ring-allocator memory (data_ unused then)
+  size_t ext_bytes_ = 0;
+  void (*ext_free_)(void*) = nullptr;
   std::string name_;
   QuantizationType qtype_ = QuantizationType::kNoQuantization;
   void* qparams_ = nullptr;  // TfLiteAffineQuantization layout, owned
@@ -61,6 +81,7 @@ class TensorRingBuffer {
  public:
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
                    int size = 128);
+  ~TensorRingBuffer();
   int Alloc();
   // takes `handle` itself (the head moves past it): a model's output slot
   // uses its request's input handle, so the input ring's per-slot
@@ -83,6 +104,10 @@ class TensorRingBuffer {
   absl::Status PutTensorToHandle(const interface::ITensor* src, int tensor_index, int handle);
   absl::Status GetTensorsFromHandle(std::vector<interface::ITensor*>& dst, int handle) const;
   absl::Status PutTensorsToHandle(const std::vector<interface::ITensor*>& src, int handle);
+  // the slot tensor of `tensor_index` for a valid handle, else nullptr: a
+  // batched pass reads a request's input from / writes its output into it
+  // directly (a handle stays valid while its request is unfinished)
+  Tensor* SlotTensor(int tensor_index, int handle);
 
  private:
   int Slot(int handle) const { return handle % size_; }
@@ -93,6 +118,11 @@ class TensorRingBuffer {
   mutable std::mutex head_mtx_;
   std::condition_variable slot_cv_;
   std::vector<char> busy_;  // per slot: taken by AllocBlocking[N], not yet released
+  // per tensor: one page-locked block holding every slot's bytes at a fixed
+  // stride (consecutive handles are adjacent, so a batched pass copies a
+  // run of them in one DMA); empty when no ring host allocator is set
+  std::vector<char*> blocks_;
+  void (*block_free_)(void*) = nullptr;
   int head_ = 0;
   int outstanding_ = 0;
 };

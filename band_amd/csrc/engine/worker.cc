@@ -180,21 +180,32 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   for (Job& p : partners) jobs.push_back(&p);
   const int n = static_cast<int>(jobs.size());
   const SubgraphKey key = head->subgraph_key;
-  std::vector<bool> copied(n, false);
+  std::vector<bool> copied(n, true);
   const int64_t t_in = time::NowMicros();
-  for (int i = 0; i < n; ++i) {
-    copied[i] = engine_->TryCopyInputTensorsToSlot(*jobs[i], n, i).ok();
-    if (!copied[i]) {
-      BAND_LOG(LogSeverity::kError, "worker %d failed to copy input of job %d", worker_id_, jobs[i]->job_id);
-      jobs[i]->status = JobStatus::kInputCopyFailure;
-    }
-  }
-  const int64_t invoke_time = time::NowMicros();
+  // the pass's I/O straight between the request rings and the device when
+  // the executor and the rings allow it; else staged through the slot views
+  int64_t invoke_time = time::NowMicros();
   {
     std::lock_guard<std::mutex> lock(device_mtx_);
     head->invoke_time = invoke_time;
   }
-  const absl::Status status = engine_->InvokeJobBatch(key, n);
+  absl::Status status = engine_->InvokeJobBatchDirect(key, jobs);
+  const bool direct = !absl::IsUnimplemented(status);
+  if (!direct) {
+    for (int i = 0; i < n; ++i) {
+      copied[i] = engine_->TryCopyInputTensorsToSlot(*jobs[i], n, i).ok();
+      if (!copied[i]) {
+        BAND_LOG(LogSeverity::kError, "worker %d failed to copy input of job %d", worker_id_, jobs[i]->job_id);
+        jobs[i]->status = JobStatus::kInputCopyFailure;
+      }
+    }
+    invoke_time = time::NowMicros();
+    {
+      std::lock_guard<std::mutex> lock(device_mtx_);
+      head->invoke_time = invoke_time;
+    }
+    status = engine_->InvokeJobBatch(key, n);
+  }
   const int64_t end_time = time::NowMicros();
   phase_us_[0].fetch_add(invoke_time - t_in, std::memory_order_relaxed);
   phase_us_[1].fetch_add(end_time - invoke_time, std::memory_order_relaxed);
@@ -205,6 +216,10 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
     if (!copied[i]) continue;
     if (!status.ok()) {
       j.status = JobStatus::kInvokeFailure;
+      continue;
+    }
+    if (direct) {  // the outputs are already in the request's output slot
+      j.status = JobStatus::kSuccess;
       continue;
     }
     const absl::Status out = engine_->TryCopyOutputTensorsFromSlot(j, n, i);

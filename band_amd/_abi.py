@@ -9,7 +9,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libband_hip.so")
+# BAND_HIP_LIB_VARIANT=x loads libband_hip_x.so instead: an in-tree build of
+# the same sources with one compile-time switch flipped, for A-B timing
+LIB_PATH = os.path.join(_HERE, "libband_hip%s.so" % (
+    "_" + os.environ["BAND_HIP_LIB_VARIANT"] if os.environ.get("BAND_HIP_LIB_VARIANT") else ""))
 
 c_int, c_int32, c_void_p, c_size_t = ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, ctypes.c_size_t
 

@@ -132,6 +132,23 @@ __device__ __forceinline__ ChanQ chan_q(int32_t mu, int32_t sh, int32_t zp) {
   return q;
 }
 
+// clamp to [lo, hi] in one v_med3_i32 (min(max()) compiles to two VALU
+// when both bounds are wave-uniform: gfx9's VOP3 reads one SGPR, so the
+// compiler will not form the med3 itself); BH_MED3=0 at build time keeps
+// min / max
+#ifndef BH_MED3
+#define BH_MED3 1
+#endif
+__device__ __forceinline__ int32_t med3_clamp(int32_t v, int32_t lo, int32_t hi) {
+#if BH_MED3
+  int32_t r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(v), "s"(lo), "v"(hi));
+  return r;
+#else
+  return min(max(v, lo), hi);
+#endif
+}
+
 template <bool FAST>
 __device__ __forceinline__ int32_t requant_out(int32_t acc, const ChanQ& q, int32_t zp, int32_t lo, int32_t hi) {
   int32_t v;
@@ -142,7 +159,7 @@ __device__ __forceinline__ int32_t requant_out(int32_t acc, const ChanQ& q, int3
   } else {
     v = requant(acc, q.mu, q.sh) + zp;
   }
-  return min(max(v, lo), hi);
+  return med3_clamp(v, lo, hi);
 }
 
 // requant + zero point + clamp, the single-step identity when `fast`

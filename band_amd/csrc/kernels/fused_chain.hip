@@ -266,8 +266,15 @@ __device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsig
   }
 }
 
+// BH_CHAIN_WPE (build-time A-B switch): ask the register allocator for at
+// least that many waves per SIMD on the raster chain forms
+#ifdef BH_CHAIN_WPE
+#define BH_CHAIN_OCC __attribute__((amdgpu_waves_per_eu(BH_CHAIN_WPE)))
+#else
+#define BH_CHAIN_OCC
+#endif
 template <int RB, bool FAST, int KX, int NW, bool AM, int DA = 2>
-__global__ __launch_bounds__(NW * 64) void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
+__global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];

@@ -539,7 +539,7 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     D.barrier()
     busy = sorted((((c1[k] - c0.get(k, 0.0)) / (t1 - t0), k[1]) for k in c1), reverse=True)
     HOST_THREADS.clear()
-    HOST_THREADS.update(busiest=[[n, round(b, 3)] for b, n in busy[:6]],
+    HOST_THREADS.update(busiest=[[n, round(b, 3)] for b, n in busy[:12]],
                         process_cpu_cores=round(sum(b for b, _ in busy), 2))
     # where the workers' wall time went over the timed loop (fractions of
     # workers x wall): input copies, invoke (launch + device sync), output

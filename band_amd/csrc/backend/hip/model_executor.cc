@@ -535,6 +535,10 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "nochain") == 0) allow_chain_ = false;
   if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
   if (f && std::strcmp(f, "forcetile") == 0) force_chain_ = force_tile_chain_ = true;  // ... in the tile form
+  if (f && std::strcmp(f, "forcetilepipe") == 0) {  // ... in the persistent tile form
+    force_chain_ = force_tile_chain_ = true;
+    tile_pipe_ = true;
+  }
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
@@ -1051,7 +1055,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 4;
+constexpr int kChainTuneVersion = 5;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1317,8 +1321,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
     if (force_tile_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
-      q.tile = 1;
-      if (bh_chain_lds_bytes(&q) > 0) choice += 400;
+      q.tile = tile_pipe_ ? 2 : 1;
+      if (bh_chain_lds_bytes(&q) > 0) choice += tile_pipe_ ? 500 : 400;
     }
     if (force_deep_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
@@ -1348,6 +1352,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
         // {.., tile}: the 2-D tile form (8 x 8 pixels, one LDS-DMA burst)
         // {.., deep}: the deep-issue raster forms
+        // (the persistent tile form, tile 2, measured slower than the
+        // one-tile workgroups on every MobileNetV2 chain,
+        // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
         const int forms[10][5] = {{4, 4, 0, 0, 0}, {2, 4, 0, 0, 0}, {1, 4, 0, 0, 0}, {1, 8, 0, 0, 0},
                                   {1, 16, 0, 0, 0}, {4, 4, 1, 0, 0}, {4, 4, 0, 1, 0}, {2, 4, 0, 0, 1},
                                   {1, 4, 0, 0, 1}, {1, 8, 0, 0, 1}};
@@ -1372,7 +1379,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0) + (pw[3] ? 400 : 0) + (pw[4] ? 1000 : 0);
+                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) + (pw[4] ? 1000 : 0);
             }
           }
         }
@@ -1386,7 +1393,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
-    // form, +1000 for the deep-issue form
+    // form, +500 for the persistent tile form, +1000 for the deep-issue form
     const int deep = choice >= 1000 ? 1 : 0;
     choice %= 1000;
     const bool three = choice > 0 && choice % 100 < 10;
@@ -1401,7 +1408,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.px_blocks = choice % 10;
     F.chain.waves = choice >= 300 && choice < 400 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
-    F.chain.tile = choice >= 400 && choice < 500 ? 1 : 0;
+    F.chain.tile = choice >= 400 && choice < 500 ? 1 : (choice >= 500 && choice < 600 ? 2 : 0);
     F.chain.deep = deep;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then

@@ -222,6 +222,7 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   bool allow_chain_ = true;   // BAND_HIP_FUSION=nochain
   bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
   bool force_tile_chain_ = false;  // BAND_HIP_FUSION=forcetile: every feasible chain in the tile form
+  bool tile_pipe_ = false;         // BAND_HIP_FUSION=forcetilepipe: ... in the persistent tile form
   bool no_tile_chain_ = false;     // BAND_HIP_FUSION=notile: the tuner skips the tile form
   bool no_deep_chain_ = false;     // BAND_HIP_FUSION=nodeep: the tuner skips the deep-issue forms
   bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form

@@ -116,11 +116,14 @@ struct TileGeom {
   int u_patch;         // 16-byte units of the patch
   int off_res, off_blob, blob_units;
   int off_dl, off_pl, off_o1, off_add, off_out;
+  int buf_bytes;  // patch + residual region (pipe: the second one follows it)
   TileBlob blob;
   size_t bytes;
 };
 
-__host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, int TW) {
+// pipe: the persistent form's layout - two patch + residual buffers (the
+// next tile's DMA lands in one while the other is computed), then the rest
+__host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, int TW, bool pipe = false) {
   TileGeom g{};
   const bh_dwconv_params& d = p.dw;
   const int C = d.out_c;
@@ -142,6 +145,9 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
   size_t o = (size_t)g.u_patch * 16;
   g.off_res = (int)o;
   o += p.pw1.residual ? (size_t)rows * N1 : 0;
+  o = (o + 15) / 16 * 16;
+  g.buf_bytes = (int)o;  // one patch + residual buffer
+  if (pipe) o += g.buf_bytes;
   g.off_blob = (int)o;
   g.blob = tile_blob(p);
   g.blob_units = g.blob.bytes / 16;
@@ -167,6 +173,8 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
 
 struct TileDivs {
   FastDiv tiles_x, txy, patch_ru, res_ru4;
+  int per;     // PIPE: consecutive tiles per workgroup
+  int ntiles;  // batch x tiles
 };
 
 // the staged [rows][Nc] tile (row = tile pixel) to HBM: tile row i (TW
@@ -217,7 +225,11 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
   *(uint32_t*)(blob + o) = v;
 }
 
-template <int TH, int TW, bool FAST, int KX>
+// PIPE: the persistent form - a workgroup walks dv.per consecutive tiles,
+// the constant block staged once, and each tile's patch + residual DMA is
+// issued into the other buffer before the current tile's phases run, so it
+// lands under their compute (bh_chain_params.tile == 2)
+template <int TH, int TW, bool FAST, int KX, bool PIPE>
 __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv) {
   static_assert(TH * TW == 64, "4 pixel blocks of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -233,11 +245,18 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   const int OH = d.out_h, OW = d.out_w;
 
   const int logical = xcd_block(blockIdx.x, gridDim.x);
-  const int n = dv.txy.div(logical);  // grid = batch x tiles (launch-side exact)
-  const int rem = logical - n * (int)dv.txy.d;
-  const int ty = dv.tiles_x.div(rem);
-  const int tx = rem - ty * G.tiles_x;
-  const int oy0 = ty * TH, ox0 = tx * TW;
+  // this workgroup's tiles: one (grid = batch x tiles), or PIPE's run of
+  // dv.per consecutive ones (neighbours share their halo rows in one L2)
+  const int t_first = PIPE ? logical * dv.per : logical;
+  const int t_count = PIPE ? min(dv.per, dv.ntiles - t_first) : 1;
+  if (t_count <= 0) return;
+  auto tile_xy = [&](int t, int& n, int& oy0, int& ox0) {
+    n = dv.txy.div(t);
+    const int rem = t - n * (int)dv.txy.d;
+    const int ty = dv.tiles_x.div(rem);
+    oy0 = ty * TH;
+    ox0 = (rem - ty * G.tiles_x) * TW;
+  };
   unsigned long long* stamps =
       cp.debug_stamps ? (unsigned long long*)cp.debug_stamps + 8 * (long)blockIdx.x : nullptr;
 #define TILE_STAMP(k) \
@@ -245,8 +264,11 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   TILE_STAMP(0)
   if (stamps && tid == 0) stamps[7] = t_entry;
 
-  // ---- one burst of LDS-DMA: patch, residual, constant block ---------------
-  {
+  // ---- LDS-DMA: patch + residual of a tile into buffer `buf`; the constant
+  // block once -----------------------------------------------------------
+  auto issue_tile = [&](int t, unsigned char* buf) {
+    int n, oy0, ox0;
+    tile_xy(t, n, oy0, ox0);
     const int C = d.out_c;
     const uint8_t* in = (const uint8_t*)d.input;
     const long in_last = (long)d.batch * d.in_h * d.in_w * C - 16;
@@ -260,7 +282,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
         const int y = min(max(y0 + r, 0), d.in_h - 1);
         long off = (row0 + y) * d.in_w * C + xoff + (u - r * G.patch_ru) * 16;
         off = off < 0 ? 0 : (off > in_last ? in_last : off);
-        dma16(in + off, smem + base * 16);
+        dma16(in + off, buf + base * 16);
       }
     }
     if (a.residual) {
@@ -275,10 +297,13 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
           const int y = min(oy0 + r, OH - 1);
           long off = ((long)(n * OH + y) * OW + ox0) * N1 + (u - r * G.res_ru4) * 4;
           off = off > res_last ? res_last : off;
-          dma4(res + off, smem + G.off_res + base * 4);
+          dma4(res + off, buf + G.off_res + base * 4);
         }
       }
     }
+  };
+  issue_tile(t_first, smem);
+  {
     const unsigned char* blob = (const unsigned char*)cp.tile_blob;
     for (int base = wave * 64; base < G.blob_units; base += 256)
       if (base + lane < G.blob_units) dma16(blob + (base + lane) * 16, smem + G.off_blob + base * 16);
@@ -299,14 +324,22 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   TILE_STAMP(2)
 
   const unsigned char* cb = smem + G.off_blob;
-  const unsigned char* patch = smem;
-  const unsigned char* resl = smem + G.off_res;
   unsigned char* dl = smem + G.off_dl;
   unsigned char* pl = smem + G.off_pl;
   unsigned char* o1 = smem + G.off_o1;
-  unsigned char* ol = smem + G.off_out;
   const int pb = wave;               // this wave's 16-pixel block of the tile
   const int orow = pb * 16 + 4 * g;  // first of this lane's 4 result rows
+
+  for (int it = 0; it < t_count; ++it) {
+  unsigned char* cur = smem + (PIPE ? (it & 1) * G.buf_bytes : 0);
+  const unsigned char* patch = cur;
+  const unsigned char* resl = cur + G.off_res;
+  // the second 1x1's staging: the current patch (dead after phase A) when it fits
+  unsigned char* ol = G.off_out == 0 ? cur : smem + G.off_out;
+  int n, oy0, ox0;
+  tile_xy(t_first + it, n, oy0, ox0);
+  // the next tile's patch + residual into the other buffer, under this one's phases
+  if (PIPE && it + 1 < t_count) issue_tile(t_first + it + 1, smem + ((it + 1) & 1) * G.buf_bytes);
 
   // ---- phase A: depthwise 3x3 from the patch -> dl ------------------------
   {
@@ -433,7 +466,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   __syncthreads();
   TILE_STAMP(4)
   if (a.output) tile_copy_out(o1, (uint8_t*)a.output, a.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256);
-  if (!cp.has_pw2) return;
+  if (cp.has_pw2) {
 
   // ---- phase C: second 1x1 from pl -> ol (staged) -> HBM -------------------
   {
@@ -477,16 +510,24 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   TILE_STAMP(5)
   tile_copy_out(ol, (uint8_t*)b.output, b.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256);
   TILE_STAMP(6)
+  }  // has_pw2
+  if (PIPE && it + 1 < t_count) {
+    // the next tile's DMA has landed (this wave's part; the barrier covers
+    // every wave's), and every read of this tile's buffers is done
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  }  // tiles
 #undef TILE_STAMP
 }
 
-template <int TH, int TW, bool FAST, int KX>
+template <int TH, int TW, bool FAST, int KX, bool PIPE>
 static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s) {
   static thread_local int opted_device = -1;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (opted_device != dev) {
-    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX>,
+    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX, PIPE>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     opted_device = dev;
   }
@@ -495,8 +536,27 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
   dv.txy = FastDiv(G.tiles_x * G.tiles_y);
   dv.patch_ru = FastDiv(G.patch_ru);
   dv.res_ru4 = FastDiv(G.res_ru4 > 0 ? G.res_ru4 : 1);
-  const int blocks = p.dw.batch * G.tiles_y * G.tiles_x;
-  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv);
+  dv.ntiles = p.dw.batch * G.tiles_y * G.tiles_x;
+  dv.per = 1;
+  int blocks = dv.ntiles;
+  if (PIPE) {
+    // one wave of resident workgroups (LDS and registers permitting, <= 4 per
+    // CU on 256 CUs), each taking a run of consecutive tiles
+    static thread_local size_t cached_lds = 0;
+    static thread_local int cached_per_cu = 1;
+    if (cached_lds != G.bytes) {
+      int nb = 0;
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_tile_kernel<TH, TW, FAST, KX, PIPE>, 256, G.bytes) !=
+          hipSuccess)
+        nb = 1;
+      cached_per_cu = std::max(1, std::min(4, nb));
+      cached_lds = G.bytes;
+    }
+    const int slots = 256 * cached_per_cu;
+    dv.per = (dv.ntiles + slots - 1) / slots;
+    blocks = (dv.ntiles + dv.per - 1) / dv.per;
+  }
+  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX, PIPE>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv);
 }
 
 }  // namespace bh
@@ -507,13 +567,13 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
 extern "C" size_t bh_chain_tile_lds_bytes(const bh_chain_params* pp) {
   const bh_chain_params& p = *pp;
   const bh_dwconv_params& d = p.dw;
-  if (p.tile != 1) return 0;
+  if (p.tile != 1 && p.tile != 2) return 0;  // 2: the persistent pipelined form
   if (d.stride_h < 1 || d.stride_h > 2 || d.stride_w < 1 || d.stride_w > 2 || d.dil_h < 1 || d.dil_h > 2 ||
       d.dil_w < 1 || d.dil_w > 2)
     return 0;
   if (p.has_pw2 && p.pw2.k_pad > 64 * 5) return 0;
   if ((long)d.batch * d.in_h * d.in_w * d.in_c < 16) return 0;
-  const bh::TileGeom G = bh::tile_geom(p, 8, 8);
+  const bh::TileGeom G = bh::tile_geom(p, 8, 8, p.tile == 2);
   // a workgroup's grid index and the DMA unit counts stay in int range
   if ((long)d.batch * G.tiles_y * G.tiles_x >= INT32_MAX / 2) return 0;
   return G.bytes <= 160 * 1024 ? G.bytes : 0;
@@ -546,16 +606,24 @@ extern "C" int bh_chain_tile_launch(const bh_chain_params* pp, bh_stream_t strea
     bh_set_last_error("bh_chain_i8: the tile form needs tile_blob (bh_chain_tile_pack)");
     return BH_EINVAL;
   }
-  const bh::TileGeom G = bh::tile_geom(p, 8, 8);
+  const bool pipe = p.tile == 2;
+  const bh::TileGeom G = bh::tile_geom(p, 8, 8, pipe);
   const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast);
   const bool k2 = !p.has_pw2 || p.pw2.k_pad <= 128;
   hipStream_t s = (hipStream_t)stream;
-  if (k2) {
-    if (fast) bh::launch_tile<8, 8, true, 2>(p, G, s);
-    else bh::launch_tile<8, 8, false, 2>(p, G, s);
-  } else {
-    if (fast) bh::launch_tile<8, 8, true, 5>(p, G, s);
-    else bh::launch_tile<8, 8, false, 5>(p, G, s);
+#define BH_TILE(PIPE)                                                  \
+  if (k2) {                                                            \
+    if (fast) bh::launch_tile<8, 8, true, 2, PIPE>(p, G, s);           \
+    else bh::launch_tile<8, 8, false, 2, PIPE>(p, G, s);               \
+  } else {                                                             \
+    if (fast) bh::launch_tile<8, 8, true, 5, PIPE>(p, G, s);           \
+    else bh::launch_tile<8, 8, false, 5, PIPE>(p, G, s);               \
   }
+  if (pipe) {
+    BH_TILE(true)
+  } else {
+    BH_TILE(false)
+  }
+#undef BH_TILE
   return bh_check_launch("chain_tile_kernel");
 }

@@ -336,7 +336,10 @@ typedef struct bh_chain_params {
    * output pixels and stages its depthwise input patch (tile + halo), the
    * residual tile, both 1x1 filters and every table in LDS with one burst of
    * LDS-DMA; stride / dilation 1 or 2, pw2 K <= 320.  px_blocks, waves and
-   * persist are ignored */
+   * persist are ignored.  2: the same tile in a persistent workgroup that
+   * walks a run of consecutive tiles, the constant block staged once and
+   * each tile's patch + residual DMA issued into a second buffer under the
+   * previous tile's phases */
   int tile;
   /* tile form: the chain's constant block (both 1x1 filters swizzled for
    * LDS, every table, the depthwise filter) built once by

@@ -75,10 +75,10 @@ def test_chain_general(gpu_lib, args):
         _check(c, gpu_lib, 4, persist=1)
 
 
-def _tile_fits(c, lib):
+def _tile_fits(c, lib, tile=1):
     import ctypes
     keep = []
-    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, 4, keep, 4, 0, 1))) > 0
+    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, 4, keep, 4, 0, tile))) > 0
 
 
 @pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)
@@ -94,9 +94,14 @@ def test_chain_tile_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
             # stay with the raster forms
             assert ce >= 384, "tile form should cover the %dx%dx%d chain" % (h, h, ce)
             continue
+        pipe = _tile_fits(c, gpu_lib, 2)  # persistent, double-buffered: two patches in LDS
         _check(c, gpu_lib, 4, tile=1)
+        if pipe:
+            _check(c, gpu_lib, 4, tile=2)
         c.fast = False
         _check(c, gpu_lib, 4, tile=1)
+        if pipe:
+            _check(c, gpu_lib, 4, tile=2)
 
 
 @pytest.mark.parametrize("args", [
@@ -118,6 +123,8 @@ def test_chain_tile_general(gpu_lib, args):
     c = ChainCase(rng, **args)
     assert _tile_fits(c, gpu_lib)
     _check(c, gpu_lib, 4, tile=1)
+    if _tile_fits(c, gpu_lib, 2):
+        _check(c, gpu_lib, 4, tile=2)
 
 
 def test_chain_tile_rejects(gpu_lib):
@@ -126,7 +133,7 @@ def test_chain_tile_rejects(gpu_lib):
     keep = []
     c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep, tile=1)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
-    c.tile = 2  # no such form
+    c.tile = 3  # no such form (2 is the persistent tile form)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
     assert gpu_lib.bh_chain_i8(ctypes.byref(c), None) != 0
     c.tile = 1
@@ -163,7 +170,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile", "forcedeep"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param
@@ -189,7 +196,7 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
     key = SubgraphKey(41, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
     assert "chain_kernel" in kernels or "chain_tile_kernel" in kernels, kernels
-    if forcechain == "forcetile":
+    if forcechain in ("forcetile", "forcetilepipe"):
         assert "chain_tile_kernel" in kernels, kernels
     for rep in range(2):  # eager, then graph replay
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]

@@ -21,8 +21,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,1d,1w8d,2d",
-                    help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form")
+    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,tp,1d,1w8d,2d",
+                    help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form, "
+                         "tp = its persistent double-buffered variant")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
@@ -39,8 +40,8 @@ def main():
         c = ChainCase(np.random.default_rng(1), a.batch, h, h, ce, s, cout, res, ce2)
         row = []
         for form in a.px.split(","):
-            tile = int(form == "t")
-            persist = int(form.endswith("p"))
+            tile = 1 if form == "t" else (2 if form == "tp" else 0)
+            persist = int(form.endswith("p") and not tile)
             deep = int(form.endswith("d"))
             f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)

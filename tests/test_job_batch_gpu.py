@@ -74,11 +74,15 @@ def test_job_batches_refused_for_custom_ops(gpu_lib):
     assert ex.MaxJobBatch(key) == 1
 
 
+@pytest.mark.parametrize("direct", ["1", "0"])
 @pytest.mark.parametrize("sched,workers", [(SchedulerType.kFixedWorker, 1), (SchedulerType.kRoundRobin, 2)])
-def test_engine_batches_queued_jobs_bit_exact(gpu_lib, tmp_path, sched, workers):
+def test_engine_batches_queued_jobs_bit_exact(gpu_lib, tmp_path, monkeypatch, sched, workers, direct):
     """max_job_batch 8: fixed_worker's queued jobs / round_robin's same-model
     requests handed to an idle worker run together (same invoke / end time
-    in their job records), each output equal to the oracle's"""
+    in their job records), each output equal to the oracle's; with the
+    passes' I/O DMA'd straight between the page-locked request rings and the
+    device (direct, the default) and staged through the slot views"""
+    monkeypatch.setenv("BAND_HIP_DIRECT_IO", direct)
     e = Engine(make_config([sched], [DeviceFlag.kGPU] * workers, max_job_batch=8))
     rng = np.random.default_rng(4)
     models = []
@@ -109,4 +113,43 @@ def test_engine_batches_queued_jobs_bit_exact(gpu_lib, tmp_path, sched, workers)
         for k, t in enumerate(sorted(om.outputs)):
             np.testing.assert_array_equal(outs[k].data().reshape(-1), ref[t].reshape(-1))
     assert max(len(v) for v in invoke.values()) > 1, "no two jobs shared a batched pass"
+    e.close()
+
+
+def test_engine_direct_io_across_ring_wrap(gpu_lib, tmp_path, monkeypatch):
+    """more requests of one model than its request ring has slots (20), in
+    rounds of 16 submitted at once: batched passes whose slots straddle the
+    ring's end are split into contiguous DMA runs; every output equals the
+    oracle's"""
+    monkeypatch.setenv("BANDX_REQUEST_RING_SLOTS", "20")
+    e = Engine(make_config([SchedulerType.kFixedWorker], [DeviceFlag.kGPU], max_job_batch=8))
+    buf = tflite_synth.mobilenet_v2(np.int8, size=96)
+    path = str(tmp_path / "mnv2.tflite")
+    with open(path, "wb") as f:
+        f.write(buf)
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    om = OModel(buf)
+    rng = np.random.default_rng(12)
+    shared = 0
+    for rnd in range(3):
+        jobs = []
+        for i in range(16):
+            t = e.CreateInputTensor(m, 0)
+            x = rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8)
+            t.data()[...] = x
+            outs = [e.CreateOutputTensor(m, k) for k in range(e.GetNumOutputTensors(m))]
+            jobs.append((e.RequestAsync(m, [t]), x, outs))
+        invoke = {}
+        for h, x, outs in jobs:
+            assert h >= 0 and e.Wait(h, outs) == kBandOk
+            r = e.GetJobRecord(h)
+            assert r.status == JobStatus.kSuccess
+            invoke.setdefault((r.invoke_time_us, r.end_time_us), []).append(h)
+            ref = OracleInterpreter(om).run({om.inputs[0]: x})
+            for k, t in enumerate(sorted(om.outputs)):
+                np.testing.assert_array_equal(outs[k].data().reshape(-1), ref[t].reshape(-1))
+        shared += max(len(v) for v in invoke.values()) > 1
+    assert shared > 0, "no batched pass"
     e.close()

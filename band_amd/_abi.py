@@ -180,6 +180,12 @@ KERNEL_SYMBOLS = {
     "bh_graph_destroy": (c_int, [c_void_p]),
     "bh_event_create": (c_int, [ctypes.POINTER(c_void_p)]),
     "bh_event_create_blocking": (c_int, [ctypes.POINTER(c_void_p)]),
+    "bh_capture_end_keep": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p)]),
+    "bh_graph_free": (c_int, [c_void_p]),
+    "bh_graph_memcpy_nodes": (c_int, [c_void_p, ctypes.POINTER(c_void_p), ctypes.POINTER(c_void_p),
+                                      ctypes.POINTER(c_void_p), ctypes.POINTER(c_size_t), c_int,
+                                      ctypes.POINTER(c_int)]),
+    "bh_graph_exec_set_memcpy": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_int]),
     "bh_event_destroy": (c_int, [c_void_p]),
     "bh_event_record": (c_int, [c_void_p, c_void_p]),
     "bh_event_sync": (c_int, [c_void_p]),

@@ -83,8 +83,7 @@ HipModelExecutor::~HipModelExecutor() {
   if (ordinal_ >= 0) {
     bh_set_device(ordinal_);
     if (stream_) bh_stream_sync(stream_);
-    for (auto& kv : subgraphs_)
-      if (kv.second->graph) bh_graph_destroy(kv.second->graph);
+    for (auto& kv : subgraphs_) DropGraph(kv.second.get());
     if (done_event_) bh_event_destroy(done_event_);
   }
   subgraphs_.clear();
@@ -2195,7 +2194,7 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
   }
   SubgraphKey key(model->GetId(), worker_id_, unit_indices);
   auto old = subgraphs_.find(key);
-  if (old != subgraphs_.end() && old->second->graph) bh_graph_destroy(old->second->graph);
+  if (old != subgraphs_.end()) DropGraph(old->second.get());
   subgraphs_[key] = std::move(sg);
   return absl::OkStatus();
 }
@@ -2262,10 +2261,7 @@ std::shared_ptr<interface::ITensorView> HipModelExecutor::GetTensorView(const Su
     sg->host[index] = std::move(buf);
     sg->extra_d2h.insert(index);
     if (ordinal_ >= 0) bh_set_device(ordinal_);
-    if (sg->graph) {
-      bh_graph_destroy(sg->graph);
-      sg->graph = nullptr;
-    }
+    DropGraph(sg);
     if (sg->fused_tensors.count(index)) {
       // the tensor was folded away by an epilogue fusion: re-lower with it materialised
       sg->no_fuse.insert(index);
@@ -2363,9 +2359,82 @@ absl::Status HipModelExecutor::EnqueueLaunches(PreparedSubgraph* sg) {
   return absl::OkStatus();
 }
 
+void HipModelExecutor::DropGraph(PreparedSubgraph* sg) {
+  if (sg->graph) bh_graph_destroy(sg->graph);
+  if (sg->graph_tmpl) bh_graph_free(sg->graph_tmpl);
+  sg->graph = nullptr;
+  sg->graph_tmpl = nullptr;
+  sg->io_nodes.clear();
+  sg->io_retargeted = false;
+}
+
+absl::Status HipModelExecutor::RestoreIoNodes(PreparedSubgraph* sg) {
+  if (!sg->io_retargeted) return absl::OkStatus();
+  char* arena = static_cast<char*>(sg->arena->ptr());
+  for (const auto& n : sg->io_nodes) {
+    char* dev = arena + sg->offset.at(n.tensor);
+    char* host = sg->host.at(n.tensor)->data();
+    const int rc = bh_graph_exec_set_memcpy(sg->graph, n.node, n.h2d ? (void*)dev : (void*)host,
+                                            n.h2d ? (const void*)host : (const void*)dev, meta_[n.tensor]->bytes,
+                                            n.h2d ? 1 : 0);
+    if (rc) return HipErr(rc, "graph copy node");
+  }
+  sg->io_retargeted = false;
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::CaptureGraph(PreparedSubgraph* sg) {
+  size_t io_bytes = 0;
+  for (int t : sg->inputs) io_bytes += meta_[t]->bytes;
+  for (int t : sg->outputs) io_bytes += meta_[t]->bytes;
+  for (int t : sg->extra_d2h) io_bytes += meta_[t]->bytes;
+  sg->io_in_graph = io_mode_ == 0 || (io_mode_ == 2 && io_bytes < io_stream_bytes_);
+  int rc = bh_capture_begin(stream_);
+  if (rc) return HipErr(rc, "capture begin");
+  absl::Status s = sg->io_in_graph ? Enqueue(sg) : EnqueueLaunches(sg);
+  bh_graph_exec_t g = nullptr;
+  void* tmpl = nullptr;
+  rc = bh_capture_end_keep(stream_, &g, &tmpl);
+  if (!s.ok()) {
+    if (!rc) {
+      bh_graph_destroy(g);
+      bh_graph_free(tmpl);
+    }
+    return s;
+  }
+  if (rc) return HipErr(rc, "capture end");
+  sg->graph = g;
+  sg->graph_tmpl = tmpl;
+  sg->io_nodes.clear();
+  sg->io_retargeted = false;
+  if (sg->io_in_graph) {
+    // the copy nodes, told apart by their device-side address: input t's
+    // H2D writes arena + offset(t), output t's D2H reads it
+    constexpr int kMax = 64;
+    void* nodes[kMax];
+    void* dsts[kMax];
+    const void* srcs[kMax];
+    size_t bytes[kMax];
+    int n = 0;
+    char* arena = static_cast<char*>(sg->arena->ptr());
+    if (bh_graph_memcpy_nodes(tmpl, nodes, dsts, srcs, bytes, kMax, &n) == 0 && n <= kMax) {
+      for (int i = 0; i < n; ++i) {
+        for (int t : sg->inputs)
+          if (dsts[i] == arena + sg->offset.at(t) && bytes[i] == meta_[t]->bytes) sg->io_nodes.push_back({nodes[i], t, true});
+        for (int t : sg->outputs)
+          if (srcs[i] == arena + sg->offset.at(t) && bytes[i] == meta_[t]->bytes) sg->io_nodes.push_back({nodes[i], t, false});
+      }
+      if (sg->io_nodes.size() != sg->inputs.size() + sg->outputs.size()) sg->io_nodes.clear();
+    }
+  }
+  return absl::OkStatus();
+}
+
 absl::Status HipModelExecutor::EnqueuePass(PreparedSubgraph* sg) {
   if (!use_graph_ || !sg->graph) return Enqueue(sg);
+  RETURN_STATUS_IF(RestoreIoNodes(sg));
   if (!sg->io_in_graph) RETURN_STATUS_IF(EnqueueInputs(sg));
+
   const int rc = bh_graph_launch(sg->graph, stream_);
   if (rc) return HipErr(rc, "graph launch");
   return sg->io_in_graph ? absl::OkStatus() : EnqueueOutputs(sg);
@@ -2459,21 +2528,7 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   PinCallingThreadToGpu(ordinal_);
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
-  if (use_graph_ && !sg->graph && sg->runs > 0) {
-    rc = bh_capture_begin(stream_);
-    if (rc) return HipErr(rc, "capture begin");
-    size_t io_bytes = 0;
-    for (int t : sg->inputs) io_bytes += meta_[t]->bytes;
-    for (int t : sg->outputs) io_bytes += meta_[t]->bytes;
-    for (int t : sg->extra_d2h) io_bytes += meta_[t]->bytes;
-    sg->io_in_graph = io_mode_ == 0 || (io_mode_ == 2 && io_bytes < io_stream_bytes_);
-    absl::Status s = sg->io_in_graph ? Enqueue(sg) : EnqueueLaunches(sg);
-    bh_graph_exec_t g = nullptr;
-    rc = bh_capture_end(stream_, &g);
-    if (!s.ok()) return s;
-    if (rc) return HipErr(rc, "capture end");
-    sg->graph = g;
-  }
+  if (use_graph_ && !sg->graph && sg->runs > 0) RETURN_STATUS_IF(CaptureGraph(sg));
   RETURN_STATUS_IF(EnqueuePass(sg));
   if (block_sync_) {
     if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
@@ -2561,8 +2616,52 @@ absl::Status HipModelExecutor::ExecuteJobBatch(const SubgraphKey& key, int n) {
 absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int n,
                                                      const std::vector<const interface::ITensor*>& in,
                                                      const std::vector<interface::ITensor*>& out) {
-  if (device_flag_ != DeviceFlag::kGPU || n < 2 || !direct_io_) return absl::UnimplementedError("direct job batch I/O");
+  if (device_flag_ != DeviceFlag::kGPU || n < 1 || !direct_io_) return absl::UnimplementedError("direct job batch I/O");
   PreparedSubgraph* base = Find(key);
+  if (n == 1) {
+    // one job: the captured graph's own copy nodes, pointed at the job's
+    // ring slots for this pass (back at the mirrors before any staged pass)
+    if (!base || !use_graph_ || !base->graph || !base->io_in_graph || base->io_nodes.empty() ||
+        !base->extra_d2h.empty() || in.size() != base->inputs.size() || out.size() != base->outputs.size())
+      return absl::UnimplementedError("direct job batch I/O");
+    for (size_t k = 0; k < in.size(); ++k)
+      if (!in[k] || in[k]->GetBytes() != meta_[base->inputs[k]]->bytes)
+        return absl::InternalError("direct job I/O: input size");
+    for (size_t k = 0; k < out.size(); ++k)
+      if (out[k] && out[k]->GetBytes() != meta_[base->outputs[k]]->bytes)
+        return absl::InternalError("direct job I/O: output size");
+    PinCallingThreadToGpu(ordinal_);
+    int rc = bh_set_device(ordinal_);
+    if (rc) return HipErr(rc, "hipSetDevice");
+    char* arena = static_cast<char*>(base->arena->ptr());
+    for (const auto& nd : base->io_nodes) {
+      char* dev = arena + base->offset.at(nd.tensor);
+      const size_t bytes = meta_[nd.tensor]->bytes;
+      if (nd.h2d) {
+        const size_t k = std::find(base->inputs.begin(), base->inputs.end(), nd.tensor) - base->inputs.begin();
+        rc = bh_graph_exec_set_memcpy(base->graph, nd.node, dev, in[k]->GetData(), bytes, 1);
+      } else {
+        const size_t k = std::find(base->outputs.begin(), base->outputs.end(), nd.tensor) - base->outputs.begin();
+        char* host = out[k] ? out[k]->GetData() : base->host.at(nd.tensor)->data();
+        rc = bh_graph_exec_set_memcpy(base->graph, nd.node, host, dev, bytes, 0);
+      }
+      if (rc) return HipErr(rc, "graph copy node");
+    }
+    base->io_retargeted = true;
+    rc = bh_graph_launch(base->graph, stream_);
+    if (rc) return HipErr(rc, "graph launch");
+    if (block_sync_) {
+      if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
+      rc = bh_event_record(done_event_, stream_);
+      if (!rc) rc = bh_event_sync(done_event_);
+    } else {
+      rc = bh_stream_sync(stream_);
+    }
+    if (rc) return HipErr(rc, "stream sync");
+    ++base->runs;
+    return absl::OkStatus();
+  }
+
   const JobBatchVariant* v = VariantFor(key, n);
   if (!base || !v) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
   if (in.size() != base->inputs.size() * n || out.size() != base->outputs.size() * n)
@@ -2590,16 +2689,9 @@ absl::Status HipModelExecutor::RunDirect(PreparedSubgraph* sg, int n, const std:
   PinCallingThreadToGpu(ordinal_);
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
-  if (use_graph_ && !sg->graph && sg->runs > 0) {  // kernels-only graph
-    rc = bh_capture_begin(stream_);
-    if (rc) return HipErr(rc, "capture begin");
-    absl::Status s = EnqueueLaunches(sg);
-    bh_graph_exec_t g = nullptr;
-    rc = bh_capture_end(stream_, &g);
-    if (!s.ok()) return s;
-    if (rc) return HipErr(rc, "capture end");
-    sg->graph = g;
-    sg->io_in_graph = false;
+  if (use_graph_ && !sg->graph && sg->runs > 0) {  // kernels-only graph (variants stream their I/O)
+    RETURN_STATUS_IF(CaptureGraph(sg));
+    if (sg->io_in_graph) return absl::UnimplementedError("direct job batch I/O");
   }
   char* arena = static_cast<char*>(sg->arena->ptr());
   // jobs whose host tensors are adjacent (consecutive ring slots of one

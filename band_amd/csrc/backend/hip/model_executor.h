@@ -104,6 +104,17 @@ struct PreparedSubgraph {
   std::vector<std::shared_ptr<DeviceBlob>> consts;
   bh_graph_exec_t graph = nullptr;
   bool io_in_graph = true;  // the graph holds the host copies (set at capture)
+  // with io_in_graph: the captured graph and its host-copy nodes, so a
+  // one-job pass can point them at the request rings' slots
+  // (ExecuteJobBatchDirect, n == 1) and back at the host mirrors
+  void* graph_tmpl = nullptr;
+  struct IoNode {
+    void* node;
+    int tensor;
+    bool h2d;
+  };
+  std::vector<IoNode> io_nodes;
+  bool io_retargeted = false;  // the nodes point at ring slots
   int runs = 0;
 };
 
@@ -195,6 +206,12 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   absl::Status EnqueueOutputs(PreparedSubgraph* sg);
   // one pass: the graph (captured on first use) or the eager launches
   absl::Status EnqueuePass(PreparedSubgraph* sg);
+  // captures sg's pass into its graph (host copies inside when io_in_graph)
+  absl::Status CaptureGraph(PreparedSubgraph* sg);
+  // drops sg's graph (and its captured template / copy nodes)
+  void DropGraph(PreparedSubgraph* sg);
+  // points sg's graph copy nodes at the host mirrors again
+  absl::Status RestoreIoNodes(PreparedSubgraph* sg);
   // a job-batch variant's pass with each job's I/O copied straight between
   // host tensors and its slot of the boundary tensors (per_job: the
   // batch-1 bytes of each input, then of each output)

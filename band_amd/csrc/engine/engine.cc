@@ -746,7 +746,7 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
   auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
   interface::IModelExecutor* exec = GetModelExecutor(key);
   const int n = static_cast<int>(jobs.size());
-  if (!jb || !exec || n < 2) return absl::UnimplementedError("direct job batch I/O");
+  if (!jb || !exec || n < 1) return absl::UnimplementedError("direct job batch I/O");
   const ModelId model = jobs[0]->model_id;
   auto in_it = model_input_buffer_.find(model);
   auto out_it = model_output_buffer_.find(model);
@@ -758,7 +758,7 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
   std::vector<interface::ITensor*> out(outs.size() * n, nullptr);
   for (int s = 0; s < n; ++s) {
     const Job& j = *jobs[s];
-    if (j.model_id != model || j.input_handle < 0 || j.output_handle < 0)
+    if (j.model_id != model || j.input_handle < 0 || j.output_handle < 0 || !j.following_jobs.empty())
       return absl::UnimplementedError("job without request slots");
     for (size_t k = 0; k < ins.size(); ++k) {
       Tensor* t = in_it->second->SlotTensor(ins[k], j.input_handle);
@@ -766,7 +766,9 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
       in[k * n + s] = t;
     }
     for (size_t k = 0; k < outs.size(); ++k) {
-      if (!out_it->second->IsTensorIndexValid(outs[k])) continue;
+      // a subgraph output outside the output ring feeds a later subgraph:
+      // it must reach the executor's own views
+      if (!out_it->second->IsTensorIndexValid(outs[k])) return absl::UnimplementedError("intermediate output");
       Tensor* t = out_it->second->SlotTensor(outs[k], j.output_handle);
       if (!t || !t->IsRingMemory()) return absl::UnimplementedError("output slot not page-locked");
       out[k * n + s] = t;

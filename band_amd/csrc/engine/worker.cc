@@ -132,7 +132,27 @@ void Worker::Work() {
       }
     }
     const int64_t t_in = time::NowMicros();
-    if (engine_->TryCopyInputTensors(*job).ok()) {
+    // a whole-model job whose executor reads / writes the request ring slots
+    // directly (no staging copies); Unimplemented: the copy path below
+    absl::Status direct = absl::UnimplementedError("");
+    if (job->following_jobs.empty()) {
+      lock.lock();
+      job->invoke_time = time::NowMicros();
+      lock.unlock();
+      direct = engine_->InvokeJobBatchDirect(key, {job});
+    }
+    if (!absl::IsUnimplemented(direct)) {
+      job->end_time = time::NowMicros();
+      phase_us_[1].fetch_add(job->end_time - job->invoke_time, std::memory_order_relaxed);
+      if (direct.ok()) {
+        engine_->UpdateLatency(key, job->end_time - job->invoke_time);
+        job->status = JobStatus::kSuccess;
+      } else {
+        BAND_LOG(LogSeverity::kError, "worker %d failed to invoke job %d: %s", worker_id_, job->job_id,
+                 direct.message().c_str());
+        job->status = JobStatus::kInvokeFailure;
+      }
+    } else if (engine_->TryCopyInputTensors(*job).ok()) {
       lock.lock();
       job->invoke_time = time::NowMicros();
       lock.unlock();

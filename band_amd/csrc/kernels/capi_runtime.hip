@@ -3,6 +3,7 @@
 // and events.  Every function returns 0 or the hipError_t it hit, and
 // records a message retrievable with bh_last_error().
 #include <algorithm>
+#include <vector>
 #include <stdio.h>
 #include <string.h>
 
@@ -144,6 +145,57 @@ extern "C" int bh_capture_end(bh_stream_t s, bh_graph_exec_t* exec) {
   (void)hipGraphDestroy(g);
   *exec = (bh_graph_exec_t)ge;
   return rc;
+}
+// capture end that keeps the captured graph (its node handles address the
+// instance's nodes for bh_graph_exec_set_memcpy); free it with bh_graph_free
+extern "C" int bh_capture_end_keep(bh_stream_t s, bh_graph_exec_t* exec, void** graph) {
+  hipGraph_t g = nullptr;
+  int rc = ck(hipStreamEndCapture((hipStream_t)s, &g), "hipStreamEndCapture");
+  if (rc) return rc;
+  hipGraphExec_t ge = nullptr;
+  rc = ck(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0), "hipGraphInstantiate");
+  if (rc) {
+    (void)hipGraphDestroy(g);
+    return rc;
+  }
+  *exec = (bh_graph_exec_t)ge;
+  *graph = (void*)g;
+  return 0;
+}
+extern "C" int bh_graph_free(void* graph) { return graph ? ck(hipGraphDestroy((hipGraph_t)graph), "hipGraphDestroy") : 0; }
+// the graph's memcpy nodes: node handle, destination, source and bytes of
+// each (up to max; *n = how many there are)
+extern "C" int bh_graph_memcpy_nodes(void* graph, void** nodes, void** dsts, const void** srcs, size_t* bytes,
+                                     int max, int* n) {
+  size_t count = 0;
+  int rc = ck(hipGraphGetNodes((hipGraph_t)graph, nullptr, &count), "hipGraphGetNodes");
+  if (rc) return rc;
+  std::vector<hipGraphNode_t> all(count);
+  rc = ck(hipGraphGetNodes((hipGraph_t)graph, all.data(), &count), "hipGraphGetNodes");
+  if (rc) return rc;
+  int k = 0;
+  for (size_t i = 0; i < count; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(all[i], &t) != hipSuccess || t != hipGraphNodeTypeMemcpy) continue;
+    hipMemcpy3DParms m{};
+    if (hipGraphMemcpyNodeGetParams(all[i], &m) != hipSuccess) continue;
+    if (k < max) {
+      nodes[k] = (void*)all[i];
+      dsts[k] = m.dstPtr.ptr;
+      srcs[k] = m.srcPtr.ptr;
+      bytes[k] = m.extent.width * m.extent.height * m.extent.depth;
+    }
+    ++k;
+  }
+  *n = k;
+  return 0;
+}
+// retarget one captured 1-D memcpy node of an instantiated graph
+extern "C" int bh_graph_exec_set_memcpy(bh_graph_exec_t e, void* node, void* dst, const void* src, size_t bytes,
+                                        int h2d) {
+  return ck(hipGraphExecMemcpyNodeSetParams1D((hipGraphExec_t)e, (hipGraphNode_t)node, dst, src, bytes,
+                                              h2d ? hipMemcpyHostToDevice : hipMemcpyDeviceToHost),
+            "hipGraphExecMemcpyNodeSetParams1D");
 }
 extern "C" int bh_graph_launch(bh_graph_exec_t e, bh_stream_t s) {
   return ck(hipGraphLaunch((hipGraphExec_t)e, (hipStream_t)s), "hipGraphLaunch");

@@ -88,6 +88,14 @@ int bh_memcpy_d2h(void* dst, const void* src, size_t bytes);
 int bh_capture_begin(bh_stream_t s);
 int bh_capture_end(bh_stream_t s, bh_graph_exec_t* exec);
 int bh_graph_launch(bh_graph_exec_t exec, bh_stream_t s);
+/* capture end that also returns the captured graph (free: bh_graph_free),
+ * whose memcpy nodes bh_graph_memcpy_nodes lists (handle, dst, src, bytes;
+ * up to max, *n = the count) and bh_graph_exec_set_memcpy retargets in the
+ * instance (a 1-D host<->device copy of the same size) */
+int bh_capture_end_keep(bh_stream_t s, bh_graph_exec_t* exec, void** graph);
+int bh_graph_free(void* graph);
+int bh_graph_memcpy_nodes(void* graph, void** nodes, void** dsts, const void** srcs, size_t* bytes, int max, int* n);
+int bh_graph_exec_set_memcpy(bh_graph_exec_t exec, void* node, void* dst, const void* src, size_t bytes, int h2d);
 int bh_graph_destroy(bh_graph_exec_t exec);
 
 /* ---- events (timing) ---------------------------------------------------- */

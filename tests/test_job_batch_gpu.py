@@ -95,14 +95,16 @@ def test_engine_batches_queued_jobs_bit_exact(gpu_lib, tmp_path, monkeypatch, sc
         assert m.FromPath(path)
         assert e.RegisterModel(m)
         models.append((m, OModel(buf)))
-    jobs = []
-    for i in range(24):
+    prepared = []
+    for i in range(48):
         m, om = models[i % 2]
         t = e.CreateInputTensor(m, 0)
         x = rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8)
         t.data()[...] = x
         outs = [e.CreateOutputTensor(m, k) for k in range(e.GetNumOutputTensors(m))]
-        jobs.append((e.RequestAsync(m, [t]), m, om, x, outs))
+        prepared.append((m, om, t, x, outs))
+    # submitted back to back, so requests queue while the workers are busy
+    jobs = [(e.RequestAsync(m, [t]), m, om, x, outs) for m, om, t, x, outs in prepared]
     invoke = {}
     for h, m, om, x, outs in jobs:
         assert h >= 0 and e.Wait(h, outs) == kBandOk

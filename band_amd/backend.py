@@ -48,6 +48,8 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_executor_destroy": (None, [c_void_p]),
     "bhx_gpu_numa_node": (c_int, [c_int]),
     "bhx_gpu_numa_cpus": (c_int, [c_int, ctypes.POINTER(c_int), c_int]),
+    "bhx_pin_process_to_gpu": (c_int, [c_int]),
+    "bhx_pin_process_to_cpus": (c_int, [ctypes.POINTER(c_int), c_int]),
     "bhx_investigate_model_spec": (c_int, [c_void_p, c_void_p, ctypes.c_char_p, c_size_t,
                                            ctypes.POINTER(c_size_t)]),
     "bhx_prepare_subgraph": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int), c_int,
@@ -514,3 +516,18 @@ def GpuNumaCpus(ordinal):
     arr = (c_int * cap)()
     n = int(lib.bhx_gpu_numa_cpus(int(ordinal), arr, cap))
     return node, [arr[i] for i in range(min(n, cap))]
+
+
+def PinProcessToGpu(ordinal):
+    """pins every thread of this process to GPU `ordinal`'s NUMA node
+    (backend/hip/affinity.h PinProcessToGpu); returns the threads pinned
+    (0: nothing to do)"""
+    return int(_abi.load().bhx_pin_process_to_gpu(int(ordinal)))
+
+
+def PinProcessToCpus(cpus):
+    """pins every thread of this process to `cpus` (the core of
+    PinProcessToGpu); returns the threads pinned, -1 on failure"""
+    cpus = list(cpus)
+    arr = (c_int * max(1, len(cpus)))(*cpus)
+    return int(_abi.load().bhx_pin_process_to_cpus(arr, len(cpus)))

@@ -1,5 +1,6 @@
 #include "backend/hip/affinity.h"
 
+#include <dirent.h>
 #include <sched.h>
 #include <unistd.h>
 
@@ -126,6 +127,41 @@ bool PinCallingThreadToGpu(int ordinal) {
   if (cpus.empty() || cpus.size() == ProcessCpus().size()) return ok;
   ok = PinThread(pthread_self(), cpus);
   return ok;
+}
+
+int PinProcessToCpus(const std::vector<int>& cpus) {
+  cpu_set_t m;
+  CPU_ZERO(&m);
+  int n = 0;
+  for (int c : cpus)
+    if (c >= 0 && c < CPU_SETSIZE) {
+      CPU_SET(c, &m);
+      ++n;
+    }
+  if (n == 0) return -1;
+  DIR* d = opendir("/proc/self/task");
+  if (!d) return -1;
+  int pinned = 0;
+  bool failed = false;
+  while (dirent* ent = readdir(d)) {
+    char* end = nullptr;
+    const long tid = std::strtol(ent->d_name, &end, 10);
+    if (end == ent->d_name || *end != '\0' || tid <= 0) continue;
+    if (sched_setaffinity(static_cast<pid_t>(tid), sizeof(m), &m) == 0)
+      ++pinned;
+    else
+      failed = true;  // a thread that exited meanwhile also lands here
+  }
+  closedir(d);
+  return failed && pinned == 0 ? -1 : pinned;
+}
+
+int PinProcessToGpu(int ordinal) {
+  const char* env = std::getenv("BANDX_NUMA_PIN");
+  if (env && env[0] == '0') return 0;
+  const std::vector<int> cpus = GpuNumaCpus(ordinal);
+  if (cpus.empty() || cpus.size() == ProcessCpus().size()) return 0;
+  return PinProcessToCpus(cpus);
 }
 
 }  // namespace hip

@@ -38,6 +38,17 @@ std::vector<int> GpuNumaCpus(int ordinal);
 // pins the calling thread to GpuNumaCpus(ordinal), once per (thread,
 // ordinal); returns whether the thread is now pinned to that node
 bool PinCallingThreadToGpu(int ordinal);
+// pins EVERY thread the process has now (/proc/self/task) to
+// GpuNumaCpus(ordinal); threads they create later inherit the mask.  For a
+// one-GPU process (bench.py's ranks): the request driver's submit/read
+// threads, the planner and the HIP runtime's own threads then share the GPU's
+// socket with the workers and the page-locked request rings.  Returns the
+// number of threads pinned (0: nothing to do, BANDX_NUMA_PIN=0 or no NUMA
+// information), -1 when a thread could not be pinned.
+int PinProcessToGpu(int ordinal);
+// the same for an explicit CPU list: every current thread to `cpus`
+// (threads pinned, -1 on failure or an empty list)
+int PinProcessToCpus(const std::vector<int>& cpus);
 
 }  // namespace hip
 }  // namespace band

@@ -126,6 +126,13 @@ int bhx_gpu_numa_cpus(int ordinal, int* cpus, int cap) {
   return static_cast<int>(v.size());
 }
 
+int bhx_pin_process_to_gpu(int ordinal) { return band::hip::PinProcessToGpu(ordinal); }
+
+int bhx_pin_process_to_cpus(const int* cpus, int n_cpus) {
+  if (n_cpus <= 0 || !cpus) return -1;
+  return band::hip::PinProcessToCpus(std::vector<int>(cpus, cpus + n_cpus));
+}
+
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed) {
   if (!e || !m) return Fail("null argument");
   auto r = e->exec->InvestigateModelSpec(m->model.get());

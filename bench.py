@@ -615,6 +615,16 @@ def main():
         D.close()
         return
 
+    # a one-GPU process: every thread (request driver, planner, HIP runtime)
+    # to the GPU's NUMA node, where the workers pin themselves and the
+    # page-locked request rings live; threads created later inherit the mask
+    # (BANDX_NUMA_PIN=0: off).  Restored for the CPU baseline.
+    if args.device == "gpu" and not args.single_engine:
+        from band_amd import backend as _backend
+        node, _ = _backend.GpuNumaCpus(D.local_rank)
+        hinfo["numa_pin"] = {"gpu_numa_node": node, "threads_pinned": _backend.PinProcessToGpu(D.local_rank),
+                             "affinity_after": len(os.sched_getaffinity(0))}
+
     needs_cpu = args.model in ("efficientdet_lite2_int8", "mix_c5")
     n_cpu = args.cpu_workers if args.cpu_workers >= 0 else (1 if needs_cpu else 0)
     if args.model == "mix_c5" and args.scheduler == "round_robin":

@@ -83,6 +83,14 @@ void bhx_executor_destroy(bhx_executor* e);
  * where a kGPU executor pins its worker thread (affinity.h) */
 int bhx_gpu_numa_node(int ordinal);
 int bhx_gpu_numa_cpus(int ordinal, int* cpus, int cap);
+/* pins every thread of the process (and, by inheritance, the threads it
+ * creates later) to those CPUs: for a process that drives one GPU.  Returns
+ * threads pinned, 0 when there is nothing to do (BANDX_NUMA_PIN=0, no NUMA
+ * information, or the node is every CPU the process has), -1 on failure. */
+int bhx_pin_process_to_gpu(int ordinal);
+/* the same for an explicit list cpus[0..n_cpus): every current thread of the
+ * process to it; threads pinned, -1 on failure */
+int bhx_pin_process_to_cpus(const int* cpus, int n_cpus);
 /* InvestigateModelSpec -> ModelSpec serialised as JSON into buf.
  * *needed receives the full length (+1); the call fails if cap < needed. */
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed);

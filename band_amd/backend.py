@@ -50,6 +50,7 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_gpu_numa_cpus": (c_int, [c_int, ctypes.POINTER(c_int), c_int]),
     "bhx_pin_process_to_gpu": (c_int, [c_int]),
     "bhx_pin_process_to_cpus": (c_int, [ctypes.POINTER(c_int), c_int]),
+    "bhx_ring_page_nodes": (c_int, [ctypes.POINTER(ctypes.c_longlong), c_int]),
     "bhx_investigate_model_spec": (c_int, [c_void_p, c_void_p, ctypes.c_char_p, c_size_t,
                                            ctypes.POINTER(c_size_t)]),
     "bhx_prepare_subgraph": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int), c_int,
@@ -531,3 +532,12 @@ def PinProcessToCpus(cpus):
     cpus = list(cpus)
     arr = (c_int * max(1, len(cpus)))(*cpus)
     return int(_abi.load().bhx_pin_process_to_cpus(arr, len(cpus)))
+
+
+def RingPageNodes():
+    """{node: bytes} of the page-locked request-ring memory allocated so far
+    (-1: node unknown), sampled every 16th page"""
+    cap = 65
+    arr = (ctypes.c_longlong * cap)()
+    n = int(_abi.load().bhx_ring_page_nodes(arr, cap))
+    return {(i if i < 64 else -1): int(arr[i]) for i in range(min(n, cap)) if arr[i]}

@@ -34,6 +34,11 @@ class UtilCreator : public Creator<interface::IBackendUtil> {
   interface::IBackendUtil* Create() const override { return new HipUtil(); }
 };
 
+// page-locked request-ring memory per NUMA node (bhx_ring_page_nodes):
+// CountRingPages samples a new ring block, RingPageNodes reads the totals
+void CountRingPages(const void* p, size_t bytes);
+int RingPageNodes(long long* bytes_per_node, int cap);
+
 }  // namespace hip
 
 bool TfLiteRegisterCreators();

@@ -126,6 +126,11 @@ int bhx_gpu_numa_cpus(int ordinal, int* cpus, int cap) {
   return static_cast<int>(v.size());
 }
 
+int bhx_ring_page_nodes(long long* bytes_per_node, int cap) {
+  if (cap < 0 || (cap > 0 && !bytes_per_node)) return Fail("bad arguments");
+  return band::hip::RingPageNodes(bytes_per_node, cap);
+}
+
 int bhx_pin_process_to_gpu(int ordinal) { return band::hip::PinProcessToGpu(ordinal); }
 
 int bhx_pin_process_to_cpus(const int* cpus, int n_cpus) {

@@ -47,6 +47,8 @@ struct BandEngine {
   explicit BandEngine(std::unique_ptr<band::Engine> e) : impl(std::move(e)) {}
   std::list<std::shared_ptr<band::Model>> models;
   std::unique_ptr<band::Engine> impl;
+  // the last DriveRequests call (BandxEngineGetDriverStats)
+  double driver_stats[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 };
 
 namespace {
@@ -458,11 +460,25 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     long seq;         // submission number within its model
   };
   std::mutex mu;
-  std::condition_variable cv;
+  // readers wait on cv_read (a finished request, or the end), submitters on
+  // cv_sub (a retired request): each event wakes only the side it concerns
+  std::condition_variable cv_read, cv_sub;
   std::unordered_map<band::JobId, Pending> pending;  // submitted, not yet read
   std::deque<band::JobId> done;                      // finished, ready to read
   std::set<band::JobId> early;  // finished before its submitter recorded it
   int inflight = 0, retired = 0, taken = 0;
+  // stats (under mu): time integrals of the requests inside the engine
+  // (submitted, end-of-request not yet seen) and of the finished ones waiting
+  // for a reader; submitter wait / call and reader busy / idle time
+  int in_engine = 0;
+  double int_engine = 0, int_done = 0, submit_wait = 0, submit_call = 0, read_busy = 0, read_idle = 0;
+  int64_t last_tick = band::time::NowMicros();
+  auto tick = [&] {  // under mu, before in_engine or done changes
+    const int64_t now = band::time::NowMicros();
+    int_engine += double(in_engine) * double(now - last_tick);
+    int_done += double(done.size()) * double(now - last_tick);
+    last_tick = now;
+  };
   std::vector<int> unread(n_models, 0), ring(n_models, 0);
   for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
   std::vector<long> next_seq(n_models, 0);
@@ -473,11 +489,14 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
   const band::CallbackId cb = e.SetOnEndRequest([&](int id, absl::Status) {
     std::lock_guard<std::mutex> lk(mu);
-    if (pending.count(id))
+    tick();
+    --in_engine;
+    if (pending.count(id)) {
       done.push_back(id);
-    else
+      cv_read.notify_one();
+    } else {
       early.insert(id);
-    cv.notify_all();
+    }
   });
   auto retire = [&](const Pending& item, bool ok) {  // under mu
     if (!ok && !failed) failed = true;
@@ -492,12 +511,16 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     threads.emplace_back([&, r] {
       pthread_setname_np(pthread_self(), "bandx-reader");
       while (true) {
+        const int64_t w0 = band::time::NowMicros();
         std::unique_lock<std::mutex> lk(mu);
-        cv.wait(lk, [&] { return !done.empty() || taken >= n_jobs; });
+        cv_read.wait(lk, [&] { return !done.empty() || taken >= n_jobs; });
+        const int64_t w1 = band::time::NowMicros();
+        read_idle += double(w1 - w0);
         if (done.empty()) break;
+        tick();
         const band::JobId id = done.front();
         done.pop_front();
-        ++taken;
+        if (++taken >= n_jobs) cv_read.notify_all();  // the other readers may leave
         const Pending item = pending.at(id);
         pending.erase(id);
         lk.unlock();
@@ -514,8 +537,9 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
         if (model_index) model_index[item.index] = item.model;
         lk.lock();
+        read_busy += double(band::time::NowMicros() - w1);
         retire(item, ok);
-        cv.notify_all();
+        cv_sub.notify_all();
       }
     });
   }
@@ -529,9 +553,10 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         const int m = arrival.second;
         const long span = std::max(1, ring[m] - lanes);
         long seq;
+        const int64_t w0 = band::time::NowMicros();
         {
           std::unique_lock<std::mutex> lk(mu);
-          cv.wait(lk, [&] {
+          cv_sub.wait(lk, [&] {
             return inflight < max_inflight && unread[m] < ring[m] &&
                    (unread_seq[m].empty() || next_seq[m] - *unread_seq[m].begin() < span);
           });
@@ -539,26 +564,47 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
           ++unread[m];
           seq = next_seq[m]++;
           unread_seq[m].insert(seq);
+          tick();
+          ++in_engine;
         }
+        const int64_t w1 = band::time::NowMicros();
         auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
         std::lock_guard<std::mutex> lk(mu);
+        submit_wait += double(w1 - w0);
+        submit_call += double(band::time::NowMicros() - w1);
         const Pending item{j, m, t0 + arrival.first, seq};
         if (!id.ok()) {
           BAND_LOG(band::LogSeverity::kError, "request driver: submit of job %d failed: %s", j,
                    std::string(id.status().message()).c_str());
-          ++taken;
+          if (++taken >= n_jobs) cv_read.notify_all();
+          tick();
+          --in_engine;
           retire(item, false);
+          cv_sub.notify_all();
         } else {
           pending[id.value()] = item;
-          if (early.erase(id.value())) done.push_back(id.value());
+          if (early.erase(id.value())) {
+            done.push_back(id.value());
+            cv_read.notify_one();
+          }
         }
-        cv.notify_all();
       }
     });
   }
   for (auto& t : threads) t.join();
   (void)e.UnsetOnEndRequest(cb);
-  if (wall_s) *wall_s = (band::time::NowMicros() - t0) * 1e-6;
+  const double wall_us = double(band::time::NowMicros() - t0);
+  tick();
+  double* st = engine->driver_stats;
+  st[0] = wall_us;
+  st[1] = wall_us > 0 ? int_engine / wall_us : 0;
+  st[2] = wall_us > 0 ? int_done / wall_us : 0;
+  st[3] = submit_wait;
+  st[4] = submit_call;
+  st[5] = read_busy;
+  st[6] = read_idle;
+  st[7] = double(readers) + 1000.0 * lanes;
+  if (wall_s) *wall_s = wall_us * 1e-6;
   return failed ? kBandErr : kBandOk;
 }
 }  // namespace
@@ -593,6 +639,12 @@ int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id) {
   if (!engine || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return -1;
   const band::Worker* w = engine->impl->GetWorker(worker_id);
   return w ? w->GetJobsRun() : -1;
+}
+
+int BandxEngineGetDriverStats(BandEngine* engine, double out[8]) {
+  if (!engine || !out) return -1;
+  for (int i = 0; i < 8; ++i) out[i] = engine->driver_stats[i];
+  return 0;
 }
 
 int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int worker_id, int64_t out[4]) {

@@ -1,5 +1,9 @@
 #include "engine/tensor.h"
 
+#include <immintrin.h>
+
+#include <algorithm>
+#include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -43,6 +47,55 @@ Affine* CloneAffine(const Affine* src) {
 }  // namespace
 
 namespace {
+// Request inputs are copied into page-locked ring slots that the GPU's DMA
+// engines read next; no CPU reads them back.  Streaming (non-temporal)
+// stores skip the read-for-ownership of every destination line that plain
+// stores pay (the slot was last touched by the DMA, so each line would come
+// from DRAM) and leave the caches to the caller.  Large copies into ring
+// memory only; BANDX_RING_NT=0 keeps memcpy.
+bool UseStreamingStores() {
+  static const bool on = [] {
+    const char* e = std::getenv("BANDX_RING_NT");
+    return !(e && e[0] == '0') && __builtin_cpu_supports("avx2");
+  }();
+  return on;
+}
+
+__attribute__((target("avx2"))) void StreamCopy(char* dst, const char* src, size_t n) {
+  // head: up to the next 32-byte boundary of dst
+  const size_t head = std::min(n, static_cast<size_t>((32 - (reinterpret_cast<uintptr_t>(dst) & 31)) & 31));
+  std::memcpy(dst, src, head);
+  dst += head;
+  src += head;
+  n -= head;
+  size_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i));
+    const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 32));
+    const __m256i c = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 64));
+    const __m256i d = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i + 96));
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i), a);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 32), b);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 64), c);
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i + 96), d);
+  }
+  for (; i + 32 <= n; i += 32)
+    _mm256_stream_si256(reinterpret_cast<__m256i*>(dst + i),
+                        _mm256_loadu_si256(reinterpret_cast<const __m256i*>(src + i)));
+  std::memcpy(dst + i, src + i, n - i);
+  _mm_sfence();  // the streamed lines are globally visible before the request is queued
+}
+
+// src -> a ring slot tensor
+absl::Status PutIntoSlot(Tensor* slot, const interface::ITensor* src) {
+  constexpr size_t kStreamMin = 64 << 10;
+  if (!src || !slot->IsRingMemory() || slot->GetBytes() < kStreamMin || !UseStreamingStores() ||
+      *static_cast<const interface::ITensor*>(slot) != *src)
+    return slot->CopyDataFrom(src);  // the checks and errors of ITensor::CopyDataFrom
+  StreamCopy(slot->GetData(), src->GetData(), slot->GetBytes());
+  return absl::OkStatus();
+}
+
 std::mutex g_ring_alloc_mu;
 RingHostAllocator g_ring_alloc;
 }  // namespace
@@ -235,7 +288,7 @@ absl::Status TensorRingBuffer::PutTensorToHandle(const interface::ITensor* src, 
     return absl::InternalError("PutTensorToHandle: Invalid tensor index: " + std::to_string(tensor_index));
   if (!IsHandleValid(handle))
     return absl::InternalError("PutTensorToHandle: Invalid memory handle: " + std::to_string(handle));
-  return slots_[Slot(handle)][it->second]->CopyDataFrom(src);
+  return PutIntoSlot(slots_[Slot(handle)][it->second].get(), src);
 }
 
 absl::Status TensorRingBuffer::GetTensorsFromHandle(std::vector<interface::ITensor*>& dst, int handle) const {
@@ -253,7 +306,8 @@ absl::Status TensorRingBuffer::PutTensorsToHandle(const std::vector<interface::I
     return absl::InternalError("PutTensorsToHandle: Invalid memory handle: " + std::to_string(handle));
   if (src.size() != num_tensors_) return absl::InternalError("Invalid tensor length");
   for (size_t i = 0; i < num_tensors_; ++i)
-    if (!slots_[Slot(handle)][i]->CopyDataFrom(src[i]).ok()) return absl::InternalError("Failed to copy tensors.");
+    if (!PutIntoSlot(slots_[Slot(handle)][i].get(), src[i]).ok())
+      return absl::InternalError("Failed to copy tensors.");
   return absl::OkStatus();
 }
 

@@ -136,6 +136,7 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineWaitAll": (None, [c_void_p]),
     "BandxEngineGetWorkerJobCount": (c_int64, [c_void_p, c_int]),
     "BandxEngineGetWorkerPhaseTimes": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64)]),
+    "BandxEngineGetDriverStats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double)]),
     "BandxEngineRequestsAsync": (c_int, [c_void_p, POINTER(c_void_p), c_int, POINTER(c_void_p), POINTER(c_int)]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
@@ -404,6 +405,17 @@ class Engine:
         if self.lib.BandxEngineGetWorkerPhaseTimes(self.handle, int(worker_id), out) != 0:
             raise _abi.BandHipError("GetWorkerPhaseTimes: bad worker id %d" % worker_id)
         return dict(copy_in_us=out[0], invoke_us=out[1], copy_out_us=out[2], passes=out[3])
+
+    def GetDriverStats(self):
+        """the last RunClosedLoop / RunPoisson call: wall time, mean requests
+        inside the engine and waiting for a reader, submitter and reader time
+        (include/band_c_api.h BandxEngineGetDriverStats)"""
+        out = (ctypes.c_double * 8)()
+        self.lib.BandxEngineGetDriverStats(self.handle, out)
+        readers, lanes = int(out[7]) % 1000, int(out[7]) // 1000
+        return dict(wall_us=out[0], mean_in_engine=out[1], mean_awaiting_read=out[2], submit_wait_us=out[3],
+                    submit_call_us=out[4], read_busy_us=out[5], read_idle_us=out[6], readers=readers,
+                    submitters=lanes)
 
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))

@@ -536,6 +536,7 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     t1 = time.perf_counter()
     c1 = thread_cpu()
     p1 = [engine.GetWorkerPhaseTimes(w) for w in range(n_workers)]
+    drv = engine.GetDriverStats()
     D.barrier()
     busy = sorted((((c1[k] - c0.get(k, 0.0)) / (t1 - t0), k[1]) for k in c1), reverse=True)
     HOST_THREADS.clear()
@@ -553,6 +554,25 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
             us_per_pass=dict(copy_in=round(ph["copy_in_us"] / ph["passes"], 1),
                              invoke=round(ph["invoke_us"] / ph["passes"], 1),
                              copy_out=round(ph["copy_out_us"] / ph["passes"], 1))))
+    # NUMA nodes of the page-locked request rings (MB per node)
+    try:
+        from band_amd import backend as _backend
+        HOST_THREADS.update(ring_page_nodes_mb={str(k): round(v / 2 ** 20, 1)
+                                                for k, v in _backend.RingPageNodes().items()})
+    except Exception as ex:  # diagnostics only
+        HOST_THREADS.update(ring_page_nodes_mb=repr(ex))
+    # the request driver: requests inside the engine vs finished and waiting
+    # for a reader (means over the loop), and its threads' busy shares
+    if drv["wall_us"] > 0:
+        w = drv["wall_us"]
+        HOST_THREADS.update(request_driver=dict(
+            mean_in_engine=round(drv["mean_in_engine"], 1), mean_awaiting_read=round(drv["mean_awaiting_read"], 1),
+            submit_wait=round(drv["submit_wait_us"] / (w * drv["submitters"]), 3),
+            submit_call=round(drv["submit_call_us"] / (w * drv["submitters"]), 3),
+            submit_call_us_per_job=round(drv["submit_call_us"] / max(1, n_timed), 2),
+            read_busy=round(drv["read_busy_us"] / (w * drv["readers"]), 3),
+            read_us_per_job=round(drv["read_busy_us"] / max(1, n_timed), 2),
+            readers=drv["readers"], submitters=drv["submitters"]))
     return D.max(t1 - t0), lat_us, worker_ids
 
 

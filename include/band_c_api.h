@@ -223,6 +223,13 @@ BAND_CAPI_EXPORT int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int wo
  * microseconds, and out[3] the passes run (a batched pass counts once).
  * Returns 0, or -1 for a bad id. */
 BAND_CAPI_EXPORT int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int worker_id, int64_t out[4]);
+/* the last BandxEngineRunClosedLoop / BandxEngineRunPoisson call: out[0] its
+ * wall time (us), out[1] the mean requests inside the engine (submitted, not
+ * yet finished), out[2] the mean finished requests waiting for a reader,
+ * out[3] / out[4] submitter time waiting for a free slot / inside
+ * RequestAsync, out[5] / out[6] reader time reading / waiting (us, summed
+ * over threads), out[7] readers + 1000 x submitters.  Returns 0. */
+BAND_CAPI_EXPORT int BandxEngineGetDriverStats(BandEngine* engine, double out[8]);
 /* One RequestAsync call for n requests (band/engine.cc:455-529, the batched
  * overload Band's own benchmark tool uses): request i runs models[i] on the
  * input tensors inputs[i] (that model's inputs, in order).  handles[i]

@@ -91,6 +91,11 @@ int bhx_pin_process_to_gpu(int ordinal);
 /* the same for an explicit list cpus[0..n_cpus): every current thread of the
  * process to it; threads pinned, -1 on failure */
 int bhx_pin_process_to_cpus(const int* cpus, int n_cpus);
+/* bytes of page-locked request-ring memory allocated so far on each NUMA
+ * node (sampled every 16th page): bytes_per_node[i] for node i, the entry
+ * after the last node counts pages whose node was unknown.  Returns the
+ * number of entries that exist (up to cap written). */
+int bhx_ring_page_nodes(long long* bytes_per_node, int cap);
 /* InvestigateModelSpec -> ModelSpec serialised as JSON into buf.
  * *needed receives the full length (+1); the call fails if cap < needed. */
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed);

@@ -5,6 +5,7 @@
 // Built and run by tests/test_engine_native.py.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <deque>
 #include <map>
 #include <memory>
@@ -15,6 +16,7 @@
 #include "engine/json.h"
 #include "engine/model_analyzer.h"
 #include "engine/scheduler.h"
+#include "engine/tensor.h"
 #include "engine/worker.h"
 
 using namespace band;
@@ -329,6 +331,72 @@ static void TestJson() {
   CHECK(!json::Parse("{\"a\": [1,}", &w));
 }
 
+// ---- request-ring slots in ring-allocator memory: the streaming-store copy
+// into a slot (engine/tensor.cc PutIntoSlot) returns the bytes unchanged, for
+// aligned and misaligned sources and sizes that are not a multiple of 32
+struct ViewTensor : public interface::ITensor {
+  ViewTensor(std::vector<int> d, char* p) : dims(std::move(d)), data(p) {}
+  DataType GetType() const override { return DataType::kUInt8; }
+  void SetType(DataType) override {}
+  const char* GetData() const override { return data; }
+  char* GetData() override { return data; }
+  const int* GetDims() const override { return dims.data(); }
+  size_t GetNumDims() const override { return dims.size(); }
+  void SetDims(const std::vector<int>& d) override { dims = d; }
+  const char* GetName() const override { return "view"; }
+  Quantization GetQuantization() const override { return Quantization(QuantizationType::kNoQuantization, nullptr); }
+  absl::Status SetQuantization(Quantization) override { return absl::OkStatus(); }
+  std::vector<int> dims;
+  char* data;
+};
+
+static void TestRingSlotCopies() {
+  RingHostAllocator a;
+  a.alloc = [](size_t n) -> void* { return std::aligned_alloc(4096, (n + 4095) / 4096 * 4096); };
+  a.free = [](void* p) { std::free(p); };
+  SetRingHostAllocator(a);
+  const std::vector<std::vector<int>> shapes = {{1, 224, 224, 3}, {1, 70001}, {1, 100}};
+  std::vector<std::vector<char>> backing;
+  std::vector<std::shared_ptr<interface::ITensor>> views;
+  for (const auto& d : shapes) {
+    size_t n = 1;
+    for (int x : d) n *= static_cast<size_t>(x);
+    backing.emplace_back(n + 64, 0);
+    views.push_back(std::make_shared<ViewTensor>(d, backing.back().data()));
+  }
+  {
+    TensorRingBuffer ring(views, {0, 1, 2}, 3);
+    for (int round = 0; round < 5; ++round) {
+      const int h = ring.AllocBlocking();
+      std::vector<std::unique_ptr<ViewTensor>> src, dst;
+      std::vector<interface::ITensor*> src_p, dst_p;
+      for (size_t i = 0; i < shapes.size(); ++i) {
+        const size_t n = views[i]->GetBytes();
+        char* base = backing[i].data() + (round % 4) * 3;  // misaligned sources too
+        for (size_t k = 0; k < n; ++k) base[k] = static_cast<char>((k * 131 + i * 7 + round) & 0xff);
+        src.emplace_back(new ViewTensor(shapes[i], base));
+        src_p.push_back(src.back().get());
+      }
+      CHECK(ring.PutTensorsToHandle(src_p, h).ok());
+      CHECK(ring.SlotTensor(0, h) && ring.SlotTensor(0, h)->IsRingMemory());
+      std::vector<std::vector<char>> out;
+      for (size_t i = 0; i < shapes.size(); ++i) out.emplace_back(views[i]->GetBytes(), 0);
+      for (size_t i = 0; i < shapes.size(); ++i) {
+        dst.emplace_back(new ViewTensor(shapes[i], out[i].data()));
+        dst_p.push_back(dst.back().get());
+      }
+      CHECK(ring.GetTensorsFromHandle(dst_p, h).ok());
+      for (size_t i = 0; i < shapes.size(); ++i)
+        CHECK(std::memcmp(out[i].data(), src[i]->GetData(), out[i].size()) == 0);
+      // a source of another shape is refused, as ITensor::CopyDataFrom does
+      ViewTensor wrong({1, 224, 224, 4}, backing[0].data());
+      CHECK(!ring.PutTensorToHandle(&wrong, 0, h).ok());
+      ring.Release(h);
+    }
+  }
+  SetRingHostAllocator(RingHostAllocator());
+}
+
 int main() {
   TestRoundRobin();
   TestFixedWorker();
@@ -338,6 +406,7 @@ int main() {
   TestFixedWorkerGlobalQueue();
   TestModelAnalyzer();
   TestJson();
+  TestRingSlotCopies();
   std::printf("%d checks, %d failures\n", g_checks, g_failures);
   return g_failures ? 1 : 0;
 }

@@ -20,6 +20,7 @@
 
 #include "engine/engine.h"
 #include "engine/logger.h"
+#include "engine/planner.h"
 #include "engine/time.h"
 
 struct BandConfigBuilder {
@@ -432,12 +433,12 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     }
   }
   // Submitters (BANDX_DRIVER_LANES, default 1) copy requests into the rings
-  // (150 KB per 224x224 job); readers (BANDX_DRIVER_READERS, default 2) copy
+  // (150 KB per 224x224 job); readers (BANDX_DRIVER_READERS, default 6) copy
   // results out (DeepLab's are 1 MB), each into output tensors of its own.
   int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
   lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
-  int readers = 2;
+  int readers = 6;
   if (const char* rv = std::getenv("BANDX_DRIVER_READERS")) readers = std::max(1, std::atoi(rv));
   readers = std::max(1, std::min(readers, n_jobs > 0 ? n_jobs : 1));
   std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> reader_outs(readers);
@@ -458,14 +459,19 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     int index, model;
     int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
     long seq;         // submission number within its model
+    long gseq;        // submission number over all models
   };
   std::mutex mu;
   // readers wait on cv_read (a finished request, or the end), submitters on
   // cv_sub (a retired request): each event wakes only the side it concerns
   std::condition_variable cv_read, cv_sub;
   std::unordered_map<band::JobId, Pending> pending;  // submitted, not yet read
-  std::deque<band::JobId> done;                      // finished, ready to read
-  std::set<band::JobId> early;  // finished before its submitter recorded it
+  // finished, ready to read, with the finished-job record taken in the
+  // end-of-request callback: the planner keeps only the last 1000 records
+  // (band/planner.h kNumFinishedRecords), and with many requests in flight a
+  // slow one can fall out of that window before a reader gets to it
+  std::deque<std::pair<band::JobId, band::Job>> done;
+  std::unordered_map<band::JobId, band::Job> early;  // finished before its submitter recorded it
   int inflight = 0, retired = 0, taken = 0;
   // stats (under mu): time integrals of the requests inside the engine
   // (submitted, end-of-request not yet seen) and of the finished ones waiting
@@ -483,19 +489,29 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
   std::vector<long> next_seq(n_models, 0);
   std::vector<std::set<long>> unread_seq(n_models);
+  // requests submitted and not yet finished, by gseq: a request must finish
+  // fewer than the planner's record window of submissions after its own, or
+  // its finished-job record is gone before the callback can read it
+  std::set<long> unfinished;
+  long next_gseq = 0;
+  const long record_span = std::max(1, band::Planner::kNumFinishedRecords - lanes);
   bool failed = false;
   // arrivals are drawn in job order (the open-loop schedule is one sequence)
   std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
   for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
   const band::CallbackId cb = e.SetOnEndRequest([&](int id, absl::Status) {
+    band::Job rec = e.GetFinishedJob(id);  // outside mu: the planner's own lock
     std::lock_guard<std::mutex> lk(mu);
     tick();
     --in_engine;
-    if (pending.count(id)) {
-      done.push_back(id);
+    auto pit = pending.find(id);
+    if (pit != pending.end()) {
+      unfinished.erase(pit->second.gseq);
+      cv_sub.notify_all();
+      done.emplace_back(id, std::move(rec));
       cv_read.notify_one();
     } else {
-      early.insert(id);
+      early.emplace(id, std::move(rec));
     }
   });
   auto retire = [&](const Pending& item, bool ok) {  // under mu
@@ -518,14 +534,14 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         read_idle += double(w1 - w0);
         if (done.empty()) break;
         tick();
-        const band::JobId id = done.front();
+        const band::JobId id = done.front().first;
+        const band::Job j = std::move(done.front().second);
         done.pop_front();
         if (++taken >= n_jobs) cv_read.notify_all();  // the other readers may leave
         const Pending item = pending.at(id);
         pending.erase(id);
         lk.unlock();
-        band::Job j = e.GetFinishedJob(id);
-        absl::Status st = j.job_id == id ? e.GetOutputTensors(id, reader_out_ptrs[r][item.model])
+        absl::Status st = j.job_id == id ? e.GetOutputTensorsOf(j, reader_out_ptrs[r][item.model])
                                          : absl::InternalError("no finished record");
         const bool ok = st.ok() && j.status == band::JobStatus::kSuccess;
         if (!ok)
@@ -552,18 +568,21 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
         const int m = arrival.second;
         const long span = std::max(1, ring[m] - lanes);
-        long seq;
+        long seq, gseq;
         const int64_t w0 = band::time::NowMicros();
         {
           std::unique_lock<std::mutex> lk(mu);
           cv_sub.wait(lk, [&] {
             return inflight < max_inflight && unread[m] < ring[m] &&
-                   (unread_seq[m].empty() || next_seq[m] - *unread_seq[m].begin() < span);
+                   (unread_seq[m].empty() || next_seq[m] - *unread_seq[m].begin() < span) &&
+                   (unfinished.empty() || next_gseq - *unfinished.begin() < record_span);
           });
           ++inflight;
           ++unread[m];
           seq = next_seq[m]++;
           unread_seq[m].insert(seq);
+          gseq = next_gseq++;
+          unfinished.insert(gseq);
           tick();
           ++in_engine;
         }
@@ -572,19 +591,24 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         std::lock_guard<std::mutex> lk(mu);
         submit_wait += double(w1 - w0);
         submit_call += double(band::time::NowMicros() - w1);
-        const Pending item{j, m, t0 + arrival.first, seq};
+        const Pending item{j, m, t0 + arrival.first, seq, gseq};
         if (!id.ok()) {
           BAND_LOG(band::LogSeverity::kError, "request driver: submit of job %d failed: %s", j,
                    std::string(id.status().message()).c_str());
           if (++taken >= n_jobs) cv_read.notify_all();
           tick();
           --in_engine;
+          unfinished.erase(gseq);
           retire(item, false);
           cv_sub.notify_all();
         } else {
           pending[id.value()] = item;
-          if (early.erase(id.value())) {
-            done.push_back(id.value());
+          auto ea = early.find(id.value());
+          if (ea != early.end()) {
+            unfinished.erase(gseq);
+            cv_sub.notify_all();
+            done.emplace_back(id.value(), std::move(ea->second));
+            early.erase(ea);
             cv_read.notify_one();
           }
         }

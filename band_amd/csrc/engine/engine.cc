@@ -380,7 +380,11 @@ absl::Status Engine::GetOutputTensors(JobId job_id, Tensors outputs) {
   if (outputs.empty() || job_id == -1)
     return absl::InternalError("Invalid job id / num outputs to copy: (" + std::to_string(job_id) + ", " +
                                std::to_string(outputs.size()) + ")");
-  Job job = planner_->GetFinishedJob(job_id);
+  return GetOutputTensorsOf(planner_->GetFinishedJob(job_id), outputs);
+}
+
+absl::Status Engine::GetOutputTensorsOf(const Job& job, Tensors outputs) {
+  if (outputs.empty()) return absl::InternalError("Invalid num outputs to copy: 0");
   if (job.job_id == -1) return absl::InternalError("Invalid job id / not finished or invalidated.");
   if (job.output_handle == -1)
     return absl::InternalError("Invalid output handle : " + std::to_string(job.output_handle));

@@ -70,6 +70,10 @@ class Engine : public IEngine {
   absl::Status Wait(std::vector<JobId> job_ids, std::vector<Tensors> outputs = {});
   void WaitAll();
   absl::Status GetOutputTensors(JobId job_id, Tensors outputs);
+  // the same for a finished-job record the caller already holds (a record
+  // read in the end-of-request callback stays usable after the planner's
+  // 1000-record window has moved past the job)
+  absl::Status GetOutputTensorsOf(const Job& job, Tensors outputs);
   CallbackId SetOnEndRequest(std::function<void(int, absl::Status)> on_end_request);
   absl::Status UnsetOnEndRequest(CallbackId callback_id);
 

@@ -291,6 +291,22 @@ def test_closed_loop_beyond_ring_capacity(tmp_path):
     e.close()
 
 
+def test_closed_loop_beyond_the_finished_record_window(golden_dir, monkeypatch):
+    """more requests in flight than the planner keeps finished-job records
+    (1000, band/planner.h kNumFinishedRecords) over 1500-slot rings: the
+    driver takes each record in the end-of-request callback and holds back a
+    submission that would push an unfinished request out of the window, so no
+    request fails with 'no finished record'"""
+    monkeypatch.setenv("BANDX_REQUEST_RING_SLOTS", "1500")
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU, DeviceFlag.kCPU], num_threads=[1, 1]))
+    m = Model()
+    assert m.FromPath(os.path.join(golden_dir, "add.tflite"))
+    assert e.RegisterModel(m)
+    lat, wid, wall = e.RunClosedLoop([m], 3000, 1400)
+    assert len(lat) == 3000 and (lat > 0).all()
+    e.close()
+
+
 def test_batched_request_larger_than_ring_is_refused(tmp_path):
     """one RequestAsync of 129 same-model jobs (ring 128) used to
     take slots one by one and wait forever for the 129th; it is refused with

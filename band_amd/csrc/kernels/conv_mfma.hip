@@ -236,12 +236,22 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   const int wt = wave % (WAVES_M * WAVES_N);
   const int wave_m = wt % WAVES_M;
   const int wave_n = wt / WAVES_M;
-  // 1-D grid, N-blocks fastest; with xcd each XCD (hardware ids i % 8) runs
-  // a contiguous run of logical blocks, so all N-blocks of a pixel block -
-  // which read the same input rows - share one L2
+  // 1-D grid; with xcd each XCD (hardware ids i % 8) runs a contiguous run
+  // of logical blocks.  xcd 1: N-blocks fastest, so all N-blocks of a pixel
+  // block - which read the same input rows - share one L2 (the filters are
+  // read once per XCD).  xcd 2 (filters larger than the input): pixel blocks
+  // fastest, so each XCD reads only its slice of the filters and the small
+  // input is the operand read once per XCD.
   const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  const int bm = logical / nblocks;
-  const int bn = logical - bm * nblocks;
+  int bm, bn;
+  if (xcd == 2) {
+    const int gm = gridDim.x / nblocks;
+    bn = logical / gm;
+    bm = logical - bn * gm;
+  } else {
+    bm = logical / nblocks;
+    bn = logical - bm * nblocks;
+  }
   const int m0 = bm * TM + wave_m * WM * 16;
   const int n0 = bn * TN + wave_n * WN * 16;
   const int r16 = lane & 15;
@@ -369,10 +379,15 @@ static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t 
   dv.in_c = FastDiv(p.in_c);
   dv.k_w = FastDiv(p.k_w);
   const int gm = (M + TM - 1) / TM, gn = (N + TN - 1) / TN;
-  static const int xcd = [] {
-    const char* e = std::getenv("BH_CONV_XCD");  // A-B runs: 0 = plain order
-    return e ? std::atoi(e) : 1;
+  static const int xcd_env = [] {
+    const char* e = std::getenv("BH_CONV_XCD");  // A-B runs: 0 plain order, 1 / 2 forced
+    return e ? std::atoi(e) : -1;
   }();
+  // replicate the smaller operand over the 8 XCDs' L2s: 8 x filters + input
+  // (xcd 1) against filters + 8 x input (xcd 2)
+  const long in_bytes = (long)p.batch * p.in_h * p.in_w * p.in_c;
+  const long w_bytes = (long)N * K;
+  const int xcd = xcd_env >= 0 ? xcd_env : (w_bytes > in_bytes ? 2 : 1);
   BH_LAUNCH((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
                      s, p, M, K, N, kchunk, dv, gn, xcd);
   return bh_check_launch("conv_mfma_kernel");
@@ -428,9 +443,17 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_con
   __shared__ __attribute__((aligned(16))) uint8_t lds[NB * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  // xcd: as in conv_mfma_kernel (1 = N-blocks fastest, 2 = pixel blocks fastest)
   const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  const int bm = logical / nblocks;
-  const int bn = logical - bm * nblocks;
+  int bm, bn;
+  if (xcd == 2) {
+    const int gm = gridDim.x / nblocks;
+    bn = logical / gm;
+    bm = logical - bn * gm;
+  } else {
+    bm = logical / nblocks;
+    bn = logical - bm * nblocks;
+  }
   const int tm0 = bm * BM;
   const int tn0 = bn * BN;
   const int N = p.out_c;
@@ -518,8 +541,13 @@ static int launch_gemm(const bh_conv_params& p, int M, int K, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   const int gm = (M + BM - 1) / BM, gn = (p.out_c + BN - 1) / BN;
+  static const int xcd_env = [] {
+    const char* e = std::getenv("BH_CONV_XCD");
+    return e ? std::atoi(e) : -1;
+  }();
+  const int xcd = xcd_env >= 0 ? xcd_env : ((long)p.out_c * K > (long)M * K ? 2 : 1);
   BH_LAUNCH((conv_gemm_kernel<WM, WN, WAVES_M, WAVES_N, NB>), dim3(gm * gn), dim3(WAVES_M * WAVES_N * 64), 0, s,
-            p, M, K, gn, (K + 63) / 64, 1);
+            p, M, K, gn, (K + 63) / 64, xcd);
   return bh_check_launch("conv_gemm_kernel");
 }
 

@@ -213,10 +213,14 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   bh::DirectDivs dv;
   dv.out_w = bh::FastDiv(p.out_w);
   dv.out_h = bh::FastDiv(p.out_h);
-  // >= ~512 workgroups: split the output channels over grid.y (8 at a time)
+  // >= ~min_wg workgroups: split the output channels over grid.y (8 at a time)
+  static const int min_wg = [] {
+    const char* e = std::getenv("BH_STEM_MIN_WG");  // A-B runs
+    return e ? std::atoi(e) : 512;
+  }();
   const int gx = (M + 255) / 256;
   const int groups = p.out_c / 8;
-  int gy = (512 + gx - 1) / gx;
+  int gy = (min_wg + gx - 1) / gx;
   gy = gy < 1 ? 1 : (gy > groups ? groups : gy);
   const int ch_per_y = (groups + gy - 1) / gy * 8;
   gy = (p.out_c + ch_per_y - 1) / ch_per_y;

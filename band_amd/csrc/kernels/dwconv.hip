@@ -9,6 +9,7 @@
 // NHWC), the 3x3 taps are fully unrolled with every in-bounds tap load
 // issued before the arithmetic, and (x' - zp_in) * (w' - zp_w) accumulates
 // exactly in int32.  Taps outside the image are skipped, as TFLite does.
+#include <climits>
 #include <cstdlib>
 
 #include "common.hpp"
@@ -590,12 +591,16 @@ static void launch3x3(const bh_dwconv_params& p, long pixels, hipStream_t s) {
 namespace {
 enum DwRoute { kRun1, kRun2, kRunD2, kDot16, kDot8, kDot4, kTap16, kTap8, kTap4, kGeneric, kMfma };
 
-// MFMA form from this many 16x16 output tiles (BH_DW_MFMA_MIN_TILES
-// overrides; A-B timing); below it the per-pixel / run forms
+// MFMA form from this many 16x16 output tiles (BH_DW_MFMA_MIN_TILES; the
+// round-2 default was 4096).  Off by default since round 3: the VALU run
+// form is faster on the standalone depthwise layers of the batch-24 C3 mix
+// (64 layers unfused: 397 vs 510 us; default fused tree: kernel sum 1432 vs
+// 1447 us, PoseNet -13.5 us; profiles/r03aw_dwab_*), and it keeps MFMA on
+// the dense contractions.  kernel_hint BH_DW_MFMA still forces it.
 long MfmaMinTiles() {
   static const long v = [] {
     const char* e = std::getenv("BH_DW_MFMA_MIN_TILES");
-    return e ? std::atol(e) : 4096L;
+    return e ? std::atol(e) : LONG_MAX;
   }();
   return v;
 }

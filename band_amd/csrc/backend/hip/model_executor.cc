@@ -969,7 +969,7 @@ absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in
         p.input = in_ptr;
         p.output = out_ptr;
         L->kind = Launch::kResizeBilinear;
-        L->kernel = "resize_bilinear_kernel";  // (row form resize_bilinear_rows_kernel when the rows fit LDS)
+        L->kernel = "resize_bilinear_kernel";  // (row forms resize_bilinear_rows_kernel / resize_bilinear_cols_kernel when the rows fit LDS)
       }
       return absl::OkStatus();
     }

@@ -255,6 +255,70 @@ __global__ __launch_bounds__(256) void resize_bilinear_rows_kernel(bh_resize_bil
   }
 }
 
+// Column-blend row form for channels >= 16 (DeepLab's 21-class logits):
+// the two input rows are blended VERTICALLY once per workgroup into int32
+// V[xi][c] = r0[xi][c] (1 - fy) + r1[xi][c] fy (dynamic LDS, in_w * C
+// words), so each output byte is (V[x0][c] (1 - fx) + V[x1][c] fx), the same
+// exact integer sum as TFLite's four terms (|s| <= 2^29, no overflow).  With
+// C >= 16 a thread's 16 consecutive bytes span at most two output pixels:
+// their column entries are read once (not per byte) and each byte picks one
+// of the two with a select, so a byte costs 2 LDS reads and ~12 VALU instead
+// of 7 LDS reads and ~30 VALU (the row kernel above was VALU-bound).
+__global__ __launch_bounds__(256) void resize_bilinear_cols_kernel(bh_resize_bilinear_params p, FastDiv chans,
+                                                                   int vec_ok) {
+  extern __shared__ __attribute__((aligned(16))) int32_t rz_lds[];
+  const int y = blockIdx.x % p.out_h;
+  const int n = blockIdx.x / p.out_h;
+  const int C = p.channels;
+  const int in_row = p.in_w * C;
+  int32_t* V = rz_lds;                // [in_row]
+  int32_t* X0 = rz_lds + in_row;      // [out_w]: x0 * C
+  int32_t* X1 = X0 + p.out_w;         // [out_w]: x1 * C
+  int32_t* FX = X1 + p.out_w;         // [out_w]: fx
+  constexpr int32_t one = 1 << 10;
+  const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1], iy = p.y_tab[3 * y + 2];
+  const int32_t fy = iy - one * y0;
+  const int8_t* src0 = (const int8_t*)p.input + ((long)n * p.in_h + y0) * in_row;
+  const int8_t* src1 = (const int8_t*)p.input + ((long)n * p.in_h + y1) * in_row;
+  for (int i = threadIdx.x; i < in_row; i += 256)
+    V[i] = (int32_t)src0[i] * (one - fy) + (int32_t)src1[i] * fy;
+  for (int x = threadIdx.x; x < p.out_w; x += 256) {
+    const int x0 = p.x_tab[3 * x];
+    X0[x] = x0 * C;
+    X1[x] = p.x_tab[3 * x + 1] * C;
+    FX[x] = p.x_tab[3 * x + 2] - one * x0;
+  }
+  __syncthreads();
+  const int row_bytes = p.out_w * C;
+  int8_t* dst = (int8_t*)p.output + ((long)n * p.out_h + y) * row_bytes;
+  for (int f0 = threadIdx.x * 16; f0 < row_bytes; f0 += 256 * 16) {
+    const int x = (int)chans.div((uint32_t)f0);
+    const int ch0 = f0 - x * C;
+    const int k = C - ch0;  // bytes b < k belong to pixel x, the rest to x + 1
+    const int xn = x + 1 < p.out_w ? x + 1 : x;
+    // per-pixel bases with the byte index folded out: byte b reads V[base + b]
+    const int a0 = X0[x] + ch0, a1 = X1[x] + ch0, fa = FX[x];
+    const int b0 = X0[xn] - k, b1 = X1[xn] - k, fb = FX[xn];
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const bool first = b < k;
+      const int o0 = (first ? a0 : b0) + b, o1 = (first ? a1 : b1) + b;
+      const int32_t fx = first ? fa : fb;
+      const int32_t v0 = V[o0], v1 = V[o1];
+      const int32_t s = v0 * (one - fx) + v1 * fx;
+      const int32_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
+      const uint32_t v = (uint32_t)(uint8_t)(int8_t)((s + rnd) / (1 << 20));
+      w[b >> 2] |= v << (8 * (b & 3));
+    }
+    if (vec_ok && f0 + 16 <= row_bytes) {
+      *(v4i*)(dst + f0) = (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
+    } else {
+      for (int b = 0; b < 16 && f0 + b < row_bytes; ++b) dst[f0 + b] = (int8_t)(w[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
 // ---- softmax ----------------------------------------------------------------
 // One thread per row; the float operations are issued exactly as the
 // reference's loop runs them (no contraction: explicit _rn intrinsics).
@@ -461,6 +525,16 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
       (long)p.batch * p.out_h < INT32_MAX) {
     // 16-byte stores when every output row starts 16-byte aligned
     const int vec_ok = ((p.out_w * p.channels) % 16 == 0 && ((uintptr_t)p.output & 15) == 0) ? 1 : 0;
+    static const bool rows_only = [] {
+      const char* e = std::getenv("BH_RESIZE_ROWS");  // A-B: the byte-blend row kernel only
+      return e && e[0] == '1';
+    }();
+    const size_t lds = ((size_t)p.in_w * p.channels + 3 * (size_t)p.out_w) * sizeof(int32_t);
+    if (!rows_only && p.channels >= 16 && lds <= 64 * 1024) {
+      BH_LAUNCH(bh::resize_bilinear_cols_kernel, dim3(p.batch * p.out_h), dim3(256), lds, (hipStream_t)s, p,
+                bh::FastDiv(p.channels), vec_ok);
+      return bh_check_launch("resize_bilinear_cols_kernel");
+    }
     BH_LAUNCH(bh::resize_bilinear_rows_kernel, dim3(p.batch * p.out_h), dim3(256), 0, (hipStream_t)s, p,
               bh::FastDiv(p.channels), vec_ok);
     return bh_check_launch("resize_bilinear_rows_kernel");

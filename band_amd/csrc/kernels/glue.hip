@@ -66,19 +66,26 @@ __global__ __launch_bounds__(256) void quantize_f32_kernel(const float* __restri
 struct ConcatDivs {
   FastDiv row[BH_CONCAT_MAX_INPUTS];
   long off[BH_CONCAT_MAX_INPUTS];  // byte offset of input k inside an output row
+  int blk0[BH_CONCAT_MAX_INPUTS + 1];  // first workgroup of input k (1-D grid)
   long out_row;
   int vec4;                        // every row / offset / pointer dword aligned
 };
 
-// blockIdx.y = input k; its outer x row bytes are copied (dwords when
-// aligned), through its rescale table when one is given
+// One 1-D grid over the inputs' own ranges (input k owns workgroups
+// [blk0[k], blk0[k+1]), found by a wave-uniform scan), so no workgroup exits
+// idle for the smaller inputs (a grid.y per input launched max-input-sized
+// ranges for every input: SSD's 6-input class concat ran 6x the workgroups
+// it needed).  A thread copies 4 bytes: one dword when everything is
+// aligned, else 4 bytes that may cross an output row, through the input's
+// rescale table when one is given.
 __global__ __launch_bounds__(256) void concat_kernel(bh_concat_params p, ConcatDivs dv) {
-  const int k = blockIdx.y;
+  int k = 0;
+  for (int q = 1; q < p.n_inputs; ++q) k += (int)blockIdx.x >= dv.blk0[q];
   const uint8_t* src = (const uint8_t*)p.input[k];
   const uint8_t* tab = (const uint8_t*)p.table[k];
   uint8_t* dst = (uint8_t*)p.output + dv.off[k];
   const long row = p.row[k];
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const long i = (long)((int)blockIdx.x - dv.blk0[k]) * 256 + threadIdx.x;  // 4-byte unit
   if (dv.vec4 && !tab) {
     const long units = p.outer * (row / 4);
     if (i >= units) return;
@@ -86,11 +93,22 @@ __global__ __launch_bounds__(256) void concat_kernel(bh_concat_params p, ConcatD
     const long j = 4 * i - (long)o * row;
     *(uint32_t*)(dst + o * dv.out_row + j) = *(const uint32_t*)(src + 4 * i);
   } else {
-    if (i >= p.outer * row) return;
-    const uint32_t o = dv.row[k].div((uint32_t)i);
-    const long j = i - (long)o * row;
-    const uint8_t v = src[i];
-    dst[o * dv.out_row + j] = tab ? tab[v] : v;
+    const long total = p.outer * row;
+    const long b0 = 4 * i;
+    if (b0 >= total) return;
+    long o = dv.row[k].div((uint32_t)b0);
+    long j = b0 - o * row;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      if (b0 + b < total) {
+        const uint8_t v = src[b0 + b];
+        dst[o * dv.out_row + j] = tab ? tab[v] : v;
+      }
+      if (++j == row) {
+        j = 0;
+        ++o;
+      }
+    }
   }
 }
 
@@ -442,8 +460,15 @@ extern "C" int bh_concat(const bh_concat_params* pp, bh_stream_t s) {
     return BH_EINVAL;
   }
   if (maxbytes == 0) return 0;
-  const dim3 grid(bh::blocks(maxbytes), (unsigned)p.n_inputs);
-  BH_LAUNCH(bh::concat_kernel, grid, dim3(256), 0, (hipStream_t)s, p, dv);
+  // 4 bytes per thread; input k's workgroups follow input k-1's
+  int blk = 0;
+  for (int k = 0; k < p.n_inputs; ++k) {
+    dv.blk0[k] = blk;
+    blk += (int)bh::blocks((p.outer * p.row[k] + 3) / 4);
+  }
+  dv.blk0[p.n_inputs] = blk;
+  if (blk == 0) return 0;
+  BH_LAUNCH(bh::concat_kernel, dim3((unsigned)blk), dim3(256), 0, (hipStream_t)s, p, dv);
   return bh_check_launch("concat_kernel");
 }
 

@@ -51,6 +51,9 @@ _abi.BACKEND_SYMBOLS.update({
     "bhx_pin_process_to_gpu": (c_int, [c_int]),
     "bhx_pin_process_to_cpus": (c_int, [ctypes.POINTER(c_int), c_int]),
     "bhx_ring_page_nodes": (c_int, [ctypes.POINTER(ctypes.c_longlong), c_int]),
+    "bhx_ring_host_alloc": (c_void_p, [c_size_t]),
+    "bhx_ring_host_free": (None, [c_void_p]),
+    "bhx_pin_worker_thread": (c_int, [c_int]),
     "bhx_investigate_model_spec": (c_int, [c_void_p, c_void_p, ctypes.c_char_p, c_size_t,
                                            ctypes.POINTER(c_size_t)]),
     "bhx_prepare_subgraph": (c_int, [c_void_p, c_void_p, ctypes.POINTER(c_int), c_int,
@@ -413,7 +416,7 @@ class HipModelExecutor:
     def ExecuteSubgraph(self, key):
         return Status.from_rc(self.lib.bhx_execute_subgraph(self.handle, *key._args()))
 
-    # ---- job batching (band/interface/job_batching.h) -------------------
+    # ---- job batching (backend/hip/job_batching.h) -------------------
     def PrepareJobBatches(self, model, key, max_batch):
         return Status.from_rc(self.lib.bhx_prepare_job_batches(self.handle, model.handle, *key._args(),
                                                                int(max_batch)))

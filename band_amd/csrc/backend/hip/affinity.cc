@@ -11,6 +11,7 @@
 #include <mutex>
 #include <sstream>
 
+#include "band/device/cpu.h"
 #include "band_hip_kernels.h"
 
 namespace band {
@@ -54,6 +55,16 @@ const std::vector<int>& ProcessCpus() {
     if (sched_getaffinity(getpid(), sizeof(m), &m) != 0) return std::vector<int>();
     return MaskCpus(m);
   }();
+  return cpus;
+}
+
+std::vector<int> PinnableCpus(const CpuSet& set) {
+  std::vector<int> cpus;
+  const int n = static_cast<int>(std::min<size_t>(GetCPUCount(), CPU_SETSIZE));
+  for (int i = 0; i < n; ++i)
+    if (set.IsEnabled(i)) cpus.push_back(i);
+  const std::vector<int>& allowed = ProcessCpus();
+  if (cpus.empty() || std::includes(cpus.begin(), cpus.end(), allowed.begin(), allowed.end())) return {};
   return cpus;
 }
 

@@ -7,11 +7,14 @@
 // pool to it.  An empty set (what BandCPUMaskGetSet returns on Linux,
 // band/device/cpu.cc:377-381) leaves the threads where they are.
 //
-// kGPU executors pin the calling worker thread to the CPUs of its GPU's NUMA
-// node (PCI sysfs numa_node of hipDeviceGetPCIBusId), intersected with the
-// CPUs the process may use, before the thread's first GPU call: the job's
-// host copies (request ring -> pinned input mirror -> H2D) then stay on the
-// socket the GPU hangs off.  BANDX_NUMA_PIN=0 turns this off.
+// kGPU executors never move the thread that calls them (it may be the
+// application's own).  An engine that owns its GPU worker threads may pin
+// each one to the CPUs of its GPU's NUMA node (PCI sysfs numa_node of
+// hipDeviceGetPCIBusId), intersected with the CPUs the process may use,
+// through the optional bhx_pin_worker_thread hook (include/band_hip_backend.h;
+// this repo's harness calls it from Worker::Work when the worker's CpuSet
+// names no CPUs): the job's host copies then stay on the socket the GPU hangs
+// off.  BANDX_NUMA_PIN=0 turns this off.
 #pragma once
 
 #include <pthread.h>
@@ -20,7 +23,15 @@
 #include <vector>
 
 namespace band {
+class CpuSet;
 namespace hip {
+
+// The CPUs a CpuSet asks for, read with the reference's own API
+// (band/device/cpu.h:21-40: IsEnabled(i) for i < GetCPUCount()).  Empty -
+// "do not pin" - when the set enables nothing or every CPU the process may
+// use: the reference's Linux build reports every CPU enabled
+// (band/device/cpu.cc:72-92), and an all-CPU mask is no constraint.
+std::vector<int> PinnableCpus(const CpuSet& set);
 
 // "0-3,8,10-11" -> {0,1,2,3,8,10,11}; malformed pieces are skipped
 std::vector<int> ParseCpuList(const std::string& s);

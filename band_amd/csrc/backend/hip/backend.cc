@@ -6,30 +6,13 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <unordered_map>
 
+#include "band_hip_backend.h"
 #include "band_hip_kernels.h"
-#include "engine/tensor.h"
 
 namespace band {
-
-namespace {
-// request-ring slots in page-locked memory when a GPU is present, so batched
-// passes DMA them directly (HipModelExecutor::ExecuteJobBatchDirect);
-// BAND_HIP_PINNED_RINGS=0 keeps them on the heap
-void* RingAlloc(size_t bytes) {
-  static const bool on = [] {
-    const char* e = std::getenv("BAND_HIP_PINNED_RINGS");
-    int n = 0;
-    return !(e && e[0] == '0') && bh_device_count(&n) == 0 && n > 0;
-  }();
-  void* p = nullptr;
-  if (!on || bh_host_alloc(&p, bytes) != 0) return nullptr;
-  hip::CountRingPages(p, bytes);
-  return p;
-}
-void RingFree(void* p) { bh_host_free(p); }
-}  // namespace
-
 namespace hip {
 namespace {
 constexpr int kMaxNodes = 64;
@@ -61,10 +44,6 @@ int RingPageNodes(long long* bytes_per_node, int cap) {
 bool HipRegisterCreators() {
   BackendFactory::RegisterBackendCreators(BackendType::kTfLite, new hip::ModelExecutorCreator,
                                           new hip::ModelCreator, new hip::UtilCreator);
-  RingHostAllocator a;
-  a.alloc = RingAlloc;
-  a.free = RingFree;
-  SetRingHostAllocator(a);
   return true;
 }
 
@@ -72,3 +51,57 @@ bool HipRegisterCreators() {
 bool TfLiteRegisterCreators() { return HipRegisterCreators(); }
 
 }  // namespace band
+
+namespace {
+std::mutex g_ring_mu;
+long long g_ring_pinned_bytes = 0;
+std::unordered_map<void*, long long> g_ring_blocks;
+}  // namespace
+
+// request-ring slots in page-locked memory (include/band_hip_backend.h):
+// the engine asks only for models a GPU worker runs whole, so batched and
+// one-job passes DMA them directly (HipModelExecutor::ExecuteJobBatchDirect)
+extern "C" void* bhx_ring_host_alloc(size_t bytes) {
+  static const bool on = [] {
+    const char* e = std::getenv("BAND_HIP_PINNED_RINGS");
+    int n = 0;
+    return !(e && e[0] == '0') && bh_device_count(&n) == 0 && n > 0;
+  }();
+  static const long long cap = [] {
+    const char* e = std::getenv("BAND_HIP_PINNED_RING_MB");
+    const long long mb = e ? std::atoll(e) : 8192;
+    return (mb > 0 ? mb : 0) << 20;
+  }();
+  if (!on || bytes == 0) return nullptr;
+  const long long b = static_cast<long long>(bytes);
+  {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    if (g_ring_pinned_bytes + b > cap) return nullptr;
+    g_ring_pinned_bytes += b;
+  }
+  void* p = nullptr;
+  if (bh_host_alloc(&p, bytes) != 0 || !p) {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    g_ring_pinned_bytes -= b;
+    return nullptr;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    g_ring_blocks[p] = b;
+  }
+  band::hip::CountRingPages(p, bytes);
+  return p;
+}
+
+extern "C" void bhx_ring_host_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    auto it = g_ring_blocks.find(p);
+    if (it != g_ring_blocks.end()) {
+      g_ring_pinned_bytes -= it->second;
+      g_ring_blocks.erase(it);
+    }
+  }
+  bh_host_free(p);
+}

@@ -108,7 +108,7 @@ int bhx_executor_create(int model_id, int worker_id, int device_flag, int num_th
 int bhx_executor_create_masked(int model_id, int worker_id, int device_flag, int num_threads, const int* cpus,
                                int n_cpus, bhx_executor** out) {
   if (!out || device_flag < 0 || device_flag > 3 || n_cpus < 0 || (n_cpus > 0 && !cpus)) return Fail("bad arguments");
-  band::CpuSet mask = band::BandCPUMaskGetSet(band::CPUMaskFlag::kAll);
+  band::CpuSet mask;  // empty: "no constraint", like an all-CPU set
   for (int i = 0; i < n_cpus; ++i) mask.Enable(cpus[i]);
   auto* e = BackendFactory::CreateModelExecutor(BackendType::kTfLite, model_id, worker_id,
                                                 static_cast<DeviceFlag>(device_flag), mask, num_threads);
@@ -132,6 +132,12 @@ int bhx_ring_page_nodes(long long* bytes_per_node, int cap) {
 }
 
 int bhx_pin_process_to_gpu(int ordinal) { return band::hip::PinProcessToGpu(ordinal); }
+
+int bhx_pin_worker_thread(int worker_id) {
+  const int ordinal = band::hip::DeviceRegistry::Get().FindWorkerOrdinal(worker_id);
+  if (ordinal < 0) return -1;
+  return band::hip::PinCallingThreadToGpu(ordinal) ? 1 : 0;
+}
 
 int bhx_pin_process_to_cpus(const int* cpus, int n_cpus) {
   if (n_cpus <= 0 || !cpus) return -1;
@@ -383,14 +389,14 @@ int bhx_profile_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int i
 }
 
 int bhx_prepare_job_batches(bhx_executor* e, bhx_model* m, int mid, int wid, uint64_t mask, int max_batch) {
-  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  auto* b = e ? dynamic_cast<band::hip::IJobBatching*>(e->exec.get()) : nullptr;
   if (!b || !m) return Fail("executor without job batching");
   auto s = b->PrepareJobBatches(m->model.get(), Key(mid, wid, mask), max_batch);
   return s.ok() ? 0 : Fail(s);
 }
 
 int bhx_max_job_batch(bhx_executor* e, int mid, int wid, uint64_t mask, int* max_batch) {
-  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  auto* b = e ? dynamic_cast<band::hip::IJobBatching*>(e->exec.get()) : nullptr;
   if (!max_batch) return Fail("null argument");
   *max_batch = b ? b->MaxJobBatch(Key(mid, wid, mask)) : 1;
   return 0;
@@ -398,13 +404,13 @@ int bhx_max_job_batch(bhx_executor* e, int mid, int wid, uint64_t mask, int* max
 
 int bhx_job_slot_view(bhx_executor* e, int mid, int wid, uint64_t mask, int t, int n, int slot,
                       bhx_tensor_info* info) {
-  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  auto* b = e ? dynamic_cast<band::hip::IJobBatching*>(e->exec.get()) : nullptr;
   if (!b || !info) return Fail("executor without job batching");
   return FillInfo(b->GetJobSlotView(Key(mid, wid, mask), t, n, slot), info);
 }
 
 int bhx_execute_job_batch(bhx_executor* e, int mid, int wid, uint64_t mask, int n) {
-  auto* b = e ? dynamic_cast<band::interface::IJobBatching*>(e->exec.get()) : nullptr;
+  auto* b = e ? dynamic_cast<band::hip::IJobBatching*>(e->exec.get()) : nullptr;
   if (!b) return Fail("executor without job batching");
   auto s = b->ExecuteJobBatch(Key(mid, wid, mask), n);
   return s.ok() ? 0 : Fail(s);

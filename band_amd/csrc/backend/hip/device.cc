@@ -92,6 +92,12 @@ int DeviceRegistry::OrdinalForWorker(int worker_id) {
   return ord;
 }
 
+int DeviceRegistry::FindWorkerOrdinal(int worker_id) {
+  std::lock_guard<std::mutex> l(mu_);
+  auto it = worker_ordinal_.find(worker_id);
+  return it != worker_ordinal_.end() ? it->second : -1;
+}
+
 bh_stream_t DeviceRegistry::StreamForWorker(int worker_id) {
   const int ord = OrdinalForWorker(worker_id);
   std::lock_guard<std::mutex> l(mu_);

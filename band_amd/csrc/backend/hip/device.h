@@ -75,6 +75,8 @@ class DeviceRegistry {
   bool GpuAvailable();  // at least one gfx950 device
   void SetWorkerOrdinal(int worker_id, int ordinal);
   int OrdinalForWorker(int worker_id);
+  // the ordinal already mapped to worker_id (-1: none yet); assigns nothing
+  int FindWorkerOrdinal(int worker_id);
   bh_stream_t StreamForWorker(int worker_id);
 
   // Device-resident constant operands shared by every executor of a model on

@@ -64,9 +64,10 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
     stream_ = DeviceRegistry::Get().StreamForWorker(worker_id_);
   } else if (device_flag_ == DeviceFlag::kCPU) {
     // host execution of the lowered program (cpu_kernels.h)
-    // pinned to the executor's CpuSet when it names CPUs (affinity.h)
+    // pinned to the executor's CpuSet when it names a proper subset of the
+    // process's CPUs (affinity.h PinnableCpus)
     cpu_pool_ = std::make_unique<CpuPool>(num_threads_ > 0 ? num_threads_ : 1,
-                                          thread_affinity_mask_.GetMaskBitsVector());
+                                          PinnableCpus(thread_affinity_mask_));
   }
   const char* g = std::getenv("BAND_HIP_GRAPH");
   if (g && g[0] == '0') use_graph_ = false;
@@ -2524,8 +2525,6 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (!sg) return absl::InternalError("Cannot find subgraph");
   if (device_flag_ == DeviceFlag::kCPU) return ExecuteOnHost(sg);
   if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("Unsupported device type");
-  // the worker thread goes to its GPU's NUMA node before its first GPU call
-  PinCallingThreadToGpu(ordinal_);
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) RETURN_STATUS_IF(CaptureGraph(sg));
@@ -2630,10 +2629,12 @@ absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int
     for (size_t k = 0; k < out.size(); ++k)
       if (out[k] && out[k]->GetBytes() != meta_[base->outputs[k]]->bytes)
         return absl::InternalError("direct job I/O: output size");
-    PinCallingThreadToGpu(ordinal_);
     int rc = bh_set_device(ordinal_);
     if (rc) return HipErr(rc, "hipSetDevice");
     char* arena = static_cast<char*>(base->arena->ptr());
+    // set first: a retarget that fails part-way leaves the nodes already
+    // changed pointing at ring slots, and RestoreIoNodes must reset them all
+    base->io_retargeted = true;
     for (const auto& nd : base->io_nodes) {
       char* dev = arena + base->offset.at(nd.tensor);
       const size_t bytes = meta_[nd.tensor]->bytes;
@@ -2647,7 +2648,6 @@ absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int
       }
       if (rc) return HipErr(rc, "graph copy node");
     }
-    base->io_retargeted = true;
     rc = bh_graph_launch(base->graph, stream_);
     if (rc) return HipErr(rc, "graph launch");
     if (block_sync_) {
@@ -2686,7 +2686,6 @@ absl::Status HipModelExecutor::RunDirect(PreparedSubgraph* sg, int n, const std:
     if (!in[i] || in[i]->GetBytes() != per_job[i / n]) return absl::InternalError("direct job batch I/O: input size");
   for (size_t i = 0; i < out.size(); ++i)
     if (out[i] && out[i]->GetBytes() != per_job[ni + i / n]) return absl::InternalError("direct job batch I/O: output size");
-  PinCallingThreadToGpu(ordinal_);
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) {  // kernels-only graph (variants stream their I/O)

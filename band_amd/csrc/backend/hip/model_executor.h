@@ -28,7 +28,7 @@
 #include "backend/hip/device.h"
 #include "backend/hip/model.h"
 #include "backend/hip/tensor.h"
-#include "band/interface/job_batching.h"
+#include "backend/hip/job_batching.h"
 #include "band/interface/model_executor.h"
 #include "band_hip_kernels.h"
 
@@ -118,7 +118,7 @@ struct PreparedSubgraph {
   int runs = 0;
 };
 
-class HipModelExecutor : public interface::IModelExecutor, public interface::IJobBatching {
+class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
  public:
   HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceFlag device_flag,
                    CpuSet thread_affinity_mask, int num_threads);
@@ -140,7 +140,7 @@ class HipModelExecutor : public interface::IModelExecutor, public interface::IJo
   absl::Status ExecuteSubgraph(const SubgraphKey& key) override;
   void ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) override;
 
-  // --- job batching (band/interface/job_batching.h; kGPU executors) ---
+  // --- job batching (backend/hip/job_batching.h; kGPU executors) ---
   // Variants for 2, 4, 8, ... and max_batch jobs: each is an executor of a
   // batch-B copy of the model (HipModel::CloneWithJobBatch) over the same op
   // set, on this executor's stream, sharing its device weights.

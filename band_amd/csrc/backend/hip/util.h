@@ -3,6 +3,9 @@
 // CPU worker to host every model: band/engine.cc:248-252); kGPU when a
 // gfx950 device is visible.
 #pragma once
+#include <set>
+
+#include "band/common.h"
 #include "band/interface/backend.h"
 
 namespace band {

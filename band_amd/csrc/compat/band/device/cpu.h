@@ -1,35 +1,56 @@
-// Stand-in for band/device/cpu.h: the CpuSet handed to every executor
-// (band/interface/model_executor.h:41-50).  Affinity is only honoured by
-// the reference on mobile builds (band/device/util.h:12-16); the HIP
-// backend records it and otherwise ignores it.
+// Stand-in for band/device/cpu.h, signature-identical to
+// /root/reference/band/device/cpu.h:21-57 (CpuSet, GetCPUCount,
+// SetCPUThreadAffinity, BandCPUMaskGetSet).  The set holds a real cpu_set_t,
+// as the reference's BAND_IS_MOBILE build does (band/device/cpu.cc:39-70);
+// on this x86 harness every CPUMaskFlag maps to "all CPUs the process may
+// use" (no big.LITTLE clusters), which the HIP backend reads as "no pinning",
+// exactly as it reads the reference's Linux build, where IsEnabled() is
+// always true (band/device/cpu.cc:72-92).
 #pragma once
+
+#include <limits.h>
+#include <sched.h>
+#include <stddef.h>
+
+#include <string>
 #include <vector>
 
+#include "absl/status/status.h"
 #include "band/common.h"
 
 namespace band {
+
 class CpuSet {
  public:
-  CpuSet() = default;
-  void Enable(int cpu) { if (cpu >= 0) { if ((int)bits_.size() <= cpu) bits_.resize(cpu + 1, false); bits_[cpu] = true; } }
-  bool IsEnabled(int cpu) const { return cpu >= 0 && cpu < (int)bits_.size() && bits_[cpu]; }
-  int NumEnabled() const { int n = 0; for (bool b : bits_) n += b; return n; }
-  std::vector<int> GetMaskBitsVector() const {
-    std::vector<int> v;
-    for (int i = 0; i < (int)bits_.size(); ++i) if (bits_[i]) v.push_back(i);
-    return v;
-  }
-  CPUMaskFlag GetCPUMaskFlag() const { return flag_; }
-  void SetFlag(CPUMaskFlag f) { flag_ = f; }
+  CpuSet();
+  void Enable(int cpu);
+  void Disable(int cpu);
+  void DisableAll();
+  bool IsEnabled(int cpu) const;
+  size_t NumEnabled() const;
+  CPUMaskFlag GetCPUMaskFlag() const;
+  // the raw cpu_set_t words (band/device/cpu.cc:52-56)
+  const unsigned long* GetMaskBits() const;
+  std::vector<unsigned long> GetMaskBitsVector() const;
+  std::string ToString() const;
+  bool operator==(const CpuSet& rhs) const;
+
+  const cpu_set_t& GetCpuSet() const { return cpu_set_; }
+  cpu_set_t& GetCpuSet() { return cpu_set_; }
 
  private:
-  std::vector<bool> bits_;
-  CPUMaskFlag flag_ = CPUMaskFlag::kAll;
+  cpu_set_t cpu_set_;
 };
 
-inline CpuSet BandCPUMaskGetSet(CPUMaskFlag flag) {
-  CpuSet s;
-  s.SetFlag(flag);
-  return s;
-}
+// cpu info
+size_t GetCPUCount();
+size_t GetLittleCPUCount();
+size_t GetBigCPUCount();
+
+// set explicit thread affinity (calling thread)
+absl::Status SetCPUThreadAffinity(const CpuSet& thread_affinity_mask);
+absl::Status GetCPUThreadAffinity(CpuSet& thread_affinity_mask);
+
+// convenient wrapper
+const CpuSet& BandCPUMaskGetSet(CPUMaskFlag flag);
 }  // namespace band

@@ -2,7 +2,7 @@
 
 #include <cstdlib>
 
-#include "band/interface/job_batching.h"
+#include "backend/hip/job_batching.h"
 
 #include <algorithm>
 #include <cassert>
@@ -15,6 +15,12 @@
 #include "band/backend_factory.h"
 #include "band/interface/tensor_view.h"
 #include "engine/time.h"
+
+// Optional page-locked ring memory from the HIP backend
+// (include/band_hip_backend.h); weak, so an engine linked without that
+// backend keeps heap rings.
+extern "C" void* bhx_ring_host_alloc(size_t bytes) __attribute__((weak));
+extern "C" void bhx_ring_host_free(void* p) __attribute__((weak));
 
 namespace band {
 
@@ -135,7 +141,7 @@ absl::Status Engine::RegisterModel(Model* model) {
       // job batching for whole-model subgraphs on GPU workers (config extension)
       if (max_job_batch_ > 1 && GetWorkerDevice(def.worker_id) == DeviceFlag::kGPU &&
           static_cast<int>(def.op_indices.size()) == spec.num_ops) {
-        if (auto* jb = dynamic_cast<interface::IJobBatching*>(exec)) {
+        if (auto* jb = dynamic_cast<hip::IJobBatching*>(exec)) {
           absl::Status bs = jb->PrepareJobBatches(backend_model, key, max_job_batch_);
           if (!bs.ok())
             BAND_LOG(LogSeverity::kWarning, "model %d runs unbatched on worker %d: %s", model_id, def.worker_id,
@@ -204,15 +210,35 @@ absl::Status Engine::RegisterModel(Model* model) {
     // several workers want more)
     int slots = 128;
     if (const char* rs = std::getenv("BANDX_REQUEST_RING_SLOTS")) slots = std::max(1, std::atoi(rs));
+    const RingHostAllocator ring_alloc = RingAllocatorFor(model_id, spec.num_ops);
     model_input_buffer_[model_id].reset(new TensorRingBuffer(
-        in_views, std::vector<int>(spec.input_tensors.begin(), spec.input_tensors.end()), slots));
+        in_views, std::vector<int>(spec.input_tensors.begin(), spec.input_tensors.end()), slots, ring_alloc));
     model_output_buffer_[model_id].reset(new TensorRingBuffer(
-        out_views, std::vector<int>(spec.output_tensors.begin(), spec.output_tensors.end()), slots));
+        out_views, std::vector<int>(spec.output_tensors.begin(), spec.output_tensors.end()), slots, ring_alloc));
 
     absl::Status ls = latency_estimator_->ProfileModel(model_id);
     if (!ls.ok()) return ls;
   }
   return absl::OkStatus();
+}
+
+// Page-locked rings pay only where a GPU worker runs the whole model (its
+// one-job and batched passes DMA the ring slots directly); every other model
+// keeps heap rings, so CPU-only engines pin nothing and initialise no GPU.
+RingHostAllocator Engine::RingAllocatorFor(ModelId model_id, int num_ops) const {
+  RingHostAllocator a;
+  if (!bhx_ring_host_alloc || !bhx_ring_host_free) return a;
+  for (WorkerId w = 0; w < static_cast<WorkerId>(workers_.size()); ++w) {
+    if (GetWorkerDevice(w) != DeviceFlag::kGPU) continue;
+    const SubgraphKey key = GetLargestSubgraphKey(model_id, w);
+    const interface::IModelExecutor* exec = key.IsValid() ? GetModelExecutor(key) : nullptr;
+    if (exec && static_cast<int>(exec->GetNumNodes(key)) == num_ops) {
+      a.alloc = bhx_ring_host_alloc;
+      a.free = bhx_ring_host_free;
+      break;
+    }
+  }
+  return a;
 }
 
 absl::Status Engine::UnregisterModel(Model* model) {
@@ -300,6 +326,10 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
     }
     if (i < inputs.size() && (!model_input_buffer_.count(model_ids[i]) || !model_output_buffer_.count(model_ids[i])))
       return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
+    // every input is checked before any run is enqueued, so a refused call
+    // has started no job
+    if (i < inputs.size() && !model_input_buffer_.at(model_ids[i])->CheckTensors(inputs[i]).ok())
+      return absl::InternalError("Input copy failure for model " + std::to_string(model_ids[i]));
     jobs.push_back(std::move(job));
   }
   // Ring slots are taken per run of consecutive same-model requests, all of
@@ -351,6 +381,18 @@ void Engine::ReleaseRequest(const Job& job) {
   if (job.input_handle < 0) return;
   auto it = model_input_buffer_.find(job.model_id);
   if (it != model_input_buffer_.end()) it->second->Release(job.input_handle);
+}
+
+void Engine::HoldOutput(const Job& job) {
+  if (job.output_handle < 0) return;
+  auto it = model_output_buffer_.find(job.model_id);
+  if (it != model_output_buffer_.end()) it->second->Hold(job.output_handle);
+}
+
+void Engine::UnholdOutput(const Job& job) {
+  if (job.output_handle < 0) return;
+  auto it = model_output_buffer_.find(job.model_id);
+  if (it != model_output_buffer_.end()) it->second->Unhold(job.output_handle);
 }
 
 int Engine::RequestRingSize(ModelId model_id) const {
@@ -716,6 +758,9 @@ absl::Status Engine::CopyOutputs(const Job& job, const ViewFn& view) {
   auto ring = model_output_buffer_.find(job.model_id);
   if (ring == model_output_buffer_.end())
     return absl::InternalError("Failed to find output tensor ring buffer for model " + std::to_string(job.model_id));
+  // the slot becomes this request's (after any callback still reading the
+  // previous request's outputs there has returned)
+  ring->second->AcquireForWrite(job.output_handle);
   for (int t : exec->GetOutputs(key)) {
     if (!ring->second->IsTensorIndexValid(t)) continue;
     auto src = view(t);
@@ -728,26 +773,26 @@ absl::Status Engine::CopyOutputs(const Job& job, const ViewFn& view) {
 
 int Engine::MaxJobBatch(const SubgraphKey& key) const {
   if (max_job_batch_ <= 1) return 1;
-  auto* jb = dynamic_cast<const interface::IJobBatching*>(GetModelExecutor(key));
+  auto* jb = dynamic_cast<const hip::IJobBatching*>(GetModelExecutor(key));
   return jb ? jb->MaxJobBatch(key) : 1;
 }
 
 absl::Status Engine::TryCopyInputTensorsToSlot(const Job& job, int n, int slot) {
   if (job.input_handle < 0) return absl::OkStatus();
   const SubgraphKey& key = job.subgraph_key;
-  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  auto* jb = dynamic_cast<hip::IJobBatching*>(GetModelExecutor(key));
   if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
   return CopyInputs(job, [&](int t) { return jb->GetJobSlotView(key, t, n, slot); });
 }
 
 absl::Status Engine::InvokeJobBatch(const SubgraphKey& key, int n) {
-  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  auto* jb = dynamic_cast<hip::IJobBatching*>(GetModelExecutor(key));
   if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
   return jb->ExecuteJobBatch(key, n);
 }
 
 absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vector<Job*>& jobs) {
-  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  auto* jb = dynamic_cast<hip::IJobBatching*>(GetModelExecutor(key));
   interface::IModelExecutor* exec = GetModelExecutor(key);
   const int n = static_cast<int>(jobs.size());
   if (!jb || !exec || n < 1) return absl::UnimplementedError("direct job batch I/O");
@@ -769,10 +814,12 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
       if (!t || !t->IsRingMemory()) return absl::UnimplementedError("input slot not page-locked");
       in[k * n + s] = t;
     }
-    for (size_t k = 0; k < outs.size(); ++k) {
+    for (size_t k = 0; k < outs.size(); ++k)
       // a subgraph output outside the output ring feeds a later subgraph:
       // it must reach the executor's own views
       if (!out_it->second->IsTensorIndexValid(outs[k])) return absl::UnimplementedError("intermediate output");
+    out_it->second->AcquireForWrite(j.output_handle);  // as in CopyOutputs
+    for (size_t k = 0; k < outs.size(); ++k) {
       Tensor* t = out_it->second->SlotTensor(outs[k], j.output_handle);
       if (!t || !t->IsRingMemory()) return absl::UnimplementedError("output slot not page-locked");
       out[k * n + s] = t;
@@ -784,7 +831,7 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
 absl::Status Engine::TryCopyOutputTensorsFromSlot(const Job& job, int n, int slot) {
   if (job.output_handle < 0) return absl::OkStatus();
   const SubgraphKey& key = job.subgraph_key;
-  auto* jb = dynamic_cast<interface::IJobBatching*>(GetModelExecutor(key));
+  auto* jb = dynamic_cast<hip::IJobBatching*>(GetModelExecutor(key));
   if (!jb) return absl::InternalError("no batching executor for " + key.ToString());
   return CopyOutputs(job, [&](int t) { return jb->GetJobSlotView(key, t, n, slot); });
 }

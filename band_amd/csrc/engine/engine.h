@@ -127,6 +127,8 @@ class Engine : public IEngine {
   void PrepareReenqueue(Job& job) override { planner_->PrepareReenqueue(job); }
   void EnqueueFinishedJob(Job& job) override { planner_->EnqueueFinishedJob(job); }
   void ReleaseRequest(const Job& job) override;
+  void HoldOutput(const Job& job) override;
+  void UnholdOutput(const Job& job) override;
   // request-ring slots per model: the most unfinished requests it can have
   int RequestRingSize(ModelId model_id) const;
   bool EnqueueToWorker(const ScheduleAction& action) override { return planner_->EnqueueToWorker({action}); }
@@ -148,6 +150,7 @@ class Engine : public IEngine {
   Engine() = default;
   absl::Status Init(const RuntimeConfig& config);
   const interface::IModelExecutor* GetModelExecutor(const SubgraphKey& key) const;
+  RingHostAllocator RingAllocatorFor(ModelId model_id, int num_ops) const;
 
   SubgraphConfig subgraph_config_;
   int max_job_batch_ = 1;

@@ -64,7 +64,7 @@ class IEngine {
   // snapshot a non-final subgraph's outputs into the job's following jobs
   virtual absl::Status SaveIntermediates(Job& job) { return absl::OkStatus(); }
 
-  // job batching (interface/job_batching.h): n jobs of one subgraph, job i
+  // job batching (backend/hip/job_batching.h): n jobs of one subgraph, job i
   // in slot i; MaxJobBatch == 1 means the worker never batches `key`
   virtual int MaxJobBatch(const SubgraphKey& key) const { return 1; }
   virtual absl::Status TryCopyInputTensorsToSlot(const Job& job, int n, int slot) {
@@ -95,6 +95,11 @@ class IEngine {
   virtual void EnqueueFinishedJob(Job& job) = 0;
   // a finished request frees its request-ring slot (ring back-pressure)
   virtual void ReleaseRequest(const Job& job) {}
+  // keeps a finished request's output slot from being rewritten by a newer
+  // request while the end-request callbacks read it (Hold before the input
+  // slot is released, Unhold after the callbacks)
+  virtual void HoldOutput(const Job& job) {}
+  virtual void UnholdOutput(const Job& job) {}
   virtual bool EnqueueToWorker(const ScheduleAction& action) = 0;
   virtual bool EnqueueToWorkerBatch(const std::vector<ScheduleAction>& actions) = 0;
 };

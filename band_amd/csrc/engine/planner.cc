@@ -140,12 +140,19 @@ void Planner::EnqueueFinishedJob(Job& job) {
   }
   lock.unlock();  // callbacks may re-enter the engine
   // the request's input slot was consumed when the job started: free it
-  // before the callbacks, which may submit into this model's full ring
+  // before the callbacks, which may submit into this model's full ring; the
+  // output slot stays held until they return, so a request that reuses the
+  // slot cannot overwrite (or invalidate) the outputs a callback reads
+  const bool callbacks = job.require_callback && finished;
+  if (callbacks) engine_.HoldOutput(job);
   if (finished) engine_.ReleaseRequest(job);
-  if (job.require_callback && finished) {
-    std::lock_guard<std::mutex> cb_lock(on_end_request_mtx_);
-    const absl::Status s = job.status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
-    for (auto& cb : on_end_request_callbacks_) cb.second(job.job_id, s);
+  if (callbacks) {
+    {
+      std::lock_guard<std::mutex> cb_lock(on_end_request_mtx_);
+      const absl::Status s = job.status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
+      for (auto& cb : on_end_request_callbacks_) cb.second(job.job_id, s);
+    }
+    engine_.UnholdOutput(job);
   }
 }
 

@@ -95,33 +95,14 @@ absl::Status PutIntoSlot(Tensor* slot, const interface::ITensor* src) {
   StreamCopy(slot->GetData(), src->GetData(), slot->GetBytes());
   return absl::OkStatus();
 }
-
-std::mutex g_ring_alloc_mu;
-RingHostAllocator g_ring_alloc;
 }  // namespace
 
-void SetRingHostAllocator(RingHostAllocator a) {
-  std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
-  g_ring_alloc = a;
-}
-
-Tensor::Tensor(const interface::ITensor* view, bool copy_data, bool ring_memory)
+Tensor::Tensor(const interface::ITensor* view, bool copy_data)
     : type_(view->GetType()),
       dims_(view->GetDims(), view->GetDims() + view->GetNumDims()),
       name_(view->GetName() ? view->GetName() : "") {
   const size_t bytes = view->GetBytes();
-  if (ring_memory && bytes > 0) {
-    RingHostAllocator a;
-    {
-      std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
-      a = g_ring_alloc;
-    }
-    if (a.alloc && a.free && (ext_ = static_cast<char*>(a.alloc(bytes))) != nullptr) {
-      ext_bytes_ = bytes;
-      ext_free_ = a.free;
-    }
-  }
-  if (!ext_) data_.resize(bytes);
+  data_.resize(bytes);
   Quantization q = view->GetQuantization();
   if (q.GetType() == QuantizationType::kAffineQuantization && q.GetParams()) {
     qtype_ = QuantizationType::kAffineQuantization;
@@ -145,7 +126,6 @@ Tensor::Tensor(const interface::ITensor* view, char* external)
 
 Tensor::~Tensor() {
   FreeQuant();
-  if (ext_ && ext_free_) ext_free_(ext_);
 }
 
 void Tensor::FreeQuant() {
@@ -162,10 +142,8 @@ void Tensor::SetDims(const std::vector<int>& dims) {
   size_t n = GetDataTypeBytes(type_);
   for (int d : dims_) n *= static_cast<size_t>(d);
   if (ext_ && n != ext_bytes_) {  // a resized ring slot falls back to heap memory
-    if (ext_free_) ext_free_(ext_);
     ext_ = nullptr;
     ext_bytes_ = 0;
-    ext_free_ = nullptr;
   }
   if (!ext_) data_.resize(n);
 }
@@ -181,13 +159,13 @@ absl::Status Tensor::SetQuantization(Quantization q) {
 }
 
 TensorRingBuffer::TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors,
-                                   std::vector<int> tensor_indices, int size)
-    : size_(size > 0 ? size : 1), num_tensors_(tensors.size()), slots_(size_), busy_(size_, 0) {
-  RingHostAllocator a;
-  {
-    std::lock_guard<std::mutex> lk(g_ring_alloc_mu);
-    a = g_ring_alloc;
-  }
+                                   std::vector<int> tensor_indices, int size, RingHostAllocator a)
+    : size_(size > 0 ? size : 1),
+      num_tensors_(tensors.size()),
+      slots_(size_),
+      busy_(size_, 0),
+      owner_(size_, -1),
+      held_(size_, 0) {
   std::vector<size_t> stride(tensors.size(), 0);
   if (a.alloc && a.free) {
     block_free_ = a.free;
@@ -257,6 +235,30 @@ void TensorRingBuffer::Release(int handle) {
   slot_cv_.notify_all();  // waiters may need different slot counts
 }
 
+void TensorRingBuffer::AcquireForWrite(int handle) {
+  if (handle < 0) return;
+  std::unique_lock<std::mutex> lock(head_mtx_);
+  const int s = Slot(handle);
+  slot_cv_.wait(lock, [&] { return !held_[s] || owner_[s] == handle; });
+  owner_[s] = handle;
+}
+
+void TensorRingBuffer::Hold(int handle) {
+  if (handle < 0) return;
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  if (owner_[Slot(handle)] == handle) held_[Slot(handle)] = 1;
+}
+
+void TensorRingBuffer::Unhold(int handle) {
+  if (handle < 0) return;
+  {
+    std::lock_guard<std::mutex> lock(head_mtx_);
+    if (owner_[Slot(handle)] != handle || !held_[Slot(handle)]) return;
+    held_[Slot(handle)] = 0;
+  }
+  slot_cv_.notify_all();
+}
+
 int TensorRingBuffer::Outstanding() const {
   std::lock_guard<std::mutex> lock(head_mtx_);
   return outstanding_;
@@ -264,7 +266,7 @@ int TensorRingBuffer::Outstanding() const {
 
 bool TensorRingBuffer::IsHandleValid(int handle) const {
   std::lock_guard<std::mutex> lock(head_mtx_);
-  return handle >= 0 && head_ - size_ <= handle && handle < head_;
+  return handle >= 0 && ((head_ - size_ <= handle && handle < head_) || owner_[Slot(handle)] == handle);
 }
 
 Tensor* TensorRingBuffer::SlotTensor(int tensor_index, int handle) {
@@ -307,6 +309,14 @@ absl::Status TensorRingBuffer::PutTensorsToHandle(const std::vector<interface::I
   if (src.size() != num_tensors_) return absl::InternalError("Invalid tensor length");
   for (size_t i = 0; i < num_tensors_; ++i)
     if (!PutIntoSlot(slots_[Slot(handle)][i].get(), src[i]).ok())
+      return absl::InternalError("Failed to copy tensors.");
+  return absl::OkStatus();
+}
+
+absl::Status TensorRingBuffer::CheckTensors(const std::vector<interface::ITensor*>& src) const {
+  if (src.size() != num_tensors_) return absl::InternalError("Invalid tensor length");
+  for (size_t i = 0; i < num_tensors_; ++i)
+    if (!src[i] || *static_cast<const interface::ITensor*>(slots_[0][i].get()) != *src[i])
       return absl::InternalError("Failed to copy tensors.");
   return absl::OkStatus();
 }

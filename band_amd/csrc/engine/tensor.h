@@ -14,21 +14,20 @@
 
 namespace band {
 
-// Host memory for the request rings' slots.  A backend may install an
-// allocator of page-locked memory (the HIP backend does), so a batched pass
-// can DMA a request's input from its ring slot and its outputs into its
-// output slot with no staging copy; `alloc` may return nullptr, and then
-// plain heap memory is used.
+// Host memory for the request rings' slots.  The engine hands a ring the
+// backend's optional page-locked allocator (Engine::RingAllocatorFor: the
+// HIP backend's bhx_ring_host_alloc, when a GPU worker runs the whole model)
+// so a batched pass can DMA a request's input from its ring slot and its
+// outputs into its output slot with no staging copy; `alloc` may return
+// nullptr, and then plain heap memory is used.
 struct RingHostAllocator {
   void* (*alloc)(size_t bytes) = nullptr;
   void (*free)(void* p) = nullptr;
 };
-void SetRingHostAllocator(RingHostAllocator a);
 
 class Tensor : public interface::ITensor {
  public:
-  // ring_memory: the bytes come from the ring host allocator, if one is set
-  explicit Tensor(const interface::ITensor* view, bool copy_data = false, bool ring_memory = false);
+  explicit Tensor(const interface::ITensor* view, bool copy_data = false);
   // a slot of a request ring's page-locked block: `external` holds
   // view->GetBytes() bytes, owned by the ring
   Tensor(const interface::ITensor* view, char* external);
@@ -44,7 +43,7 @@ class Tensor : public interface::ITensor {
   size_t GetNumDims() const override { return dims_.size(); }
   void SetDims(const std::vector<int>& dims) override;
   size_t GetBytes() const override { return ext_ ? ext_bytes_ : data_.size(); }
-  // the bytes came from the ring host allocator (page-locked)
+  // the bytes came from a ring host allocator (page-locked)
   bool IsRingMemory() const { return ext_ != nullptr; }
   const char* GetName() const override { return name_.c_str(); }
   Quantization GetQuantization() const override;
@@ -55,9 +54,8 @@ class Tensor : public interface::ITensor {
   DataType type_;
   std::vector<int> dims_;
   std::vector<char> data_;
-  char* ext_ = nullptr;  // ring-allocator memory (data_ unused then)
+  char* ext_ = nullptr;  // a slot of a ring's page-locked block (data_ unused then)
   size_t ext_bytes_ = 0;
-  void (*ext_free_)(void*) = nullptr;
   std::string name_;
   QuantizationType qtype_ = QuantizationType::kNoQuantization;
   void* qparams_ = nullptr;  // TfLiteAffineQuantization layout, owned
@@ -80,7 +78,7 @@ class Tensor : public interface::ITensor {
 class TensorRingBuffer {
  public:
   TensorRingBuffer(const std::vector<std::shared_ptr<interface::ITensor>>& tensors, std::vector<int> tensor_indices,
-                   int size = 128);
+                   int size = 128, RingHostAllocator alloc = RingHostAllocator());
   ~TensorRingBuffer();
   int Alloc();
   // takes `handle` itself (the head moves past it): a model's output slot
@@ -95,6 +93,16 @@ class TensorRingBuffer {
   int AllocBlockingN(int n);
   // frees the slot of a handle taken with AllocBlocking[N]
   void Release(int handle);
+  // Output-ring ownership.  A slot's outputs belong to the request whose job
+  // wrote them last (AcquireForWrite, before the write); that handle stays
+  // readable (IsHandleValid) until a newer request writes the slot, even
+  // once newer submissions have moved the handle window past it.  Hold keeps
+  // the owner's outputs in place - a newer writer waits in AcquireForWrite -
+  // until Unhold (Planner::EnqueueFinishedJob brackets the end-request
+  // callbacks with them).
+  void AcquireForWrite(int handle);
+  void Hold(int handle);
+  void Unhold(int handle);
   int size() const { return size_; }
   int Outstanding() const;
   bool IsTensorIndexValid(int tensor_index) const { return tensor_to_buffer_.count(tensor_index) != 0; }
@@ -104,6 +112,9 @@ class TensorRingBuffer {
   absl::Status PutTensorToHandle(const interface::ITensor* src, int tensor_index, int handle);
   absl::Status GetTensorsFromHandle(std::vector<interface::ITensor*>& dst, int handle) const;
   absl::Status PutTensorsToHandle(const std::vector<interface::ITensor*>& src, int handle);
+  // whether PutTensorsToHandle would accept `src` (count, and each tensor's
+  // type and dims, as ITensor::CopyDataFrom checks)
+  absl::Status CheckTensors(const std::vector<interface::ITensor*>& src) const;
   // the slot tensor of `tensor_index` for a valid handle, else nullptr: a
   // batched pass reads a request's input from / writes its output into it
   // directly (a handle stays valid while its request is unfinished)
@@ -118,9 +129,11 @@ class TensorRingBuffer {
   mutable std::mutex head_mtx_;
   std::condition_variable slot_cv_;
   std::vector<char> busy_;  // per slot: taken by AllocBlocking[N], not yet released
+  std::vector<int> owner_;  // per slot: handle whose outputs it holds (-1: none)
+  std::vector<char> held_;  // per slot: the owner's outputs are being read
   // per tensor: one page-locked block holding every slot's bytes at a fixed
   // stride (consecutive handles are adjacent, so a batched pass copies a
-  // run of them in one DMA); empty when no ring host allocator is set
+  // run of them in one DMA); empty when the ring has no host allocator
   std::vector<char*> blocks_;
   void (*block_free_)(void*) = nullptr;
   int head_ = 0;

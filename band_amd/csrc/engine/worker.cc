@@ -10,7 +10,30 @@
 
 #include "engine/time.h"
 
+// Optional hook of the HIP backend (include/band_hip_backend.h): pins the
+// calling worker thread to its GPU's NUMA node.  Weak, so a harness linked
+// without that backend simply does not pin.
+extern "C" int bhx_pin_worker_thread(int worker_id) __attribute__((weak));
+
 namespace band {
+
+namespace {
+// the CPUs a worker's CpuSet names, read as Band reads a mask
+// (band/device/cpu.h:21-40); empty when it names none or all of them
+std::vector<int> NamedCpus(const CpuSet& set) {
+  std::vector<int> cpus;
+  const int n = static_cast<int>(std::min<size_t>(GetCPUCount(), CPU_SETSIZE));
+  for (int i = 0; i < n; ++i)
+    if (set.IsEnabled(i)) cpus.push_back(i);
+  cpu_set_t proc;
+  CPU_ZERO(&proc);
+  if (cpus.empty() || sched_getaffinity(0, sizeof(proc), &proc) != 0) return {};
+  bool all = true;
+  for (int c = 0; c < CPU_SETSIZE && all; ++c)
+    if (CPU_ISSET(c, &proc) && !set.IsEnabled(c)) all = false;
+  return all ? std::vector<int>() : cpus;
+}
+}  // namespace
 
 Worker::Worker(IEngine* engine, WorkerId worker_id, DeviceFlag device_flag)
     : engine_(engine), worker_id_(worker_id), device_flag_(device_flag) {}
@@ -34,18 +57,15 @@ void Worker::Start() {
     started_ = true;
     thread_ = std::thread([this] {
       // named for per-thread profiles (tools/planner_ceiling.py); a CpuSet
-      // that names CPUs pins the worker thread (band/worker.cc:195-205 does
-      // this on mobile builds, where BandCPUMaskGetSet fills the sets)
+      // that names a proper subset of the CPUs pins the worker thread
+      // (band/worker.cc:195-205 does this on mobile builds, where
+      // BandCPUMaskGetSet fills the sets)
       char name[16];
       std::snprintf(name, sizeof(name), "band-w%d", worker_id_);
       pthread_setname_np(pthread_self(), name);
-      const std::vector<int> cpus = cpu_set_.GetMaskBitsVector();
-      if (!cpus.empty()) {
-        cpu_set_t m;
-        CPU_ZERO(&m);
-        for (int c : cpus)
-          if (c < CPU_SETSIZE) CPU_SET(c, &m);
-        if (pthread_setaffinity_np(pthread_self(), sizeof(m), &m) != 0)
+      if (!NamedCpus(cpu_set_).empty()) {
+        cpu_pinned_ = true;
+        if (!SetCPUThreadAffinity(cpu_set_).ok())
           BAND_LOG(LogSeverity::kWarning, "worker %d: could not set its CPU affinity", worker_id_);
       }
       Work();
@@ -116,6 +136,12 @@ void Worker::Work() {
       }
       continue;
     }
+
+    // a GPU worker whose CpuSet names no CPUs goes to its GPU's NUMA node
+    // once that GPU is known (its first executor exists), before its first
+    // job's GPU call; only this engine-owned thread moves
+    if (!cpu_pinned_ && device_flag_ == DeviceFlag::kGPU && bhx_pin_worker_thread)
+      cpu_pinned_ = bhx_pin_worker_thread(worker_id_) >= 0;
 
     const SubgraphKey key = job->subgraph_key;
     const int max_batch = engine_->MaxJobBatch(key);

@@ -84,6 +84,9 @@ class Worker {
   bool is_paused_ = false;
   bool is_throttling_ = false;
   CpuSet cpu_set_;
+  // the thread's placement is settled: its CpuSet pinned it, or the GPU
+  // backend's NUMA hook ran (worker thread only)
+  bool cpu_pinned_ = false;
   int num_threads_ = -1;
   int availability_check_interval_ms_ = 30000;
   // expected latency of the batch partners of the running pass (device_mtx_):

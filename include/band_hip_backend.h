@@ -96,6 +96,19 @@ int bhx_pin_process_to_cpus(const int* cpus, int n_cpus);
  * after the last node counts pages whose node was unknown.  Returns the
  * number of entries that exist (up to cap written). */
 int bhx_ring_page_nodes(long long* bytes_per_node, int cap);
+/* Optional hooks for a Band-compatible engine, looked up as weak symbols
+ * (engine/engine.cc, engine/worker.cc); Band itself never needs them.
+ * bhx_ring_host_alloc: page-locked memory for a request ring's slots, so a
+ * GPU worker DMAs a job's I/O straight from / into its ring slot; NULL (use
+ * the heap) when no GPU is visible, BAND_HIP_PINNED_RINGS=0, or the total
+ * would pass BAND_HIP_PINNED_RING_MB (default 8192).
+ * bhx_pin_worker_thread: pins the calling engine-owned worker thread to the
+ * CPUs of the NUMA node of the GPU `worker_id` runs on (affinity.h); 1 pinned,
+ * 0 nothing to do (BANDX_NUMA_PIN=0, no NUMA information), -1 the worker has
+ * no GPU ordinal yet (no kGPU executor created for it). */
+void* bhx_ring_host_alloc(size_t bytes);
+void bhx_ring_host_free(void* p);
+int bhx_pin_worker_thread(int worker_id);
 /* InvestigateModelSpec -> ModelSpec serialised as JSON into buf.
  * *needed receives the full length (+1); the call fails if cap < needed. */
 int bhx_investigate_model_spec(bhx_executor* e, bhx_model* m, char* buf, size_t cap, size_t* needed);
@@ -155,7 +168,7 @@ int bhx_run_mixed_jobs(int n_models, bhx_executor* const* execs, const int* mode
  * back to back on the executor's stream (graph replay when captured) */
 int bhx_time_subgraph(bhx_executor* e, int model_id, int worker_id, uint64_t unit_mask, int iters, double* us);
 
-/* --- job batching (extension, band/interface/job_batching.h) -------------
+/* --- job batching (extension, backend/hip/job_batching.h) -------------
  * Not in the reference interface: Band runs one job per ExecuteSubgraph
  * (band/worker.cc:222-323).  A prepared kGPU subgraph gets batch variants
  * for up to max_batch jobs; slot views are batch-1 views into a variant's

@@ -354,7 +354,6 @@ static void TestRingSlotCopies() {
   RingHostAllocator a;
   a.alloc = [](size_t n) -> void* { return std::aligned_alloc(4096, (n + 4095) / 4096 * 4096); };
   a.free = [](void* p) { std::free(p); };
-  SetRingHostAllocator(a);
   const std::vector<std::vector<int>> shapes = {{1, 224, 224, 3}, {1, 70001}, {1, 100}};
   std::vector<std::vector<char>> backing;
   std::vector<std::shared_ptr<interface::ITensor>> views;
@@ -365,7 +364,7 @@ static void TestRingSlotCopies() {
     views.push_back(std::make_shared<ViewTensor>(d, backing.back().data()));
   }
   {
-    TensorRingBuffer ring(views, {0, 1, 2}, 3);
+    TensorRingBuffer ring(views, {0, 1, 2}, 3, a);
     for (int round = 0; round < 5; ++round) {
       const int h = ring.AllocBlocking();
       std::vector<std::unique_ptr<ViewTensor>> src, dst;
@@ -394,7 +393,6 @@ static void TestRingSlotCopies() {
       ring.Release(h);
     }
   }
-  SetRingHostAllocator(RingHostAllocator());
 }
 
 int main() {

@@ -431,3 +431,84 @@ def test_sel_shared_estimates_identical_workers(golden_dir):
             # equal estimates break round-robin: every worker near its share
             assert (counts >= 0.5 * counts.mean()).all(), counts
         e.close()
+
+
+def test_callback_reads_own_outputs_while_ring_is_full(tmp_path, monkeypatch):
+    """the input slot is freed before the end-request callbacks
+    run, so with a 4-slot ring a submitter waiting on it takes handle h + 4 at
+    once and another worker runs that job meanwhile.  The finished request's
+    output slot stays held until its callbacks return: a callback that reads
+    its own job's outputs (slowly) always gets them, bit-exact.  (Without
+    the hold, the idle worker overwrites the slot during the callback.)"""
+    import threading
+    import time
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    monkeypatch.setenv("BANDX_REQUEST_RING_SLOTS", "4")
+    path, buf = _slow_cpu_model(tmp_path)
+    # more workers than the ring's other requests: one is idle to run h + 4
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU] * 5, num_threads=[1] * 5))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    om = OModel(buf)
+    rng = np.random.default_rng(3)
+    xs = [rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8) for _ in range(6)]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]].reshape(-1) for x in xs]
+    o = e.CreateOutputTensor(m, 0)
+    got = {}
+    opt = RequestOptionGetDefault()
+    opt.require_callback = True
+
+    def on_end(job, status):
+        time.sleep(0.03)  # long enough for a newer job of the slot to run
+        rc = e.Wait(job, [o])
+        got[job] = (rc, o.data().reshape(-1).copy())
+
+    e.SetOnEndRequest(on_end)
+    handles = []
+    t = e.CreateInputTensor(m, 0)
+
+    def submit():
+        for j in range(48):
+            t.data()[...] = xs[j % 6]
+            handles.append(e.RequestAsync(m, [t], opt))
+
+    th = threading.Thread(target=submit)
+    th.start()
+    th.join(timeout=180)
+    assert not th.is_alive(), "submitter deadlocked"
+    e.WaitAll()
+    deadline = time.time() + 30
+    while len(got) < 48 and time.time() < deadline:
+        time.sleep(0.01)
+    assert len(got) == 48
+    for j, h in enumerate(handles):
+        rc, out = got[h]
+        assert rc == kBandOk, (j, h)
+        np.testing.assert_array_equal(out, refs[j % 6])
+    e.close()
+
+
+def test_batched_request_with_a_bad_input_enqueues_nothing(tmp_path):
+    """a RequestsAsync whose LATER input has the wrong shape is
+    refused before any run is enqueued (no job of the call starts)"""
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], num_threads=[1]))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    m2 = Model()
+    assert m2.FromPath(path)
+    assert e.RegisterModel(m2)
+    good = e.CreateInputTensor(m, 0)
+    bad = e.CreateOutputTensor(m2, 0)  # right model, wrong tensor shape
+    before = e.GetWorkerJobCount(0)
+    assert e.RequestsAsync([m, m, m2], [[good], [good], [bad]]) is None
+    e.WaitAll()
+    assert e.GetWorkerJobCount(0) == before
+    h = e.RequestAsync(m, [good])
+    assert h >= 0
+    e.WaitAll()
+    assert e.GetJobRecord(h).status == JobStatus.kSuccess
+    e.close()

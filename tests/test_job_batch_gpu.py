@@ -1,4 +1,4 @@
-"""Job batching on the MI355X (band/interface/job_batching.h extension):
+"""Job batching on the MI355X (backend/hip/job_batching.h extension):
 n queued whole-model jobs of one model run as one pass over a batch-B
 variant of the subgraph; every job's outputs stay bit-exact with the oracle.
 

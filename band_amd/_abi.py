@@ -189,6 +189,8 @@ KERNEL_SYMBOLS = {
     "bh_event_destroy": (c_int, [c_void_p]),
     "bh_event_record": (c_int, [c_void_p, c_void_p]),
     "bh_event_sync": (c_int, [c_void_p]),
+    "bh_event_query": (c_int, [c_void_p]),
+    "bh_event_create_untimed": (c_int, [ctypes.POINTER(c_void_p)]),
     "bh_event_elapsed_ms": (c_int, [c_void_p, c_void_p, ctypes.POINTER(ctypes.c_float)]),
     "bh_spin_us": (c_int, [c_void_p, c_int]),
     "bh_empty_launch": (c_int, [c_void_p]),

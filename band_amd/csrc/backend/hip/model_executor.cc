@@ -1,8 +1,12 @@
 #include "backend/hip/model_executor.h"
 
+#include <sys/prctl.h>
+#include <time.h>
+
 #include "backend/hip/affinity.h"
 
 #include <algorithm>
+#include <chrono>
 #include <limits>
 #include <cmath>
 #include <cstdio>
@@ -76,7 +80,11 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
     io_mode_ = m == "graph" ? 0 : m == "stream" ? 1 : 2;
   }
   if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
-  if (const char* sy = std::getenv("BAND_HIP_SYNC")) block_sync_ = std::string(sy) == "block";
+  if (const char* sy = std::getenv("BAND_HIP_SYNC")) {
+    const std::string m(sy);
+    sync_mode_ = m == "block" ? kSyncBlock : (m == "poll" ? kSyncPoll : kSyncSpin);
+  }
+  block_sync_ = sync_mode_ == kSyncBlock;
   if (const char* d = std::getenv("BAND_HIP_DIRECT_IO")) direct_io_ = d[0] != '0';
 }
 
@@ -1172,7 +1180,9 @@ void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
       // tile, and the unfused launches, timed on the real buffers; the
       // winner is cached per block geometry), else the static model.
       int tile = 0;
-      const std::string key = IrbKey(ordinal_, q);
+      bh_irb_params kq = q;
+      if (tune_batch_ > 0) kq.batch = tune_batch_;  // a job-batch variant reuses its anchor's choice
+      const std::string key = IrbKey(ordinal_, kq);
       bool cached = false;
       if (autotune_) {
         std::lock_guard<std::mutex> lk(g_tune_mu);
@@ -1315,7 +1325,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // = px_blocks of the 2-launch form (the second conv stays a launch),
     // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
-    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", kChainTuneVersion, ordinal_, D.dw.batch, D.dw.in_h,
+    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", kChainTuneVersion, ordinal_,
+                  tune_batch_ > 0 ? tune_batch_ : D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
                   ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
@@ -2149,9 +2160,19 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
   // host-pinned boundary mirrors (Band memcpy's job I/O through these)
   const bool pinned = device_flag_ == DeviceFlag::kGPU;
   const bool cpu = device_flag_ == DeviceFlag::kCPU;
-  for (int t : sg->inputs) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
+  // a job-batch variant views the largest variant's mirrors (slot s of a
+  // tensor sits at s * batch-1 bytes in every variant)
+  auto mirror = [&](int t) -> std::unique_ptr<PinnedBuffer> {
+    if (shared_host_from_) {
+      auto it = shared_host_from_->host.find(t);
+      if (it != shared_host_from_->host.end() && it->second->bytes() >= meta_[t]->bytes)
+        return std::make_unique<PinnedBuffer>(it->second->data(), meta_[t]->bytes);
+    }
+    return std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
+  };
+  for (int t : sg->inputs) sg->host[t] = mirror(t);
   for (int t : sg->outputs)
-    if (!sg->host.count(t)) sg->host[t] = std::make_unique<PinnedBuffer>(meta_[t]->bytes, pinned);
+    if (!sg->host.count(t)) sg->host[t] = mirror(t);
   for (auto& kv : sg->host)
     if (!kv.second->ok()) return absl::InternalError("pinned host allocation failed");
 
@@ -2179,7 +2200,10 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
       total += (meta_[t]->bytes + kAlign - 1) / kAlign * kAlign;
     }
     for (const auto& kv : alias) sg->offset[kv.first] = sg->offset.at(kv.second);
-    sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
+    if (shared_arena_ && shared_arena_->bytes() >= total && shared_arena_->ordinal() == ordinal_)
+      sg->arena = shared_arena_;  // job-batch variant: the largest variant's arena
+    else
+      sg->arena = std::make_shared<DeviceBlob>(ordinal_, total);
     if (!sg->arena->ok()) return absl::InternalError("arena allocation failed");
     if (cpu) {
       // a host executor's boundary tensors ARE its arena slots (every tensor
@@ -2529,15 +2553,44 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) RETURN_STATUS_IF(CaptureGraph(sg));
   RETURN_STATUS_IF(EnqueuePass(sg));
-  if (block_sync_) {
-    if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
-    rc = bh_event_record(done_event_, stream_);
-    if (!rc) rc = bh_event_sync(done_event_);
-  } else {
-    rc = bh_stream_sync(stream_);
-  }
-  if (rc) return HipErr(rc, "stream sync");
+  RETURN_STATUS_IF(WaitPass(sg));
   ++sg->runs;
+  return absl::OkStatus();
+}
+
+absl::Status HipModelExecutor::WaitPass(PreparedSubgraph* sg) {
+  int rc = 0;
+  if (sync_mode_ == kSyncSpin) {
+    rc = bh_stream_sync(stream_);
+    return rc ? HipErr(rc, "stream sync") : absl::OkStatus();
+  }
+  if (!done_event_ && (sync_mode_ == kSyncBlock ? bh_event_create_blocking(&done_event_)
+                                                : bh_event_create_untimed(&done_event_)) != 0)
+    return HipErr(1, "event create");
+  rc = bh_event_record(done_event_, stream_);
+  if (rc) return HipErr(rc, "event record");
+  if (sync_mode_ == kSyncBlock) {
+    rc = bh_event_sync(done_event_);
+    return rc ? HipErr(rc, "event sync") : absl::OkStatus();
+  }
+  // poll: sleep through ~3/4 of the expected time, then poll every kPollUs
+  // (timer slack cut to 1 us for this thread, so the sleeps are that short)
+  thread_local bool slack = [] { return prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0) == 0; }();
+  (void)slack;
+  constexpr int kPollUs = 8;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto sleep_us = [](double us) {
+    if (us < 1.0) return;
+    timespec ts{0, static_cast<long>(us * 1000.0)};
+    nanosleep(&ts, nullptr);
+  };
+  if (sg && sg->wait_us > 2 * kPollUs) sleep_us(0.75 * sg->wait_us - kPollUs);
+  while ((rc = bh_event_query(done_event_)) == BH_ENOTREADY) sleep_us(kPollUs);
+  if (rc) return HipErr(rc, "event query");
+  if (sg) {
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    sg->wait_us = sg->wait_us > 0 ? 0.9 * sg->wait_us + 0.1 * us : us;
+  }
   return absl::OkStatus();
 }
 
@@ -2549,15 +2602,24 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
   if (!hm || hm != model_) return absl::InternalError("job batching: not the model this executor prepared");
   job_batches_.erase(key);
   if (max_batch <= 1) return absl::OkStatus();
-  std::vector<int> sizes;
-  for (int b = 2; b < max_batch; b *= 2) sizes.push_back(b);
-  sizes.push_back(max_batch);
+  // anchors (2, 4, 8, .., max_batch) measure their fusion choices; every
+  // other size reuses the next anchor's.  Anchors are prepared first, the
+  // largest first of all: its arena and mirrors serve every variant.
+  int step = 1;
+  if (const char* e = std::getenv("BAND_HIP_BATCH_STEP")) step = std::max(1, std::atoi(e));
+  std::vector<int> anchors;
+  for (int b = 2; b < max_batch; b *= 2) anchors.push_back(b);
+  anchors.push_back(max_batch);
+  std::vector<int> order(anchors.rbegin(), anchors.rend());
+  for (int b = max_batch - 1; b >= 2; --b)
+    if ((b % step == 0) && std::find(anchors.begin(), anchors.end(), b) == anchors.end()) order.push_back(b);
   // a whole-model subgraph is prepared as one (model-order I/O), not as its op set
   std::set<int> ops;
   if (base->ops.size() != hm->desc().ops.size()) ops.insert(base->ops.begin(), base->ops.end());
   const std::set<int> units = key.GetUnitIndicesSet();
   std::vector<JobBatchVariant> variants;
-  for (int b : sizes) {
+  HipModelExecutor* largest = nullptr;
+  for (int b : order) {
     JobBatchVariant v;
     v.batch = b;
     RETURN_STATUS_IF(hm->CloneWithJobBatch(b, &v.model));
@@ -2568,14 +2630,27 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
     v.exec->io_mode_ = direct_io_ ? 1 : io_mode_;
     v.exec->direct_io_ = direct_io_;
     v.exec->block_sync_ = block_sync_;
+    v.exec->sync_mode_ = sync_mode_;
     v.exec->io_stream_bytes_ = io_stream_bytes_;
+    if (largest) {
+      PreparedSubgraph* ls = largest->Find(key);
+      v.exec->shared_arena_ = ls ? ls->arena : nullptr;
+      v.exec->shared_host_from_ = ls;
+    }
+    if (std::find(anchors.begin(), anchors.end(), b) == anchors.end())
+      v.exec->tune_batch_ = *std::lower_bound(anchors.begin(), anchors.end(), b);
     // the base subgraph's op set (a whole-model key prepares all ops)
     RETURN_STATUS_IF(v.exec->PrepareSubgraph(v.model.get(), ops, units));
     PreparedSubgraph* vs = v.exec->Find(key);
     if (!vs || vs->inputs != base->inputs || vs->outputs != base->outputs)
       return absl::InternalError("job batching: variant I/O differs from the subgraph's");
+    if (!largest) largest = v.exec.get();
     variants.push_back(std::move(v));
   }
+  // ascending batch (VariantFor takes the smallest >= n); the largest
+  // variant, whose arena / mirrors the others view, is destroyed last
+  std::sort(variants.begin(), variants.end(),
+            [](const JobBatchVariant& a, const JobBatchVariant& b) { return a.batch < b.batch; });
   job_batches_[key] = std::move(variants);
   return absl::OkStatus();
 }
@@ -2650,14 +2725,7 @@ absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int
     }
     rc = bh_graph_launch(base->graph, stream_);
     if (rc) return HipErr(rc, "graph launch");
-    if (block_sync_) {
-      if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
-      rc = bh_event_record(done_event_, stream_);
-      if (!rc) rc = bh_event_sync(done_event_);
-    } else {
-      rc = bh_stream_sync(stream_);
-    }
-    if (rc) return HipErr(rc, "stream sync");
+    RETURN_STATUS_IF(WaitPass(base));
     ++base->runs;
     return absl::OkStatus();
   }
@@ -2727,14 +2795,7 @@ absl::Status HipModelExecutor::RunDirect(PreparedSubgraph* sg, int n, const std:
       s0 = s1;
     }
   }
-  if (block_sync_) {
-    if (!done_event_ && bh_event_create_blocking(&done_event_) != 0) return HipErr(1, "event create");
-    rc = bh_event_record(done_event_, stream_);
-    if (!rc) rc = bh_event_sync(done_event_);
-  } else {
-    rc = bh_stream_sync(stream_);
-  }
-  if (rc) return HipErr(rc, "stream sync");
+  RETURN_STATUS_IF(WaitPass(sg));
   ++sg->runs;
   return absl::OkStatus();
 }

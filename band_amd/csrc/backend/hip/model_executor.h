@@ -116,6 +116,9 @@ struct PreparedSubgraph {
   std::vector<IoNode> io_nodes;
   bool io_retargeted = false;  // the nodes point at ring slots
   int runs = 0;
+  // poll-wait (BAND_HIP_SYNC=poll): running mean of a pass's device time as
+  // the waiting thread saw it (us), so it sleeps through most of the next one
+  double wait_us = 0.0;
 };
 
 class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
@@ -141,9 +144,14 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   void ForEachSubgraph(std::function<void(const SubgraphKey&)> visitor) override;
 
   // --- job batching (backend/hip/job_batching.h; kGPU executors) ---
-  // Variants for 2, 4, 8, ... and max_batch jobs: each is an executor of a
-  // batch-B copy of the model (HipModel::CloneWithJobBatch) over the same op
-  // set, on this executor's stream, sharing its device weights.
+  // A variant for every batch 2 .. max_batch (BAND_HIP_BATCH_STEP, default
+  // 1), so a pass of n jobs computes exactly n images: each is an executor
+  // of a batch-B copy of the model (HipModel::CloneWithJobBatch) over the
+  // same op set, on this executor's stream, sharing its device weights.  All
+  // variants of one subgraph share ONE activation arena and one set of
+  // page-locked boundary mirrors, sized for max_batch (a worker runs one
+  // pass at a time).  Measured fusion choices are taken at the anchor
+  // batches 2, 4, 8, 16, .., max_batch and reused by the sizes between.
   absl::Status PrepareJobBatches(interface::IModel* model, const SubgraphKey& key, int max_batch) override;
   int MaxJobBatch(const SubgraphKey& key) const override;
   std::shared_ptr<interface::ITensorView> GetJobSlotView(const SubgraphKey& key, int index, int n,
@@ -256,16 +264,31 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // stream | auto (default: stream from io_stream_bytes_ of host I/O per
   // pass, BAND_HIP_IO_STREAM_BYTES)
   int io_mode_ = 2;  // 0 graph, 1 stream, 2 auto
-  // BAND_HIP_SYNC=block: ExecuteSubgraph waits on a blocking-sync event
-  // (the worker thread sleeps until the GPU's interrupt) instead of spinning
-  // in hipStreamSynchronize - frees a core per GPU worker
-  bool block_sync_ = false;
+  // How a pass is waited for.  spin (default): hipStreamSynchronize, which
+  // busy-polls - a core per GPU worker for the whole pass, and the lowest
+  // completion latency.  block (BAND_HIP_SYNC=block): a blocking-sync event.
+  // poll (BAND_HIP_SYNC=poll): the thread sleeps through most of the pass's
+  // expected device time, then polls the pass's event every few us
+  // (WaitPass).  On the C3 mix poll frees ~7 cores but the late wake-ups
+  // cost 15-20 % of throughput, and block still spins inside HIP
+  // (profiles/r04e_*: spin 83 / 94 k, poll 76 / 78 k, block 79 / 80 k).
+  enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2 };
+  int sync_mode_ = kSyncSpin;
+  bool block_sync_ = false;  // sync_mode_ == kSyncBlock
+  // waits for everything enqueued on stream_ (the pass of `sg`)
+  absl::Status WaitPass(PreparedSubgraph* sg);
   // batched passes copy each job's I/O straight between the request rings'
   // page-locked slots and the device (ExecuteJobBatchDirect);
   // BAND_HIP_DIRECT_IO=0 stages them through the slot views instead
   bool direct_io_ = true;
   bh_event_t done_event_ = nullptr;
   size_t io_stream_bytes_ = 512 << 10;
+  // job-batch variants: the arena / boundary mirrors of the largest variant
+  // (PrepareSubgraph uses them when big enough), and the anchor batch whose
+  // measured fusion choices this variant reuses (0: its own batch)
+  std::shared_ptr<DeviceBlob> shared_arena_;
+  const PreparedSubgraph* shared_host_from_ = nullptr;
+  int tune_batch_ = 0;
   static const std::vector<int> kEmpty;
 };
 

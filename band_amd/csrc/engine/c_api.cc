@@ -671,6 +671,12 @@ int BandxEngineGetDriverStats(BandEngine* engine, double out[8]) {
   return 0;
 }
 
+int BandxEngineGetRequestPhaseTimes(BandEngine* engine, int64_t out[4]) {
+  if (!engine || !out) return -1;
+  engine->impl->GetRequestPhaseTimes(out);
+  return 0;
+}
+
 int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int worker_id, int64_t out[4]) {
   if (!engine || !out || worker_id < 0 || worker_id >= static_cast<int>(engine->impl->GetNumWorkers())) return -1;
   const band::Worker* w = engine->impl->GetWorker(worker_id);

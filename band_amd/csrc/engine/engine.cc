@@ -353,11 +353,16 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
   ids.reserve(jobs.size());
   for (size_t i = 0; i < jobs.size();) {
     size_t j = i;
+    int64_t t_copy_start = time::NowMicros();
     if (i < n_in) {
       while (j < n_in && model_ids[j] == model_ids[i]) ++j;
       TensorRingBuffer* in_ring = model_input_buffer_.at(model_ids[i]).get();
       // blocks while the model's ring has fewer than j - i free slots
+      const int64_t t_alloc = time::NowMicros();
       const int first = in_ring->AllocBlockingN(static_cast<int>(j - i));
+      const int64_t t_copy = time::NowMicros();
+      req_alloc_us_ += t_copy - t_alloc;
+      t_copy_start = t_copy;
       for (size_t k = i; k < j; ++k) {
         const int handle = first + static_cast<int>(k - i);
         if (!in_ring->PutTensorsToHandle(inputs[k], handle).ok()) {
@@ -370,11 +375,23 @@ absl::StatusOr<std::vector<JobId>> Engine::RequestAsync(std::vector<ModelId> mod
     } else {
       j = jobs.size();  // requests without inputs (no ring slot)
     }
+    const int64_t t_enq = time::NowMicros();
     std::vector<Job> run(std::make_move_iterator(jobs.begin() + i), std::make_move_iterator(jobs.begin() + j));
     for (JobId id : EnqueueBatch(std::move(run))) ids.push_back(id);
+    const int64_t t_end = time::NowMicros();
+    req_copy_us_ += t_enq - t_copy_start;
+    req_enqueue_us_ += t_end - t_enq;
+    req_jobs_ += static_cast<int64_t>(j - i);
     i = j;
   }
   return ids;
+}
+
+void Engine::GetRequestPhaseTimes(int64_t out[4]) const {
+  out[0] = req_jobs_.load();
+  out[1] = req_alloc_us_.load();
+  out[2] = req_copy_us_.load();
+  out[3] = req_enqueue_us_.load();
 }
 
 void Engine::ReleaseRequest(const Job& job) {

@@ -131,6 +131,9 @@ class Engine : public IEngine {
   void UnholdOutput(const Job& job) override;
   // request-ring slots per model: the most unfinished requests it can have
   int RequestRingSize(ModelId model_id) const;
+  // RequestAsync's cost split (extension): {jobs, us waiting for ring slots,
+  // us copying inputs into them, us enqueueing to the planner}
+  void GetRequestPhaseTimes(int64_t out[4]) const;
   bool EnqueueToWorker(const ScheduleAction& action) override { return planner_->EnqueueToWorker({action}); }
   bool EnqueueToWorkerBatch(const std::vector<ScheduleAction>& actions) override {
     return planner_->EnqueueToWorker(actions);
@@ -171,6 +174,7 @@ class Engine : public IEngine {
   std::map<ModelId, std::unique_ptr<TensorRingBuffer>> model_input_buffer_;
   std::map<ModelId, std::unique_ptr<TensorRingBuffer>> model_output_buffer_;
   mutable std::map<std::pair<ModelId, unsigned long long>, std::pair<SubgraphKey, int64_t>> cache_;
+  std::atomic<int64_t> req_jobs_{0}, req_alloc_us_{0}, req_copy_us_{0}, req_enqueue_us_{0};
 };
 
 }  // namespace band

@@ -218,11 +218,22 @@ extern "C" int bh_event_create_blocking(bh_event_t* ev) {
   *ev = (bh_event_t)e;
   return rc;
 }
+extern "C" int bh_event_create_untimed(bh_event_t* ev) {
+  hipEvent_t e = nullptr;
+  int rc = ck(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreateWithFlags");
+  *ev = (bh_event_t)e;
+  return rc;
+}
 extern "C" int bh_event_destroy(bh_event_t ev) { return ck(hipEventDestroy((hipEvent_t)ev), "hipEventDestroy"); }
 extern "C" int bh_event_record(bh_event_t ev, bh_stream_t s) {
   return ck(hipEventRecord((hipEvent_t)ev, (hipStream_t)s), "hipEventRecord");
 }
 extern "C" int bh_event_sync(bh_event_t ev) { return ck(hipEventSynchronize((hipEvent_t)ev), "hipEventSynchronize"); }
+extern "C" int bh_event_query(bh_event_t ev) {
+  const hipError_t e = hipEventQuery((hipEvent_t)ev);
+  if (e == hipErrorNotReady) return BH_ENOTREADY;
+  return ck(e, "hipEventQuery");
+}
 extern "C" int bh_event_elapsed_ms(bh_event_t a, bh_event_t b, float* ms) {
   return ck(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
 }

@@ -137,6 +137,7 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxEngineGetWorkerJobCount": (c_int64, [c_void_p, c_int]),
     "BandxEngineGetWorkerPhaseTimes": (c_int, [c_void_p, c_int, ctypes.POINTER(c_int64)]),
     "BandxEngineGetDriverStats": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_double)]),
+    "BandxEngineGetRequestPhaseTimes": (c_int, [c_void_p, ctypes.POINTER(ctypes.c_int64)]),
     "BandxEngineRequestsAsync": (c_int, [c_void_p, POINTER(c_void_p), c_int, POINTER(c_void_p), POINTER(c_int)]),
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
@@ -416,6 +417,13 @@ class Engine:
         return dict(wall_us=out[0], mean_in_engine=out[1], mean_awaiting_read=out[2], submit_wait_us=out[3],
                     submit_call_us=out[4], read_busy_us=out[5], read_idle_us=out[6], readers=readers,
                     submitters=lanes)
+
+    def GetRequestPhaseTimes(self):
+        """{jobs, alloc_us, copy_us, enqueue_us}: cumulative RequestAsync cost
+        split (include/band_c_api.h BandxEngineGetRequestPhaseTimes)"""
+        out = (ctypes.c_int64 * 4)()
+        self.lib.BandxEngineGetRequestPhaseTimes(self.handle, out)
+        return dict(jobs=out[0], alloc_us=out[1], copy_us=out[2], enqueue_us=out[3])
 
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))

@@ -88,6 +88,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
     p.add_argument("--no-graph", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--sample-threads", action="store_true",
+                   help="diagnostics: sample every thread's /proc state through the timed loop")
     p.add_argument("--no-roofline", action="store_true",
                    help="skip the per-launch roofline / device-time profile (e.g. under a rocprofv3 trace)")
     p.add_argument("--cpu-baseline-seconds", type=float, default=8.0, help="per CPU-baseline mode")
@@ -520,6 +522,80 @@ def thread_cpu():
 
 
 HOST_THREADS = {}
+HOST_THREAD_STATES = {}
+
+
+def cgroup_cpu_stat():
+    """cgroup v2 cpu.stat counters (usage / throttling), {} when absent"""
+    out = {}
+    try:
+        with open("/sys/fs/cgroup/cpu.stat") as f:
+            for line in f:
+                k, v = line.split()
+                out[k] = int(v)
+    except (OSError, ValueError):
+        pass
+    return out
+SAMPLE_THREADS = False
+
+
+class ThreadSampler:
+    """Diagnostics (--sample-threads): a Python thread reads every thread's
+    /proc/self/task/<tid>/syscall each ~0.5 ms while the native loop runs
+    (the GIL is released there): 'running' (user space), or the syscall it is
+    blocked in and the library its PC falls in.  Answers what an unnamed
+    runtime thread near 1.0 CPU is doing."""
+
+    def __init__(self):
+        import threading
+        self.counts = {}
+        self.stop_flag = False
+        self.maps = []
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split()
+                if len(parts) >= 6 and "x" in parts[1]:
+                    lo, hi = (int(x, 16) for x in parts[0].split("-"))
+                    self.maps.append((lo, hi, os.path.basename(parts[5])))
+        self.th = threading.Thread(target=self.run, daemon=True)
+        self.th.start()
+
+    def lib_of(self, pc):
+        for lo, hi, name in self.maps:
+            if lo <= pc < hi:
+                return name
+        return "?"
+
+    def run(self):
+        while not self.stop_flag:
+            for tid in os.listdir("/proc/self/task"):
+                try:
+                    with open("/proc/self/task/%s/comm" % tid) as f:
+                        name = f.read().strip()
+                    with open("/proc/self/task/%s/syscall" % tid) as f:
+                        sc = f.read().split()
+                except OSError:
+                    continue
+                if not sc:
+                    continue
+                if sc[0] == "running":
+                    state = "running"
+                else:
+                    state = "sys%s@%s" % (sc[0], self.lib_of(int(sc[-1], 16)) if len(sc) > 2 else "?")
+                key = "%s/%s" % (name, tid)
+                d = self.counts.setdefault(key, {})
+                d[state] = d.get(state, 0) + 1
+            time.sleep(0.0005)
+
+    def stop(self):
+        self.stop_flag = True
+        self.th.join()
+        out = {}
+        for k, d in self.counts.items():
+            n = sum(d.values())
+            if d.get("running", 0) / n > 0.05 or k.startswith("python"):
+                out[k] = {s: round(c / n, 3) for s, c in sorted(d.items(), key=lambda x: -x[1])[:4]}
+        return out
 
 
 def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
@@ -530,18 +606,34 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     D.barrier()
     n_workers = engine.GetNumWorkers()
     p0 = [engine.GetWorkerPhaseTimes(w) for w in range(n_workers)]
+    r0 = engine.GetRequestPhaseTimes()
     c0 = thread_cpu()
+    g0 = cgroup_cpu_stat()
+    sampler = ThreadSampler() if SAMPLE_THREADS else None
     t0 = time.perf_counter()
     lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
     t1 = time.perf_counter()
     c1 = thread_cpu()
+    g1 = cgroup_cpu_stat()
+    if sampler:
+        HOST_THREAD_STATES.clear()
+        HOST_THREAD_STATES.update(sampler.stop())
     p1 = [engine.GetWorkerPhaseTimes(w) for w in range(n_workers)]
     drv = engine.GetDriverStats()
+    r1 = engine.GetRequestPhaseTimes()
     D.barrier()
     busy = sorted((((c1[k] - c0.get(k, 0.0)) / (t1 - t0), k[1]) for k in c1), reverse=True)
     HOST_THREADS.clear()
     HOST_THREADS.update(busiest=[[n, round(b, 3)] for b, n in busy[:12]],
                         process_cpu_cores=round(sum(b for b, _ in busy), 2))
+    # the container's CPU quota: time its threads were throttled (CFS) and its
+    # whole CPU use over the loop (cores), when cgroup v2 reports them
+    if g0 and g1:
+        dt = t1 - t0
+        HOST_THREADS.update(cgroup=dict(
+            usage_cores=round((g1.get("usage_usec", 0) - g0.get("usage_usec", 0)) * 1e-6 / dt, 2),
+            throttled_share=round((g1.get("throttled_usec", 0) - g0.get("throttled_usec", 0)) * 1e-6 / dt, 3),
+            nr_throttled=g1.get("nr_throttled", 0) - g0.get("nr_throttled", 0)))
     # where the workers' wall time went over the timed loop (fractions of
     # workers x wall): input copies, invoke (launch + device sync), output
     # copies; the rest is waiting for work
@@ -573,6 +665,13 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
             read_busy=round(drv["read_busy_us"] / (w * drv["readers"]), 3),
             read_us_per_job=round(drv["read_busy_us"] / max(1, n_timed), 2),
             readers=drv["readers"], submitters=drv["submitters"]))
+        # inside RequestAsync: waiting for ring slots / copying the input into
+        # the slot / handing the job to the planner, us per job
+        nj = max(1, r1["jobs"] - r0["jobs"])
+        HOST_THREADS["request_driver"].update(request_async_us_per_job=dict(
+            ring_wait=round((r1["alloc_us"] - r0["alloc_us"]) / nj, 2),
+            input_copy=round((r1["copy_us"] - r0["copy_us"]) / nj, 2),
+            enqueue=round((r1["enqueue_us"] - r0["enqueue_us"]) / nj, 2)))
     return D.max(t1 - t0), lat_us, worker_ids
 
 
@@ -612,6 +711,8 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
 
 def main():
     args = parse()
+    global SAMPLE_THREADS
+    SAMPLE_THREADS = args.sample_threads
     # hardware queues are fixed at HIP runtime init: one per concurrently
     # running Band GPU worker stream (must be set before libband_hip loads)
     # (explicit assignment: the GPU box exports HIP's default of 4)
@@ -709,6 +810,8 @@ def main():
         else:
             elapsed, lat_us, worker_ids = run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D)
             host_threads = dict(HOST_THREADS)
+            if HOST_THREAD_STATES:
+                host_threads["thread_states"] = dict(HOST_THREAD_STATES)
         jobs_per_worker = np.bincount(worker_ids, minlength=n_cpu + W).tolist()
         # every subgraph execution per worker (warm-up included): a split
         # model's GPU share is invisible in the last-subgraph counts above

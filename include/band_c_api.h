@@ -230,6 +230,10 @@ BAND_CAPI_EXPORT int BandxEngineGetWorkerPhaseTimes(BandEngine* engine, int work
  * RequestAsync, out[5] / out[6] reader time reading / waiting (us, summed
  * over threads), out[7] readers + 1000 x submitters.  Returns 0. */
 BAND_CAPI_EXPORT int BandxEngineGetDriverStats(BandEngine* engine, double out[8]);
+/* Cumulative RequestAsync cost split since the engine was created:
+ * out = {jobs submitted, us waiting for request-ring slots, us copying
+ * inputs into them, us enqueueing to the planner}. */
+BAND_CAPI_EXPORT int BandxEngineGetRequestPhaseTimes(BandEngine* engine, int64_t out[4]);
 /* One RequestAsync call for n requests (band/engine.cc:455-529, the batched
  * overload Band's own benchmark tool uses): request i runs models[i] on the
  * input tensors inputs[i] (that model's inputs, in order).  handles[i]

@@ -103,9 +103,15 @@ int bh_event_create(bh_event_t* ev);
 /* an event whose bh_event_sync sleeps until the GPU signals it (no
  * timing); replaces bh_stream_sync's spin-wait */
 int bh_event_create_blocking(bh_event_t* ev);
+/* an event with no timing whose waits spin (for bh_event_query polling) */
+int bh_event_create_untimed(bh_event_t* ev);
 int bh_event_destroy(bh_event_t ev);
 int bh_event_record(bh_event_t ev, bh_stream_t s);
 int bh_event_sync(bh_event_t ev);
+/* 0 when the work before the event's record has finished, BH_ENOTREADY while
+ * it is still running, else an error (non-blocking: hipEventQuery) */
+#define BH_ENOTREADY (-2)
+int bh_event_query(bh_event_t ev);
 int bh_event_elapsed_ms(bh_event_t start, bh_event_t end, float* ms);
 /* hold the stream for `us` microseconds (<= 100 ms): lets a profiler enqueue
  * a launch sequence before the GPU starts it, so events time execution */

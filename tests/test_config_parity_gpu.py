@@ -1,7 +1,7 @@
 """Whole-model parity at the configurations the bench numbers come from.
 
 * C3: every mix model (MobileNetV2, SSD-MobileNetV2, DeepLabV3, PoseNet) at
-  224x224 int8, run through job batching's ExecuteJobBatch at n in {1, 7, 24}
+  224x224 int8, run through job batching's ExecuteJobBatch at n in {1, 7, 17, 24, 2, 13}
   - the passes bench.py's headline is made of - every slot's every output
   bit-exact vs the oracle (the TFLite 2.9.2 restatement), eager pass and
   graph replay both.
@@ -57,7 +57,7 @@ def test_c3_job_batches_224_bit_exact(gpu_lib, arch):
     key = SubgraphKey(31, 1)
     assert ex.PrepareJobBatches(m, key, N_SLOTS).ok()
     assert ex.MaxJobBatch(key) == N_SLOTS
-    for n in (1, 7, N_SLOTS):
+    for n in (1, 7, 17, N_SLOTS, 2, 13):  # every size has its own variant, all on one arena
         # slot s of the n-job pass carries input (s * 5 + n) % 24: every
         # slot a different input, and a different one in each pass
         pick = [(s * 5 + n) % N_SLOTS for s in range(n)]

@@ -403,8 +403,11 @@ def test_poisson_latency_counts_submission_delay(golden_dir):
     # ~all 200 arrivals are due within the first ~0.2 ms, so the last job's
     # latency is close to the whole run, not to one job's service time
     assert lat[-1] > 0.5 * wall * 1e6
-    # latency grows with the submission index (each job waits for all before it)
-    assert np.corrcoef(np.arange(len(lat)), lat)[0, 1] > 0.8
+    # latency grows with the submission index (each job waits for all before
+    # it); quartile medians, so a scheduling hiccup of a loaded host does not
+    # decide the test
+    q = len(lat) // 4
+    assert np.median(lat[-q:]) > 2.0 * np.median(lat[:q])
     e.close()
 
 

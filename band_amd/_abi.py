@@ -26,7 +26,12 @@ class ConvParams(ctypes.Structure):
         (n, c_int32) for n in ("add_y_off", "add_r_off", "add_o_off", "add_left_shift", "add_y_mult",
                                "add_y_shift", "add_r_mult", "add_r_shift", "add_o_mult", "add_o_shift",
                                "add_act_min", "add_act_max")] + [("out_table", c_void_p), ("requant_fast", c_int32),
-                                                                  ("kernel_hint", c_int32)]
+                                                                  ("kernel_hint", c_int32),
+                                                                  ("out_img_stride", ctypes.c_int64)]
+
+
+class ConvGroup(ctypes.Structure):
+    _fields_ = [("n", c_int), ("blocks", c_int), ("is1x1", c_int), ("table", c_void_p)]
 
 
 class DwConvParams(ctypes.Structure):
@@ -201,6 +206,10 @@ KERNEL_SYMBOLS = {
     "bh_pack_dw_taps": (c_int, [c_void_p, c_int, c_void_p, c_int32, c_int32, c_void_p]),
     "bh_conv_requant_fast_ok": (c_int, [c_void_p, c_void_p, c_int, c_int, ctypes.c_int64]),
     "bh_conv2d_i8": (c_int, [ctypes.POINTER(ConvParams), c_void_p]),
+    "bh_conv_group_ok": (c_int, [ctypes.POINTER(ConvParams)]),
+    "bh_conv_group_table_bytes": (ctypes.c_size_t, [c_int]),
+    "bh_conv_group_plan": (c_int, [ctypes.POINTER(ConvParams), c_int, c_void_p, ctypes.POINTER(ConvGroup)]),
+    "bh_conv_group_i8": (c_int, [ctypes.POINTER(ConvGroup), c_void_p]),
     "bh_conv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(ConvParams)]),
     "bh_dwconv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(DwConvParams)]),
     "bh_lut_u8": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),

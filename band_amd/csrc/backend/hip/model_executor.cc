@@ -541,6 +541,7 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "noirb") == 0) allow_irb_ = false;   // diagnostics: one fusion kind at a time
   if (f && std::strcmp(f, "noadd") == 0) allow_add_ = false;
   if (f && std::strcmp(f, "nochain") == 0) allow_chain_ = false;
+  if (f && std::strcmp(f, "nogroup") == 0) allow_group_ = false;
   if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
   if (f && std::strcmp(f, "forcetile") == 0) force_chain_ = force_tile_chain_ = true;  // ... in the tile form
   if (f && std::strcmp(f, "forcetilepipe") == 0) {  // ... in the persistent tile form
@@ -1000,6 +1001,222 @@ absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubg
   if (allow_fusion_ && allow_chain_ && device_flag_ == DeviceFlag::kGPU) FuseChains(model, sg);
   if (allow_fusion_ && allow_irb_ && device_flag_ == DeviceFlag::kGPU) FuseBlocks(model, sg);
   if (allow_fusion_) FuseGlue(model, sg);
+  if (allow_fusion_ && allow_group_ && device_flag_ == DeviceFlag::kGPU) RETURN_STATUS_IF(GroupConvs(sg));
+  return absl::OkStatus();
+}
+
+namespace {
+// Device pointers a launch reads and writes (tensor bases or slices inside
+// the arena; constants are filtered out by the caller).  false: a launch kind
+// not analysed here - grouping treats it as a barrier.
+bool LaunchIo(const Launch& l, std::vector<const void*>* rd, std::vector<const void*>* wr) {
+  switch (l.kind) {
+    case Launch::kConv:
+      *rd = {l.conv.input, l.conv.residual};
+      *wr = {l.conv.output};
+      return true;
+    case Launch::kDwConv:
+      *rd = {l.dw.input};
+      *wr = {l.dw.output};
+      return true;
+    case Launch::kChain:
+      *rd = {l.chain.dw.input, l.chain.pw1.residual};
+      *wr = {l.chain.pw1.output, l.chain.has_pw2 ? l.chain.pw2.output : nullptr};
+      return true;
+    case Launch::kIrb:
+      *rd = {l.irb.input};
+      *wr = {l.irb.output};
+      return true;
+    case Launch::kFc:
+      *rd = {l.fc.input};
+      *wr = {l.fc.output};
+      return true;
+    case Launch::kEltwise:
+      *rd = {l.elt.a, l.elt.b};
+      *wr = {l.elt.out};
+      return true;
+    case Launch::kPool:
+      *rd = {l.pool.input};
+      *wr = {l.pool.output};
+      return true;
+    case Launch::kLutU8:
+    case Launch::kCopy:
+      *rd = {l.src};
+      *wr = {l.dst};
+      return true;
+    case Launch::kConcat:
+      rd->assign(l.concat.input, l.concat.input + l.concat.n_inputs);
+      *wr = {l.concat.output};
+      return true;
+    case Launch::kConvGroup:
+      rd->clear();
+      wr->clear();
+      for (const bh_conv_params& m : l.members) {
+        rd->push_back(m.input);
+        rd->push_back(m.residual);
+        wr->push_back(m.output);
+      }
+      return true;
+    default:
+      return false;
+  }
+}
+}  // namespace
+
+// Detector and pose heads are many small convs that read feature maps
+// produced long before and write tensors read only at the end (SSD's 12
+// box / class predictors feed two CONCATENATIONs; PoseNet's four heads are
+// the outputs).  Each alone is a dispatch at the ~4 us empty-kernel floor.
+// Walking the launches in order, a conv that routes to the general MFMA
+// kernel joins a pending set instead of being emitted; a later launch that
+// reads or overwrites a pending conv's output, or writes a pending conv's
+// input, first flushes that conv (alone); a launch kind not analysed here
+// flushes everything.  What stays pending to the end of a run is emitted as
+// one conv_group launch at the position of the first launch that needs any
+// of it - every member then still runs after its producers and before its
+// consumers.  Members of a group never read each other's outputs.
+absl::Status HipModelExecutor::GroupConvs(PreparedSubgraph* sg) {
+  // accesses by arena slot (the tensor slot, aliases excluded, holding the
+  // pointer) and byte interval within it: [lo, hi) in every image at
+  // `stride` (0: one interval).  Only conv outputs are known exactly (heads
+  // writing per-image slices of one concatenated tensor must not conflict
+  // with each other); anything else covers its whole slot.
+  std::vector<std::pair<uintptr_t, uintptr_t>> slots;
+  {
+    const uintptr_t base = reinterpret_cast<uintptr_t>(sg->arena->ptr());
+    std::map<size_t, size_t> by_off;
+    for (const auto& kv : sg->offset) {
+      size_t& b = by_off[kv.second];
+      b = std::max(b, meta_[kv.first]->bytes);
+    }
+    for (const auto& kv : by_off) slots.emplace_back(base + kv.first, base + kv.first + kv.second);
+  }
+  struct Acc {
+    int slot;
+    long lo, hi, stride;
+  };
+  constexpr long kAll = std::numeric_limits<long>::max();
+  auto acc_of = [&](const void* p, long bytes, long stride) -> Acc {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    auto it = std::upper_bound(slots.begin(), slots.end(), std::make_pair(a, ~uintptr_t(0)));
+    if (!p || it == slots.begin()) return Acc{-1, 0, 0, 0};
+    --it;
+    if (a >= it->second) return Acc{-1, 0, 0, 0};
+    const long lo = static_cast<long>(a - it->first);
+    return Acc{static_cast<int>(it - slots.begin()), bytes > 0 ? lo : 0, bytes > 0 ? lo + bytes : kAll, stride};
+  };
+  auto accesses = [&](const std::vector<const void*>& ps) {
+    std::vector<Acc> out;
+    for (const void* p : ps) {
+      const Acc a = acc_of(p, 0, 0);
+      if (a.slot >= 0) out.push_back(a);
+    }
+    return out;
+  };
+  auto conv_write = [&](const bh_conv_params& c) {
+    const long hwn = static_cast<long>(c.out_h) * c.out_w * c.out_c;
+    return c.out_img_stride ? acc_of(c.output, hwn, c.out_img_stride) : acc_of(c.output, hwn * c.batch, 0);
+  };
+  auto overlap = [&](const Acc& a, const Acc& b) {
+    if (a.slot != b.slot) return false;
+    if (a.stride != b.stride) return true;  // (per-image vs whole-tensor: conservative)
+    return a.lo < b.hi && b.lo < a.hi;
+  };
+  auto intersects = [&](const std::vector<Acc>& x, const std::vector<Acc>& y) {
+    for (const Acc& a : x)
+      for (const Acc& b : y)
+        if (overlap(a, b)) return true;
+    return false;
+  };
+  struct Pending {
+    Launch l;
+    std::vector<Acc> rd, wr;
+  };
+  std::vector<Launch> out;
+  std::vector<Pending> pending;
+  // emits `set` (mutually independent convs) as one group per window type
+  auto emit = [&](std::vector<Pending>& set) -> absl::Status {
+    for (int one = 1; one >= 0; --one) {
+      std::vector<const Launch*> ms;
+      for (const Pending& p : set) {
+        const bh_conv_params& c = p.l.conv;
+        const int is1 = c.k_h == 1 && c.k_w == 1 && c.pad_h == 0 && c.pad_w == 0;
+        if (is1 == one) ms.push_back(&p.l);
+      }
+      if (ms.empty()) continue;
+      if (ms.size() == 1) {
+        out.push_back(*ms[0]);
+        continue;
+      }
+      Launch G;
+      G.kind = Launch::kConvGroup;
+      G.op_index = ms[0]->op_index;
+      G.out_tensor = ms[0]->out_tensor;
+      G.kernel = "conv_group_kernel";
+      for (const Launch* m : ms) {
+        G.members.push_back(m->conv);
+        G.alg_bytes += m->alg_bytes;
+        G.alg_ops += m->alg_ops;
+      }
+      std::vector<char> host(bh_conv_group_table_bytes(static_cast<int>(ms.size())));
+      if (host.empty() || bh_conv_group_plan(G.members.data(), static_cast<int>(ms.size()), host.data(),
+                                             &G.cgroup) != 0) {
+        for (const Launch* m : ms) out.push_back(*m);  // not groupable after all: keep them
+        continue;
+      }
+      auto blob = std::make_shared<DeviceBlob>(ordinal_, host.size());
+      if (!blob->ok() || !blob->Upload(0, host.data(), host.size())) return HipErr(1, "upload conv group table");
+      sg->consts.push_back(blob);
+      G.cgroup.table = blob->ptr();
+      out.push_back(std::move(G));
+    }
+    set.clear();
+    return absl::OkStatus();
+  };
+  const size_t max_members = 32;
+  for (Launch& l : sg->launches) {
+    std::vector<const void*> rdp, wrp;
+    if (!LaunchIo(l, &rdp, &wrp)) {
+      RETURN_STATUS_IF(emit(pending));
+      out.push_back(std::move(l));
+      continue;
+    }
+    const std::vector<Acc> rd = accesses(rdp);
+    std::vector<Acc> wr = accesses(wrp);
+    if (l.kind == Launch::kConv) {
+      const Acc w = conv_write(l.conv);
+      wr.clear();
+      if (w.slot >= 0) wr.push_back(w);
+    }
+    const bool groupable = l.kind == Launch::kConv && bh_conv_group_ok(&l.conv) && !rd.empty() && !wr.empty();
+    // pending convs this launch depends on (reads or overwrites their
+    // output) or that depend on it (it overwrites their input)
+    std::vector<Pending> hit, keep;
+    for (Pending& p : pending)
+      (intersects(rd, p.wr) || intersects(wr, p.wr) || intersects(wr, p.rd) ? hit : keep).push_back(std::move(p));
+    pending = std::move(keep);
+    if (!hit.empty()) {
+      if (groupable) {
+        // a conv consuming pending ones (a detector's next extra layer):
+        // only those go now, the rest keep waiting for more members
+        RETURN_STATUS_IF(emit(hit));
+      } else {
+        // a consumer of the group (CONCATENATION, ...): everything pending
+        // runs here, as one launch
+        for (Pending& p : hit) pending.push_back(std::move(p));
+        RETURN_STATUS_IF(emit(pending));
+      }
+    }
+    if (groupable && pending.size() < max_members) {
+      pending.push_back(Pending{std::move(l), rd, wr});
+      continue;
+    }
+    // a launch that stays put: pending convs it does not touch are deferred
+    // past it
+    out.push_back(std::move(l));
+  }
+  RETURN_STATUS_IF(emit(pending));
+  sg->launches = std::move(out);
   return absl::OkStatus();
 }
 
@@ -1503,43 +1720,72 @@ void HipModelExecutor::FuseGlue(const HipModel& model, PreparedSubgraph* sg) {
     return -1;
   };
   std::vector<bool> dead(sg->launches.size(), false);
-  // (1) byte tables into the producer's epilogue
+  // (1) byte tables into the producer's epilogue; a CONCATENATION without
+  // rescale tables takes the table as every input's copy table (and may
+  // hand it on to its producers in (2))
   for (size_t i = 0; i < sg->launches.size(); ++i) {
     Launch& L = sg->launches[i];
     if (L.kind != Launch::kLutU8) continue;
     const int j = producer_of(i, L.src);
     if (j < 0 || dead[j]) continue;
     Launch& P = sg->launches[j];
-    const void** ts = TableSlot(P);
     std::vector<int> chain;
-    if (!ts || *ts || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
-    *ts = L.table;
-    *OutSlot(P) = L.dst;
+    if (P.kind == Launch::kConcat) {
+      bool plain = P.concat.output == L.src;
+      for (int k = 0; k < P.concat.n_inputs && plain; ++k) plain = P.concat.table[k] == nullptr;
+      if (!plain || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
+      for (int k = 0; k < P.concat.n_inputs; ++k) P.concat.table[k] = L.table;
+      P.concat.output = L.dst;
+    } else {
+      const void** ts = TableSlot(P);
+      if (!ts || *ts || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
+      *ts = L.table;
+      *OutSlot(P) = L.dst;
+    }
     P.out_tensor = L.out_tensor;
     P.alg_bytes += 0;  // same bytes: the table gather happens on the stored value
     for (int t : chain) sg->fused_tensors.insert(t);
     sg->fused_ops.insert(L.op_index);
     dead[i] = true;
   }
-  // (2) CONCATENATION whose inputs are contiguous slices of the output
+  // (2) CONCATENATION whose inputs are slices of the output: contiguous
+  // ones (outer size 1) from any producer; per-image slices (outer = batch
+  // > 1, a detector's per-anchor concat) from convs, which store each image
+  // at the concat's row stride (bh_conv_params.out_img_stride); an input
+  // copy table moves into the producer's epilogue table
   for (size_t i = 0; i < sg->launches.size(); ++i) {
     Launch& C = sg->launches[i];
-    if (C.kind != Launch::kConcat || C.concat.outer != 1) continue;
+    if (C.kind != Launch::kConcat) continue;
+    const bool strided = C.concat.outer != 1;
+    if (strided && device_flag_ != DeviceFlag::kGPU) continue;  // (the host conv stores dense images)
+    long total_row = 0;
+    for (int k = 0; k < C.concat.n_inputs; ++k) total_row += C.concat.row[k];
     bool ok = true;
     std::vector<int> prod(C.concat.n_inputs, -1);
     std::vector<int> chain;
     for (int k = 0; k < C.concat.n_inputs && ok; ++k) {
-      if (C.concat.table[k]) ok = false;
-      const int j = ok ? producer_of(i, C.concat.input[k]) : -1;
-      ok = ok && j >= 0 && !dead[j] && OutSlot(sg->launches[j]) &&
+      const int j = producer_of(i, C.concat.input[k]);
+      ok = j >= 0 && !dead[j] && OutSlot(sg->launches[j]) &&
            private_chain(sg->launches[j].out_tensor, C.op_index, &chain);
+      if (ok && C.concat.table[k]) {
+        const void** ts = TableSlot(sg->launches[j]);
+        ok = ts && *ts == nullptr;
+      }
+      if (ok && strided) {
+        const Launch& P = sg->launches[j];
+        ok = P.kind == Launch::kConv && P.conv.out_img_stride == 0 && P.conv.batch == C.concat.outer &&
+             static_cast<long>(P.conv.out_h) * P.conv.out_w * P.conv.out_c == C.concat.row[k];
+      }
       if (ok) prod[k] = j;
       for (int kk = 0; kk < k && ok; ++kk) ok = prod[kk] != j;  // one producer per slice
     }
     if (!ok) continue;
     long off = 0;
     for (int k = 0; k < C.concat.n_inputs; ++k) {
-      *OutSlot(sg->launches[prod[k]]) = static_cast<char*>(C.concat.output) + off;
+      Launch& P = sg->launches[prod[k]];
+      *OutSlot(P) = static_cast<char*>(C.concat.output) + off;
+      if (C.concat.table[k]) *TableSlot(P) = C.concat.table[k];
+      if (strided) P.conv.out_img_stride = total_row;
       off += C.concat.row[k];
     }
     for (int t : chain) sg->fused_tensors.insert(t);
@@ -2307,6 +2553,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
     case Launch::kChain: rc = bh_chain_i8(&l.chain, stream_); break;
+    case Launch::kConvGroup: rc = bh_conv_group_i8(&l.cgroup, stream_); break;
     case Launch::kCopy: {
       // a kernel copy, not a blit: graphs replayed under rocprofv3's kernel
       // trace crash on blit (memcpy) nodes; BAND_HIP_BLIT_COPY=1 restores them

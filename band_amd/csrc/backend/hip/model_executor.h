@@ -42,7 +42,8 @@ struct Launch {
     kConvF32, kFcF32, kEltwiseF32, kPoolF32, kUnaryF32, kSoftmaxF32,  // float32 graphs
     kResizeBilinearU8,
     kDetectionPost,  // CPU-only TFLite_Detection_PostProcess
-    kMean            // CPU-only MEAN
+    kMean,           // CPU-only MEAN
+    kConvGroup       // independent small convs in one dispatch (GroupConvs)
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
@@ -53,6 +54,9 @@ struct Launch {
   bh_pool_params pool{};
   bh_irb_params irb{};
   bh_chain_params chain{};
+  // kConvGroup: the member convs (program order) and the planned group
+  std::vector<bh_conv_params> members;
+  bh_conv_group cgroup{};
   bh_concat_params concat{};
   bh_pad_params pad{};
   bh_resize_nearest_params rnear{};
@@ -192,6 +196,9 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
   // CONCATENATION with outer size 1 elided (producers write their slices)
   void FuseGlue(const HipModel& model, PreparedSubgraph* sg);
+  // independent small convs (detector / pose heads) deferred past later
+  // launches that do not touch them and issued as one conv_group launch
+  absl::Status GroupConvs(PreparedSubgraph* sg);
   // Mean device time (us) of one pass over `ls`, or < 0 when it cannot be
   // measured (no GPU stream, or a launch failed).
   double TimeLaunches(const std::vector<const Launch*>& ls, int iters);
@@ -245,6 +252,7 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   bool allow_irb_ = true;  // BAND_HIP_FUSION=noirb / noadd: diagnostics
   bool allow_add_ = true;
   bool allow_chain_ = true;   // BAND_HIP_FUSION=nochain
+  bool allow_group_ = true;   // BAND_HIP_FUSION=nogroup: one launch per conv
   bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
   bool force_tile_chain_ = false;  // BAND_HIP_FUSION=forcetile: every feasible chain in the tile form
   bool tile_pipe_ = false;         // BAND_HIP_FUSION=forcetilepipe: ... in the persistent tile form

@@ -139,8 +139,9 @@ struct Chan4 {
 
 __device__ __forceinline__ Chan4 chan4(const bh_conv_params& p, int nb, int N) {
   Chan4 c;
-  // (a concat-elided output may start at any byte)
-  c.vec = (N & 3) == 0 && (((uintptr_t)p.output | (uintptr_t)p.residual) & 3) == 0;
+  // (a concat-elided output may start at any byte, and its images at any
+  // stride)
+  c.vec = (N & 3) == 0 && (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.out_img_stride) & 3) == 0;
   int32_t mu[4], sh[4];
   if (c.vec) {
     const v4i b4 = *(const v4i*)(p.bias_eff + nb);
@@ -204,7 +205,13 @@ __device__ __forceinline__ void conv_store4(const bh_conv_params& p, v4i acc, in
     const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
     packed |= byte << (8 * r);
   }
-  uint8_t* out = (uint8_t*)p.output + o;
+  long oo = o;
+  if (p.out_img_stride) {  // a slice of a concatenation: image n at n * stride (uniform branch)
+    const int hw = p.out_h * p.out_w;
+    const int img = m / hw;
+    oo = (long)img * p.out_img_stride + (long)(m - img * hw) * N + nb;
+  }
+  uint8_t* out = (uint8_t*)p.output + oo;
   if (c.vec) {
     *(uint32_t*)out = packed;
   } else {
@@ -223,9 +230,11 @@ __device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc,
 constexpr int KU = 4;  // K-steps whose loads are issued together
 
 // WM x WN 16x16 tiles per wave; waves arranged WAVES_M x WAVES_N x SPLITK.
+// One workgroup's tile: `logical` is its block index in the layer's
+// gm x nblocks grid (conv_mfma_kernel, or a member of a grouped launch).
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
-__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv,
-                                                        int nblocks, int xcd) {
+__device__ __forceinline__ void conv_mfma_tile(const bh_conv_params& p, int M, int K, int N, int kchunk,
+                                               const ConvDivs& dv, int nblocks, int xcd, int logical, int total) {
   static_assert(WAVES_M * WAVES_N * SPLITK == 4, "4 waves per workgroup");
   constexpr int TM = WAVES_M * WM * 16;
   constexpr int TN = WAVES_N * WN * 16;
@@ -236,16 +245,9 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
   const int wt = wave % (WAVES_M * WAVES_N);
   const int wave_m = wt % WAVES_M;
   const int wave_n = wt / WAVES_M;
-  // 1-D grid; with xcd each XCD (hardware ids i % 8) runs a contiguous run
-  // of logical blocks.  xcd 1: N-blocks fastest, so all N-blocks of a pixel
-  // block - which read the same input rows - share one L2 (the filters are
-  // read once per XCD).  xcd 2 (filters larger than the input): pixel blocks
-  // fastest, so each XCD reads only its slice of the filters and the small
-  // input is the operand read once per XCD.
-  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
   int bm, bn;
   if (xcd == 2) {
-    const int gm = gridDim.x / nblocks;
+    const int gm = total / nblocks;
     bn = logical / gm;
     bm = logical - bn * gm;
   } else {
@@ -365,6 +367,51 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M,
 #pragma unroll
       for (int j = 0; j < WN; ++j) conv_epilogue4(p, acc[i][j], rs[i], m0 + i * 16 + r16, n0 + j * 16 + 4 * g, M, N);
   }
+}
+
+template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
+__global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv,
+                                                        int nblocks, int xcd) {
+  // 1-D grid; with xcd each XCD (hardware ids i % 8) runs a contiguous run
+  // of logical blocks.  xcd 1: N-blocks fastest, so all N-blocks of a pixel
+  // block - which read the same input rows - share one L2 (the filters are
+  // read once per XCD).  xcd 2 (filters larger than the input): pixel blocks
+  // fastest, so each XCD reads only its slice of the filters and the small
+  // input is the operand read once per XCD.
+  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  conv_mfma_tile<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>(p, M, K, N, kchunk, dv, nblocks, xcd, logical,
+                                                               (int)gridDim.x);
+}
+
+// ---------------------------------------------------------------------------
+// Grouped launch of independent small CONV_2D layers (conv_group_kernel):
+// the heads of a detector / pose model (SSD's 12 box / class predictors,
+// PoseNet's four 1x1 heads) are each a few hundred workgroups of work that
+// would otherwise pay a whole dispatch (~4 us of fixed cost at the empty-
+// kernel floor) one after another.  One launch carries
+// all of them: workgroup b belongs to the member whose [blk0, blk0 + blocks)
+// range holds b, and runs that member's conv_mfma_kernel tile - the same
+// arithmetic, so the results are the members' own, bit for bit.  The member
+// table (host-built, bh_conv_group_plan) lives in device memory.
+// ---------------------------------------------------------------------------
+struct ConvGroupMember {
+  bh_conv_params p;
+  ConvDivs dv;
+  int M, K, N, kchunk, gn, form, blk0, blocks;
+};
+constexpr int kConvGroupMax = 32;
+
+template <bool IS1X1>
+__global__ __launch_bounds__(256) void conv_group_kernel(const ConvGroupMember* __restrict__ tab, int n) {
+  const int b = (int)blockIdx.x;
+  int i = 0;
+  while (i + 1 < n && tab[i + 1].blk0 <= b) ++i;  // uniform: scalar loads of the table
+  const ConvGroupMember& e = tab[i];
+  const int local = b - e.blk0;
+  if (e.form == 0)
+    conv_mfma_tile<1, 1, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks);
+  else
+    conv_mfma_tile<1, 1, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks);
 }
 
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
@@ -659,6 +706,7 @@ enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm };
 
 Route route(const bh_conv_params& p, long M, int K, int N) {
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
+  if (p.out_img_stride) return kMfma;  // only conv_mfma_kernel's epilogue stores strided images
   // RGB-stem-like layers (tiny K, byte-granular gather): direct VALU kernel
   if (!is1x1 && K <= 64 && p.in_c < 8) {
     const bool stem = p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && N % 8 == 0 && !p.residual;
@@ -712,6 +760,76 @@ extern "C" int bh_pack_conv_weights(const void* w, int w_signed, int out_c, int 
     bias_eff[c] = (int32_t)be;
   }
   return 0;
+}
+
+extern "C" int bh_conv_group_ok(const bh_conv_params* pp) {
+  if (!pp) return 0;
+  const bh_conv_params& p = *pp;
+  const long M = (long)p.batch * p.out_h * p.out_w;
+  const int K = p.k_h * p.k_w * p.in_c;
+  const int N = p.out_c;
+  if (M <= 0 || M > INT32_MAX || K <= 0 || N <= 0 || p.k_pad < K || p.n_pad < N || (p.k_pad % 64) ||
+      (p.n_pad % 64) || !p.input || !p.output || !p.weights || !p.bias_eff || !p.mult || !p.shift ||
+      p.stride_h <= 0 || p.stride_w <= 0 || p.in_c % 16)
+    return 0;
+  return route(p, M, K, N) == kMfma ? 1 : 0;
+}
+
+extern "C" size_t bh_conv_group_table_bytes(int n) {
+  return n > 0 && n <= bh::kConvGroupMax ? (size_t)n * sizeof(bh::ConvGroupMember) : 0;
+}
+
+extern "C" int bh_conv_group_plan(const bh_conv_params* members, int n, void* host_table, bh_conv_group* g) {
+  if (!members || !host_table || !g || n < 1 || n > bh::kConvGroupMax) return BH_EINVAL;
+  auto* tab = static_cast<bh::ConvGroupMember*>(host_table);
+  int is1x1 = -1;
+  long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    const bh_conv_params& p = members[i];
+    if (!bh_conv_group_ok(&p)) return BH_EINVAL;
+    const int one = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
+    if (is1x1 >= 0 && one != is1x1) return BH_EINVAL;  // one instantiation per group
+    is1x1 = one;
+    bh::ConvGroupMember e{};
+    e.p = p;
+    e.M = p.batch * p.out_h * p.out_w;
+    e.K = p.k_h * p.k_w * p.in_c;
+    e.N = p.out_c;
+    e.dv.out_w = bh::FastDiv(p.out_w);
+    e.dv.out_h = bh::FastDiv(p.out_h);
+    e.dv.in_c = bh::FastDiv(p.in_c);
+    e.dv.k_w = bh::FastDiv(p.k_w);
+    const int ksteps = (e.K + 63) / 64;
+    // deep K: 16 x 16 tiles with K split over the 4 waves; else 32 x 32
+    // tiles over 2 x 2 waves (conv_mfma_kernel's small-grid forms)
+    e.form = ksteps >= 3 ? 0 : 1;
+    const int tm = e.form == 0 ? 16 : 32, tn = tm;
+    e.kchunk = e.form == 0 ? (ksteps + 3) / 4 * 64 : ksteps * 64;
+    e.gn = (e.N + tn - 1) / tn;
+    e.blocks = ((e.M + tm - 1) / tm) * e.gn;
+    e.blk0 = (int)blocks;
+    blocks += e.blocks;
+    tab[i] = e;
+  }
+  if (blocks <= 0 || blocks > INT32_MAX / 2) return BH_EINVAL;
+  g->n = n;
+  g->blocks = (int)blocks;
+  g->is1x1 = is1x1;
+  return 0;
+}
+
+extern "C" int bh_conv_group_i8(const bh_conv_group* g, bh_stream_t stream) {
+  if (!g || !g->table || g->n < 1 || g->n > bh::kConvGroupMax || g->blocks < 1) {
+    bh_set_last_error("bh_conv_group_i8: invalid group");
+    return BH_EINVAL;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const auto* tab = static_cast<const bh::ConvGroupMember*>(g->table);
+  if (g->is1x1)
+    BH_LAUNCH((bh::conv_group_kernel<true>), dim3(g->blocks), dim3(256), 0, s, tab, g->n);
+  else
+    BH_LAUNCH((bh::conv_group_kernel<false>), dim3(g->blocks), dim3(256), 0, s, tab, g->n);
+  return bh_check_launch("conv_group_kernel");
 }
 
 extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {

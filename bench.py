@@ -347,13 +347,13 @@ def profiled_batch(args):
     return args.job_batch if args.job_batch > 1 and args.model not in ("efficientdet_lite2_int8", "mix_c5") else 1
 
 
-def profile_executors(args, D, models, paths):
+def profile_executors(args, D, models, paths, batch=None):
     """profiling executors (outside the engine, same backend code) over the
     passes the workers run: with job batching, the same models with a
-    leading batch of B"""
+    leading batch of B (`batch` overrides it)"""
     import band_amd
     from band_amd import DeviceFlag, HipModel, HipModelExecutor, SubgraphKey
-    B = profiled_batch(args)
+    B = batch or profiled_batch(args)
     tmp = []
     if B > 1:
         paths = tmp = write_models(model_list(args.model, args.size, batch=B), "band_prof")
@@ -849,6 +849,19 @@ def main():
     roof, dev = None, None
     if on_gpu and D.rank == 0 and not args.no_roofline:
         roof, dev, _ = profile_roofline(args, D, models, paths)
+        # the same kernel-time figure at the pass size the timed loop really
+        # ran (mean jobs per worker pass), not only at full B-job passes
+        wp = (host_threads or {}).get("worker_phases", {})
+        if wp.get("passes") and profiled_batch(args) > 1:
+            b_mean = max(1, int(round(n_timed / wp["passes"])))
+            if b_mean != profiled_batch(args):
+                execs_m, _ = profile_executors(args, D, models, paths, batch=b_mean)
+                us = 0.0
+                for ex, key in execs_m:
+                    us += sum(r["ms"] * 1e3 for r in ex.ProfileSubgraph(key, iters=args.profile_iters))
+                dev["gpu_us_per_inference_at_mean_pass"] = dict(pass_batch=b_mean, us=us / len(models) / b_mean)
+            else:
+                dev["gpu_us_per_inference_at_mean_pass"] = dict(pass_batch=b_mean, us=dev["gpu_us_per_inference"])
 
     cpu = None
     if D.rank == 0 and D.world == 1 and not args.no_cpu_baseline:
@@ -896,6 +909,7 @@ def main():
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
             single["p99_job_latency_ms"],
             "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
+            "gpu_kernel_us_per_inference_at_mean_pass": dev.get("gpu_us_per_inference_at_mean_pass") if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
             "device_us_per_model": dev["device_us"] if dev else None,
             "band_one_job_per_pass": batch1,

@@ -172,7 +172,29 @@ typedef struct bh_conv_params {
   /* kernel choice: BH_CONV_AUTO (by shape), or force one form where the
    * layer allows it (parity tests cover every form; A-B timing) */
   int32_t kernel_hint;
+  /* 0: dense NHWC output.  Else output image n starts at output +
+   * n * out_img_stride bytes (its out_h*out_w*out_c bytes contiguous): the
+   * conv writes its slice of a CONCATENATION along a non-batch axis directly
+   * (the concat launch is elided).  Such a layer runs conv_mfma_kernel. */
+  int64_t out_img_stride;
 } bh_conv_params;
+
+/* Grouped launch of independent CONV_2D layers that each route to the
+ * general MFMA kernel (bh_conv_group_ok): one dispatch runs every member's
+ * workgroups (conv_group_kernel), each member computing exactly what its own
+ * bh_conv2d_i8 launch would.  The members must not read each other's
+ * outputs, and share one window type (all 1x1 unpadded, or none).
+ * bh_conv_group_plan fills `host_table` (bh_conv_group_table_bytes(n)
+ * bytes, n <= 32) and *g; the caller copies the table to device memory and
+ * sets g->table before bh_conv_group_i8. */
+typedef struct bh_conv_group {
+  int n, blocks, is1x1;
+  const void* table; /* device copy of the member table */
+} bh_conv_group;
+int bh_conv_group_ok(const bh_conv_params* p);
+size_t bh_conv_group_table_bytes(int n);
+int bh_conv_group_plan(const bh_conv_params* members, int n, void* host_table, bh_conv_group* g);
+int bh_conv_group_i8(const bh_conv_group* g, bh_stream_t stream);
 #define BH_CONV_AUTO 0
 #define BH_CONV_MFMA 1 /* conv_mfma_kernel: per-wave fragments from L2, split-K deep layers */
 #define BH_CONV_GEMM 2 /* conv_gemm_kernel: LDS-staged GEMM (1x1 s1, int8 in, symmetric filters) */

@@ -302,3 +302,75 @@ def test_fully_connected(gpu_lib, rows, depth, units, dtype):
                       bias_eff=db.value, mult=dm.value, shift=ds.value)
     _abi.check(gpu_lib.bh_fc_i8(ctypes.byref(p), None), "fc")
     np.testing.assert_array_equal(dy.download(dtype, ref.shape), ref)
+
+
+# conv_group_kernel (bh_conv_group_i8): independent small convs in ONE
+# dispatch - detector / pose heads - each member bit-exact with the oracle
+# (the same tile arithmetic as its own bh_conv2d_i8 launch): deep and shallow
+# K (the split-K and 2x2-wave member forms), N tails, uint8 with a filter zero
+# point, batch > 1, and a 3x3 group (the general-window instantiation)
+@pytest.mark.parametrize("cases,is1x1", [
+    ([(24, 7, 1280, 24), (24, 4, 512, 546), (24, 2, 256, 24), (24, 1, 128, 546), (24, 14, 576, 12)], 1),
+    ([(1, 14, 1024, 17), (1, 14, 1024, 34), (1, 14, 1024, 32), (1, 14, 1024, 32)], 1),
+    ([(3, 5, 48, 20, np.uint8), (2, 9, 64, 100)], 1),
+    ([(4, 7, 256, 64, np.int8, 3), (4, 4, 128, 40, np.int8, 3)], 0),
+])
+def test_conv_group(gpu_lib, cases, is1x1):
+    import ctypes
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(7100 + len(cases) + is1x1)
+    convs, keep, params = [], [], []
+    for c in cases:
+        b, sp, ic, oc = c[:4]
+        dtype = c[4] if len(c) > 4 else np.int8
+        k = c[5] if len(c) > 5 else 1
+        cc = ConvCase(rng, b, sp, sp, ic, oc, k, k, dtype=dtype, act=3)
+        convs.append(cc)
+        params.append(cc.params(gpu_lib, keep))
+        cc._dy_keep = cc._dy
+    for cc, p in zip(convs, params):
+        assert gpu_lib.bh_conv_group_ok(ctypes.byref(p)) == 1
+    arr = (_abi.ConvParams * len(params))(*params)
+    nbytes = gpu_lib.bh_conv_group_table_bytes(len(params))
+    host = np.zeros(nbytes, np.uint8)
+    g = _abi.ConvGroup()
+    _abi.check(gpu_lib.bh_conv_group_plan(arr, len(params), host.ctypes.data_as(ctypes.c_void_p), ctypes.byref(g)),
+               "plan")
+    assert g.n == len(params) and g.is1x1 == is1x1
+    dt = DeviceBuffer.from_array(host)
+    g.table = dt.value
+    _abi.check(gpu_lib.bh_conv_group_i8(ctypes.byref(g), None), "bh_conv_group_i8")
+    for i, cc in enumerate(convs):
+        got = cc._dy_keep.download(cc.dtype, (cc.b, cc.oh, cc.ow, cc.oc))
+        np.testing.assert_array_equal(got, cc.oracle(), err_msg="member %d" % i)
+    del keep, dt
+
+
+# a conv storing each image at a row stride into a wider tensor
+# (bh_conv_params.out_img_stride: a CONCATENATION slice written in place),
+# bytes outside the slice untouched; odd channel counts take the byte path
+@pytest.mark.parametrize("b,sp,ic,oc,off,extra", [(4, 7, 64, 12, 0, 100), (3, 4, 96, 273, 37, 555),
+                                                   (2, 2, 128, 546, 1001, 3)])
+def test_conv_strided_image_output(gpu_lib, b, sp, ic, oc, off, extra):
+    import ctypes
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(7300 + oc)
+    c = ConvCase(rng, b, sp, sp, ic, oc, 1, 1, act=3)
+    keep = []
+    p = c.params(gpu_lib, keep)
+    per = sp * sp * oc
+    stride = off + per + extra
+    fill = np.full(b * stride, 0x5a, np.uint8)
+    dbig = DeviceBuffer.from_array(fill)
+    p.output = dbig.value + off
+    p.out_img_stride = stride
+    _abi.check(gpu_lib.bh_conv2d_i8(ctypes.byref(p), None), "bh_conv2d_i8")
+    got = dbig.download(np.uint8, (b * stride,))
+    ref = c.oracle().reshape(b, per).view(np.uint8)
+    for n in range(b):
+        np.testing.assert_array_equal(got[n * stride + off:n * stride + off + per], ref[n], err_msg="image %d" % n)
+        assert (got[n * stride:n * stride + off] == 0x5a).all()
+        assert (got[n * stride + off + per:(n + 1) * stride] == 0x5a).all()
+    del keep

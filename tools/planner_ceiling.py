@@ -47,10 +47,14 @@ def thread_cpu():
     return out
 
 
-def measure(n_workers, n_jobs, inflight, n_models, job_batch=None):
+def measure(n_workers, n_jobs, inflight, n_models, job_batch=None, gpu=False):
     from band_amd import engine as E
 
-    cfg = E.make_config([E.SchedulerType.kRoundRobin], [0] * n_workers, num_threads=[1] * n_workers,
+    # gpu: GPU workers (DeviceFlag kGPU = 1) whose passes can carry up to
+    # job_batch jobs (job batching): the per-job dispatch cost with batched
+    # assignments; the add.tflite pass is a few us of device work
+    flag = 1 if gpu else 0
+    cfg = E.make_config([E.SchedulerType.kRoundRobin], [flag] * n_workers, num_threads=[1] * n_workers,
                         max_job_batch=job_batch)
     eng = E.Engine(cfg)
     models = []
@@ -70,6 +74,8 @@ def measure(n_workers, n_jobs, inflight, n_models, job_batch=None):
     busy = sorted((((t1[k] - t0.get(k, 0.0)) / wall, k[1]) for k in t1), reverse=True)
     used = np.bincount(wid, minlength=n_workers)
     out = {
+        "worker_device": "gpu" if gpu else "cpu",
+        "job_batch": job_batch or 1,
         "workers": n_workers,
         "models": n_models,
         "inflight": inflight,
@@ -94,10 +100,13 @@ def main():
     ap.add_argument("--jobs", type=int, default=200000)
     ap.add_argument("--inflight", type=int, default=0, help="default: min(4 x workers, 128 x models)")
     ap.add_argument("--models", type=int, default=8, help="registered copies of add.tflite (128 ring slots each)")
+    ap.add_argument("--gpu", action="store_true", help="GPU workers (job batching possible)")
+    ap.add_argument("--job-batch", type=int, default=0, help="max jobs per worker pass (GPU workers)")
     a = ap.parse_args()
     for w in [int(x) for x in a.workers.split(",")]:
-        inflight = a.inflight or min(4 * w, 128 * a.models)
-        print(json.dumps(measure(w, a.jobs, inflight, a.models)), flush=True)
+        jb = a.job_batch or 1
+        inflight = a.inflight or min(4 * w * jb, 128 * a.models)
+        print(json.dumps(measure(w, a.jobs, inflight, a.models, a.job_batch or None, a.gpu)), flush=True)
 
 
 if __name__ == "__main__":

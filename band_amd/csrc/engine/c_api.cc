@@ -411,8 +411,8 @@ namespace {
 // ring handles in a different order, by at most the submitter count).
 BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models, int n_jobs,
                          int max_inflight, bool open_loop,
-                         const std::function<std::pair<int64_t, int>(int)>& next_arrival, double* latency_us,
-                         int* worker_ids, int* model_index, double* wall_s) {
+                         const std::function<std::pair<int64_t, int>(int, int)>& next_arrival, double* latency_us,
+                         int* worker_ids, int* model_index, double* wall_s, int burst_hint = 1) {
   if (!engine || !models || n_models <= 0 || n_jobs < 0 || max_inflight <= 0) return kBandErr;
   band::Engine& e = *engine->impl;
   // per model: one input tensor (copied into the request ring at submit)
@@ -438,6 +438,13 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
   lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
+  // requests of one model submitted per RequestAsync call (closed loop:
+  // the job -> model order is run-major, `burst` jobs per model in turn)
+  int burst = burst_hint > 0 ? burst_hint : 1;
+  if (const char* bv = std::getenv("BANDX_DRIVER_BURST")) burst = std::max(1, std::atoi(bv));
+  burst = std::max(1, std::min(burst, max_inflight / std::max(1, lanes)));
+  for (int m = 0; m < n_models; ++m)
+    burst = std::max(1, std::min(burst, e.RequestRingSize(models[m]->impl->GetId()) / (2 * lanes)));
   int readers = 6;
   if (const char* rv = std::getenv("BANDX_DRIVER_READERS")) readers = std::max(1, std::atoi(rv));
   readers = std::max(1, std::min(readers, n_jobs > 0 ? n_jobs : 1));
@@ -494,11 +501,11 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // its finished-job record is gone before the callback can read it
   std::set<long> unfinished;
   long next_gseq = 0;
-  const long record_span = std::max(1, band::Planner::kNumFinishedRecords - lanes);
+  const long record_span = std::max(1, band::Planner::kNumFinishedRecords - lanes * burst);
   bool failed = false;
   // arrivals are drawn in job order (the open-loop schedule is one sequence)
   std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
-  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j);
+  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j, burst);
   const band::CallbackId cb = e.SetOnEndRequest([&](int id, absl::Status) {
     band::Job rec = e.GetFinishedJob(id);  // outside mu: the planner's own lock
     std::lock_guard<std::mutex> lk(mu);
@@ -559,55 +566,85 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
       }
     });
   }
+  // Runs: consecutive jobs of one model that are due are submitted as ONE
+  // vector RequestAsync (band/engine.cc:455-529, the overload Band's own
+  // benchmark tool uses with batch_size >= 2), up to `burst` requests: one
+  // ring allocation, one planner enqueue and one wake-up per run instead of
+  // per request.  Lane l takes runs l, l + lanes, ...
+  std::vector<std::pair<int, int>> runs;  // (first job, length)
+  for (int j = 0; j < n_jobs;) {
+    int k = j + 1;
+    while (k < n_jobs && k - j < burst && arrivals[k].second == arrivals[j].second &&
+           arrivals[k].first == arrivals[j].first)
+      ++k;
+    runs.emplace_back(j, k - j);
+    j = k;
+  }
   for (int l = 0; l < lanes; ++l) {
     threads.emplace_back([&, l] {
       pthread_setname_np(pthread_self(), "bandx-submit");
-      for (int j = l; j < n_jobs; j += lanes) {
-        const auto& arrival = arrivals[j];
+      std::vector<band::ModelId> ids;
+      std::vector<band::RequestOption> opts;
+      std::vector<band::Tensors> ins;
+      std::vector<long> seqs, gseqs;
+      for (size_t ri = l; ri < runs.size(); ri += lanes) {
+        const int j0 = runs[ri].first, r = runs[ri].second;
+        const auto& arrival = arrivals[j0];
         const int64_t now = band::time::NowMicros() - t0;
         if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
         const int m = arrival.second;
-        const long span = std::max(1, ring[m] - lanes);
-        long seq, gseq;
+        const long span = std::max(1, ring[m] - lanes * burst);
         const int64_t w0 = band::time::NowMicros();
+        seqs.clear();
+        gseqs.clear();
         {
           std::unique_lock<std::mutex> lk(mu);
           cv_sub.wait(lk, [&] {
-            return inflight < max_inflight && unread[m] < ring[m] &&
-                   (unread_seq[m].empty() || next_seq[m] - *unread_seq[m].begin() < span) &&
-                   (unfinished.empty() || next_gseq - *unfinished.begin() < record_span);
+            return inflight + r <= max_inflight && unread[m] + r <= ring[m] &&
+                   (unread_seq[m].empty() || next_seq[m] + r - 1 - *unread_seq[m].begin() < span) &&
+                   (unfinished.empty() || next_gseq + r - 1 - *unfinished.begin() < record_span);
           });
-          ++inflight;
-          ++unread[m];
-          seq = next_seq[m]++;
-          unread_seq[m].insert(seq);
-          gseq = next_gseq++;
-          unfinished.insert(gseq);
+          inflight += r;
+          unread[m] += r;
           tick();
-          ++in_engine;
+          in_engine += r;
+          for (int k = 0; k < r; ++k) {
+            seqs.push_back(next_seq[m]++);
+            unread_seq[m].insert(seqs.back());
+            gseqs.push_back(next_gseq++);
+            unfinished.insert(gseqs.back());
+          }
         }
         const int64_t w1 = band::time::NowMicros();
-        auto id = e.RequestAsync(models[m]->impl->GetId(), band::RequestOption::GetDefaultOption(), in_ptrs[m]);
+        ids.assign(r, models[m]->impl->GetId());
+        opts.assign(r, band::RequestOption::GetDefaultOption());
+        ins.assign(r, in_ptrs[m]);
+        auto handles = e.RequestAsync(ids, opts, ins);
+        const int64_t w2 = band::time::NowMicros();
         std::lock_guard<std::mutex> lk(mu);
         submit_wait += double(w1 - w0);
-        submit_call += double(band::time::NowMicros() - w1);
-        const Pending item{j, m, t0 + arrival.first, seq, gseq};
-        if (!id.ok()) {
-          BAND_LOG(band::LogSeverity::kError, "request driver: submit of job %d failed: %s", j,
-                   std::string(id.status().message()).c_str());
-          if (++taken >= n_jobs) cv_read.notify_all();
-          tick();
-          --in_engine;
-          unfinished.erase(gseq);
-          retire(item, false);
-          cv_sub.notify_all();
-        } else {
-          pending[id.value()] = item;
-          auto ea = early.find(id.value());
-          if (ea != early.end()) {
-            unfinished.erase(gseq);
+        submit_call += double(w2 - w1);
+        for (int k = 0; k < r; ++k) {
+          const Pending item{j0 + k, m, t0 + arrivals[j0 + k].first, seqs[k], gseqs[k]};
+          if (!handles.ok()) {
+            if (k == 0)
+              BAND_LOG(band::LogSeverity::kError, "request driver: submit of jobs %d..%d failed: %s", j0, j0 + r - 1,
+                       std::string(handles.status().message()).c_str());
+            if (++taken >= n_jobs) cv_read.notify_all();
+            tick();
+            --in_engine;
+            unfinished.erase(gseqs[k]);
+            retire(item, false);
             cv_sub.notify_all();
-            done.emplace_back(id.value(), std::move(ea->second));
+            continue;
+          }
+          const band::JobId id = handles.value()[k];
+          pending[id] = item;
+          auto ea = early.find(id);
+          if (ea != early.end()) {
+            unfinished.erase(gseqs[k]);
+            cv_sub.notify_all();
+            done.emplace_back(id, std::move(ea->second));
             early.erase(ea);
             cv_read.notify_one();
           }
@@ -636,10 +673,11 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
 BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
                                     int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
                                     double* wall_s) {
+  // closed loop: runs of `burst` requests per model, models in turn
   return DriveRequests(
       engine, models, inputs, n_models, n_jobs, max_inflight, false,
-      [&](int j) { return std::make_pair(int64_t(0), j % std::max(n_models, 1)); }, latency_us, worker_ids,
-      nullptr, wall_s);
+      [&](int j, int burst) { return std::make_pair(int64_t(0), (j / burst) % std::max(n_models, 1)); },
+      latency_us, worker_ids, nullptr, wall_s, 4);
 }
 
 BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
@@ -652,11 +690,11 @@ BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTen
   double t = 0;
   return DriveRequests(
       engine, models, inputs, n_models, n_jobs, max_inflight, true,
-      [&](int) {
+      [&](int, int) {
         t += gap(rng) * 1e6;
         return std::make_pair(static_cast<int64_t>(t), pick(rng));
       },
-      latency_us, worker_ids, model_index, wall_s);
+      latency_us, worker_ids, model_index, wall_s, 1);
 }
 
 int64_t BandxEngineGetWorkerJobCount(BandEngine* engine, int worker_id) {

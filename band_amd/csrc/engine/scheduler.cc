@@ -86,21 +86,29 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
         count[j->model_id] = 0;  // later requests of a model are not its oldest
       }
     }
-    Job job = std::move(*it);
-    it = requests.erase(it);
-    const SubgraphKey key = engine_.GetLargestSubgraphKey(job.model_id, w);
+    const SubgraphKey key = engine_.GetLargestSubgraphKey(it->model_id, w);
     // job batching (extension): the idle worker also takes the next queued
     // requests of the same model, up to its batch, and runs them in one pass;
-    // one EnqueueToWorkerBatch call keeps their FIFO order if it is refused
-    std::vector<ScheduleAction> actions{{std::move(job), key}};
-    for (int more = engine_.MaxJobBatch(key) - 1; more > 0 && it != requests.end();) {
-      if (it->model_id == key.GetModelId()) {
-        actions.emplace_back(std::move(*it), key);
-        it = requests.erase(it);
-        --more;
-      } else {
-        ++it;
+    // one EnqueueToWorkerBatch call keeps their FIFO order if it is refused.
+    // One stable pass over the queue takes them out (erasing each from the
+    // middle of the deque moved the whole tail per job: with hundreds of
+    // queued requests and 24-job batches that made the planner thread the
+    // bottleneck)
+    std::vector<ScheduleAction> actions;
+    const int batch = std::max(1, engine_.MaxJobBatch(key));
+    actions.reserve(batch);
+    if (batch == 1) {
+      actions.emplace_back(std::move(*it), key);
+      requests.erase(it);
+    } else {
+      JobQueue rest;
+      for (auto j = requests.begin(); j != requests.end(); ++j) {
+        if (j >= it && static_cast<int>(actions.size()) < batch && j->model_id == key.GetModelId())
+          actions.emplace_back(std::move(*j), key);
+        else
+          rest.push_back(std::move(*j));
       }
+      requests.swap(rest);
     }
     ok &= engine_.EnqueueToWorkerBatch(actions);
     next_ = w + 1;

@@ -185,8 +185,12 @@ __device__ __forceinline__ void tile_copy_out(const unsigned char* src, uint8_t*
   const int vr = min(TH, OH - oy0);
   const int rb = vc * Nc;               // valid bytes per tile row (multiple of 4)
   const int cpr = (TW * Nc + 15) >> 4;  // 16-byte chunks per staged row
+  // i / cpr without the ~35-instruction integer division: (i + 0.5) / cpr
+  // in float is within 2^-20 relative of the quotient, far from the next
+  // integer for i < 2^16
+  const float rcp = 1.0f / (float)cpr;
   for (int i = tid; i < vr * cpr; i += nthreads) {
-    const int r = i / cpr;
+    const int r = (int)(((float)i + 0.5f) * rcp);
     const int c = i - r * cpr;
     const int b = c * 16;
     if (b >= rb) continue;

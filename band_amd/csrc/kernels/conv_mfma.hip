@@ -408,10 +408,12 @@ __global__ __launch_bounds__(256) void conv_group_kernel(const ConvGroupMember* 
   while (i + 1 < n && tab[i + 1].blk0 <= b) ++i;  // uniform: scalar loads of the table
   const ConvGroupMember& e = tab[i];
   const int local = b - e.blk0;
-  if (e.form == 0)
-    conv_mfma_tile<1, 1, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks);
-  else
-    conv_mfma_tile<1, 1, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks);
+  switch (e.form) {
+    case 0: conv_mfma_tile<1, 1, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
+    case 1: conv_mfma_tile<1, 1, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
+    case 2: conv_mfma_tile<2, 2, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
+    default: conv_mfma_tile<2, 2, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
+  }
 }
 
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
@@ -800,11 +802,16 @@ extern "C" int bh_conv_group_plan(const bh_conv_params* members, int n, void* ho
     e.dv.in_c = bh::FastDiv(p.in_c);
     e.dv.k_w = bh::FastDiv(p.k_w);
     const int ksteps = (e.K + 63) / 64;
-    // deep K: 16 x 16 tiles with K split over the 4 waves; else 32 x 32
-    // tiles over 2 x 2 waves (conv_mfma_kernel's small-grid forms)
-    e.form = ksteps >= 3 ? 0 : 1;
-    const int tm = e.form == 0 ? 16 : 32, tn = tm;
-    e.kchunk = e.form == 0 ? (ksteps + 3) / 4 * 64 : ksteps * 64;
+    // conv_mfma_kernel's forms by size: deep K splits K over the 4 waves of
+    // a 16 x 16 (form 0) or, with >= 256 such workgroups, 32 x 32 tile
+    // (form 2); shallow K takes 32 x 32 tiles over 2 x 2 waves (form 1) or
+    // 64 x 64 ones (form 3) once those give >= 256 workgroups
+    if (ksteps >= 3)
+      e.form = bh::wgs(e.M, e.N, 32, 32) >= 256 ? 2 : 0;
+    else
+      e.form = bh::wgs(e.M, e.N, 64, 64) >= 256 ? 3 : 1;
+    const int tm = e.form == 0 ? 16 : (e.form == 3 ? 64 : 32), tn = tm;
+    e.kchunk = (e.form == 0 || e.form == 2) ? (ksteps + 3) / 4 * 64 : ksteps * 64;
     e.gn = (e.N + tn - 1) / tn;
     e.blocks = ((e.M + tm - 1) / tm) * e.gn;
     e.blk0 = (int)blocks;

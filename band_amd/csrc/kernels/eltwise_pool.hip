@@ -159,8 +159,12 @@ __global__ __launch_bounds__(256) void pool_kernel(bh_pool_params p, int total, 
 // 4th tap of the clipped window with up to 16 loads in flight, then the 4
 // partial sums / maxima meet in LDS - one memory round trip instead of one
 // per 8 taps.
-__global__ __launch_bounds__(256) void pool_wide_kernel(bh_pool_params p, PoolDivs dv) {
-  __shared__ int32_t part[3][64][4];
+// NW waves per workgroup: 16 when the window holds more taps than 4 waves
+// take in one round of 16 loads each (DeepLab's 14x14 image pooling: 196
+// taps, 4 rounds on 4 waves)
+template <int NW>
+__global__ __launch_bounds__(NW * 64) void pool_wide_kernel(bh_pool_params p, PoolDivs dv) {
+  __shared__ int32_t part[NW - 1][64][4];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int pix = blockIdx.x;
@@ -181,11 +185,11 @@ __global__ __launch_bounds__(256) void pool_wide_kernel(bh_pool_params p, PoolDi
   const bool avg = p.kind == BH_POOL_AVG;
   const int32_t init = avg ? 0 : (sg ? -128 : 0);
   int32_t acc[4] = {init, init, init, init};
-  for (int t0 = wave; t0 < cnt_total; t0 += 4 * 16) {
+  for (int t0 = wave; t0 < cnt_total; t0 += NW * 16) {
     uint32_t w[16];
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      const int tt = t0 + 4 * u;
+      const int tt = t0 + NW * u;
       w[u] = 0;
       if (active && tt < cnt_total) {
         const int ry = small_div(tt, wx);
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(256) void pool_wide_kernel(bh_pool_params p, PoolDi
     }
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
-      if (t0 + 4 * u >= cnt_total) break;
+      if (t0 + NW * u >= cnt_total) break;
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         const int32_t q = sg ? sbyte(w[u], v) : (int32_t)((w[u] >> (8 * v)) & 0xff);
@@ -210,7 +214,7 @@ __global__ __launch_bounds__(256) void pool_wide_kernel(bh_pool_params p, PoolDi
   __syncthreads();
   if (wave > 0 || !active) return;
 #pragma unroll
-  for (int z = 0; z < 3; ++z)
+  for (int z = 0; z < NW - 1; ++z)
 #pragma unroll
     for (int v = 0; v < 4; ++v) acc[v] = avg ? acc[v] + part[z][lane][v] : max(acc[v], part[z][lane][v]);
   const int cnt = cnt_total > 0 ? cnt_total : 1;
@@ -278,7 +282,10 @@ extern "C" int bh_pool_i8(const bh_pool_params* pp, bh_stream_t stream) {
   if (p.channels % 4 == 0 && pixels * (p.channels / 4) <= 65536 && p.f_h * p.f_w >= 16 && pixels <= 65535) {
     dv.groups = bh::FastDiv(p.channels / 4);
     const dim3 grid((unsigned)pixels, (unsigned)((p.channels / 4 + 63) / 64));
-    BH_LAUNCH(bh::pool_wide_kernel, grid, dim3(256), 0, s, p, dv);
+    if (p.f_h * p.f_w > 4 * 16)
+      BH_LAUNCH(bh::pool_wide_kernel<16>, grid, dim3(1024), 0, s, p, dv);
+    else
+      BH_LAUNCH(bh::pool_wide_kernel<4>, grid, dim3(256), 0, s, p, dv);
   } else if (p.channels % 4 == 0) {
     const int total = (int)(pixels * (p.channels / 4));
     dv.groups = bh::FastDiv(p.channels / 4);

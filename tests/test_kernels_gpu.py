@@ -242,6 +242,9 @@ def test_mul(gpu_lib, dtype):
     dict(shape=(2, 9, 9, 40), f=(5, 5), s=(3, 3), same=True, dtype=np.int8),
     dict(shape=(1, 20, 20, 8), f=(8, 8), s=(4, 4), same=True, dtype=np.uint8),
     dict(shape=(1, 12, 12, 260), f=(12, 12), s=(1, 1), same=False, dtype=np.int8),
+    # > 64 taps: 16 waves per workgroup (DeepLab's image pooling; clipped windows)
+    dict(shape=(16, 14, 14, 320), f=(14, 14), s=(1, 1), same=False, dtype=np.int8),
+    dict(shape=(3, 30, 30, 12), f=(10, 10), s=(7, 7), same=True, dtype=np.uint8),
 ])
 def test_pool(gpu_lib, kind, cfg):
     from band_amd import _abi
@@ -313,6 +316,7 @@ def test_fully_connected(gpu_lib, rows, depth, units, dtype):
     ([(24, 7, 1280, 24), (24, 4, 512, 546), (24, 2, 256, 24), (24, 1, 128, 546), (24, 14, 576, 12)], 1),
     ([(1, 14, 1024, 17), (1, 14, 1024, 34), (1, 14, 1024, 32), (1, 14, 1024, 32)], 1),
     ([(3, 5, 48, 20, np.uint8), (2, 9, 64, 100)], 1),
+    ([(24, 14, 576, 200), (5, 20, 128, 512), (2, 3, 32, 8)], 1),  # member forms 2 / 3 / 1
     ([(4, 7, 256, 64, np.int8, 3), (4, 4, 128, 40, np.int8, 3)], 0),
 ])
 def test_conv_group(gpu_lib, cases, is1x1):

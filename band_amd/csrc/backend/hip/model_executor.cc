@@ -26,6 +26,12 @@
 namespace band {
 namespace hip {
 
+namespace {
+// set while PrepareJobBatches constructs a variant executor: a kCPU variant
+// then makes no host pool of its own
+thread_local bool t_variant_ctor = false;
+}  // namespace
+
 const std::vector<int> HipModelExecutor::kEmpty;
 
 namespace {
@@ -66,12 +72,12 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   if (device_flag_ == DeviceFlag::kGPU && DeviceRegistry::Get().GpuAvailable()) {
     ordinal_ = DeviceRegistry::Get().OrdinalForWorker(worker_id_);
     stream_ = DeviceRegistry::Get().StreamForWorker(worker_id_);
-  } else if (device_flag_ == DeviceFlag::kCPU) {
-    // host execution of the lowered program (cpu_kernels.h)
-    // pinned to the executor's CpuSet when it names a proper subset of the
-    // process's CPUs (affinity.h PinnableCpus)
-    cpu_pool_ = std::make_unique<CpuPool>(num_threads_ > 0 ? num_threads_ : 1,
-                                          PinnableCpus(thread_affinity_mask_));
+  } else if (device_flag_ == DeviceFlag::kCPU && !t_variant_ctor) {
+    // host execution of the lowered program (cpu_kernels.h), pinned to the
+    // executor's CpuSet when it names a proper subset of the process's CPUs
+    // (affinity.h PinnableCpus); job-batch variants share their base
+    // executor's pool instead (PrepareJobBatches)
+    cpu_pool_ = std::make_shared<CpuPool>(num_threads_ > 0 ? num_threads_ : 1, PinnableCpus(thread_affinity_mask_));
   }
   const char* g = std::getenv("BAND_HIP_GRAPH");
   if (g && g[0] == '0') use_graph_ = false;
@@ -2745,6 +2751,8 @@ absl::Status HipModelExecutor::ExecuteOnHost(PreparedSubgraph* sg) {
     if (slot != mirror) std::memcpy(in ? slot : mirror, in ? mirror : slot, meta_[t]->bytes);
   };
   for (int t : sg->inputs) sync(t, true);
+  if (!cpu_pool_)
+    cpu_pool_ = std::make_shared<CpuPool>(num_threads_ > 0 ? num_threads_ : 1, PinnableCpus(thread_affinity_mask_));
   CpuPool& pool = *cpu_pool_;
   for (const Launch& l : sg->launches) {
     switch (l.kind) {
@@ -2842,7 +2850,10 @@ absl::Status HipModelExecutor::WaitPass(PreparedSubgraph* sg) {
 }
 
 absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const SubgraphKey& key, int max_batch) {
-  if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("job batching needs a kGPU executor");
+  // kGPU: batched graphs on the device; kCPU: the same lowering at batch n
+  // run by the host kernels (one pass over n images instead of n passes)
+  if (device_flag_ != DeviceFlag::kGPU && device_flag_ != DeviceFlag::kCPU)
+    return absl::InternalError("job batching needs a kGPU or kCPU executor");
   PreparedSubgraph* base = Find(key);
   if (!base) return absl::InternalError("Cannot find subgraph");
   auto* hm = dynamic_cast<HipModel*>(model);
@@ -2870,14 +2881,22 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
     JobBatchVariant v;
     v.batch = b;
     RETURN_STATUS_IF(hm->CloneWithJobBatch(b, &v.model));
+    t_variant_ctor = true;
     v.exec = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
                                                 num_threads_);
+    t_variant_ctor = false;
     v.exec->use_graph_ = use_graph_;
     // direct job I/O captures the variants' graphs without host copies
     v.exec->io_mode_ = direct_io_ ? 1 : io_mode_;
     v.exec->direct_io_ = direct_io_;
     v.exec->block_sync_ = block_sync_;
     v.exec->sync_mode_ = sync_mode_;
+    if (device_flag_ == DeviceFlag::kCPU) {  // one host pool per worker
+      if (!cpu_pool_)
+        cpu_pool_ = std::make_shared<CpuPool>(num_threads_ > 0 ? num_threads_ : 1,
+                                              PinnableCpus(thread_affinity_mask_));
+      v.exec->cpu_pool_ = cpu_pool_;
+    }
     v.exec->io_stream_bytes_ = io_stream_bytes_;
     if (largest) {
       PreparedSubgraph* ls = largest->Find(key);

@@ -263,7 +263,7 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;
   bh_stream_t stream_ = nullptr;
-  std::unique_ptr<CpuPool> cpu_pool_;  // kCPU executors
+  std::shared_ptr<CpuPool> cpu_pool_;  // kCPU executors (shared with their job-batch variants)
   bool use_graph_ = true;
   // Where a graph pass's host copies go: captured into the graph (blit
   // kernels on the compute queue; lowest latency for small transfers) or

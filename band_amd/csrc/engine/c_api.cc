@@ -506,20 +506,27 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // arrivals are drawn in job order (the open-loop schedule is one sequence)
   std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
   for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j, burst);
-  const band::CallbackId cb = e.SetOnEndRequest([&](int id, absl::Status) {
-    band::Job rec = e.GetFinishedJob(id);  // outside mu: the planner's own lock
+  // one call per group of finished requests (a batched pass ends up to its
+  // batch at once): one lock of mu and one wake-up per side for the group
+  const band::CallbackId cb = e.SetOnEndRequests([&](const std::vector<const band::Job*>& jobs) {
     std::lock_guard<std::mutex> lk(mu);
     tick();
-    --in_engine;
-    auto pit = pending.find(id);
-    if (pit != pending.end()) {
-      unfinished.erase(pit->second.gseq);
-      cv_sub.notify_all();
-      done.emplace_back(id, std::move(rec));
-      cv_read.notify_one();
-    } else {
-      early.emplace(id, std::move(rec));
+    int to_read = 0;
+    for (const band::Job* rec : jobs) {
+      --in_engine;
+      auto pit = pending.find(rec->job_id);
+      if (pit != pending.end()) {
+        unfinished.erase(pit->second.gseq);
+        done.emplace_back(rec->job_id, *rec);
+        ++to_read;
+      } else {
+        early.emplace(rec->job_id, *rec);
+      }
     }
+    if (to_read == 0) return;
+    cv_sub.notify_all();
+    if (to_read == 1) cv_read.notify_one();
+    else cv_read.notify_all();
   });
   auto retire = [&](const Pending& item, bool ok) {  // under mu
     if (!ok && !failed) failed = true;

@@ -139,7 +139,8 @@ absl::Status Engine::RegisterModel(Model* model) {
       if (!std::includes(outputs.begin(), outputs.end(), eout_set.begin(), eout_set.end()))
         return absl::InternalError("Output format is not correct for worker " + std::to_string(def.worker_id));
       // job batching for whole-model subgraphs on GPU workers (config extension)
-      if (max_job_batch_ > 1 && GetWorkerDevice(def.worker_id) == DeviceFlag::kGPU &&
+      if (max_job_batch_ > 1 &&
+          (GetWorkerDevice(def.worker_id) == DeviceFlag::kGPU || GetWorkerDevice(def.worker_id) == DeviceFlag::kCPU) &&
           static_cast<int>(def.op_indices.size()) == spec.num_ops) {
         if (auto* jb = dynamic_cast<hip::IJobBatching*>(exec)) {
           absl::Status bs = jb->PrepareJobBatches(backend_model, key, max_job_batch_);

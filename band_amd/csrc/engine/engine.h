@@ -76,6 +76,9 @@ class Engine : public IEngine {
   absl::Status GetOutputTensorsOf(const Job& job, Tensors outputs);
   CallbackId SetOnEndRequest(std::function<void(int, absl::Status)> on_end_request);
   absl::Status UnsetOnEndRequest(CallbackId callback_id);
+  // extension: one call per group of finished requests with their records
+  // (Planner::SetOnEndRequests)
+  CallbackId SetOnEndRequests(Planner::EndRequestsCallback cb) { return planner_->SetOnEndRequests(std::move(cb)); }
 
   // harness extensions (job tracer / benchmark / profile persistence)
   Job GetFinishedJob(JobId job_id) { return planner_->GetFinishedJob(job_id); }
@@ -126,6 +129,7 @@ class Engine : public IEngine {
   }
   void PrepareReenqueue(Job& job) override { planner_->PrepareReenqueue(job); }
   void EnqueueFinishedJob(Job& job) override { planner_->EnqueueFinishedJob(job); }
+  void EnqueueFinishedJobs(const std::vector<Job*>& jobs) override { planner_->EnqueueFinishedJobs(jobs); }
   void ReleaseRequest(const Job& job) override;
   void HoldOutput(const Job& job) override;
   void UnholdOutput(const Job& job) override;

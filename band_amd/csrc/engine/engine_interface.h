@@ -93,6 +93,11 @@ class IEngine {
   virtual std::vector<JobId> EnqueueBatch(std::vector<Job> jobs, bool push_front = false) = 0;
   virtual void PrepareReenqueue(Job& job) = 0;
   virtual void EnqueueFinishedJob(Job& job) = 0;
+  // the jobs of one batched pass, in order: one record update and one
+  // callback round instead of one per job
+  virtual void EnqueueFinishedJobs(const std::vector<Job*>& jobs) {
+    for (Job* j : jobs) EnqueueFinishedJob(*j);
+  }
   // a finished request frees its request-ring slot (ring back-pressure)
   virtual void ReleaseRequest(const Job& job) {}
   // keeps a finished request's output slot from being rewritten by a newer

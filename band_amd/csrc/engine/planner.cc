@@ -128,32 +128,51 @@ void Planner::WaitAll() {
   end_invoke_.wait(lock, [this] { return num_finished_jobs_ >= num_submitted_jobs_; });
 }
 
-void Planner::EnqueueFinishedJob(Job& job) {
-  std::unique_lock<std::mutex> lock(job_finished_mtx_);
-  const bool finished = engine_.IsEnd(job.subgraph_key) || job.status != JobStatus::kSuccess;
-  if (finished) {
-    Job& rec = jobs_finished_record_[RecordIndex(job.job_id)];
-    rec = job;
-    rec.following_jobs.clear();  // the record only needs the times / status
-    num_finished_jobs_++;
-    end_invoke_.notify_all();
-  }
-  lock.unlock();  // callbacks may re-enter the engine
-  // the request's input slot was consumed when the job started: free it
-  // before the callbacks, which may submit into this model's full ring; the
-  // output slot stays held until they return, so a request that reuses the
-  // slot cannot overwrite (or invalidate) the outputs a callback reads
-  const bool callbacks = job.require_callback && finished;
-  if (callbacks) engine_.HoldOutput(job);
-  if (finished) engine_.ReleaseRequest(job);
-  if (callbacks) {
-    {
-      std::lock_guard<std::mutex> cb_lock(on_end_request_mtx_);
-      const absl::Status s = job.status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
-      for (auto& cb : on_end_request_callbacks_) cb.second(job.job_id, s);
+void Planner::EnqueueFinishedJob(Job& job) { EnqueueFinishedJobs({&job}); }
+
+// The finished records of a group of jobs (one batched pass, or a single
+// job) under one lock and one wake-up of the waiters; then every request
+// slot is freed and the callbacks run once for the group.  Per job the order
+// is the reference's (band/planner.cc:133-165): record, then callbacks.
+void Planner::EnqueueFinishedJobs(const std::vector<Job*>& jobs) {
+  std::vector<const Job*> ended;  // requests that end here (not a split job's inner subgraph)
+  ended.reserve(jobs.size());
+  {
+    std::lock_guard<std::mutex> lock(job_finished_mtx_);
+    for (Job* job : jobs) {
+      if (!engine_.IsEnd(job->subgraph_key) && job->status == JobStatus::kSuccess) continue;
+      Job& rec = jobs_finished_record_[RecordIndex(job->job_id)];
+      rec = *job;
+      rec.following_jobs.clear();  // the record only needs the times / status
+      num_finished_jobs_++;
+      ended.push_back(job);
     }
-    engine_.UnholdOutput(job);
+    if (!ended.empty()) end_invoke_.notify_all();
   }
+  // callbacks may re-enter the engine, so they run outside the lock.  The
+  // request's input slot was consumed when the job started: free it before
+  // the callbacks, which may submit into this model's full ring; the output
+  // slot stays held until they return, so a request that reuses the slot
+  // cannot overwrite (or invalidate) the outputs a callback reads
+  std::vector<const Job*> notify;
+  for (const Job* job : ended) {
+    if (job->require_callback) {
+      engine_.HoldOutput(*job);
+      notify.push_back(job);
+    }
+    engine_.ReleaseRequest(*job);
+  }
+  if (notify.empty()) return;
+  {
+    std::lock_guard<std::mutex> cb_lock(on_end_request_mtx_);
+    for (auto& cb : on_end_requests_callbacks_) cb.second(notify);
+    for (const Job* job : notify) {
+      const absl::Status s =
+          job->status == JobStatus::kSuccess ? absl::OkStatus() : absl::InternalError("Job failed.");
+      for (auto& cb : on_end_request_callbacks_) cb.second(job->job_id, s);
+    }
+  }
+  for (const Job* job : notify) engine_.UnholdOutput(*job);
 }
 
 void Planner::PrepareReenqueue(Job& job) {
@@ -199,9 +218,16 @@ CallbackId Planner::SetOnEndRequest(std::function<void(int, absl::Status)> on_en
   return next_callback_id_++;
 }
 
+CallbackId Planner::SetOnEndRequests(EndRequestsCallback on_end_requests) {
+  std::lock_guard<std::mutex> lock(on_end_request_mtx_);
+  on_end_requests_callbacks_[next_callback_id_] = std::move(on_end_requests);
+  return next_callback_id_++;
+}
+
 absl::Status Planner::UnsetOnEndRequest(CallbackId id) {
   std::lock_guard<std::mutex> lock(on_end_request_mtx_);
-  if (!on_end_request_callbacks_.erase(id)) return absl::InternalError("Callback id not found.");
+  if (!on_end_request_callbacks_.erase(id) && !on_end_requests_callbacks_.erase(id))
+    return absl::InternalError("Callback id not found.");
   return absl::OkStatus();
 }
 

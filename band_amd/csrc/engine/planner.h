@@ -49,6 +49,7 @@ class Planner {
   void Wait(const std::vector<int>& job_ids);
   void WaitAll();
   void EnqueueFinishedJob(Job& job);
+  void EnqueueFinishedJobs(const std::vector<Job*>& jobs);
   void PrepareReenqueue(Job& job);
   bool EnqueueToWorker(const std::vector<ScheduleAction>& actions);
   void Trigger() { planner_safe_bool_.notify(); }
@@ -57,6 +58,11 @@ class Planner {
   int GetWorkerType() const;
   Job GetFinishedJob(int job_id);
   CallbackId SetOnEndRequest(std::function<void(int, absl::Status)> on_end_request);
+  // extension: one call per group of finished requests (a batched pass ends
+  // many at once) with their finished records; same id space and mutex as the
+  // per-request callbacks, removed by UnsetOnEndRequest
+  using EndRequestsCallback = std::function<void(const std::vector<const Job*>&)>;
+  CallbackId SetOnEndRequests(EndRequestsCallback on_end_requests);
   absl::Status UnsetOnEndRequest(CallbackId id);
   std::map<ModelId, WorkerId>& GetModelWorkerMap() { return model_worker_map_; }
   // all finished records still in the ring, oldest first (job tracer)
@@ -90,6 +96,7 @@ class Planner {
 
   std::mutex on_end_request_mtx_;
   std::map<CallbackId, std::function<void(int, absl::Status)>> on_end_request_callbacks_;
+  std::map<CallbackId, EndRequestsCallback> on_end_requests_callbacks_;
   CallbackId next_callback_id_ = 0;
   std::map<ModelId, WorkerId> model_worker_map_;
 };

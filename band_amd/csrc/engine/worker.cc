@@ -278,8 +278,9 @@ void Worker::WorkBatch(Job* head, std::vector<Job>& partners) {
   jobs_run_.fetch_add(n, std::memory_order_relaxed);
   phase_us_[2].fetch_add(time::NowMicros() - end_time, std::memory_order_relaxed);
   phase_us_[3].fetch_add(1, std::memory_order_relaxed);
-  for (int i = 1; i < n; ++i) engine_->EnqueueFinishedJob(*jobs[i]);
-  engine_->EnqueueFinishedJob(*head);
+  // partners first, the head (still at the queue front) last, as one group
+  std::rotate(jobs.begin(), jobs.begin() + 1, jobs.end());
+  engine_->EnqueueFinishedJobs(jobs);
   {
     std::lock_guard<std::mutex> lock(device_mtx_);
     partners_expected_us_ = 0;

@@ -515,3 +515,35 @@ def test_batched_request_with_a_bad_input_enqueues_nothing(tmp_path):
     e.WaitAll()
     assert e.GetJobRecord(h).status == JobStatus.kSuccess
     e.close()
+
+
+def test_cpu_workers_run_job_batches_bit_exact(tmp_path):
+    """job batching on kCPU workers (max_job_batch > 1): each worker pass
+    runs up to 8 queued jobs of one model as one batch-n lowering on the host
+    kernels; every job's outputs bit-exact vs the oracle, and fewer passes
+    than jobs"""
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    path, buf = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU, DeviceFlag.kCPU], num_threads=[2, 2],
+                           max_job_batch=8))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    om = OModel(buf)
+    rng = np.random.default_rng(11)
+    xs = [rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8) for _ in range(5)]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]].reshape(-1) for x in xs]
+    ins = [e.CreateInputTensor(m, 0) for _ in range(40)]
+    hs = []
+    for j, t in enumerate(ins):
+        t.data()[...] = xs[j % 5]
+        hs.append(e.RequestAsync(m, [t]))
+    e.WaitAll()
+    o = e.CreateOutputTensor(m, 0)
+    for j, h in enumerate(hs):
+        assert e.Wait(h, [o]) == kBandOk
+        np.testing.assert_array_equal(o.data().reshape(-1), refs[j % 5], err_msg="job %d" % j)
+    passes = sum(e.GetWorkerPhaseTimes(w)["passes"] for w in range(2))
+    assert 0 < passes < 40, passes
+    e.close()

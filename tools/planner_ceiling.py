@@ -66,8 +66,15 @@ def measure(n_workers, n_jobs, inflight, n_models, job_batch=None, gpu=False):
     # warm-up, then the timed closed loop
     eng.RunClosedLoop(models, min(n_jobs, 4 * inflight), inflight)
     t0 = thread_cpu()
+    sampler = None
+    if os.environ.get("PLANNER_CEILING_SAMPLE"):
+        from bench import ThreadSampler  # /proc state of every thread through the loop
+        sampler = ThreadSampler()
     lat, wid, wall = eng.RunClosedLoop(models, n_jobs, inflight)
     t1 = thread_cpu()
+    states = sampler.stop() if sampler else None
+    drv = eng.GetDriverStats()
+    phases = [eng.GetWorkerPhaseTimes(w) for w in range(n_workers)]
     # per-thread CPU share over the timed loop: the busiest threads name the
     # bottleneck (the planner thread is one of them; workers are named by the
     # engine only through their count, so the top shares are reported)
@@ -90,6 +97,17 @@ def measure(n_workers, n_jobs, inflight, n_models, job_batch=None, gpu=False):
         "process_cpu_cores": round(sum(b for b, _ in busy), 2),
         "host_cpus": os.cpu_count(),
     }
+    out["driver"] = dict(mean_in_engine=round(drv["mean_in_engine"], 1),
+                         mean_awaiting_read=round(drv["mean_awaiting_read"], 1),
+                         submit_wait=round(drv["submit_wait_us"] / drv["wall_us"], 3),
+                         submit_call=round(drv["submit_call_us"] / drv["wall_us"], 3))
+    # worker passes over the whole run (warm-up included): jobs per pass and
+    # the mean pass time
+    passes = sum(p["passes"] for p in phases)
+    out["jobs_per_pass"] = round(sum(eng.GetWorkerJobCount(w) for w in range(n_workers)) / max(1, passes), 2)
+    out["pass_us"] = round(sum(p["invoke_us"] for p in phases) / max(1, passes), 1)
+    if states:
+        out["thread_states"] = states
     eng.close()
     return out
 

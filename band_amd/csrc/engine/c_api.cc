@@ -548,27 +548,41 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         read_idle += double(w1 - w0);
         if (done.empty()) break;
         tick();
-        const band::JobId id = done.front().first;
-        const band::Job j = std::move(done.front().second);
-        done.pop_front();
-        if (++taken >= n_jobs) cv_read.notify_all();  // the other readers may leave
-        const Pending item = pending.at(id);
-        pending.erase(id);
+        // a fair share of what is ready (at most 8): fewer lock round trips
+        // when a batched pass finishes many requests at once
+        const size_t k = std::min<size_t>(8, (done.size() + readers - 1) / readers);
+        std::vector<std::pair<band::Job, Pending>> mine;
+        mine.reserve(k);
+        for (size_t q = 0; q < k; ++q) {
+          const band::JobId id = done.front().first;
+          auto pit = pending.find(id);
+          mine.emplace_back(std::move(done.front().second), pit->second);
+          mine.back().first.job_id = mine.back().first.job_id == id ? id : -1;
+          pending.erase(pit);
+          done.pop_front();
+          if (++taken >= n_jobs) cv_read.notify_all();  // the other readers may leave
+        }
+        if (!done.empty()) cv_read.notify_one();
         lk.unlock();
-        absl::Status st = j.job_id == id ? e.GetOutputTensorsOf(j, reader_out_ptrs[r][item.model])
-                                         : absl::InternalError("no finished record");
-        const bool ok = st.ok() && j.status == band::JobStatus::kSuccess;
-        if (!ok)
-          BAND_LOG(band::LogSeverity::kError, "request driver: job %d (model %d) failed: %s; record %d, status %s",
-                   id, item.model, std::string(st.message()).c_str(), j.job_id,
-                   band::ToString<band::JobStatus>(j.status));
-        if (latency_us)
-          latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
-        if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
-        if (model_index) model_index[item.index] = item.model;
+        std::vector<bool> oks(mine.size());
+        for (size_t q = 0; q < mine.size(); ++q) {
+          const band::Job& j = mine[q].first;
+          const Pending& item = mine[q].second;
+          absl::Status st = j.job_id >= 0 ? e.GetOutputTensorsOf(j, reader_out_ptrs[r][item.model])
+                                          : absl::InternalError("no finished record");
+          oks[q] = st.ok() && j.status == band::JobStatus::kSuccess;
+          if (!oks[q])
+            BAND_LOG(band::LogSeverity::kError, "request driver: job (model %d) failed: %s; record %d, status %s",
+                     item.model, std::string(st.message()).c_str(), j.job_id,
+                     band::ToString<band::JobStatus>(j.status));
+          if (latency_us)
+            latency_us[item.index] = static_cast<double>(j.end_time - (open_loop ? item.arrival : j.enqueue_time));
+          if (worker_ids) worker_ids[item.index] = j.subgraph_key.GetWorkerId();
+          if (model_index) model_index[item.index] = item.model;
+        }
         lk.lock();
         read_busy += double(band::time::NowMicros() - w1);
-        retire(item, ok);
+        for (size_t q = 0; q < mine.size(); ++q) retire(mine[q].second, oks[q]);
         cv_sub.notify_all();
       }
     });

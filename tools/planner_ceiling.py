@@ -70,7 +70,9 @@ def measure(n_workers, n_jobs, inflight, n_models, job_batch=None, gpu=False):
     if os.environ.get("PLANNER_CEILING_SAMPLE"):
         from bench import ThreadSampler  # /proc state of every thread through the loop
         sampler = ThreadSampler()
+    rq0 = eng.GetRequestPhaseTimes()
     lat, wid, wall = eng.RunClosedLoop(models, n_jobs, inflight)
+    rq1 = eng.GetRequestPhaseTimes()
     t1 = thread_cpu()
     states = sampler.stop() if sampler else None
     drv = eng.GetDriverStats()
@@ -106,6 +108,12 @@ def measure(n_workers, n_jobs, inflight, n_models, job_batch=None, gpu=False):
     passes = sum(p["passes"] for p in phases)
     out["jobs_per_pass"] = round(sum(eng.GetWorkerJobCount(w) for w in range(n_workers)) / max(1, passes), 2)
     out["pass_us"] = round(sum(p["invoke_us"] for p in phases) / max(1, passes), 1)
+    # RequestAsync's own cost per request (ring slot, input copy, planner enqueue)
+    nrq = max(1, rq1["jobs"] - rq0["jobs"])
+    out["request_async_us_per_job"] = {k: round((rq1[k] - rq0[k]) / nrq, 3)
+                                       for k in ("alloc_us", "copy_us", "enqueue_us")}
+    out["driver_env"] = {k: os.environ[k] for k in ("BANDX_DRIVER_BURST", "BANDX_DRIVER_LANES", "BANDX_DRIVER_READERS")
+                         if k in os.environ}
     if states:
         out["thread_states"] = states
     eng.close()
@@ -121,6 +129,11 @@ def main():
     ap.add_argument("--gpu", action="store_true", help="GPU workers (job batching possible)")
     ap.add_argument("--job-batch", type=int, default=0, help="max jobs per worker pass (GPU workers)")
     a = ap.parse_args()
+    if a.job_batch and "BANDX_DRIVER_BURST" not in os.environ:
+        # the closed loop submits each model's requests in runs of one batch
+        # (one vector RequestAsync per run): otherwise the single submitter
+        # thread, not the engine, sets the rate
+        os.environ["BANDX_DRIVER_BURST"] = str(a.job_batch)
     for w in [int(x) for x in a.workers.split(",")]:
         jb = a.job_batch or 1
         inflight = a.inflight or min(4 * w * jb, 128 * a.models)

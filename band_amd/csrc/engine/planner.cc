@@ -264,27 +264,39 @@ void Planner::CopyToLocalQueues() {
 bool Planner::EnqueueToWorker(const std::vector<ScheduleAction>& actions) {
   bool ok = true;
   std::vector<Job> rejected;  // back to the queue head in their original order
-  for (const auto& action : actions) {
-    Job job = action.first;
-    const SubgraphKey& key = action.second;
+  // consecutive actions for one subgraph key (a batched assignment) take the
+  // worker's lock once and read the key's latency estimates once
+  for (size_t i = 0; i < actions.size();) {
+    const SubgraphKey& key = actions[i].second;
+    size_t end = i + 1;
+    while (end < actions.size() && actions[end].second == key) ++end;
     Worker* worker = engine_.GetWorker(key.GetWorkerId());
-    if (worker == nullptr) {
-      BAND_LOG(LogSeverity::kWarning, "EnqueueToWorker: null worker id %d", key.GetWorkerId());
-      job.status = JobStatus::kEnqueueFailed;
-      EnqueueFinishedJob(job);
-    } else if (IsSLOViolated(job)) {
-      job.status = JobStatus::kSLOViolation;
-      job.invoke_time = -1;  // dropped before running
-      job.end_time = time::NowMicros();
-      ok = false;
-      EnqueueFinishedJob(job);
-    } else {
-      std::unique_lock<std::mutex> lock(worker->GetDeviceMtx());
+    std::vector<Job> ready;
+    ready.reserve(end - i);
+    for (; i < end; ++i) {
+      Job job = actions[i].first;
+      if (worker == nullptr) {
+        BAND_LOG(LogSeverity::kWarning, "EnqueueToWorker: null worker id %d", key.GetWorkerId());
+        job.status = JobStatus::kEnqueueFailed;
+        EnqueueFinishedJob(job);
+      } else if (IsSLOViolated(job)) {
+        job.status = JobStatus::kSLOViolation;
+        job.invoke_time = -1;  // dropped before running
+        job.end_time = time::NowMicros();
+        ok = false;
+        EnqueueFinishedJob(job);
+      } else {
+        ready.push_back(std::move(job));
+      }
+    }
+    if (ready.empty()) continue;
+    const int64_t profiled = engine_.GetProfiled(key), expected = engine_.GetExpected(key);
+    std::unique_lock<std::mutex> lock(worker->GetDeviceMtx());
+    for (Job& job : ready) {
       if (worker->IsEnqueueReady()) {
-        UpdateJobScheduleStatus(job, key);
+        UpdateJobScheduleStatus(job, key, profiled, expected);
         worker->EnqueueJob(job);
       } else {
-        lock.unlock();
         rejected.push_back(std::move(job));
       }
     }
@@ -310,10 +322,10 @@ bool Planner::IsSLOViolated(const Job& job) {
 
 // stamp the job with its subgraph and, if the subgraph does not finish the
 // model, attach the remainder as a following job (band/planner.cc:380-404)
-void Planner::UpdateJobScheduleStatus(Job& job, const SubgraphKey& key) {
+void Planner::UpdateJobScheduleStatus(Job& job, const SubgraphKey& key, int64_t profiled, int64_t expected) {
   job.subgraph_key = key;
-  job.profiled_execution_time = engine_.GetProfiled(key);
-  job.expected_execution_time = engine_.GetExpected(key);
+  job.profiled_execution_time = profiled;
+  job.expected_execution_time = expected;
   job.resolved_unit_subgraphs |= key.GetUnitIndices();
   if (!engine_.IsEnd(key)) {
     Job rest(job.model_id);

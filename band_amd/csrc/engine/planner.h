@@ -72,7 +72,7 @@ class Planner {
   absl::Status Plan();
   void CopyToLocalQueues();
   bool IsSLOViolated(const Job& job);
-  void UpdateJobScheduleStatus(Job& job, const SubgraphKey& target_key);
+  void UpdateJobScheduleStatus(Job& job, const SubgraphKey& target_key, int64_t profiled, int64_t expected);
   bool IsJobIdValid(int job_id) const { return job_id >= 0 && num_submitted_jobs_ - job_id <= kNumFinishedRecords; }
   static int RecordIndex(int job_id) { return job_id % kNumFinishedRecords; }
   void DumpLog();

@@ -60,8 +60,19 @@ __device__ __forceinline__ void dma4(const void* src, unsigned char* lds_lane0) 
   __builtin_amdgcn_global_load_lds(src, (lds_ptr_t*)lds_lane0, 4, 0, 0);
 }
 
-// chunk c (16 bytes) of filter row `row` sits at chunk swz(row, c)
-__device__ __host__ __forceinline__ int swz(int row, int c) { return (c & ~3) | ((c & 3) ^ ((row >> 2) & 3)); }
+// chunk c (16 bytes) of filter row `row` (R = k_pad / 16 chunks per row)
+// sits at chunk swz(row, c, R).  A ds_read_b128 serves 64 lanes in four
+// 16-lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32), one 256-byte
+// bank row per group; lane (r16, g) reads row 16t + r16 at chunk 4k + g.  The
+// XOR spreads each group's 16 reads over the 16 distinct 16-byte bank slots
+// for every row stride: R = 4 mod 8 puts rows r16 & 3 in 4 slot classes, R = 8
+// mod 16 in 2 and R = 0 mod 16 in 1, and the XOR with (r16 >> 2) & 2, r16 & 7
+// or r16 & 15 (within an aligned block of 4, 8 or 16 chunks, so inside the
+// row) separates the lanes a class holds (tools/lds_bank_model.py).
+__device__ __host__ __forceinline__ int swz(int row, int c, int R) {
+  const int s = (R & 15) == 0 ? (row & 15) : ((R & 15) == 8 ? (row & 7) : ((row >> 2) & 2));
+  return c ^ s;
+}
 }  // namespace
 
 // The packed constant block (byte offsets, all multiples of 16):
@@ -112,6 +123,7 @@ struct TileGeom {
   int S1, S2;          // LDS row strides of the dw output / the pw2 operand
   int T1, T2;          // 16-channel tiles of pw1 / pw2
   int patch_ru;        // 16-byte units per patch row (PW*C/16)
+  int pmask, plog;     // C/16 - 1 and log2(C/16) when C/16 is a power of 2, else 0 (patch swizzle)
   int res_ru4;         // 4-byte units per residual tile row (TW*N1/4)
   int u_patch;         // 16-byte units of the patch
   int off_res, off_blob, blob_units;
@@ -134,11 +146,22 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
   g.PW = (TW - 1) * d.stride_w + 2 * d.dil_w + 1;
   g.tiles_y = (d.out_h + TH - 1) / TH;
   g.tiles_x = (d.out_w + TW - 1) / TW;
-  g.S1 = p.pw1.k_pad + 16;
-  g.S2 = p.has_pw2 ? p.pw2.k_pad + 16 : 0;
+  // rows of k_pad + 32 bytes: the 16 rows a ds_read_b128 lane group reads
+  // (r16 * S / 16 + g slots) fall on 16 distinct bank slots (S / 16 = 2 mod 4)
+  g.S1 = p.pw1.k_pad + 32;
+  g.S2 = p.has_pw2 ? p.pw2.k_pad + 32 : 0;
   g.T1 = (N1 + 15) / 16;
   g.T2 = (N2 + 15) / 16;
   g.patch_ru = g.PW * C / 16;
+  // patch pixel (py, px) keeps its 16-byte chunk c at chunk c ^ f, f = (3 py +
+  // px) & (C/16 - 1): the 16 pixels x taps a ds_read_b128 lane group reads
+  // then spread over the bank slots (C = 128: 656 -> 48 modelled extra LDS
+  // cycles per wave, tools/lds_bank_model.py); the DMA applies it on the
+  // source side, as it writes LDS lane-linearly
+  const int m = C / 16;
+  g.pmask = (m & (m - 1)) == 0 ? m - 1 : 0;
+  g.plog = 0;
+  while (g.pmask && (1 << g.plog) < m) ++g.plog;
   g.res_ru4 = p.pw1.residual ? TW * N1 / 4 : 0;
   g.u_patch = g.PH * g.patch_ru;
   const int rows = TH * TW;
@@ -211,7 +234,9 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
   const int o = u * 4;
   auto swz_word = [](const bh_conv_params& c, int rel) {  // LDS-image byte offset -> source word
     const int row = rel / c.k_pad, col = rel - row * c.k_pad;
-    return (const uint32_t*)(c.weights + (long)row * c.k_pad + 16 * swz(row, col >> 4) + (col & 15));
+    // the word at LDS chunk col >> 4 holds source chunk swz(row, col >> 4, R)
+    // (an XOR: its own inverse)
+    return (const uint32_t*)(c.weights + (long)row * c.k_pad + 16 * swz(row, col >> 4, c.k_pad >> 4) + (col & 15));
   };
   uint32_t v;
   if (o < B.b1) v = *swz_word(p.pw1, o - B.w1);
@@ -284,7 +309,9 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       if (u < G.u_patch) {
         const int r = dv.patch_ru.div(u);
         const int y = min(max(y0 + r, 0), d.in_h - 1);
-        long off = (row0 + y) * d.in_w * C + xoff + (u - r * G.patch_ru) * 16;
+        const int q = u - r * G.patch_ru;  // unit within the patch row: pixel q >> plog, chunk q & pmask
+        const int f = (3 * r + (q >> G.plog)) & G.pmask;
+        long off = (row0 + y) * d.in_w * C + xoff + (q ^ f) * 16;
         off = off < 0 ? 0 : (off > in_last ? in_last : off);
         dma16(in + off, buf + base * 16);
       }
@@ -333,6 +360,10 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   unsigned char* o1 = smem + G.off_o1;
   const int pb = wave;               // this wave's 16-pixel block of the tile
   const int orow = pb * 16 + 4 * g;  // first of this lane's 4 result rows
+  // after quad_transpose8 the lane stores 4 channels (wcol .. wcol + 3 of a
+  // 16-channel tile) of one pixel row
+  const int wrow = orow + (r16 & 3);
+  const int wcol = r16 & ~3;
 
   for (int it = 0; it < t_count; ++it) {
   unsigned char* cur = smem + (PIPE ? (it & 1) * G.buf_bytes : 0);
@@ -355,7 +386,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
     const int p = pb * 16 + r16;     // this lane's pixel as an A-operand row
     const int ti = p / TW, tj = p % TW;
     const int oy = oy0 + ti, ox = ox0 + tj;
-    int off[3], tapc[3];
+    int off[3], tapc[3], pf[3];
     bool ok[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
@@ -366,6 +397,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       const int y = oy * d.stride_h - d.pad_h + fy * d.dil_h, x = ox * d.stride_w - d.pad_w + fx * d.dil_w;
       ok[s] = tap < 9 && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
       off[s] = tap < 9 ? (py * G.PW + px) * C : 0;  // always a valid patch address
+      pf[s] = tap < 9 ? (3 * py + px) & G.pmask : 0;
       tapc[s] = (tap < 9 ? tap : 0) * C + r16;
     }
     const int zfill = (int)splat_byte(d.in_zp);
@@ -376,7 +408,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       const int c0 = cg * 16;
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
-        const v4i v = *(const v4i*)(patch + off[s] + c0);
+        const v4i v = *(const v4i*)(patch + off[s] + ((cg ^ pf[s]) << 4));
         xf[s] = ok[s] ? v : (v4i){zfill, zfill, zfill, zfill};
         uint32_t wb = (uint32_t)dww[tapc[s] + c0];
         if (s == 2) wb &= tap8;
@@ -392,10 +424,10 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
 #pragma unroll
       for (int s = 0; s < 3; ++s) acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf[s], wf[s], acc, 0, 0, 0);
       const ChanQ q = chan_q(mu, sh, d.out_zp);
-      const int c = cg * 16 + r16;
+      int32_t v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        dl[(orow + r) * G.S1 + c] = (unsigned char)requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
+      for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
+      *(uint32_t*)(dl + wrow * G.S1 + cg * 16 + wcol) = quad_transpose8(pack4_bytes(v));
     };
     // two channel groups per iteration: both items' LDS reads issue first
     int cg = 0;
@@ -421,6 +453,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   {
     const int N1 = a.out_c;
     const int KS1 = a.k_pad >> 6;
+    const int R1 = a.k_pad >> 4;
     const unsigned char* W1 = cb + G.blob.w1;
     const int* b1 = (const int*)(cb + G.blob.b1);
     const int* m1 = (const int*)(cb + G.blob.m1);
@@ -442,11 +475,10 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
                            a.add_act_min, a.add_act_max);
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (out1) o1[(orow + r) * N1 + nch] = (unsigned char)v[r];
-        if (cp.has_pw2) pl[(orow + r) * G.S2 + nch] = (unsigned char)v[r];
-      }
+      const uint32_t pk = quad_transpose8(pack4_bytes(v));
+      const int c4 = nch - r16 + wcol;  // the quad's first channel
+      if (out1) *(uint32_t*)(o1 + wrow * N1 + c4) = pk;
+      if (cp.has_pw2) *(uint32_t*)(pl + wrow * G.S2 + c4) = pk;
     };
     // two channel tiles per iteration (their LDS reads issue together)
     for (int t = 0; t < G.T1; t += 2) {
@@ -458,8 +490,8 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       v4i acca = (v4i){ba, ba, ba, ba}, accb = (v4i){bb, bb, bb, bb};
       for (int k = 0; k < KS1; ++k) {
         const v4i xv = *(const v4i*)(xrow + k * 64);
-        const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g));
-        const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g));
+        const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g, R1));
+        const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g, R1));
         acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, w0, acca, 0, 0, 0);
         accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, w1, accb, 0, 0, 0);
       }
@@ -476,6 +508,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   {
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
+    const int R2 = b.k_pad >> 4;
     const unsigned char* W2 = cb + G.blob.w2;
     const int* b2 = (const int*)(cb + G.blob.b2);
     const int* m2 = (const int*)(cb + G.blob.m2);
@@ -487,9 +520,10 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
     auto epi = [&](int nch, v4i acc) {
       if (nch >= N2) return;
       const ChanQ q = chan_q(m2[nch], s2[nch], b.out_zp);
+      int32_t v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        ol[(orow + r) * N2 + nch] = (unsigned char)requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+      for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+      *(uint32_t*)(ol + wrow * N2 + nch - r16 + wcol) = quad_transpose8(pack4_bytes(v));
     };
     for (int t = 0; t < G.T2; t += 2) {
       const bool two = t + 1 < G.T2;
@@ -501,8 +535,8 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
 #pragma unroll
       for (int k = 0; k < KX; ++k)
         if (k < KS2) {
-          const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g));
-          const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g));
+          const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g, R2));
+          const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g, R2));
           acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], w0, acca, 0, 0, 0);
           accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], w1, accb, 0, 0, 0);
         }

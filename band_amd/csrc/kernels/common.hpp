@@ -90,6 +90,29 @@ __device__ __forceinline__ uint32_t splat_byte(int32_t v) {
   return ((uint32_t)v & 0xffu) * 0x01010101u;
 }
 
+// bytes 0 of v0..v3 -> one dword
+__device__ __forceinline__ uint32_t pack4_bytes(const int32_t v[4]) {
+  const uint32_t lo = __builtin_amdgcn_perm((uint32_t)v[1], (uint32_t)v[0], 0x0c0c0400u);
+  const uint32_t hi = __builtin_amdgcn_perm((uint32_t)v[3], (uint32_t)v[2], 0x04000c0cu);
+  return lo | hi;
+}
+
+// 4x4 byte transpose across the 4 lanes of a quad (lanes 4q .. 4q+3): lane
+// i holds [a_i0 a_i1 a_i2 a_i3] (byte k = a_ik) and gets [a_0i a_1i a_2i
+// a_3i].  Two DPP quad permutes and two v_perm_b32.  An MFMA lane (r16, g)
+// of the D = X W^T form holds 4 PIXELS of one channel; after the transpose
+// lane 4j+i holds 4 CHANNELS (4j..4j+3 of its 16) of pixel i, so the LDS
+// staging takes one ds_write_b32 per lane instead of four ds_write_b8 - and
+// byte stores of 4 lanes into one dword are 4 distinct addresses on a bank
+// (a 4-way conflict per store).  Every lane of the quad must be active.
+__device__ __forceinline__ uint32_t quad_transpose8(uint32_t p) {
+  const int i = (int)(threadIdx.x & 3);
+  const uint32_t x = (uint32_t)__builtin_amdgcn_mov_dpp((int)p, 0x4e, 0xf, 0xf, false);  // quad_perm [2,3,0,1]
+  const uint32_t n = __builtin_amdgcn_perm(x, p, (i & 2) ? 0x03020706u : 0x05040100u);
+  const uint32_t y = (uint32_t)__builtin_amdgcn_mov_dpp((int)n, 0xb1, 0xf, 0xf, false);  // quad_perm [1,0,3,2]
+  return __builtin_amdgcn_perm(y, n, (i & 1) ? 0x03070105u : 0x06020400u);
+}
+
 // Division by a runtime-invariant divisor for dividends < 2^31, by the
 // multiply-high method (Granlund & Montgomery): q = umulhi(n, m) >> s.
 // CDNA has no integer divide instruction - a plain `/` or `%` by a runtime

@@ -311,6 +311,11 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
   }
   const int prow = pb * 16 + r16;     // this lane's operand row
   const int orow = pb * 16 + 4 * g;   // first of this lane's 4 result rows
+  // after quad_transpose8 a lane stores 4 channels (wcol .. wcol + 3 of a
+  // 16-channel tile) of one pixel row: one ds_write_b32 instead of four
+  // ds_write_b8 (4 lanes' bytes in one dword are a 4-way bank conflict)
+  const int wq = r16 & 3;
+  const int wcol = r16 & ~3;
   // diagnostics (tools/tile_probe.py --raster): shader-clock stamps at the
   // phase boundaries, debug_stamps[8 * workgroup]
   unsigned long long* stamps =
@@ -378,10 +383,10 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
         acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(it.xf[s], wf, acc, 0, 0, 0);
       }
       const ChanQ q = chan_q(it.mu, it.sh, d.out_zp);
+      int32_t v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        dl[(orow + r) * S1 + cg * 16 + r16] =
-            (unsigned char)requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
+      for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
+      *(uint32_t*)(dl + (orow + wq) * S1 + cg * 16 + wcol) = quad_transpose8(pack4_bytes(v));
     };
     // DA channel groups per round: every item's loads (input taps, filter
     // bytes, epilogue operands) are issued before any item's MFMAs, so a
@@ -429,11 +434,10 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
                            a.add_act_max);
         }
       }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        if (out1) o1[(orow + r) * N1 + n] = (unsigned char)v[r];
-        if (cp.has_pw2) pl[(orow + r) * S2 + n] = (unsigned char)v[r];
-      }
+      const uint32_t pk = quad_transpose8(pack4_bytes(v));
+      const int c4 = n - r16 + wcol;  // the quad's first channel
+      if (out1) *(uint32_t*)(o1 + (orow + wq) * N1 + c4) = pk;
+      if (cp.has_pw2) *(uint32_t*)(pl + (orow + wq) * S2 + c4) = pk;
     };
     if (AM && KS1 <= KX) {
       gemm_xs4_nt<KX>(a, dl, S1, KS1, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
@@ -455,11 +459,10 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
                                a.add_act_min, a.add_act_max);
             }
           }
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            if (out1) o1[(rb + r) * N1 + n] = (unsigned char)v[r];
-            if (cp.has_pw2) pl[(rb + r) * S2 + n] = (unsigned char)v[r];
-          }
+          const uint32_t pk = quad_transpose8(pack4_bytes(v));
+          const int c4 = n - r16 + wcol;
+          if (out1) *(uint32_t*)(o1 + (rb + wq) * N1 + c4) = pk;
+          if (cp.has_pw2) *(uint32_t*)(pl + (rb + wq) * S2 + c4) = pk;
         }
       });
     } else if (KS1 <= KX) {
@@ -490,19 +493,21 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
         if (n >= N2) return;
         const ChanQ q = chan_q(mu, sh, b.out_zp);
 #pragma unroll
-        for (int pb4 = 0; pb4 < 4; ++pb4)
+        for (int pb4 = 0; pb4 < 4; ++pb4) {
+          int32_t v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            dl[(pb4 * 16 + 4 * g + r) * N2 + n] =
-                (unsigned char)requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
+          for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
+          *(uint32_t*)(dl + (pb4 * 16 + 4 * g + wq) * N2 + n - r16 + wcol) = quad_transpose8(pack4_bytes(v));
+        }
       });
     } else {
       gemm_xs_nt<KX, TTC>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
         if (n >= N2) return;
         const ChanQ q = chan_q(mu, sh, b.out_zp);
+        int32_t v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          dl[(orow + r) * N2 + n] = (unsigned char)requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+        for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+        *(uint32_t*)(dl + (orow + wq) * N2 + n - r16 + wcol) = quad_transpose8(pack4_bytes(v));
       });
     }
   }
@@ -523,8 +528,10 @@ struct ChainLds {
 static ChainLds chain_lds(const bh_chain_params& p) {
   ChainLds L;
   const int rows = p.px_blocks * 16;
-  L.S1 = p.pw1.k_pad + 16;
-  L.S2 = p.has_pw2 ? p.pw2.k_pad + 16 : 0;
+  // rows of k_pad + 32 bytes: a ds_read_b128 lane group's 16 rows land on
+  // 16 distinct bank slots (S / 16 = 2 mod 4; tools/lds_bank_model.py)
+  L.S1 = p.pw1.k_pad + 32;
+  L.S2 = p.has_pw2 ? p.pw2.k_pad + 32 : 0;
   const int dl_row = std::max(L.S1, p.has_pw2 ? (p.pw2.out_c + 15) / 16 * 16 : 0);
   L.off_pl = rows * dl_row;
   L.off_o1 = L.off_pl + rows * L.S2;

@@ -1,0 +1,106 @@
+#!/usr/bin/env python3
+"""LDS bank-conflict model of chain_tile_kernel's accesses (kernels/chain_tile.hip).
+
+Rules (MI355X_MICROARCH.md §LDS): ds_read_b128 serves a wave in four 16-lane
+groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}, +32), bank = (a/4) mod 64;
+stores serve two 32-lane halves, bank = (a/4) mod 32; every extra distinct
+address on a busy bank adds one LDS cycle.  Byte stores of several lanes into
+one dword count as distinct addresses (the model reproduces the measured
+SQ_LDS_BANK_CONFLICT of profiles/r03ba_stall.txt within 7 %: 508 vs 474
+cycles per wave for the 112x112 C=32 -> 16 -> 96 chain).
+
+Prints the modelled extra cycles per wave by access for the layout before
+round 4 (byte stores, rows of k_pad + 16, XOR (row >> 2) & 3) and after it
+(quad-transposed dword stores, rows of k_pad + 32, stride-aware XOR,
+patch chunks XORed with (3 py + px) & (C/16 - 1)).
+Usage: python tools/lds_bank_model.py [C N1 N2]
+"""
+import sys
+from collections import Counter
+
+G128 = [[*range(0, 4), *range(12, 16), *range(20, 28)], [*range(4, 12), *range(16, 20), *range(28, 32)],
+        [*range(32, 36), *range(44, 48), *range(52, 60)], [*range(36, 44), *range(48, 52), *range(60, 64)]]
+
+
+def extra_b128(addrs):
+    ex = 0
+    for grp in G128:
+        banks = {}
+        for l in grp:
+            for d in range(4):
+                w = addrs[l] // 4 + d
+                banks.setdefault(w % 64, set()).add(w)
+        ex += max(len(v) for v in banks.values()) - 1
+    return ex
+
+
+def extra_store(addrs):
+    ex = 0
+    for half in (range(32), range(32, 64)):
+        banks = {}
+        for l in half:
+            banks.setdefault((addrs[l] // 4) % 32, set()).add(addrs[l])
+        ex += max(len(v) for v in banks.values()) - 1
+    return ex
+
+
+def swz_old(row, c, R):
+    return (c & ~3) | ((c & 3) ^ ((row >> 2) & 3))
+
+
+def swz_new(row, c, R):
+    s = (row & 15) if R % 16 == 0 else ((row & 7) if R % 16 == 8 else ((row >> 2) & 2))
+    return c ^ s
+
+
+def model(C, N1, N2, new, TW=8, PW=10):
+    kp1 = (C + 63) // 64 * 64
+    kp2 = (N1 + 63) // 64 * 64
+    S1, S2 = (kp1 + 32, kp2 + 32) if new else (kp1 + 16, kp2 + 16)
+    swz = swz_new if new else swz_old
+    lanes = [(l & 15, l >> 4) for l in range(64)]
+    tot = Counter()
+
+    def store(name, addr):  # addr(row within the 16-pixel block, channel offset in the tile)
+        if new:  # quad_transpose8: lane 4j+i stores 4 channels of pixel row 4g+i
+            tot[name] += extra_store([addr(4 * g + (r16 & 3), r16 & ~3) for r16, g in lanes])
+        else:
+            for r in range(4):
+                tot[name] += extra_store([addr(4 * g + r, r16) for r16, g in lanes])
+
+    for pb in range(4):
+        for cg in range(C // 16):
+            for s in range(3):
+                addrs = []
+                for r16, g in lanes:
+                    p = pb * 16 + r16
+                    tap = 4 * s + g if 4 * s + g < 9 else 0
+                    py, px = p // TW + tap // 3, p % TW + tap % 3
+                    m = C // 16
+                    f = (3 * py + px) & (m - 1) if new and m & (m - 1) == 0 else 0
+                    addrs.append((py * PW + px) * C + (cg ^ f) * 16)
+                tot["A patch read"] += extra_b128(addrs)
+            store("A dw store", lambda row, col: (pb * 16 + row) * S1 + cg * 16 + col)
+        for t in range((N1 + 15) // 16):
+            for k in range(kp1 // 64):
+                tot["B x read"] += extra_b128([(pb * 16 + r16) * S1 + g * 16 + k * 64 for r16, g in lanes])
+                tot["B w read"] += extra_b128([(t * 16 + r16) * kp1 + 16 * swz(t * 16 + r16, 4 * k + g, kp1 // 16)
+                                               for r16, g in lanes])
+            store("B o1 store", lambda row, col: (pb * 16 + row) * N1 + t * 16 + col)
+            store("B pl store", lambda row, col: (pb * 16 + row) * S2 + t * 16 + col)
+        for k in range(kp2 // 64):
+            tot["C x read"] += extra_b128([(pb * 16 + r16) * S2 + g * 16 + k * 64 for r16, g in lanes])
+        for t in range((N2 + 15) // 16):
+            for k in range(kp2 // 64):
+                tot["C w read"] += extra_b128([(t * 16 + r16) * kp2 + 16 * swz(t * 16 + r16, 4 * k + g, kp2 // 16)
+                                               for r16, g in lanes])
+            store("C out store", lambda row, col: (pb * 16 + row) * N2 + t * 16 + col)
+    return {k: v / 4 for k, v in tot.items()}  # per wave (a workgroup is 4 waves, one pixel block each)
+
+
+if __name__ == "__main__":
+    C, N1, N2 = (int(x) for x in sys.argv[1:4]) if len(sys.argv) > 3 else (32, 16, 96)
+    for new in (False, True):
+        m = model(C, N1, N2, new)
+        print("%-6s %6.1f extra LDS cycles/wave  %s" % ("round4" if new else "before", sum(m.values()),
+                                                        {k: v for k, v in m.items() if v}))

@@ -360,10 +360,6 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   unsigned char* o1 = smem + G.off_o1;
   const int pb = wave;               // this wave's 16-pixel block of the tile
   const int orow = pb * 16 + 4 * g;  // first of this lane's 4 result rows
-  // after quad_transpose8 the lane stores 4 channels (wcol .. wcol + 3 of a
-  // 16-channel tile) of one pixel row
-  const int wrow = orow + (r16 & 3);
-  const int wcol = r16 & ~3;
 
   for (int it = 0; it < t_count; ++it) {
   unsigned char* cur = smem + (PIPE ? (it & 1) * G.buf_bytes : 0);
@@ -427,7 +423,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       int32_t v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
-      *(uint32_t*)(dl + wrow * G.S1 + cg * 16 + wcol) = quad_transpose8(pack4_bytes(v));
+      stage4(dl, G.S1, orow, cg * 16 + r16, v);  // one ds_write_b32 per lane (common.hpp)
     };
     // two channel groups per iteration: both items' LDS reads issue first
     int cg = 0;
@@ -475,10 +471,8 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
                            a.add_act_min, a.add_act_max);
         }
       }
-      const uint32_t pk = quad_transpose8(pack4_bytes(v));
-      const int c4 = nch - r16 + wcol;  // the quad's first channel
-      if (out1) *(uint32_t*)(o1 + wrow * N1 + c4) = pk;
-      if (cp.has_pw2) *(uint32_t*)(pl + wrow * G.S2 + c4) = pk;
+      if (out1) stage4(o1, N1, orow, nch, v);
+      if (cp.has_pw2) stage4(pl, G.S2, orow, nch, v);
     };
     // two channel tiles per iteration (their LDS reads issue together)
     for (int t = 0; t < G.T1; t += 2) {
@@ -523,7 +517,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       int32_t v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
-      *(uint32_t*)(ol + wrow * N2 + nch - r16 + wcol) = quad_transpose8(pack4_bytes(v));
+      stage4(ol, N2, orow, nch, v);
     };
     for (int t = 0; t < G.T2; t += 2) {
       const bool two = t + 1 < G.T2;

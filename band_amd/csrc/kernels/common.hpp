@@ -113,6 +113,23 @@ __device__ __forceinline__ uint32_t quad_transpose8(uint32_t p) {
   return __builtin_amdgcn_perm(y, n, (i & 1) ? 0x03070105u : 0x06020400u);
 }
 
+// Stages a D = X W^T epilogue's 4 values (pixels row0 .. row0 + 3 of channel
+// `col`, this lane's r16 = col % 16) into an LDS tile of row stride `stride`:
+// quad-transposed, one dword per lane (BH_QUAD_STORE=1, default), or four
+// byte stores (0; build-time A-B switch).
+#ifndef BH_QUAD_STORE
+#define BH_QUAD_STORE 1
+#endif
+__device__ __forceinline__ void stage4(unsigned char* tile, int stride, int row0, int col, const int32_t v[4]) {
+#if BH_QUAD_STORE
+  const int r16 = col & 15;
+  *(uint32_t*)(tile + (row0 + (r16 & 3)) * stride + col - r16 + (r16 & ~3)) = quad_transpose8(pack4_bytes(v));
+#else
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[(row0 + r) * stride + col] = (unsigned char)v[r];
+#endif
+}
+
 // Division by a runtime-invariant divisor for dividends < 2^31, by the
 // multiply-high method (Granlund & Montgomery): q = umulhi(n, m) >> s.
 // CDNA has no integer divide instruction - a plain `/` or `%` by a runtime

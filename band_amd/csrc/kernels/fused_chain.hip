@@ -311,11 +311,6 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
   }
   const int prow = pb * 16 + r16;     // this lane's operand row
   const int orow = pb * 16 + 4 * g;   // first of this lane's 4 result rows
-  // after quad_transpose8 a lane stores 4 channels (wcol .. wcol + 3 of a
-  // 16-channel tile) of one pixel row: one ds_write_b32 instead of four
-  // ds_write_b8 (4 lanes' bytes in one dword are a 4-way bank conflict)
-  const int wq = r16 & 3;
-  const int wcol = r16 & ~3;
   // diagnostics (tools/tile_probe.py --raster): shader-clock stamps at the
   // phase boundaries, debug_stamps[8 * workgroup]
   unsigned long long* stamps =
@@ -386,7 +381,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
       int32_t v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, d.out_zp, d.act_min, d.act_max);
-      *(uint32_t*)(dl + (orow + wq) * S1 + cg * 16 + wcol) = quad_transpose8(pack4_bytes(v));
+      stage4(dl, S1, orow, cg * 16 + r16, v);  // one ds_write_b32 per lane (common.hpp)
     };
     // DA channel groups per round: every item's loads (input taps, filter
     // bytes, epilogue operands) are issued before any item's MFMAs, so a
@@ -434,10 +429,8 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
                            a.add_act_max);
         }
       }
-      const uint32_t pk = quad_transpose8(pack4_bytes(v));
-      const int c4 = n - r16 + wcol;  // the quad's first channel
-      if (out1) *(uint32_t*)(o1 + (orow + wq) * N1 + c4) = pk;
-      if (cp.has_pw2) *(uint32_t*)(pl + (orow + wq) * S2 + c4) = pk;
+      if (out1) stage4(o1, N1, orow, n, v);
+      if (cp.has_pw2) stage4(pl, S2, orow, n, v);
     };
     if (AM && KS1 <= KX) {
       gemm_xs4_nt<KX>(a, dl, S1, KS1, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
@@ -459,10 +452,8 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
                                a.add_act_min, a.add_act_max);
             }
           }
-          const uint32_t pk = quad_transpose8(pack4_bytes(v));
-          const int c4 = n - r16 + wcol;
-          if (out1) *(uint32_t*)(o1 + (rb + wq) * N1 + c4) = pk;
-          if (cp.has_pw2) *(uint32_t*)(pl + (rb + wq) * S2 + c4) = pk;
+          if (out1) stage4(o1, N1, rb, n, v);
+          if (cp.has_pw2) stage4(pl, S2, rb, n, v);
         }
       });
     } else if (KS1 <= KX) {
@@ -497,7 +488,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
           int32_t v[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
-          *(uint32_t*)(dl + (pb4 * 16 + 4 * g + wq) * N2 + n - r16 + wcol) = quad_transpose8(pack4_bytes(v));
+          stage4(dl, N2, pb4 * 16 + 4 * g, n, v);
         }
       });
     } else {
@@ -507,7 +498,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
         int32_t v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
-        *(uint32_t*)(dl + (orow + wq) * N2 + n - r16 + wcol) = quad_transpose8(pack4_bytes(v));
+        stage4(dl, N2, orow, n, v);
       });
     }
   }

@@ -11,6 +11,9 @@ cd "$R"
 export TMPDIR=/tmp
 O=gpurun_out
 mkdir -p "$O"
+# rocprofv3's pass directories go to a scratch dir (they exceed what a GPU
+# call copies back); only the summaries land in gpurun_out
+W=$(mktemp -d /tmp/stall_XXXX)
 timeout -s KILL 60 rocprofv3 -L > "$O/${TAG}_counters.txt" 2>&1 || true
 have() { grep -qw "$1" "$O/${TAG}_counters.txt"; }
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
@@ -24,12 +27,12 @@ n=0
 for P in "$P1" "$P2"; do
   n=$((n + 1))
   [ -z "$P" ] && continue
-  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$O/${TAG}_stall$n" -o run -- \
+  timeout -s KILL 150 rocprofv3 --pmc $P --kernel-trace --output-format csv -d "$W/${TAG}_stall$n" -o run -- \
     python3 bench.py --profile-only --no-graph > "$O/${TAG}_stall$n.log" 2>&1
   rc=$?
   echo "pass $n rc=$rc" >> "$O/${TAG}_stall_passes.txt"
   [ $rc -ne 0 ] && exit $rc
 done
-python3 tools/pmc_kernels.py --full "$O/${TAG}_stall1" "$O/${TAG}_stall2" > "$O/${TAG}_stall.txt"
-rm -rf "$O/${TAG}_stall1" "$O/${TAG}_stall2"
+python3 tools/pmc_kernels.py --full "$W/${TAG}_stall1" "$W/${TAG}_stall2" > "$O/${TAG}_stall.txt"
+rm -rf "$W"
 echo "stall $TAG done"

@@ -14,17 +14,18 @@ O=gpurun_out
 mkdir -p "$O"
 S="$O/${TAG}_trace_roofline.txt"
 : > "$S"
+W=$(mktemp -d /tmp/trace_XXXX)  # trace directories stay on the box
 n=0
 for TR in "--kernel-trace" "--kernel-trace --memory-copy-trace"; do
   n=$((n + 1))
-  timeout -k 10 400 rocprofv3 $TR --stats --output-format csv -d "$O/${TAG}_tr$n" -o run -- \
+  timeout -k 10 400 rocprofv3 $TR --stats --output-format csv -d "$W/${TAG}_tr$n" -o run -- \
     python3 bench.py --no-cpu-baseline --no-batch1 --steps 8 --warmup 2 \
     > "$O/${TAG}_tr$n.json" 2> "$O/${TAG}_tr$n.err"
   rc=$?
   echo "run $n ($TR, roofline stage on): rc=$rc" >> "$S"
   tail -5 "$O/${TAG}_tr$n.err" >> "$S"
-  cp "$O/${TAG}_tr$n/run_kernel_stats.csv" "$O/${TAG}_tr${n}_kernel_stats.csv" 2>/dev/null
-  rm -rf "$O/${TAG}_tr$n"
+  cp "$W/${TAG}_tr$n/run_kernel_stats.csv" "$O/${TAG}_tr${n}_kernel_stats.csv" 2>/dev/null
+  rm -rf "$W/${TAG}_tr$n"
   [ $rc -ne 0 ] && exit $rc
 done
 echo "trace_roofline $TAG done" >> "$S"

@@ -1286,7 +1286,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 5;
+constexpr int kChainTuneVersion = 6;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1589,9 +1589,11 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // (the persistent tile form, tile 2, measured slower than the
         // one-tile workgroups on every MobileNetV2 chain,
         // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
-        const int forms[10][5] = {{4, 4, 0, 0, 0}, {2, 4, 0, 0, 0}, {1, 4, 0, 0, 0}, {1, 8, 0, 0, 0},
-                                  {1, 16, 0, 0, 0}, {4, 4, 1, 0, 0}, {4, 4, 0, 1, 0}, {2, 4, 0, 0, 1},
-                                  {1, 4, 0, 0, 1}, {1, 8, 0, 0, 1}};
+        // {.., tile 3 / 4}: runs of 2 / 4 tiles per workgroup, the constant
+        // block staged once per run
+        const int forms[12][5] = {{4, 4, 0, 0, 0}, {2, 4, 0, 0, 0}, {1, 4, 0, 0, 0}, {1, 8, 0, 0, 0},
+                                  {1, 16, 0, 0, 0}, {4, 4, 1, 0, 0}, {4, 4, 0, 1, 0}, {4, 4, 0, 3, 0},
+                                  {4, 4, 0, 4, 0}, {2, 4, 0, 0, 1}, {1, 4, 0, 0, 1}, {1, 8, 0, 0, 1}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
@@ -1613,7 +1615,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) + (pw[4] ? 1000 : 0);
+                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
+                       (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0);
             }
           }
         }
@@ -1627,7 +1630,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
-    // form, +500 for the persistent tile form, +1000 for the deep-issue form
+    // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
+    // tiles, +1000 for the deep-issue form
     const int deep = choice >= 1000 ? 1 : 0;
     choice %= 1000;
     const bool three = choice > 0 && choice % 100 < 10;
@@ -1642,7 +1646,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.px_blocks = choice % 10;
     F.chain.waves = choice >= 300 && choice < 400 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
-    F.chain.tile = choice >= 400 && choice < 500 ? 1 : (choice >= 500 && choice < 600 ? 2 : 0);
+    F.chain.tile = choice >= 400 && choice < 800 ? choice / 100 - 3 : 0;
     F.chain.deep = deep;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then

@@ -69,10 +69,10 @@ __device__ __forceinline__ void dma4(const void* src, unsigned char* lds_lane0) 
 // mod 16 in 2 and R = 0 mod 16 in 1, and the XOR with (r16 >> 2) & 2, r16 & 7
 // or r16 & 15 (within an aligned block of 4, 8 or 16 chunks, so inside the
 // row) separates the lanes a class holds (tools/lds_bank_model.py).
-__device__ __host__ __forceinline__ int swz(int row, int c, int R) {
-  const int s = (R & 15) == 0 ? (row & 15) : ((R & 15) == 8 ? (row & 7) : ((row >> 2) & 2));
-  return c ^ s;
+__device__ __host__ __forceinline__ int swz_mask(int row, int R) {
+  return (R & 15) == 0 ? (row & 15) : ((R & 15) == 8 ? (row & 7) : ((row >> 2) & 2));
 }
+__device__ __host__ __forceinline__ int swz(int row, int c, int R) { return c ^ swz_mask(row, R); }
 }  // namespace
 
 // The packed constant block (byte offsets, all multiples of 16):
@@ -258,7 +258,13 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
 // the constant block staged once, and each tile's patch + residual DMA is
 // issued into the other buffer before the current tile's phases run, so it
 // lands under their compute (bh_chain_params.tile == 2)
-template <int TH, int TW, bool FAST, int KX, bool PIPE>
+//
+// PIPE == 2: the sequential multi-tile form (bh_chain_params.tile == 3) - a
+// workgroup walks dv.per consecutive tiles through ONE patch buffer: the
+// constant block is staged once per workgroup instead of once per tile (for
+// the 112x112 x 32 chain it is 9.2 KB against a 3.2 KB patch), and each
+// further tile's patch is DMA'd after the previous tile is done
+template <int TH, int TW, bool FAST, int KX, int PIPE>
 __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv) {
   static_assert(TH * TW == 64, "4 pixel blocks of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -362,7 +368,13 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   const int orow = pb * 16 + 4 * g;  // first of this lane's 4 result rows
 
   for (int it = 0; it < t_count; ++it) {
-  unsigned char* cur = smem + (PIPE ? (it & 1) * G.buf_bytes : 0);
+  if (PIPE == 2 && it > 0) {
+    __syncthreads();  // every read of the previous tile's patch / staging is done
+    issue_tile(t_first + it, smem);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  unsigned char* cur = smem + (PIPE == 1 ? (it & 1) * G.buf_bytes : 0);
   const unsigned char* patch = cur;
   const unsigned char* resl = cur + G.off_res;
   // the second 1x1's staging: the current patch (dead after phase A) when it fits
@@ -370,7 +382,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   int n, oy0, ox0;
   tile_xy(t_first + it, n, oy0, ox0);
   // the next tile's patch + residual into the other buffer, under this one's phases
-  if (PIPE && it + 1 < t_count) issue_tile(t_first + it + 1, smem + ((it + 1) & 1) * G.buf_bytes);
+  if (PIPE == 1 && it + 1 < t_count) issue_tile(t_first + it + 1, smem + ((it + 1) & 1) * G.buf_bytes);
 
   // ---- phase A: depthwise 3x3 from the patch -> dl ------------------------
   {
@@ -449,7 +461,9 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   {
     const int N1 = a.out_c;
     const int KS1 = a.k_pad >> 6;
-    const int R1 = a.k_pad >> 4;
+    // the XOR depends on the row only through r16 (rows 16t + r16): one mask
+    // per lane for the whole phase
+    const int sx1 = swz_mask(r16, a.k_pad >> 4);
     const unsigned char* W1 = cb + G.blob.w1;
     const int* b1 = (const int*)(cb + G.blob.b1);
     const int* m1 = (const int*)(cb + G.blob.m1);
@@ -484,8 +498,8 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       v4i acca = (v4i){ba, ba, ba, ba}, accb = (v4i){bb, bb, bb, bb};
       for (int k = 0; k < KS1; ++k) {
         const v4i xv = *(const v4i*)(xrow + k * 64);
-        const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g, R1));
-        const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g, R1));
+        const v4i w0 = *(const v4i*)(wa + 16 * ((4 * k + g) ^ sx1));
+        const v4i w1 = *(const v4i*)(wb + 16 * ((4 * k + g) ^ sx1));
         acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, w0, acca, 0, 0, 0);
         accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(xv, w1, accb, 0, 0, 0);
       }
@@ -502,7 +516,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   {
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
-    const int R2 = b.k_pad >> 4;
+    const int sx2 = swz_mask(r16, b.k_pad >> 4);
     const unsigned char* W2 = cb + G.blob.w2;
     const int* b2 = (const int*)(cb + G.blob.b2);
     const int* m2 = (const int*)(cb + G.blob.m2);
@@ -529,8 +543,8 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
 #pragma unroll
       for (int k = 0; k < KX; ++k)
         if (k < KS2) {
-          const v4i w0 = *(const v4i*)(wa + 16 * swz(ra, 4 * k + g, R2));
-          const v4i w1 = *(const v4i*)(wb + 16 * swz(rb, 4 * k + g, R2));
+          const v4i w0 = *(const v4i*)(wa + 16 * ((4 * k + g) ^ sx2));
+          const v4i w1 = *(const v4i*)(wb + 16 * ((4 * k + g) ^ sx2));
           acca = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], w0, acca, 0, 0, 0);
           accb = __builtin_amdgcn_mfma_i32_16x16x64_i8(x[k], w1, accb, 0, 0, 0);
         }
@@ -543,7 +557,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   tile_copy_out(ol, (uint8_t*)b.output, b.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256);
   TILE_STAMP(6)
   }  // has_pw2
-  if (PIPE && it + 1 < t_count) {
+  if (PIPE == 1 && it + 1 < t_count) {
     // the next tile's DMA has landed (this wave's part; the barrier covers
     // every wave's), and every read of this tile's buffers is done
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -553,7 +567,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
 #undef TILE_STAMP
 }
 
-template <int TH, int TW, bool FAST, int KX, bool PIPE>
+template <int TH, int TW, bool FAST, int KX, int PIPE>
 static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s) {
   static thread_local int opted_device = -1;
   int dev = 0;
@@ -571,7 +585,11 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
   dv.ntiles = p.dw.batch * G.tiles_y * G.tiles_x;
   dv.per = 1;
   int blocks = dv.ntiles;
-  if (PIPE) {
+  if (PIPE == 2) {
+    // bh_chain_params.tile 3 / 4: runs of 2 / 4 consecutive tiles
+    dv.per = p.tile == 4 ? 4 : 2;
+    blocks = (dv.ntiles + dv.per - 1) / dv.per;
+  } else if (PIPE) {
     // one wave of resident workgroups (LDS and registers permitting, <= 4 per
     // CU on 256 CUs), each taking a run of consecutive tiles
     static thread_local size_t cached_lds = 0;
@@ -599,7 +617,9 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
 extern "C" size_t bh_chain_tile_lds_bytes(const bh_chain_params* pp) {
   const bh_chain_params& p = *pp;
   const bh_dwconv_params& d = p.dw;
-  if (p.tile != 1 && p.tile != 2) return 0;  // 2: the persistent pipelined form
+  // 2: the persistent pipelined form; 3 / 4: runs of 2 / 4 tiles per
+  // workgroup through one buffer
+  if (p.tile < 1 || p.tile > 4) return 0;
   if (d.stride_h < 1 || d.stride_h > 2 || d.stride_w < 1 || d.stride_w > 2 || d.dil_h < 1 || d.dil_h > 2 ||
       d.dil_w < 1 || d.dil_w > 2)
     return 0;
@@ -652,9 +672,11 @@ extern "C" int bh_chain_tile_launch(const bh_chain_params* pp, bh_stream_t strea
     else bh::launch_tile<8, 8, false, 5, PIPE>(p, G, s);               \
   }
   if (pipe) {
-    BH_TILE(true)
+    BH_TILE(1)
+  } else if (p.tile >= 3) {
+    BH_TILE(2)
   } else {
-    BH_TILE(false)
+    BH_TILE(0)
   }
 #undef BH_TILE
   return bh_check_launch("chain_tile_kernel");

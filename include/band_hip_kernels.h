@@ -375,7 +375,8 @@ typedef struct bh_chain_params {
    * persist are ignored.  2: the same tile in a persistent workgroup that
    * walks a run of consecutive tiles, the constant block staged once and
    * each tile's patch + residual DMA issued into a second buffer under the
-   * previous tile's phases */
+   * previous tile's phases.  3 / 4: runs of 2 / 4 consecutive tiles per
+   * workgroup through ONE buffer (the constant block staged once per run) */
   int tile;
   /* tile form: the chain's constant block (both 1x1 filters swizzled for
    * LDS, every table, the depthwise filter) built once by

@@ -96,10 +96,13 @@ def test_chain_tile_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
             continue
         pipe = _tile_fits(c, gpu_lib, 2)  # persistent, double-buffered: two patches in LDS
         _check(c, gpu_lib, 4, tile=1)
+        _check(c, gpu_lib, 4, tile=3)  # runs of 2 / 4 tiles through one buffer
+        _check(c, gpu_lib, 4, tile=4)
         if pipe:
             _check(c, gpu_lib, 4, tile=2)
         c.fast = False
         _check(c, gpu_lib, 4, tile=1)
+        _check(c, gpu_lib, 4, tile=4)
         if pipe:
             _check(c, gpu_lib, 4, tile=2)
 
@@ -123,6 +126,8 @@ def test_chain_tile_general(gpu_lib, args):
     c = ChainCase(rng, **args)
     assert _tile_fits(c, gpu_lib)
     _check(c, gpu_lib, 4, tile=1)
+    _check(c, gpu_lib, 4, tile=3)
+    _check(c, gpu_lib, 4, tile=4)
     if _tile_fits(c, gpu_lib, 2):
         _check(c, gpu_lib, 4, tile=2)
 
@@ -133,7 +138,7 @@ def test_chain_tile_rejects(gpu_lib):
     keep = []
     c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep, tile=1)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
-    c.tile = 3  # no such form (2 is the persistent tile form)
+    c.tile = 5  # no such form (2: persistent, 3 / 4: runs of tiles)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
     assert gpu_lib.bh_chain_i8(ctypes.byref(c), None) != 0
     c.tile = 1

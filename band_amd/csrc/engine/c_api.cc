@@ -5,6 +5,7 @@
 #include <unordered_map>
 #include "band_c_api.h"
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstring>
@@ -437,7 +438,8 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // results out (DeepLab's are 1 MB), each into output tensors of its own.
   int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
-  lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
+  // one submitter lane per shard of the models (below), so at most one per model
+  lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight, n_models}));
   // requests of one model submitted per RequestAsync call (closed loop:
   // the job -> model order is run-major, `burst` jobs per model in turn)
   int burst = burst_hint > 0 ? burst_hint : 1;
@@ -448,6 +450,7 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   int readers = 6;
   if (const char* rv = std::getenv("BANDX_DRIVER_READERS")) readers = std::max(1, std::atoi(rv));
   readers = std::max(1, std::min(readers, n_jobs > 0 ? n_jobs : 1));
+  readers = std::max(readers, lanes);  // every shard has a reader
   std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> reader_outs(readers);
   std::vector<std::vector<band::Tensors>> reader_out_ptrs(readers);
   for (int r = 0; r < readers; ++r) {
@@ -466,103 +469,128 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
     int index, model;
     int64_t arrival;  // open loop: scheduled arrival (NowMicros clock)
     long seq;         // submission number within its model
-    long gseq;        // submission number over all models
   };
-  std::mutex mu;
-  // readers wait on cv_read (a finished request, or the end), submitters on
-  // cv_sub (a retired request): each event wakes only the side it concerns
-  std::condition_variable cv_read, cv_sub;
-  std::unordered_map<band::JobId, Pending> pending;  // submitted, not yet read
-  // finished, ready to read, with the finished-job record taken in the
-  // end-of-request callback: the planner keeps only the last 1000 records
-  // (band/planner.h kNumFinishedRecords), and with many requests in flight a
-  // slow one can fall out of that window before a reader gets to it
-  std::deque<std::pair<band::JobId, band::Job>> done;
-  std::unordered_map<band::JobId, band::Job> early;  // finished before its submitter recorded it
-  int inflight = 0, retired = 0, taken = 0;
-  // stats (under mu): time integrals of the requests inside the engine
-  // (submitted, end-of-request not yet seen) and of the finished ones waiting
-  // for a reader; submitter wait / call and reader busy / idle time
-  int in_engine = 0;
-  double int_engine = 0, int_done = 0, submit_wait = 0, submit_call = 0, read_busy = 0, read_idle = 0;
-  int64_t last_tick = band::time::NowMicros();
-  auto tick = [&] {  // under mu, before in_engine or done changes
-    const int64_t now = band::time::NowMicros();
-    int_engine += double(in_engine) * double(now - last_tick);
-    int_done += double(done.size()) * double(now - last_tick);
-    last_tick = now;
+  // The driver's state is sharded by model: submitter lane l owns the models
+  // of shard l (and readers r = l, l + lanes, ...), with its own lock and
+  // condition variables, so lanes never contend with each other; with one
+  // lane (the default) it is a single shard.  A request's finished-job record
+  // arrives with the group end-of-request callback (Engine::SetOnEndRequests),
+  // so no request depends on the planner's 1000-record window.
+  struct Shard {
+    std::mutex mu;
+    // readers wait on cv_read (a finished request, or the end), submitters on
+    // cv_sub (a retired request): each event wakes only the side it concerns
+    std::condition_variable cv_read, cv_sub;
+    std::unordered_map<band::JobId, Pending> pending;  // submitted, not yet read
+    std::deque<std::pair<band::JobId, band::Job>> done;  // finished, with their records
+    std::unordered_map<band::JobId, band::Job> early;  // finished before the submitter recorded it
+    int inflight = 0, taken = 0, n_jobs = 0, max_inflight = 1, readers = 0;
+    // stats (under mu): time integrals of the requests inside the engine
+    // (submitted, end-of-request not yet seen) and of the finished ones
+    // waiting for a reader; submitter wait / call and reader busy / idle time
+    int in_engine = 0;
+    double int_engine = 0, int_done = 0, submit_wait = 0, submit_call = 0, read_busy = 0, read_idle = 0;
+    int64_t last_tick = band::time::NowMicros();
+    void tick() {  // under mu, before in_engine or done changes
+      const int64_t now = band::time::NowMicros();
+      int_engine += double(in_engine) * double(now - last_tick);
+      int_done += double(done.size()) * double(now - last_tick);
+      last_tick = now;
+    }
   };
-  std::vector<int> unread(n_models, 0), ring(n_models, 0);
+  const int n_shards = lanes;
+  std::vector<std::unique_ptr<Shard>> shards;
+  for (int i = 0; i < n_shards; ++i) shards.emplace_back(new Shard());
+  // a model's shard follows its engine id (a model listed twice shares one)
+  std::unordered_map<band::ModelId, int> shard_of_id;
+  std::vector<int> shard_of(n_models);
+  for (int m = 0; m < n_models; ++m) {
+    const band::ModelId id = models[m]->impl->GetId();
+    auto it = shard_of_id.emplace(id, m % n_shards).first;
+    shard_of[m] = it->second;
+  }
+  std::vector<int> models_in(n_shards, 0);
+  for (int m = 0; m < n_models; ++m) ++models_in[shard_of[m]];
+  for (int i = 0; i < n_shards; ++i)
+    shards[i]->max_inflight = std::max(1, (int)((long)max_inflight * std::max(1, models_in[i]) / n_models));
+  for (int r = 0; r < readers; ++r) ++shards[r % n_shards]->readers;
+  std::vector<int> unread(n_models, 0), ring(n_models, 0);  // under the model's shard lock
   for (int m = 0; m < n_models; ++m) ring[m] = std::max(1, e.RequestRingSize(models[m]->impl->GetId()));
   std::vector<long> next_seq(n_models, 0);
   std::vector<std::set<long>> unread_seq(n_models);
-  // requests submitted and not yet finished, by gseq: a request must finish
-  // fewer than the planner's record window of submissions after its own, or
-  // its finished-job record is gone before the callback can read it
-  std::set<long> unfinished;
-  long next_gseq = 0;
-  const long record_span = std::max(1, band::Planner::kNumFinishedRecords - lanes * burst);
-  bool failed = false;
+  std::atomic<bool> failed{false};
   // arrivals are drawn in job order (the open-loop schedule is one sequence)
   std::vector<std::pair<int64_t, int>> arrivals(n_jobs);
-  for (int j = 0; j < n_jobs; ++j) arrivals[j] = next_arrival(j, burst);
+  for (int j = 0; j < n_jobs; ++j) {
+    arrivals[j] = next_arrival(j, burst);
+    ++shards[shard_of[arrivals[j].second]]->n_jobs;
+  }
   // one call per group of finished requests (a batched pass ends up to its
-  // batch at once): one lock of mu and one wake-up per side for the group
+  // batch at once): one lock and one wake-up per side for the group
   const band::CallbackId cb = e.SetOnEndRequests([&](const std::vector<const band::Job*>& jobs) {
-    std::lock_guard<std::mutex> lk(mu);
-    tick();
-    int to_read = 0;
-    for (const band::Job* rec : jobs) {
-      --in_engine;
-      auto pit = pending.find(rec->job_id);
-      if (pit != pending.end()) {
-        unfinished.erase(pit->second.gseq);
-        done.emplace_back(rec->job_id, *rec);
-        ++to_read;
-      } else {
-        early.emplace(rec->job_id, *rec);
+    size_t i = 0;
+    while (i < jobs.size()) {
+      auto sit = shard_of_id.find(jobs[i]->model_id);
+      if (sit == shard_of_id.end()) {  // not a driver request
+        ++i;
+        continue;
       }
+      Shard& sh = *shards[sit->second];
+      std::lock_guard<std::mutex> lk(sh.mu);
+      sh.tick();
+      int to_read = 0;
+      for (; i < jobs.size(); ++i) {
+        auto nit = shard_of_id.find(jobs[i]->model_id);
+        if (nit == shard_of_id.end() || nit->second != sit->second) break;
+        const band::Job* rec = jobs[i];
+        --sh.in_engine;
+        if (sh.pending.count(rec->job_id)) {
+          sh.done.emplace_back(rec->job_id, *rec);
+          ++to_read;
+        } else {
+          sh.early.emplace(rec->job_id, *rec);
+        }
+      }
+      if (to_read == 0) continue;
+      if (to_read == 1) sh.cv_read.notify_one();
+      else sh.cv_read.notify_all();
     }
-    if (to_read == 0) return;
-    cv_sub.notify_all();
-    if (to_read == 1) cv_read.notify_one();
-    else cv_read.notify_all();
   });
-  auto retire = [&](const Pending& item, bool ok) {  // under mu
-    if (!ok && !failed) failed = true;
-    --inflight;
+  auto retire = [&](Shard& sh, const Pending& item, bool ok) {  // under sh.mu
+    if (!ok) failed = true;
+    --sh.inflight;
     --unread[item.model];
     unread_seq[item.model].erase(item.seq);
-    ++retired;
   };
   const int64_t t0 = band::time::NowMicros();
   std::vector<std::thread> threads;
   for (int r = 0; r < readers; ++r) {
     threads.emplace_back([&, r] {
       pthread_setname_np(pthread_self(), "bandx-reader");
+      Shard& sh = *shards[r % n_shards];
       while (true) {
         const int64_t w0 = band::time::NowMicros();
-        std::unique_lock<std::mutex> lk(mu);
-        cv_read.wait(lk, [&] { return !done.empty() || taken >= n_jobs; });
+        std::unique_lock<std::mutex> lk(sh.mu);
+        sh.cv_read.wait(lk, [&] { return !sh.done.empty() || sh.taken >= sh.n_jobs; });
         const int64_t w1 = band::time::NowMicros();
-        read_idle += double(w1 - w0);
-        if (done.empty()) break;
-        tick();
+        sh.read_idle += double(w1 - w0);
+        if (sh.done.empty()) break;
+        sh.tick();
         // a fair share of what is ready (at most 8): fewer lock round trips
         // when a batched pass finishes many requests at once
-        const size_t k = std::min<size_t>(8, (done.size() + readers - 1) / readers);
+        const size_t k = std::min<size_t>(8, (sh.done.size() + sh.readers - 1) / sh.readers);
         std::vector<std::pair<band::Job, Pending>> mine;
         mine.reserve(k);
         for (size_t q = 0; q < k; ++q) {
-          const band::JobId id = done.front().first;
-          auto pit = pending.find(id);
-          mine.emplace_back(std::move(done.front().second), pit->second);
+          const band::JobId id = sh.done.front().first;
+          auto pit = sh.pending.find(id);
+          mine.emplace_back(std::move(sh.done.front().second), pit->second);
           mine.back().first.job_id = mine.back().first.job_id == id ? id : -1;
-          pending.erase(pit);
-          done.pop_front();
-          if (++taken >= n_jobs) cv_read.notify_all();  // the other readers may leave
+          sh.pending.erase(pit);
+          sh.done.pop_front();
+          if (++sh.taken >= sh.n_jobs) sh.cv_read.notify_all();  // the other readers may leave
         }
-        if (!done.empty()) cv_read.notify_one();
+        if (!sh.done.empty()) sh.cv_read.notify_one();
         lk.unlock();
         std::vector<bool> oks(mine.size());
         for (size_t q = 0; q < mine.size(); ++q) {
@@ -581,9 +609,9 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
           if (model_index) model_index[item.index] = item.model;
         }
         lk.lock();
-        read_busy += double(band::time::NowMicros() - w1);
-        for (size_t q = 0; q < mine.size(); ++q) retire(mine[q].second, oks[q]);
-        cv_sub.notify_all();
+        sh.read_busy += double(band::time::NowMicros() - w1);
+        for (size_t q = 0; q < mine.size(); ++q) retire(sh, mine[q].second, oks[q]);
+        sh.cv_sub.notify_all();
       }
     });
   }
@@ -591,49 +619,48 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // vector RequestAsync (band/engine.cc:455-529, the overload Band's own
   // benchmark tool uses with batch_size >= 2), up to `burst` requests: one
   // ring allocation, one planner enqueue and one wake-up per run instead of
-  // per request.  Lane l takes runs l, l + lanes, ...
-  std::vector<std::pair<int, int>> runs;  // (first job, length)
+  // per request.  Lane l takes the runs of its shard's models, in order.
+  std::vector<std::vector<std::pair<int, int>>> runs(n_shards);  // (first job, length) per lane
   for (int j = 0; j < n_jobs;) {
     int k = j + 1;
     while (k < n_jobs && k - j < burst && arrivals[k].second == arrivals[j].second &&
            arrivals[k].first == arrivals[j].first)
       ++k;
-    runs.emplace_back(j, k - j);
+    runs[shard_of[arrivals[j].second]].emplace_back(j, k - j);
     j = k;
   }
   for (int l = 0; l < lanes; ++l) {
     threads.emplace_back([&, l] {
       pthread_setname_np(pthread_self(), "bandx-submit");
+      Shard& sh = *shards[l];
       std::vector<band::ModelId> ids;
       std::vector<band::RequestOption> opts;
       std::vector<band::Tensors> ins;
-      std::vector<long> seqs, gseqs;
-      for (size_t ri = l; ri < runs.size(); ri += lanes) {
-        const int j0 = runs[ri].first, r = runs[ri].second;
+      std::vector<long> seqs;
+      for (const auto& run : runs[l]) {
+        const int j0 = run.first, r = run.second;
         const auto& arrival = arrivals[j0];
         const int64_t now = band::time::NowMicros() - t0;
         if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
         const int m = arrival.second;
-        const long span = std::max(1, ring[m] - lanes * burst);
+        // one submitter per model: a run is < ring - burst submissions ahead
+        // of the model's oldest unread request, so its ring slots are free
+        const long span = std::max(1, ring[m] - burst);
         const int64_t w0 = band::time::NowMicros();
         seqs.clear();
-        gseqs.clear();
         {
-          std::unique_lock<std::mutex> lk(mu);
-          cv_sub.wait(lk, [&] {
-            return inflight + r <= max_inflight && unread[m] + r <= ring[m] &&
-                   (unread_seq[m].empty() || next_seq[m] + r - 1 - *unread_seq[m].begin() < span) &&
-                   (unfinished.empty() || next_gseq + r - 1 - *unfinished.begin() < record_span);
+          std::unique_lock<std::mutex> lk(sh.mu);
+          sh.cv_sub.wait(lk, [&] {
+            return sh.inflight + r <= std::max(sh.max_inflight, r) && unread[m] + r <= ring[m] &&
+                   (unread_seq[m].empty() || next_seq[m] + r - 1 - *unread_seq[m].begin() < span);
           });
-          inflight += r;
+          sh.inflight += r;
           unread[m] += r;
-          tick();
-          in_engine += r;
+          sh.tick();
+          sh.in_engine += r;
           for (int k = 0; k < r; ++k) {
             seqs.push_back(next_seq[m]++);
             unread_seq[m].insert(seqs.back());
-            gseqs.push_back(next_gseq++);
-            unfinished.insert(gseqs.back());
           }
         }
         const int64_t w1 = band::time::NowMicros();
@@ -642,41 +669,51 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         ins.assign(r, in_ptrs[m]);
         auto handles = e.RequestAsync(ids, opts, ins);
         const int64_t w2 = band::time::NowMicros();
-        std::lock_guard<std::mutex> lk(mu);
-        submit_wait += double(w1 - w0);
-        submit_call += double(w2 - w1);
+        std::lock_guard<std::mutex> lk(sh.mu);
+        sh.submit_wait += double(w1 - w0);
+        sh.submit_call += double(w2 - w1);
+        int to_read = 0;
         for (int k = 0; k < r; ++k) {
-          const Pending item{j0 + k, m, t0 + arrivals[j0 + k].first, seqs[k], gseqs[k]};
+          const Pending item{j0 + k, m, t0 + arrivals[j0 + k].first, seqs[k]};
           if (!handles.ok()) {
             if (k == 0)
               BAND_LOG(band::LogSeverity::kError, "request driver: submit of jobs %d..%d failed: %s", j0, j0 + r - 1,
                        std::string(handles.status().message()).c_str());
-            if (++taken >= n_jobs) cv_read.notify_all();
-            tick();
-            --in_engine;
-            unfinished.erase(gseqs[k]);
-            retire(item, false);
-            cv_sub.notify_all();
+            if (++sh.taken >= sh.n_jobs) sh.cv_read.notify_all();
+            sh.tick();
+            --sh.in_engine;
+            retire(sh, item, false);
+            sh.cv_sub.notify_all();
             continue;
           }
           const band::JobId id = handles.value()[k];
-          pending[id] = item;
-          auto ea = early.find(id);
-          if (ea != early.end()) {
-            unfinished.erase(gseqs[k]);
-            cv_sub.notify_all();
-            done.emplace_back(id, std::move(ea->second));
-            early.erase(ea);
-            cv_read.notify_one();
+          sh.pending[id] = item;
+          auto ea = sh.early.find(id);
+          if (ea != sh.early.end()) {
+            sh.tick();
+            sh.done.emplace_back(id, std::move(ea->second));
+            sh.early.erase(ea);
+            ++to_read;
           }
         }
+        if (to_read) sh.cv_read.notify_all();
       }
     });
   }
   for (auto& t : threads) t.join();
   (void)e.UnsetOnEndRequest(cb);
   const double wall_us = double(band::time::NowMicros() - t0);
-  tick();
+  double int_engine = 0, int_done = 0, submit_wait = 0, submit_call = 0, read_busy = 0, read_idle = 0;
+  for (auto& shp : shards) {
+    Shard& sh = *shp;
+    sh.tick();
+    int_engine += sh.int_engine;
+    int_done += sh.int_done;
+    submit_wait += sh.submit_wait;
+    submit_call += sh.submit_call;
+    read_busy += sh.read_busy;
+    read_idle += sh.read_idle;
+  }
   double* st = engine->driver_stats;
   st[0] = wall_us;
   st[1] = wall_us > 0 ? int_engine / wall_us : 0;
@@ -687,7 +724,7 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   st[6] = read_idle;
   st[7] = double(readers) + 1000.0 * lanes;
   if (wall_s) *wall_s = wall_us * 1e-6;
-  return failed ? kBandErr : kBandOk;
+  return failed.load() ? kBandErr : kBandOk;
 }
 }  // namespace
 

@@ -8,9 +8,9 @@ run() {
   env "$@" PLANNER_CEILING_SAMPLE=1 timeout -k 10 120 python tools/planner_ceiling.py --workers 8 --job-batch 24 \
     --jobs 400000 $EXTRA >> "$out" 2>/dev/null || return 1
 }
-EXTRA="" run BANDX_DRIVER_READERS=6 &&
 EXTRA="" run BANDX_DRIVER_READERS=2 &&
-EXTRA="" run BANDX_DRIVER_READERS=2 BANDX_DRIVER_LANES=2 &&
-EXTRA="" run BANDX_DRIVER_READERS=4 BANDX_DRIVER_LANES=2 BANDX_DRIVER_BURST=48 &&
+EXTRA="" run BANDX_DRIVER_READERS=4 BANDX_DRIVER_LANES=2 &&
+EXTRA="" run BANDX_DRIVER_READERS=8 BANDX_DRIVER_LANES=4 &&
+EXTRA="" run BANDX_DRIVER_READERS=8 BANDX_DRIVER_LANES=8 &&
 EXTRA="--gpu" run BANDX_DRIVER_READERS=2 &&
-EXTRA="--gpu" run BANDX_DRIVER_READERS=4 BANDX_DRIVER_LANES=2
+EXTRA="--gpu" run BANDX_DRIVER_READERS=8 BANDX_DRIVER_LANES=4

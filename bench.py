@@ -838,6 +838,10 @@ def main():
     # W workers per GPU and with one worker per GPU (north_star's "One Worker
     # per GPU via worker_device_queue")
     single_1wpg = None
+    if D.world == 1 and W != 1 and not args.no_single_engine and not poisson and on_gpu and batching:
+        # N = 1: the headline engine IS the single engine; north_star's one
+        # GPU worker per GPU (worker_device_queue) is measured beside it
+        single_1wpg = single_engine_line(args, D, paths, sched, 1, 1, n_warm, n_timed)
     if D.world > 1 and not args.no_single_engine and not poisson and on_gpu:
         D.barrier()  # every rank has closed its engines
         if D.rank == 0:

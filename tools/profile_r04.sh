@@ -3,11 +3,11 @@
 # rocprofv3's own directories stay in a scratch dir on the box):
 #   0. the default bench line, untraced; its measured kernel / fusion
 #      choices go to a tune file every later run replays;
-#   1. the graph-replay bench itself (direct ring I/O, 8 GPU workers) WITH
-#      its roofline stage under rocprofv3 --kernel-trace --stats (the
-#      --memory-copy-trace domain faults inside hipGraphLaunch once ~800
-#      graphs exist) -> kernel stats and
-#      tools/timeline_summary.py;
+#   1. the bench itself (direct ring I/O, 8 GPU workers) WITH its roofline
+#      stage under rocprofv3 --kernel-trace --stats, eager launches
+#      (--no-graph: rocprofv3 7.2 faults inside hipGraphLaunch after enough
+#      graph launches, tools/graph_copytrace_probe.hip)
+#      -> kernel stats and tools/timeline_summary.py;
 #   2. bench.py --profile-only (the batch-24 passes the roofline line
 #      reports) under --kernel-trace --stats;
 #   3./4. FETCH_SIZE and WRITE_SIZE passes (separate runs, no other traces)
@@ -32,7 +32,7 @@ step() { echo "$(date +%T) $*"; }
 timeout -k 10 500 python3 bench.py > "$O/${TAG}_bench_default.json" 2> "$O/${TAG}_bench_default.err" || exit $?
 step "0 default line done"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$W/${TAG}_full" -o run -- \
-  python3 bench.py --no-cpu-baseline --no-batch1 --steps 8 --warmup 2 \
+  python3 bench.py --no-cpu-baseline --no-batch1 --no-graph --steps 8 --warmup 2 \
   > "$O/${TAG}_bench_traced.json" 2> "$O/${TAG}_full.err" || exit $?
 python3 tools/timeline_summary.py "$W/${TAG}_full/run_kernel_trace.csv" > "$O/${TAG}_timeline.txt" || exit $?
 step "1 traced graph-replay bench done"

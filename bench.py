@@ -432,7 +432,7 @@ def profile_roofline(args, D, models, paths):
                 "attainable_tops": min(5.0e15, (o / b) * 8.0e12) / 1e12 if b else None,
                 "attainable_frac": (o / (us * 1e-6)) / min(5.0e15, (o / b) * 8.0e12) if b and o else None}
 
-    top = [roof(n, k) for n, k in ranked[:3]]
+    top = [roof(n, k) for n, k in ranked[:6]]
     dom = dict(top[0])
     dom.update(profiled_pass_batch=B, timing="per-dispatch begin/end timestamps (hipExtLaunchKernel events)",
                empty_kernel_us=float(np.mean(floors)), kernel_source_tag=tag, next_kernels=top[1:])

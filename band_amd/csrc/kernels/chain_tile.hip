@@ -128,6 +128,8 @@ struct TileGeom {
   int u_patch;         // 16-byte units of the patch
   int off_res, off_blob, blob_units;
   int off_dl, off_pl, off_o1, off_add, off_out;
+  int out_pitch;       // bytes per pixel of the second 1x1's staging (N2, or N2 + 16)
+  int o1_pitch;        // the same for the first 1x1's staging (N1, or N1 + 16)
   int buf_bytes;  // patch + residual region (pipe: the second one follows it)
   TileBlob blob;
   size_t bytes;
@@ -180,15 +182,21 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
   g.off_pl = (int)o;
   o += (size_t)rows * g.S2;
   g.off_o1 = (int)o;
-  o += p.pw1.output ? (size_t)rows * N1 : 0;
+  g.o1_pitch = (N1 % 32 == 0) ? N1 + 16 : N1;  // see out_pitch below
+  o += p.pw1.output ? (size_t)rows * g.o1_pitch : 0;
   g.off_add = (int)o;
   o += p.pw1.residual ? 512 * 4 : 0;
   // the second 1x1's staging reuses the patch (dead after phase A) when it fits
-  if ((size_t)rows * N2 <= (size_t)g.u_patch * 16) {
+  // the staged pixels 4 apart (one quad-transposed ds_write_b32 lane pair)
+  // sit 4 * pitch bytes apart: pitch = 0 mod 128 puts them on one bank, so
+  // such rows get 16 bytes of pad (16-byte multiples keep the copy-out's
+  // 16-byte reads aligned)
+  g.out_pitch = (N2 % 32 == 0 && N2 > 0) ? N2 + 16 : N2;
+  if ((size_t)rows * g.out_pitch <= (size_t)g.u_patch * 16) {
     g.off_out = 0;
   } else {
     g.off_out = (int)o;
-    o += (size_t)rows * N2;
+    o += (size_t)rows * g.out_pitch;
   }
   g.bytes = (o + 15) / 16 * 16;
   return g;
@@ -200,10 +208,12 @@ struct TileDivs {
   int ntiles;  // batch x tiles
 };
 
-// the staged [rows][Nc] tile (row = tile pixel) to HBM: tile row i (TW
-// pixels) is the contiguous run at pixel (oy0 + i, ox0)
+// the staged tile (pixel p at byte p * pitch, pitch = Nc or Nc + pad with
+// Nc % 16 == 0) to HBM: tile row i (TW pixels) is the contiguous run at
+// pixel (oy0 + i, ox0)
 __device__ __forceinline__ void tile_copy_out(const unsigned char* src, uint8_t* out, int Nc, int TH, int TW, int n,
-                                              int oy0, int ox0, int OH, int OW, int tid, int nthreads) {
+                                              int oy0, int ox0, int OH, int OW, int tid, int nthreads,
+                                              int pitch = 0) {
   const int vc = min(TW, OW - ox0);
   const int vr = min(TH, OH - oy0);
   const int rb = vc * Nc;               // valid bytes per tile row (multiple of 4)
@@ -212,12 +222,21 @@ __device__ __forceinline__ void tile_copy_out(const unsigned char* src, uint8_t*
   // in float is within 2^-20 relative of the quotient, far from the next
   // integer for i < 2^16
   const float rcp = 1.0f / (float)cpr;
+  const bool padded = pitch > Nc;
+  const int cpp = Nc >> 4;  // padded: 16-byte chunks per pixel
+  const float rcpp = padded ? 1.0f / (float)cpp : 0.0f;
   for (int i = tid; i < vr * cpr; i += nthreads) {
     const int r = (int)(((float)i + 0.5f) * rcp);
     const int c = i - r * cpr;
     const int b = c * 16;
     if (b >= rb) continue;
-    const unsigned char* s = src + r * TW * Nc + b;
+    const unsigned char* s;
+    if (padded) {
+      const int x = (int)(((float)c + 0.5f) * rcpp);  // pixel of the row; its chunk c - x * cpp
+      s = src + (r * TW + x) * pitch + (c - x * cpp) * 16;
+    } else {
+      s = src + r * TW * Nc + b;
+    }
     uint8_t* dst = out + ((long)(n * OH + oy0 + r) * OW + ox0) * Nc + b;
     if (b + 16 <= rb) {
       *(v4i*)dst = *(const v4i*)s;
@@ -485,7 +504,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
                            a.add_act_min, a.add_act_max);
         }
       }
-      if (out1) stage4(o1, N1, orow, nch, v);
+      if (out1) stage4(o1, G.o1_pitch, orow, nch, v);
       if (cp.has_pw2) stage4(pl, G.S2, orow, nch, v);
     };
     // two channel tiles per iteration (their LDS reads issue together)
@@ -509,7 +528,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   }
   __syncthreads();
   TILE_STAMP(4)
-  if (a.output) tile_copy_out(o1, (uint8_t*)a.output, a.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256);
+  if (a.output) tile_copy_out(o1, (uint8_t*)a.output, a.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256, G.o1_pitch);
   if (cp.has_pw2) {
 
   // ---- phase C: second 1x1 from pl -> ol (staged) -> HBM -------------------
@@ -531,7 +550,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       int32_t v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
-      stage4(ol, N2, orow, nch, v);
+      stage4(ol, G.out_pitch, orow, nch, v);
     };
     for (int t = 0; t < G.T2; t += 2) {
       const bool two = t + 1 < G.T2;
@@ -554,7 +573,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   }
   __syncthreads();
   TILE_STAMP(5)
-  tile_copy_out(ol, (uint8_t*)b.output, b.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256);
+  tile_copy_out(ol, (uint8_t*)b.output, b.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256, G.out_pitch);
   TILE_STAMP(6)
   }  // has_pw2
   if (PIPE == 1 && it + 1 < t_count) {

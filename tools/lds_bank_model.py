@@ -12,7 +12,8 @@ cycles per wave for the 112x112 C=32 -> 16 -> 96 chain).
 Prints the modelled extra cycles per wave by access for the layout before
 round 4 (byte stores, rows of k_pad + 16, XOR (row >> 2) & 3) and after it
 (quad-transposed dword stores, rows of k_pad + 32, stride-aware XOR,
-patch chunks XORed with (3 py + px) & (C/16 - 1)).
+patch chunks XORed with (3 py + px) & (C/16 - 1), 1x1 outputs staged at a
+pitch of N + 16 when N = 0 mod 32).
 Usage: python tools/lds_bank_model.py [C N1 N2]
 """
 import sys
@@ -86,7 +87,8 @@ def model(C, N1, N2, new, TW=8, PW=10):
                 tot["B x read"] += extra_b128([(pb * 16 + r16) * S1 + g * 16 + k * 64 for r16, g in lanes])
                 tot["B w read"] += extra_b128([(t * 16 + r16) * kp1 + 16 * swz(t * 16 + r16, 4 * k + g, kp1 // 16)
                                                for r16, g in lanes])
-            store("B o1 store", lambda row, col: (pb * 16 + row) * N1 + t * 16 + col)
+            o1p = N1 + 16 if new and N1 % 32 == 0 else N1
+            store("B o1 store", lambda row, col: (pb * 16 + row) * o1p + t * 16 + col)
             store("B pl store", lambda row, col: (pb * 16 + row) * S2 + t * 16 + col)
         for k in range(kp2 // 64):
             tot["C x read"] += extra_b128([(pb * 16 + r16) * S2 + g * 16 + k * 64 for r16, g in lanes])
@@ -94,7 +96,8 @@ def model(C, N1, N2, new, TW=8, PW=10):
             for k in range(kp2 // 64):
                 tot["C w read"] += extra_b128([(t * 16 + r16) * kp2 + 16 * swz(t * 16 + r16, 4 * k + g, kp2 // 16)
                                                for r16, g in lanes])
-            store("C out store", lambda row, col: (pb * 16 + row) * N2 + t * 16 + col)
+            op = N2 + 16 if new and N2 % 32 == 0 else N2  # round 4: padded staging pitch
+            store("C out store", lambda row, col: (pb * 16 + row) * op + t * 16 + col)
     return {k: v / 4 for k, v in tot.items()}  # per wave (a workgroup is 4 waves, one pixel block each)
 
 

@@ -556,7 +556,6 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   }
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
-  if (f && std::strcmp(f, "nosplit") == 0) no_split_chain_ = true;  // A-B: without the phase-C split forms
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
@@ -1601,7 +1600,6 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
-          if (pw[5] && no_split_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;

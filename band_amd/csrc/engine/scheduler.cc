@@ -90,10 +90,11 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
     // job batching (extension): the idle worker also takes the next queued
     // requests of the same model, up to its batch, and runs them in one pass;
     // one EnqueueToWorkerBatch call keeps their FIFO order if it is refused.
-    // One stable pass over the queue takes them out (erasing each from the
-    // middle of the deque moved the whole tail per job: with hundreds of
-    // queued requests and 24-job batches that made the planner thread the
-    // bottleneck)
+    // They are taken out by one stable compaction of the span from the first
+    // to the last taken request only (erasing each from the middle of the
+    // deque moved the whole tail per job, and rebuilding the whole queue per
+    // assignment moved every queued request: with hundreds queued and 24-job
+    // batches either made the planner thread the bottleneck)
     std::vector<ScheduleAction> actions;
     const int batch = std::max(1, engine_.MaxJobBatch(key));
     actions.reserve(batch);
@@ -101,14 +102,25 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
       actions.emplace_back(std::move(*it), key);
       requests.erase(it);
     } else {
-      JobQueue rest;
-      for (auto j = requests.begin(); j != requests.end(); ++j) {
-        if (j >= it && static_cast<int>(actions.size()) < batch && j->model_id == key.GetModelId())
-          actions.emplace_back(std::move(*j), key);
-        else
-          rest.push_back(std::move(*j));
+      const ModelId model = key.GetModelId();
+      auto last = it;  // `it` is this model's first request
+      int take = 0;
+      for (auto j = it; j != requests.end() && take < batch; ++j)
+        if (j->model_id == model) {
+          last = j;
+          ++take;
+        }
+      const auto end = std::next(last);
+      auto w = it;
+      for (auto r = it; r != end; ++r) {
+        if (r->model_id == model && static_cast<int>(actions.size()) < take) {
+          actions.emplace_back(std::move(*r), key);
+        } else {
+          if (w != r) *w = std::move(*r);
+          ++w;
+        }
       }
-      requests.swap(rest);
+      requests.erase(w, end);
     }
     ok &= engine_.EnqueueToWorkerBatch(actions);
     next_ = w + 1;

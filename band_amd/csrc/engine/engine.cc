@@ -778,7 +778,9 @@ absl::Status Engine::CopyOutputs(const Job& job, const ViewFn& view) {
     return absl::InternalError("Failed to find output tensor ring buffer for model " + std::to_string(job.model_id));
   // the slot becomes this request's (after any callback still reading the
   // previous request's outputs there has returned)
-  ring->second->AcquireForWrite(job.output_handle);
+  if (!ring->second->AcquireForWrite(job.output_handle))
+    return absl::DeadlineExceededError("output slot of request " + std::to_string(job.output_handle) + " of model " +
+                                       std::to_string(job.model_id) + " is held by an end-request callback");
   for (int t : exec->GetOutputs(key)) {
     if (!ring->second->IsTensorIndexValid(t)) continue;
     auto src = view(t);
@@ -810,6 +812,10 @@ absl::Status Engine::InvokeJobBatch(const SubgraphKey& key, int n) {
 }
 
 absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vector<Job*>& jobs) {
+  // max_job_batch 1 is Band's own contract: the worker copies through the
+  // executor's views around ExecuteSubgraph (band/worker.cc:222-323) and
+  // the engine calls nothing beyond band/interface
+  if (max_job_batch_ <= 1) return absl::UnimplementedError("job batching off");
   auto* jb = dynamic_cast<hip::IJobBatching*>(GetModelExecutor(key));
   interface::IModelExecutor* exec = GetModelExecutor(key);
   const int n = static_cast<int>(jobs.size());
@@ -836,7 +842,9 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
       // a subgraph output outside the output ring feeds a later subgraph:
       // it must reach the executor's own views
       if (!out_it->second->IsTensorIndexValid(outs[k])) return absl::UnimplementedError("intermediate output");
-    out_it->second->AcquireForWrite(j.output_handle);  // as in CopyOutputs
+    // as in CopyOutputs; a slot still held past the bound: the staged path
+    // fails that job's output copy alone
+    if (!out_it->second->AcquireForWrite(j.output_handle)) return absl::UnimplementedError("output slot held");
     for (size_t k = 0; k < outs.size(); ++k) {
       Tensor* t = out_it->second->SlotTensor(outs[k], j.output_handle);
       if (!t || !t->IsRingMemory()) return absl::UnimplementedError("output slot not page-locked");

@@ -111,16 +111,16 @@ bool RoundRobinScheduler::Schedule(JobQueue& requests) {
           ++take;
         }
       const auto end = std::next(last);
-      auto w = it;
+      auto out = it;
       for (auto r = it; r != end; ++r) {
         if (r->model_id == model && static_cast<int>(actions.size()) < take) {
           actions.emplace_back(std::move(*r), key);
         } else {
-          if (w != r) *w = std::move(*r);
-          ++w;
+          if (out != r) *out = std::move(*r);
+          ++out;
         }
       }
-      requests.erase(w, end);
+      requests.erase(out, end);
     }
     ok &= engine_.EnqueueToWorkerBatch(actions);
     next_ = w + 1;

@@ -3,10 +3,13 @@
 #include <immintrin.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+
+#include "engine/logger.h"
 
 namespace band {
 
@@ -235,12 +238,24 @@ void TensorRingBuffer::Release(int handle) {
   slot_cv_.notify_all();  // waiters may need different slot counts
 }
 
-void TensorRingBuffer::AcquireForWrite(int handle) {
-  if (handle < 0) return;
+bool TensorRingBuffer::AcquireForWrite(int handle) {
+  if (handle < 0) return true;
+  static const long hold_ms = [] {
+    const char* e = std::getenv("BANDX_OUTPUT_HOLD_MS");
+    return e ? std::max(0L, std::atol(e)) : 2000L;
+  }();
   std::unique_lock<std::mutex> lock(head_mtx_);
   const int s = Slot(handle);
-  slot_cv_.wait(lock, [&] { return !held_[s] || owner_[s] == handle; });
+  if (!slot_cv_.wait_for(lock, std::chrono::milliseconds(hold_ms),
+                         [&] { return !held_[s] || owner_[s] == handle; })) {
+    BAND_LOG(LogSeverity::kWarning,
+             "output slot %d of request %d is still held by request %d's end-request callback after %ld ms "
+             "(does the callback wait for a newer request of its model?): output write refused",
+             s, handle, owner_[s], hold_ms);
+    return false;
+  }
   owner_[s] = handle;
+  return true;
 }
 
 void TensorRingBuffer::Hold(int handle) {

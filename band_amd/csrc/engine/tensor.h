@@ -99,8 +99,13 @@ class TensorRingBuffer {
   // once newer submissions have moved the handle window past it.  Hold keeps
   // the owner's outputs in place - a newer writer waits in AcquireForWrite -
   // until Unhold (Planner::EnqueueFinishedJob brackets the end-request
-  // callbacks with them).
-  void AcquireForWrite(int handle);
+  // callbacks with them).  The wait is bounded (BANDX_OUTPUT_HOLD_MS, default
+  // 2000): a callback that waits synchronously for a newer request of its
+  // own model (RequestSync / Wait) while that request's job needs the held
+  // slot would otherwise wait for itself.  On timeout the write is refused
+  // (false, a warning is logged) and the newer job fails its output copy;
+  // the held outputs stay intact.
+  bool AcquireForWrite(int handle);
   void Hold(int handle);
   void Unhold(int handle);
   int size() const { return size_; }

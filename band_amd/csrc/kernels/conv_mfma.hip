@@ -401,16 +401,23 @@ struct ConvGroupMember {
 };
 constexpr int kConvGroupMax = 32;
 
-// The launch arguments are padded to 256 bytes (every other kernel here
-// takes a 150+ byte parameter block by value).  Observed under rocprofv3 7.2
-// --memory-copy-trace: with the 12-byte block the traced bench faulted in
-// hipGraphLaunch (profiles/r04q_tr2_copytrace_crash.txt), padded it traced
-// (r04u); the tool's fault itself reproduces with no code of ours
-// (tools/graph_copytrace_probe.hip), so the padding moves, not removes, it.
+// Profiler workaround only, off by default: -DBH_CONV_GROUP_ARGS_PAD=1 pads
+// the launch arguments to 256 bytes.  rocprofv3 7.2's hipGraphLaunch
+// interception faults on graphs that mix copy and kernel nodes
+// (tools/graph_copytrace_probe.hip reproduces it with no code of ours); one
+// traced run with the 12-byte block faulted and one padded run traced
+// (profiles/r04q_tr2_copytrace_crash.txt, r04u), so the padding moves the
+// fault rather than removing it.  Traced runs use eager launches
+// (bench.py --no-graph), which is the supported workaround.
+#ifndef BH_CONV_GROUP_ARGS_PAD
+#define BH_CONV_GROUP_ARGS_PAD 0
+#endif
 struct ConvGroupArgs {
   const ConvGroupMember* tab;
   int n;
+#if BH_CONV_GROUP_ARGS_PAD
   int pad[61];
+#endif
 };
 
 template <bool IS1X1>

@@ -409,6 +409,10 @@ def test_poisson_latency_counts_submission_delay(golden_dir):
     # preempted worker on a loaded host adds a step, never a drop)
     assert np.all(np.diff(lat) > -1000.0)
     assert lat[-1] > lat[len(lat) // 4]
+    # and it really grows (a flat latency series would pass the two checks
+    # above): the last decile's median is well above the first decile's
+    dec = len(lat) // 10
+    assert np.median(lat[-dec:]) > 2.0 * np.median(lat[:dec])
     e.close()
 
 
@@ -491,6 +495,51 @@ def test_callback_reads_own_outputs_while_ring_is_full(tmp_path, monkeypatch):
         rc, out = got[h]
         assert rc == kBandOk, (j, h)
         np.testing.assert_array_equal(out, refs[j % 6])
+    e.close()
+
+
+def test_callback_request_sync_into_held_slot_does_not_hang(tmp_path, monkeypatch):
+    """an end-request callback that calls RequestSync on its own
+    model while the 2-slot ring is full.  The new request takes the slot the
+    callback's request just freed, and its job needs that slot's outputs,
+    which stay held until the callback returns - the callback waits for
+    the job, the job for the callback.  The writer's wait is bounded
+    (BANDX_OUTPUT_HOLD_MS): the newer job fails its output copy, RequestSync
+    returns an error, and nothing hangs; the held outputs stay intact."""
+    import threading
+    monkeypatch.setenv("BANDX_REQUEST_RING_SLOTS", "2")
+    monkeypatch.setenv("BANDX_OUTPUT_HOLD_MS", "300")
+    path, _ = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU] * 3, num_threads=[1] * 3))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    t = e.CreateInputTensor(m, 0)
+    o_cb = e.CreateOutputTensor(m, 0)
+    o_first = e.CreateOutputTensor(m, 0)
+    result = {}
+    finished = threading.Event()
+    opt = RequestOptionGetDefault()
+    opt.require_callback = True
+
+    def on_end(job, status):
+        if "rc" in result or job != hs[0]:
+            return
+        result["rc"] = None
+        result["rc"] = e.RequestSync(m, [t], [o_cb])
+        result["own"] = e.Wait(job, [o_first])
+        finished.set()
+
+    hs = []
+    e.SetOnEndRequest(on_end)
+    hs.extend(e.RequestAsync(m, [t], opt) for _ in range(2))
+    assert all(h >= 0 for h in hs)
+    assert finished.wait(timeout=60), "callback waiting on a newer request of its model deadlocked"
+    # handles 0, 1 fill the ring; the callback's request is handle 2 = slot 0,
+    # the slot its own request (handle 0) holds: refused after the bound
+    assert result["rc"] != kBandOk
+    assert result["own"] == kBandOk  # the held outputs were not overwritten
+    e.WaitAll()
     e.close()
 
 

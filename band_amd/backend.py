@@ -75,6 +75,8 @@ _abi.BACKEND_SYMBOLS.update({
                                     ctypes.POINTER(ctypes.c_double)]),
     "bhx_executor_set_graph": (c_int, [c_void_p, c_int]),
     "bhx_executor_device": (c_int, [c_void_p, ctypes.POINTER(c_int)]),
+    "bhx_executor_coalescer": (c_int, [c_void_p, ctypes.POINTER(c_int), ctypes.POINTER(c_int)]),
+    "bhx_coalescer_stats": (c_int, [ctypes.POINTER(ctypes.c_longlong), c_int]),
     "bhx_profile_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(OpTiming), c_int, ctypes.POINTER(c_int),
                                             ctypes.POINTER(ctypes.c_double)]),
     "bhx_time_subgraph": (c_int, _KEY + [c_int, ctypes.POINTER(ctypes.c_double)]),
@@ -457,6 +459,13 @@ class HipModelExecutor:
         _abi.check(self.lib.bhx_executor_device(self.handle, ctypes.byref(o)), "device")
         return o.value
 
+    def Coalescer(self):
+        """(members, lanes_ready) of the job coalescer this executor's
+        whole-model subgraph joined ((0, False): none)"""
+        m, r = c_int(0), c_int(0)
+        _abi.check(self.lib.bhx_executor_coalescer(self.handle, ctypes.byref(m), ctypes.byref(r)), "coalescer")
+        return m.value, bool(r.value)
+
     def ProfileSubgraph(self, key, iters=10, with_floor=False):
         """per-launch kernel durations in program order (ms each; dispatch
         begin / end timestamps, as rocprofv3 reports them); with_floor: also
@@ -535,6 +544,15 @@ def PinProcessToCpus(cpus):
     cpus = list(cpus)
     arr = (c_int * max(1, len(cpus)))(*cpus)
     return int(_abi.load().bhx_pin_process_to_cpus(arr, len(cpus)))
+
+
+def CoalescerStats(reset=False):
+    """process-wide job coalescing totals: calls, solo passes, group passes,
+    jobs in group passes, largest group (coalescer.h)"""
+    arr = (ctypes.c_longlong * 5)()
+    _abi.check(_abi.load().bhx_coalescer_stats(arr, int(bool(reset))), "coalescer_stats")
+    keys = ("calls", "solo_passes", "group_passes", "group_jobs", "max_group")
+    return {k: int(v) for k, v in zip(keys, arr)}
 
 
 def RingPageNodes():

@@ -375,6 +375,27 @@ int bhx_executor_device(bhx_executor* e, int* ordinal) {
   return 0;
 }
 
+int bhx_executor_coalescer(bhx_executor* e, int* members, int* lanes_ready) {
+  auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;
+  if (!h || !members || !lanes_ready) return Fail("not a HIP executor");
+  const band::hip::JobCoalescer* c = h->coalescer();
+  *members = c ? c->members() : 0;
+  *lanes_ready = c && c->lanes_ready() ? 1 : 0;
+  return 0;
+}
+
+int bhx_coalescer_stats(long long* out, int reset) {
+  if (!out) return Fail("bad arguments");
+  const band::hip::JobCoalescer::Stats s = band::hip::JobCoalescer::Totals();
+  out[0] = s.calls;
+  out[1] = s.solo_passes;
+  out[2] = s.group_passes;
+  out[3] = s.group_jobs;
+  out[4] = s.max_group;
+  if (reset) band::hip::JobCoalescer::ResetTotals();
+  return 0;
+}
+
 int bhx_profile_subgraph(bhx_executor* e, int mid, int wid, uint64_t mask, int iters, bhx_op_timing* out, int cap,
                          int* n, double* floor_us) {
   auto* h = e ? dynamic_cast<band::hip::HipModelExecutor*>(e->exec.get()) : nullptr;

@@ -92,9 +92,14 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   }
   block_sync_ = sync_mode_ == kSyncBlock;
   if (const char* d = std::getenv("BAND_HIP_DIRECT_IO")) direct_io_ = d[0] != '0';
+  if (const char* c = std::getenv("BAND_HIP_COALESCE")) coalesce_max_ = std::atoi(c);
+  if (const char* c = std::getenv("BAND_HIP_COALESCE_LANES")) coalesce_lanes_ = std::max(1, std::atoi(c));
 }
 
 HipModelExecutor::~HipModelExecutor() {
+  if (coalescer_) coalescer_->Leave(this);
+  coalescer_.reset();  // the last member takes the lanes with it
+  job_batches_.clear();
   if (ordinal_ >= 0) {
     bh_set_device(ordinal_);
     if (stream_) bh_stream_sync(stream_);
@@ -102,6 +107,26 @@ HipModelExecutor::~HipModelExecutor() {
     if (done_event_) bh_event_destroy(done_event_);
   }
   subgraphs_.clear();
+  if (owned_stream_) bh_stream_destroy(owned_stream_);
+}
+
+std::unique_ptr<HipModelExecutor> HipModelExecutor::MakeLane() {
+  if (device_flag_ != DeviceFlag::kGPU || ordinal_ < 0) return nullptr;
+  auto lane = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
+                                                 num_threads_);
+  if (bh_set_device(ordinal_) != 0 || bh_stream_create(&lane->owned_stream_) != 0) return nullptr;
+  lane->ordinal_ = ordinal_;
+  lane->stream_ = lane->owned_stream_;
+  lane->coalesce_ok_ = false;
+  lane->use_graph_ = use_graph_;
+  lane->io_mode_ = io_mode_;
+  lane->io_stream_bytes_ = io_stream_bytes_;
+  lane->sync_mode_ = sync_mode_;
+  lane->block_sync_ = block_sync_;
+  // the lane's passes stage their I/O in the variants' mirrors
+  lane->direct_io_ = false;
+  lane->autotune_ = autotune_;
+  return lane;
 }
 
 namespace {
@@ -2477,6 +2502,13 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
   auto old = subgraphs_.find(key);
   if (old != subgraphs_.end()) DropGraph(old->second.get());
   subgraphs_[key] = std::move(sg);
+  // whole-model GPU subgraphs coalesce concurrent jobs with the other
+  // executors of this model on this GPU (coalescer.h)
+  if (whole && device_flag_ == DeviceFlag::kGPU && coalesce_ok_ && coalesce_max_ > 1 && !t_variant_ctor) {
+    if (coalescer_) coalescer_->Leave(this);
+    coalescer_ = JobCoalescer::Join(this, model, key, ordinal_, coalesce_max_, coalesce_lanes_);
+    coalesced_key_ = key;
+  }
   return absl::OkStatus();
 }
 
@@ -2808,6 +2840,12 @@ absl::Status HipModelExecutor::ExecuteSubgraph(const SubgraphKey& key) {
   if (!sg) return absl::InternalError("Cannot find subgraph");
   if (device_flag_ == DeviceFlag::kCPU) return ExecuteOnHost(sg);
   if (device_flag_ != DeviceFlag::kGPU) return absl::InternalError("Unsupported device type");
+  // a view of an intermediate (extra_d2h) needs this executor's own pass
+  if (coalescer_ && key == coalesced_key_ && sg->extra_d2h.empty()) return coalescer_->Run(this, sg);
+  return RunPass(sg);
+}
+
+absl::Status HipModelExecutor::RunPass(PreparedSubgraph* sg) {
   int rc = bh_set_device(ordinal_);
   if (rc) return HipErr(rc, "hipSetDevice");
   if (use_graph_ && !sg->graph && sg->runs > 0) RETURN_STATUS_IF(CaptureGraph(sg));
@@ -2863,6 +2901,11 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
   auto* hm = dynamic_cast<HipModel*>(model);
   if (!hm || hm != model_) return absl::InternalError("job batching: not the model this executor prepared");
   job_batches_.erase(key);
+  // the harness batches this executor's jobs itself: no coalescing
+  if (coalescer_) {
+    coalescer_->Leave(this);
+    coalescer_.reset();
+  }
   if (max_batch <= 1) return absl::OkStatus();
   // anchors (2, 4, 8, .., max_batch) measure their fusion choices; every
   // other size reuses the next anchor's.  Anchors are prepared first, the
@@ -2890,6 +2933,8 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
                                                 num_threads_);
     t_variant_ctor = false;
     v.exec->use_graph_ = use_graph_;
+    v.exec->stream_ = stream_;  // a lane's variants run on the lane's stream
+    v.exec->coalesce_ok_ = false;
     // direct job I/O captures the variants' graphs without host copies
     v.exec->io_mode_ = direct_io_ ? 1 : io_mode_;
     v.exec->direct_io_ = direct_io_;

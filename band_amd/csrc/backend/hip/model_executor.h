@@ -24,6 +24,7 @@
 #include <string>
 #include <vector>
 
+#include "backend/hip/coalescer.h"
 #include "backend/hip/cpu_kernels.h"
 #include "backend/hip/device.h"
 #include "backend/hip/model.h"
@@ -177,6 +178,8 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // gaps, H2D/D2H included.  The latency floor of ExecuteSubgraph's device side.
   absl::Status TimeSubgraph(const SubgraphKey& key, int iters, double* us);
   int ordinal() const { return ordinal_; }
+  // the coalescer this executor's whole-model subgraph joined (null: none)
+  const JobCoalescer* coalescer() const { return coalescer_.get(); }
 
   // Whether the GPU kernel set covers `op` of `model` (drives unsupported_ops[kGPU]).
   static bool GpuSupports(const TflModel& model, const TflOperator& op, std::string* why);
@@ -184,7 +187,14 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   static bool CpuSupports(const TflModel& model, const TflOperator& op, std::string* why);
 
  private:
+  friend class JobCoalescer;
   PreparedSubgraph* Find(const SubgraphKey& key) const;
+  // one batch-1 pass of sg on this executor's stream (graph captured on the
+  // second run), returning when its outputs are in the host mirrors
+  absl::Status RunPass(PreparedSubgraph* sg);
+  // a private executor of this one's model on this GPU with a stream of its
+  // own, for a coalescer lane (never joins a coalescer itself)
+  std::unique_ptr<HipModelExecutor> MakeLane();
   absl::Status EnsureMeta(const HipModel& model);
   absl::Status Lower(const HipModel& model, int op_index, PreparedSubgraph* sg);
   absl::Status BuildLaunches(const HipModel& model, PreparedSubgraph* sg);
@@ -297,6 +307,18 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   std::shared_ptr<DeviceBlob> shared_arena_;
   const PreparedSubgraph* shared_host_from_ = nullptr;
   int tune_batch_ = 0;
+  // Job coalescing (coalescer.h): whole-model kGPU subgraphs join the
+  // coalescer of their (model, GPU); concurrent ExecuteSubgraph calls of
+  // several executors then run as job-batch passes.  BAND_HIP_COALESCE = max
+  // jobs per pass (default 16; 0 or 1: off), BAND_HIP_COALESCE_LANES =
+  // passes in flight per (model, GPU) (default 2).  Off for lanes, job-batch
+  // variants, and executors the harness batches itself (PrepareJobBatches).
+  std::shared_ptr<JobCoalescer> coalescer_;
+  SubgraphKey coalesced_key_;
+  bool coalesce_ok_ = true;
+  int coalesce_max_ = 16;
+  int coalesce_lanes_ = 2;
+  bh_stream_t owned_stream_ = nullptr;  // a lane's own stream
   static const std::vector<int> kEmpty;
 };
 

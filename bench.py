@@ -103,6 +103,8 @@ def parse():
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
     p.add_argument("--no-batch1", action="store_true",
                    help="skip the one-job-per-pass (Band semantics) line reported beside a job-batched run")
+    p.add_argument("--band1-workers", type=int, default=8,
+                   help="GPU workers per GPU of the band_one_job_per_pass line (Band's own contract)")
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
@@ -523,6 +525,7 @@ def thread_cpu():
 
 HOST_THREADS = {}
 HOST_THREAD_STATES = {}
+COALESCE = {}  # backend job coalescing over the last timed loop (coalescer.h)
 
 
 def cgroup_cpu_stat():
@@ -610,9 +613,23 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     c0 = thread_cpu()
     g0 = cgroup_cpu_stat()
     sampler = ThreadSampler() if SAMPLE_THREADS else None
+    coalesce = None
+    try:
+        from band_amd import backend as _backend
+        coalesce = _backend.CoalescerStats
+        coalesce(reset=True)
+    except Exception:  # the CPU-only stand-in runs have no HIP library loaded
+        coalesce = None
     t0 = time.perf_counter()
     lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
     t1 = time.perf_counter()
+    COALESCE.clear()
+    if coalesce:
+        cs = coalesce()
+        if cs["calls"]:
+            cs["mean_jobs_per_group_pass"] = round(cs["group_jobs"] / max(1, cs["group_passes"]), 2)
+            cs["share_of_jobs_coalesced"] = round(cs["group_jobs"] / cs["calls"], 3)
+        COALESCE.update(cs)
     c1 = thread_cpu()
     g1 = cgroup_cpu_stat()
     if sampler:
@@ -824,14 +841,19 @@ def main():
     # batching), the same mix and scheduler over 8 GPU workers per GPU
     batch1 = None
     if batching and not poisson and not args.no_batch1 and not args.single_engine:
-        W1 = 8
+        W1 = args.band1_workers
         e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1, seed_offset=D.rank)
         n1 = max(n_timed // 4, 16 * M)
         el1, lat1, _ = run_closed(e1, bm1, in1, max(n_warm // 4, 2 * W1 * M), n1, 2 * W1, D)
         l1 = np.array([x for part in D.gather((lat1 * 1e-3).tolist()) for x in part])
         batch1 = {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "jobs": n1,
                   "p50_job_latency_ms": float(np.percentile(l1, 50)),
-                  "p99_job_latency_ms": float(np.percentile(l1, 99))}
+                  "p99_job_latency_ms": float(np.percentile(l1, 99)),
+                  "engine_calls": "band/interface only (max_job_batch 1): TryCopyInputTensors -> "
+                                  "ExecuteSubgraph -> TryCopyOutputTensors per job",
+                  "backend_coalescing": dict(COALESCE),
+                  "process_cpu_cores": HOST_THREADS.get("process_cpu_cores"),
+                  "busiest_threads": HOST_THREADS.get("busiest", [])[:6]}
         e1.close()
 
     # N > 1: the same C3 workload through ONE engine spanning every GPU, with
@@ -923,6 +945,7 @@ def main():
             "cpu_baseline": cpu,
             "host": dict(hinfo, node=platform.node()),
             "host_threads_timed": host_threads,
+            "backend_coalescing": dict(COALESCE) if not batching else None,
         }
         print(json.dumps(line), flush=True)
     for path in paths:

@@ -96,6 +96,15 @@ int bhx_pin_process_to_cpus(const int* cpus, int n_cpus);
  * after the last node counts pages whose node was unknown.  Returns the
  * number of entries that exist (up to cap written). */
 int bhx_ring_page_nodes(long long* bytes_per_node, int cap);
+/* Job coalescing totals over every coalescer of the process (coalescer.h:
+ * concurrent ExecuteSubgraph calls of one model on one GPU run as job-batch
+ * passes): out[0] calls, out[1] passes that ran one job alone, out[2]
+ * passes of >= 2 jobs, out[3] jobs in those passes, out[4] the largest such
+ * pass.  reset != 0 zeroes the totals after reading them. */
+int bhx_coalescer_stats(long long* out, int reset);
+/* members and lanes-ready flag of the coalescer executor `e`'s whole-model
+ * subgraph joined (0 / 0 when it joined none) */
+int bhx_executor_coalescer(bhx_executor* e, int* members, int* lanes_ready);
 /* Optional hooks for a Band-compatible engine, looked up as weak symbols
  * (engine/engine.cc, engine/worker.cc); Band itself never needs them.
  * bhx_ring_host_alloc: page-locked memory for a request ring's slots, so a

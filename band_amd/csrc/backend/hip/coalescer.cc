@@ -81,7 +81,10 @@ absl::Status JobCoalescer::BuildLanes(HipModelExecutor* e, interface::IModel* mo
     lane.exec = e->MakeLane();
     if (!lane.exec) return absl::InternalError("coalescer: lane stream");
     lane.stream = lane.exec->stream_;
-    absl::Status s = lane.exec->PrepareSubgraph(model, {}, key.GetUnitIndicesSet());
+    // the same op set as the member's (model-order I/O when that was {})
+    std::set<int> ops;
+    if (!base->model_order_io) ops.insert(base->ops.begin(), base->ops.end());
+    absl::Status s = lane.exec->PrepareSubgraph(model, ops, key.GetUnitIndicesSet());
     if (!s.ok()) return s;
     lane.key = SubgraphKey(key.GetModelId(), lane.exec->worker_id_, key.GetUnitIndicesSet());
     PreparedSubgraph* ls = lane.exec->Find(lane.key);

@@ -2424,6 +2424,7 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
       if (t >= 0 && !d.tensors[t].is_const()) { produced.insert(t); touched.insert(t); }
   }
   if (whole) {
+    sg->model_order_io = true;
     sg->inputs = d.inputs;
     sg->outputs = d.outputs;
   } else {
@@ -2504,7 +2505,9 @@ absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::se
   subgraphs_[key] = std::move(sg);
   // whole-model GPU subgraphs coalesce concurrent jobs with the other
   // executors of this model on this GPU (coalescer.h)
-  if (whole && device_flag_ == DeviceFlag::kGPU && coalesce_ok_ && coalesce_max_ > 1 && !t_variant_ctor) {
+  // (Band's engine names every op of a whole model explicitly)
+  if (static_cast<int>(ops.size()) == num_ops && device_flag_ == DeviceFlag::kGPU && coalesce_ok_ &&
+      coalesce_max_ > 1 && !t_variant_ctor) {
     if (coalescer_) coalescer_->Leave(this);
     coalescer_ = JobCoalescer::Join(this, model, key, ordinal_, coalesce_max_, coalesce_lanes_);
     coalesced_key_ = key;
@@ -2918,9 +2921,10 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
   std::vector<int> order(anchors.rbegin(), anchors.rend());
   for (int b = max_batch - 1; b >= 2; --b)
     if ((b % step == 0) && std::find(anchors.begin(), anchors.end(), b) == anchors.end()) order.push_back(b);
-  // a whole-model subgraph is prepared as one (model-order I/O), not as its op set
+  // the base's op set, or {} when the base was prepared as the whole model
+  // (model-order I/O): the variants' I/O order is the base's
   std::set<int> ops;
-  if (base->ops.size() != hm->desc().ops.size()) ops.insert(base->ops.begin(), base->ops.end());
+  if (!base->model_order_io) ops.insert(base->ops.begin(), base->ops.end());
   const std::set<int> units = key.GetUnitIndicesSet();
   std::vector<JobBatchVariant> variants;
   HipModelExecutor* largest = nullptr;

@@ -98,6 +98,7 @@ struct OpTiming {
 struct PreparedSubgraph {
   std::vector<int> ops;
   std::vector<int> inputs, outputs;
+  bool model_order_io = false;   // prepared with ops = {}: the model's own I/O order
   std::map<int, size_t> offset;  // arena offset of each non-constant tensor
   std::shared_ptr<DeviceBlob> arena;
   std::map<int, std::unique_ptr<PinnedBuffer>> host;  // boundary mirrors

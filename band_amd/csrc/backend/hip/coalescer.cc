@@ -4,6 +4,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <string>
 #include <tuple>
 
 #include "backend/hip/model_executor.h"
@@ -41,6 +42,7 @@ std::shared_ptr<JobCoalescer> JobCoalescer::Join(HipModelExecutor* e, interface:
       c->num_lanes_ = std::max(1, lanes);
       c->ordinal_ = ordinal;
       for (int l = 0; l < c->num_lanes_; ++l) c->free_lanes_.push_back(l);
+      if (const char* io = std::getenv("BAND_HIP_COALESCE_IO")) c->dma_io_ = std::string(io) != "copy";
       slot = c;
     }
   }
@@ -171,6 +173,8 @@ void JobCoalescer::Dispatch() {
       pending_.pop_front();
       m->group = g;
       m->slot = i;
+      g->members.push_back(m);
+      if (dma_io_ && n > 1) --g->inputs_left;  // nothing for the member to copy in
       m->cv.notify_one();
     }
     Account(n);
@@ -198,6 +202,46 @@ absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
 
   Lane& lane = lanes_[g->lane];
   const int n = g->n;
+  if (dma_io_) {
+    if (me.slot == 0) {
+      // the leader: every member's views straight to / from the lane's
+      // arena around the n-job variant's kernels-only graph
+      const size_t ni = sg->inputs.size(), no = sg->outputs.size();
+      std::vector<HipTensorView> views;
+      views.reserve((ni + no) * n);
+      std::vector<const interface::ITensor*> in(ni * n);
+      std::vector<interface::ITensor*> out(no * n);
+      for (size_t k = 0; k < ni; ++k)
+        for (int s = 0; s < n; ++s) {
+          Member* m = g->members[s];
+          const int t = sg->inputs[k];
+          views.emplace_back(m->exec->meta_[t].get(), m->sg->host.at(t)->data());
+          in[k * n + s] = &views.back();
+        }
+      for (size_t k = 0; k < no; ++k)
+        for (int s = 0; s < n; ++s) {
+          Member* m = g->members[s];
+          const int t = sg->outputs[k];
+          views.emplace_back(m->exec->meta_[t].get(), m->sg->host.at(t)->data());
+          out[k * n + s] = &views.back();
+        }
+      lock.unlock();
+      absl::Status s = lane.exec->ExecuteJobBatchDirect(lane.key, n, in, out);
+      lock.lock();
+      g->status = s;
+      g->finished = true;
+      g->cv.notify_all();
+    } else {
+      g->cv.wait(lock, [&] { return g->finished; });
+    }
+    absl::Status status = g->status;
+    if (--g->outputs_left == 0) {
+      free_lanes_.push_back(g->lane);
+      delete g;
+      Dispatch();
+    }
+    return status;
+  }
   lock.unlock();
   // this job's inputs into its slot of the lane's n-job staging (the
   // variant's page-locked boundary mirrors; slot s = the s-th batch-1 image)

@@ -92,6 +92,7 @@ class JobCoalescer {
   struct Group {
     int lane = -1;
     int n = 0;
+    std::vector<Member*> members;  // slot order
     int inputs_left = 0;   // members still copying their inputs in
     int outputs_left = 0;  // members still copying their outputs out
     bool finished = false;
@@ -119,6 +120,11 @@ class JobCoalescer {
   bool build_failed_ = false;  // also set while the one build runs
   int max_batch_ = 16;
   int num_lanes_ = 2;
+  // BAND_HIP_COALESCE_IO: "dma" (default) - the leader DMAs each member's
+  // page-locked views straight into / out of the lane's arena (no host
+  // copies; n small DMAs per tensor); "copy" - each member memcpys its job
+  // into / out of the lane's staging and the lane moves the batch in one DMA
+  bool dma_io_ = true;
   int ordinal_ = -1;
   std::vector<size_t> in_bytes_, out_bytes_;  // per boundary tensor, one job
   Stats stats_;

@@ -123,8 +123,9 @@ std::unique_ptr<HipModelExecutor> HipModelExecutor::MakeLane() {
   lane->io_stream_bytes_ = io_stream_bytes_;
   lane->sync_mode_ = sync_mode_;
   lane->block_sync_ = block_sync_;
-  // the lane's passes stage their I/O in the variants' mirrors
-  lane->direct_io_ = false;
+  // kernels-only variant graphs: the coalescer moves each pass's I/O on the
+  // lane's stream (from the members' views, or from the variants' mirrors)
+  lane->direct_io_ = true;
   lane->autotune_ = autotune_;
   return lane;
 }

@@ -20,14 +20,16 @@ from oracle.tflite_fb import Model as OModel
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("io", ["dma", "copy"])
 @pytest.mark.parametrize("arch", ["mobilenet_v2", "ssd_mobilenet_v2"])
-def test_concurrent_execute_subgraph_bit_exact(gpu_lib, monkeypatch, arch):
+def test_concurrent_execute_subgraph_bit_exact(gpu_lib, monkeypatch, arch, io):
     """6 threads, each on its own executor of one model (6 Band workers on
     GPU 0), call ExecuteSubgraph at the same moment, round after round, each
     with its own input; every output of every call equals the oracle's for
     that call's input, and some calls ran as coalesced passes."""
     monkeypatch.setenv("BAND_HIP_COALESCE", "4")
     monkeypatch.setenv("BAND_HIP_COALESCE_LANES", "2")
+    monkeypatch.setenv("BAND_HIP_COALESCE_IO", io)
     buf = getattr(tflite_synth, arch)(np.int8, size=96)
     om = OModel(buf)
     t_in = om.tensors[om.inputs[0]]

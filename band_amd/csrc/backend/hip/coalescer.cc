@@ -1,6 +1,7 @@
 #include "backend/hip/coalescer.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <map>
@@ -42,7 +43,8 @@ std::shared_ptr<JobCoalescer> JobCoalescer::Join(HipModelExecutor* e, interface:
       c->num_lanes_ = std::max(1, lanes);
       c->ordinal_ = ordinal;
       for (int l = 0; l < c->num_lanes_; ++l) c->free_lanes_.push_back(l);
-      if (const char* io = std::getenv("BAND_HIP_COALESCE_IO")) c->dma_io_ = std::string(io) != "copy";
+      if (const char* io = std::getenv("BAND_HIP_COALESCE_IO")) c->dma_io_ = std::string(io) == "dma";
+      if (const char* w = std::getenv("BAND_HIP_COALESCE_WAIT_US")) c->wait_us_ = std::max(0, std::atoi(w));
       slot = c;
     }
   }
@@ -158,8 +160,17 @@ void JobCoalescer::Account(int n) {
   g_totals.calls += n;
 }
 
-void JobCoalescer::Dispatch() {
+int JobCoalescer::want() const {
+  return lanes_ready_ && wait_us_ > 0 ? std::max(1, std::min(max_batch_, last_group_)) : 1;
+}
+
+void JobCoalescer::Dispatch(bool force) {
   while (!pending_.empty() && !free_lanes_.empty()) {
+    if (!force && static_cast<int>(pending_.size()) < want()) {
+      pending_.front()->cv.notify_one();  // the head times the wait
+      return;
+    }
+    force = false;
     const int lane = free_lanes_.back();
     free_lanes_.pop_back();
     const int n = lanes_ready_ ? std::min<int>(max_batch_, static_cast<int>(pending_.size())) : 1;
@@ -181,12 +192,34 @@ void JobCoalescer::Dispatch() {
   }
 }
 
+void JobCoalescer::Release(Group* g) {
+  free_lanes_.push_back(g->lane);
+  last_group_ = g->n;
+  delete g;
+  Dispatch();
+}
+
 absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
   Member me{e, sg};
   std::unique_lock<std::mutex> lock(mu_);
   pending_.push_back(&me);
   Dispatch();
-  me.cv.wait(lock, [&] { return me.group != nullptr; });
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(wait_us_);
+  while (!me.group) {
+    if (pending_.front() == &me && !free_lanes_.empty()) {
+      // a lane is free but fewer calls are queued than the last group had:
+      // wait (bounded) for the rest of them, then take what is there
+      if (!me.cv.wait_until(lock, deadline, [&] {
+            return me.group != nullptr || static_cast<int>(pending_.size()) >= want() || free_lanes_.empty();
+          })) {
+        if (!me.group) Dispatch(true);
+      } else if (!me.group) {
+        Dispatch();
+      }
+    } else {
+      me.cv.wait(lock);
+    }
+  }
   Group* g = me.group;
 
   if (g->n == 1) {
@@ -194,9 +227,7 @@ absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
     lock.unlock();
     absl::Status s = e->RunPass(sg);
     lock.lock();
-    free_lanes_.push_back(g->lane);
-    delete g;
-    Dispatch();
+    Release(g);
     return s;
   }
 
@@ -235,11 +266,7 @@ absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
       g->cv.wait(lock, [&] { return g->finished; });
     }
     absl::Status status = g->status;
-    if (--g->outputs_left == 0) {
-      free_lanes_.push_back(g->lane);
-      delete g;
-      Dispatch();
-    }
+    if (--g->outputs_left == 0) Release(g);
     return status;
   }
   lock.unlock();
@@ -282,12 +309,7 @@ absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
       std::memcpy(sg->host.at(sg->outputs[k])->data(), v->GetData(), out_bytes_[k]);
     }
   lock.lock();
-  if (--g->outputs_left == 0) {
-    // the lane's staging is free again
-    free_lanes_.push_back(g->lane);
-    delete g;
-    Dispatch();
-  }
+  if (--g->outputs_left == 0) Release(g);  // the lane's staging is free again
   return status;
 }
 

@@ -107,8 +107,16 @@ class JobCoalescer {
 
   JobCoalescer() = default;
   absl::Status BuildLanes(HipModelExecutor* e, interface::IModel* model, const SubgraphKey& key);
-  // forms groups from the queue while a lane is free (mu_ held)
-  void Dispatch();
+  // forms groups from the queue while a lane is free (mu_ held).  Unless
+  // `force`, a group waits for want() queued calls: the head of the queue
+  // then waits up to wait_us_ for more (JobCoalescer::Run) before it forces
+  // a smaller one
+  void Dispatch(bool force = false);
+  // calls a free lane waits for: the size of the group that finished last
+  // (its members are the calls coming back next), at most max_batch_
+  int want() const;
+  // releases a finished group's lane (mu_ held)
+  void Release(Group* g);
   void Account(int n);
 
   mutable std::mutex mu_;
@@ -119,12 +127,17 @@ class JobCoalescer {
   bool lanes_ready_ = false;
   bool build_failed_ = false;  // also set while the one build runs
   int max_batch_ = 16;
-  int num_lanes_ = 2;
-  // BAND_HIP_COALESCE_IO: "dma" (default) - the leader DMAs each member's
-  // page-locked views straight into / out of the lane's arena (no host
-  // copies; n small DMAs per tensor); "copy" - each member memcpys its job
-  // into / out of the lane's staging and the lane moves the batch in one DMA
-  bool dma_io_ = true;
+  int num_lanes_ = 1;
+  // BAND_HIP_COALESCE_IO: "copy" (default) - each member memcpys its job
+  // into / out of the lane's staging and the lane moves the batch in one
+  // DMA; "dma" - the leader DMAs each member's page-locked views straight
+  // into / out of the lane's arena (no host copies; n small DMAs per tensor:
+  // less CPU, 5-10 % less throughput on the C3 mix, profiles/r05b_*)
+  bool dma_io_ = false;
+  // BAND_HIP_COALESCE_WAIT_US (default 100): how long a free lane waits for
+  // want() calls; 0 = dispatch whatever is queued at once
+  int wait_us_ = 100;
+  int last_group_ = 1;  // size of the group that released its lane last
   int ordinal_ = -1;
   std::vector<size_t> in_bytes_, out_bytes_;  // per boundary tensor, one job
   Stats stats_;

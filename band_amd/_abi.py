@@ -211,6 +211,7 @@ KERNEL_SYMBOLS = {
     "bh_conv_group_plan": (c_int, [ctypes.POINTER(ConvParams), c_int, c_void_p, ctypes.POINTER(ConvGroup)]),
     "bh_conv_group_i8": (c_int, [ctypes.POINTER(ConvGroup), c_void_p]),
     "bh_conv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(ConvParams)]),
+    "bh_conv_gemm_big_config": (ctypes.c_int, [ctypes.c_long, ctypes.c_int]),
     "bh_dwconv2d_i8_kernel": (ctypes.c_char_p, [ctypes.POINTER(DwConvParams)]),
     "bh_lut_u8": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),
     "bh_lut_f32": (c_int, [c_void_p, c_void_p, ctypes.c_long, c_void_p, c_void_p]),

@@ -684,6 +684,7 @@ int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s);
 int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s);    // conv_direct.hip
 int bh_conv_rows_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);  // conv_rows.hip
 int bh_conv_xs_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);    // conv_rows.hip
+int bh_conv_gemm_big_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  // conv_gemm_big.hip
 
 namespace {
 // batched 1x1 layers (K <= 320) at or above this many output pixels take the
@@ -725,7 +726,7 @@ double GemmMinOps() {
   return v;
 }
 
-enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm };
+enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm, kGemmBig };
 
 Route route(const bh_conv_params& p, long M, int K, int N) {
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
@@ -746,6 +747,9 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
                        K % 16 == 0 && aligned && ((uintptr_t)p.input & 15) == 0;
   if (p.kernel_hint == BH_CONV_MFMA) return kMfma;
   if (p.kernel_hint == BH_CONV_GEMM) return gemm_ok ? kGemm : kMfma;
+  if (p.kernel_hint == BH_CONV_GEMM_BIG) return gemm_ok ? kGemmBig : kMfma;
+  // the 256-row tiles once the layer fills the chip with them (B = 32 / 256 passes)
+  if (gemm_ok && GemmMode() > 0 && bh_conv_gemm_big_config(M, N) != 0) return kGemmBig;
   if (gemm_ok && GemmMode() > 0 && (GemmMode() == 2 || 2.0 * M * N * K >= GemmMinOps())) return kGemm;
   return kMfma;
 }
@@ -754,7 +758,8 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
 extern "C" const char* bh_conv2d_i8_kernel(const bh_conv_params* p) {
   if (!p) return "";
   static const char* const names[] = {"conv_direct_kernel", "conv_stem_kernel", "conv_xs_kernel",
-                                      "conv_rows_kernel", "conv_mfma_kernel", "conv_gemm_kernel"};
+                                      "conv_rows_kernel", "conv_mfma_kernel", "conv_gemm_kernel",
+                                      "conv_gemm_big_kernel"};
   return names[route(*p, (long)p->batch * p->out_h * p->out_w, p->k_h * p->k_w * p->in_c, p->out_c)];
 }
 
@@ -884,6 +889,7 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
     case kXs: return bh_conv_xs_launch(p, M, K, N, s);
     case kRows: return bh_conv_rows_launch(p, M, K, N, s);
     case kGemm: return bh::launch_gemm_shape(p, M, K, s);
+    case kGemmBig: return bh_conv_gemm_big_launch(p, M, K, s);
     case kMfma: break;
   }
   if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);

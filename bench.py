@@ -103,7 +103,7 @@ def parse():
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
     p.add_argument("--no-batch1", action="store_true",
                    help="skip the one-job-per-pass (Band semantics) line reported beside a job-batched run")
-    p.add_argument("--band1-workers", type=int, default=8,
+    p.add_argument("--band1-workers", type=int, default=48,
                    help="GPU workers per GPU of the band_one_job_per_pass line (Band's own contract)")
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "

@@ -51,11 +51,69 @@ def test_conv1x1_gemm_vs_mfma(gpu_lib, b, spatial, ic, oc):
     rng = np.random.default_rng(6000 + b + spatial + ic + oc)
     c = ConvCase(rng, b, spatial, spatial, ic, oc, 1, 1, act=3)
     ref = c.oracle()
-    for hint in (2, 1):  # BH_CONV_GEMM, BH_CONV_MFMA
+    for hint in (3, 2, 1):  # BH_CONV_GEMM_BIG, BH_CONV_GEMM, BH_CONV_MFMA
         c.kernel_hint = hint
         for fast in (None, False):
             c.requant_fast = fast
             np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="hint %d fast %s" % (hint, fast))
+
+
+# conv_gemm_big_kernel at the sizes it is routed to (M in the tens of
+# thousands: job batches of 32 / 256): MobileNetV2's 320 -> 1280 head at
+# B = 256, K < 64, N not a multiple of 16 / of the tile, M tails
+@pytest.mark.parametrize("b,spatial,ic,oc", [
+    (256, 7, 320, 1280), (256, 14, 64, 256), (64, 28, 32, 512), (300, 7, 48, 1000), (257, 13, 16, 120)])
+def test_conv1x1_gemm_big_routed(gpu_lib, b, spatial, ic, oc):
+    rng = np.random.default_rng(6100 + b + spatial + ic + oc)
+    c = ConvCase(rng, b, spatial, spatial, ic, oc, 1, 1, act=3)
+    ref = c.oracle()
+    keep = []
+    p = c.params(gpu_lib, keep)
+    assert gpu_lib.bh_conv2d_i8_kernel(ctypes.byref(p)).decode() == (
+        "conv_gemm_big_kernel" if gpu_lib.bh_conv_gemm_big_config(b * spatial * spatial, oc) else "conv_gemm_kernel")
+    del keep
+    for fast in (None, False):
+        c.requant_fast = fast
+        np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="fast %s" % fast)
+
+
+# the big GEMM's folded residual ADD and 8-bit output table, applied per byte
+# on its copy-out path (conv_store4's arithmetic): against the oracle's conv
+# -> ADD -> table, and against conv_mfma_kernel on the same parameters
+@pytest.mark.parametrize("b,spatial,ch", [(8, 14, 256), (3, 9, 96), (16, 7, 160)])
+def test_conv1x1_gemm_big_residual_table(gpu_lib, b, spatial, ch):
+    from band_amd import _abi
+    from band_amd.device import DeviceBuffer
+    rng = np.random.default_rng(6200 + b + spatial + ch)
+    c = ConvCase(rng, b, spatial, spatial, ch, ch, 1, 1, act=0)
+    y = c.oracle()
+    r = rng.integers(-128, 128, y.shape).astype(np.int8)
+    r_scale, r_zp = 0.037, int(rng.integers(-10, 10))
+    o_scale, o_zp = 0.051, int(rng.integers(-10, 10))
+    prm = orc.add_params(c.out_scale, r_scale, o_scale)
+    amin, amax = orc.act_range(1, o_scale, o_zp, True)  # RELU on the ADD
+    z = orc.add(y, r, a_zp=c.out_zp, b_zp=r_zp, out_zp=o_zp, params=prm, amin=amin, amax=amax)
+    table = rng.permutation(256).astype(np.uint8)
+    ref = table[z.view(np.uint8)].view(np.int8)
+    outs = {}
+    for hint in (3, 1):
+        keep = []
+        p = c.params(gpu_lib, keep)
+        dr = DeviceBuffer.from_array(r)
+        dt = DeviceBuffer.from_array(table)
+        keep += [dr, dt]
+        p.residual, p.out_table = dr.value, dt.value
+        p.add_left_shift = int(prm[6])
+        p.add_y_off, p.add_r_off, p.add_o_off = -c.out_zp, -r_zp, o_zp
+        p.add_y_mult, p.add_y_shift = int(prm[0]), int(prm[1])
+        p.add_r_mult, p.add_r_shift = int(prm[2]), int(prm[3])
+        p.add_o_mult, p.add_o_shift = int(prm[4]), int(prm[5])
+        p.add_act_min, p.add_act_max = amin, amax
+        p.kernel_hint = hint
+        _abi.check(gpu_lib.bh_conv2d_i8(ctypes.byref(p), None), "bh_conv2d_i8")
+        outs[hint] = c._dy.download(np.int8, y.shape)
+        del keep
+        np.testing.assert_array_equal(outs[hint], ref, err_msg="hint %d" % hint)
 
 
 # the RGB stem kernel (conv_stem_kernel: aligned row gathers + byte path at

@@ -1312,7 +1312,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 6;
+constexpr int kChainTuneVersion = 7;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1617,9 +1617,12 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
         // {.., tile 3 / 4}: runs of 2 / 4 tiles per workgroup, the constant
         // block staged once per run
-        const int forms[12][5] = {{4, 4, 0, 0, 0}, {2, 4, 0, 0, 0}, {1, 4, 0, 0, 0}, {1, 8, 0, 0, 0},
-                                  {1, 16, 0, 0, 0}, {4, 4, 1, 0, 0}, {4, 4, 0, 1, 0}, {4, 4, 0, 3, 0},
-                                  {4, 4, 0, 4, 0}, {2, 4, 0, 0, 1}, {1, 4, 0, 0, 1}, {1, 8, 0, 0, 1}};
+        // {.., split}: the second 1x1's channel tiles over 2 workgroups per
+        // pixel block (3-launch form only)
+        const int forms[15][6] = {{4, 4, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0},
+                                  {1, 16, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0}, {4, 4, 0, 1, 0, 0}, {4, 4, 0, 3, 0, 0},
+                                  {4, 4, 0, 4, 0, 0}, {2, 4, 0, 0, 1, 0}, {1, 4, 0, 0, 1, 0}, {1, 8, 0, 0, 1, 0},
+                                  {1, 4, 0, 0, 0, 2}, {1, 8, 0, 0, 0, 2}, {2, 4, 0, 0, 0, 2}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
@@ -1631,6 +1634,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             q.persist = pw[2];
             q.tile = pw[3];
             q.deep = pw[4];
+            q.c_split = pw[5];
+            if (pw[5] > 1 && form != 0) continue;
             if (bh_chain_lds_bytes(&q) == 0) continue;
             if (q.tile && !PackChainTile(&q, sg)) continue;
             Launch F;
@@ -1642,7 +1647,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
                        (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
-                       (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0);
+                       (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) +
+                       (pw[5] == 2 ? 2000 : 0);
             }
           }
         }
@@ -1657,7 +1663,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
     // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
-    // tiles, +1000 for the deep-issue form
+    // tiles, +1000 for the deep-issue form, +2000 for the 2-way phase-C split
+    const int c_split = choice >= 2000 ? 2 : 0;
+    choice %= 2000;
     const int deep = choice >= 1000 ? 1 : 0;
     choice %= 1000;
     const bool three = choice > 0 && choice % 100 < 10;
@@ -1674,6 +1682,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
     F.chain.tile = choice >= 400 && choice < 800 ? choice / 100 - 3 : 0;
     F.chain.deep = deep;
+    F.chain.c_split = c_split;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then
     if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {

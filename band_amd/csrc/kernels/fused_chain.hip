@@ -156,6 +156,22 @@ __device__ __forceinline__ void copy_out(const unsigned char* src, uint8_t* dst,
     *(uint32_t*)(dst + n16 * 16 + threadIdx.x * 4) = *(const uint32_t*)(src + n16 * 16 + threadIdx.x * 4);
 }
 
+// A channel slice [c0, c0 + cw) of `rows` staged pixels (row stride Nc)
+// to HBM (the split phase C: each workgroup stores its channel tiles)
+__device__ __forceinline__ void copy_out_slice(const unsigned char* src, uint8_t* dst, int Nc, int c0, int cw,
+                                               int rows) {
+  const bool v16 = ((c0 | cw | Nc) & 15) == 0;
+  const int u = v16 ? cw >> 4 : cw >> 2;  // units per pixel (cw % 4 == 0)
+  const float rcp = 1.0f / (float)u;
+  for (int i = threadIdx.x; i < rows * u; i += blockDim.x) {
+    const int r = (int)(((float)i + 0.5f) * rcp);
+    const int k = i - r * u;
+    const long o = (long)r * Nc + c0;
+    if (v16) *(v4i*)(dst + o + k * 16) = *(const v4i*)(src + o + k * 16);
+    else *(uint32_t*)(dst + o + k * 4) = *(const uint32_t*)(src + o + k * 4);
+  }
+}
+
 // The non-persistent chain computes every GEMM UNtransposed, D = X W^T:
 // lane (r16, g) of v_mfma_i32_16x16x64_i8 ends with D[4g + r][r16], i.e.
 // FOUR PIXELS of ONE channel.  The channel's requantisation constants
@@ -195,11 +211,11 @@ __device__ __forceinline__ v4i gemm_tile_nt(const bh_conv_params& c, const unsig
 // finishes a tile for this lane's channel n (may be >= out_c).
 template <int KMAX, int TT = 2, typename Epi>
 __device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsigned char* xrow, int KS, int t0,
-                                           int tstep, int r16, int g, Epi&& epi) {
+                                           int tstep, int r16, int g, Epi&& epi, int t_end = -1) {
   v4i x[KMAX];
 #pragma unroll
   for (int k = 0; k < KMAX; ++k) x[k] = k < KS ? *(const v4i*)(xrow + k * 64) : (v4i){0, 0, 0, 0};
-  const int T = (c.out_c + 15) >> 4;
+  const int T = t_end >= 0 ? t_end : (c.out_c + 15) >> 4;
   for (int t = t0; t < T; t += TT * tstep) {
     int tt[TT], nn[TT], mu[TT], sh[TT];
     v4i w[TT][KMAX], acc[TT];
@@ -236,15 +252,15 @@ __device__ __forceinline__ void gemm_xs_nt(const bh_conv_params& c, const unsign
 // shift) finishes channel n for the 4 pixel blocks.
 template <int KMAX, typename Epi>
 __device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsigned char* base, int stride, int KS,
-                                            int wave, int r16, int g, Epi&& epi) {
+                                            int wave, int r16, int g, Epi&& epi, int t_begin = 0, int t_end = -1) {
   v4i x[4][KMAX];
 #pragma unroll
   for (int pb = 0; pb < 4; ++pb)
 #pragma unroll
     for (int k = 0; k < KMAX; ++k)
       x[pb][k] = k < KS ? *(const v4i*)(base + (pb * 16 + r16) * stride + g * 16 + k * 64) : (v4i){0, 0, 0, 0};
-  const int T = (c.out_c + 15) >> 4;
-  for (int t = wave; t < T; t += 4) {
+  const int T = t_end >= 0 ? t_end : (c.out_c + 15) >> 4;
+  for (int t = t_begin + wave; t < T; t += 4) {
     const int n = t * 16 + r16;
     const int nl = n < c.out_c ? n : 0;
     const int8_t* wrow = c.weights + (long)(t * 16 + r16) * c.k_pad + g * 16;
@@ -407,7 +423,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int KS1 = a.k_pad >> 6;
     const unsigned char* xrow = dl + prow * S1 + g * 16;
     const uint8_t* res = (const uint8_t*)a.residual;
-    const bool out1 = a.output != nullptr;
+    const bool out1 = a.output != nullptr && blockIdx.y == 0;  // split: slice 0 stores it
     auto epi = [&](int t, int n, v4i acc, int mu, int sh) {
       if (n >= N1) return;
       const ChanQ q = chan_q(mu, sh, a.out_zp);
@@ -469,7 +485,8 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
   }
   __syncthreads();
   CHAIN_STAMP(2)
-  if (cp.pw1.output) copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
+  if (cp.pw1.output && blockIdx.y == 0)
+    copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
   CHAIN_STAMP(3)
   if (!cp.has_pw2) return;
 
@@ -479,6 +496,9 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
     const unsigned char* xrow = pl + prow * S2 + g * 16;
+    // split (grid.y > 1): this workgroup's channel tiles [t_lo, t_hi)
+    const int T2 = (N2 + 15) >> 4;
+    const int t_lo = (int)blockIdx.y * T2 / (int)gridDim.y, t_hi = ((int)blockIdx.y + 1) * T2 / (int)gridDim.y;
     if (AM) {
       gemm_xs4_nt<KX>(b, pl, S2, KS2, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
         if (n >= N2) return;
@@ -490,21 +510,30 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
           for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
           stage4(dl, N2, pb4 * 16 + 4 * g, n, v);
         }
-      });
+      }, t_lo, t_hi);
     } else {
-      gemm_xs_nt<KX, TTC>(b, xrow, KS2, wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
+      gemm_xs_nt<KX, TTC>(b, xrow, KS2, t_lo + wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
         if (n >= N2) return;
         const ChanQ q = chan_q(mu, sh, b.out_zp);
         int32_t v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
         stage4(dl, N2, orow, n, v);
-      });
+      }, t_hi);
     }
   }
   __syncthreads();
   CHAIN_STAMP(4)
-  copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
+  if (gridDim.y == 1) {
+    copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
+  } else {
+    const int N2 = cp.pw2.out_c;
+    const int T2 = (N2 + 15) >> 4;
+    const int c_lo = (int)blockIdx.y * T2 / (int)gridDim.y * 16;
+    const int c_hi = min(N2, ((int)blockIdx.y + 1) * T2 / (int)gridDim.y * 16);
+    if (c_hi > c_lo)
+      copy_out_slice(dl, (uint8_t*)cp.pw2.output + (long)m0 * N2, N2, c_lo, c_hi - c_lo, rows);
+  }
   CHAIN_STAMP(5)
 #undef CHAIN_STAMP
 }
@@ -834,8 +863,9 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_w = FastDiv(p.dw.out_w);
   dv.out_h = FastDiv(p.dw.out_h);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
-  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA>), dim3(blocks), dim3(NW * 64), lds, s, p, P, L.S1, L.S2, L.off_pl, L.off_o1,
-            L.off_add, dv);
+  const int split = p.has_pw2 && p.c_split > 1 ? p.c_split : 1;
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA>), dim3(blocks, split), dim3(NW * 64), lds, s, p, P, L.S1, L.S2,
+            L.off_pl, L.off_o1, L.off_add, dv);
 }
 
 template <bool FAST, int KX>
@@ -902,6 +932,8 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   }
   const long widest = std::max<long>(std::max(d.out_c, p.pw1.out_c), p.has_pw2 ? p.pw2.out_c : 0);
   if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
+  if (p.c_split < 0 || p.c_split > 4) return 0;
+  if (p.c_split > 1 && (p.tile || p.persist || !p.has_pw2 || (p.pw2.out_c + 15) / 16 < p.c_split)) return 0;
   if (p.tile) return bh_chain_tile_lds_bytes(pp);
   if (p.deep && (p.persist || !((p.px_blocks == 1 && (p.waves == 0 || p.waves == 4 || p.waves == 8)) ||
                                 (p.px_blocks == 2 && (p.waves == 0 || p.waves == 4)))))

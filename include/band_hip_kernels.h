@@ -395,6 +395,12 @@ typedef struct bh_chain_params {
    * groups per round (instead of 2) and the x-stationary 1x1 GEMMs take 3-6
    * channel tiles per round; px_blocks 1 (4 or 8 waves) or 2 (4 waves) */
   int deep;
+  /* raster forms with a second 1x1 (0 / 1: off): the second 1x1's channel
+   * tiles are split over c_split workgroups per pixel block (grid.y); each
+   * recomputes the depthwise and first 1x1 for its pixels and stores its
+   * channel slice - more, shorter workgroups for the few-pixel 14x14 / 7x7
+   * layers.  2..4 */
+  int c_split;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */

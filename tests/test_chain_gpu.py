@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist, tile, deep)
+    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -218,3 +218,37 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
             got = ex.GetJobSlotView(key, o, 5, s).GetData()
             np.testing.assert_array_equal(got, refs[s][o].reshape(got.shape), err_msg="%s slot %d" % (arch, s))
     ex._model_ref = m
+
+
+@pytest.mark.parametrize("h,ce,s,cout,res,ce2", [c for c in MNV2_CHAINS if c[5]])
+def test_chain_split_phase_c(gpu_lib, h, ce, s, cout, res, ce2):
+    """the second 1x1's channel tiles split over 2 / 3 workgroups per pixel
+    block (c_split, grid.y): every slice recomputes the depthwise and first
+    1x1 and stores its channel range; the first 1x1's output (when stored)
+    comes from slice 0.  Batch 2, 4- and 8-wave and 2-block forms, both
+    requant forms, bit-exact"""
+    import ctypes
+    rng = np.random.default_rng(h * 7 + ce + cout)
+    c = ChainCase(rng, 2, h, h, ce, s, cout, res, ce2, store_pw1=True)
+    for px, waves, split in ((1, 4, 2), (1, 8, 2), (2, 4, 2), (1, 4, 3)):
+        keep = []
+        if gpu_lib.bh_chain_lds_bytes(ctypes.byref(c.params(gpu_lib, px, keep, waves, 0, 0, 0, split))) == 0:
+            continue
+        _check(c, gpu_lib, px, waves, c_split=split)
+    c.fast = False
+    _check(c, gpu_lib, 1, 4, c_split=2)
+
+
+def test_chain_split_rejects(gpu_lib):
+    import ctypes
+    rng = np.random.default_rng(3)
+    keep = []
+    q = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 1, keep, c_split=2)
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) > 0
+    q.c_split = 5  # at most 4
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
+    q.c_split = 4  # 48 channels = 3 tiles < 4 slices
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
+    q.c_split = 2
+    q.persist = 1  # raster forms only
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0

@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,tp,1d,1w8d,2d",
                     help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form, "
-                         "tp = its persistent double-buffered variant, t3 / t4 = runs of 2 / 4 tiles per workgroup")
+                         "tp = its persistent double-buffered variant, t3 / t4 = runs of 2 / 4 tiles per workgroup; "
+                         "sN suffix = the phase-C split over N workgroups")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
@@ -40,13 +41,16 @@ def main():
         c = ChainCase(np.random.default_rng(1), a.batch, h, h, ce, s, cout, res, ce2)
         row = []
         for form in a.px.split(","):
+            split = 0
+            if "s" in form and not form.startswith("t"):  # "1s2": the phase-C split over 2 workgroups
+                form, split = form.split("s")[0], int(form.split("s")[1])
             tile = {"t": 1, "tp": 2, "t3": 3, "t4": 4}.get(form, 0)
             persist = int(form.endswith("p") and not tile)
             deep = int(form.endswith("d"))
             f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves, persist, tile, deep)
+            q = c.params(lib, px, keep, waves, persist, tile, deep, split)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue

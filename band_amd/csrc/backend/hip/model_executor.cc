@@ -582,6 +582,7 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   }
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
+  if (f && std::strcmp(f, "nosplit") == 0) no_split_chain_ = true;  // A-B: without the phase-C split forms
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
@@ -1312,7 +1313,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 7;
+constexpr int kChainTuneVersion = 8;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1617,15 +1618,17 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
         // {.., tile 3 / 4}: runs of 2 / 4 tiles per workgroup, the constant
         // block staged once per run
-        // {.., split}: the second 1x1's channel tiles over 2 workgroups per
-        // pixel block (3-launch form only)
-        const int forms[15][6] = {{4, 4, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0},
+        // {.., split}: the second 1x1's channel tiles over 2..4 workgroups
+        // per pixel block (3-launch form only; BAND_HIP_FUSION=nosplit: none)
+        const int forms[19][6] = {{4, 4, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0},
                                   {1, 16, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0}, {4, 4, 0, 1, 0, 0}, {4, 4, 0, 3, 0, 0},
                                   {4, 4, 0, 4, 0, 0}, {2, 4, 0, 0, 1, 0}, {1, 4, 0, 0, 1, 0}, {1, 8, 0, 0, 1, 0},
-                                  {1, 4, 0, 0, 0, 2}, {1, 8, 0, 0, 0, 2}, {2, 4, 0, 0, 0, 2}};
+                                  {1, 4, 0, 0, 0, 2}, {1, 8, 0, 0, 0, 2}, {2, 4, 0, 0, 0, 2}, {1, 16, 0, 0, 0, 2},
+                                  {1, 4, 0, 0, 0, 3}, {1, 8, 0, 0, 0, 3}, {1, 4, 0, 0, 0, 4}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
+          if (pw[5] && no_split_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;
@@ -1648,7 +1651,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
                        (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
                        (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) +
-                       (pw[5] == 2 ? 2000 : 0);
+                       (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0);
             }
           }
         }
@@ -1663,8 +1666,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
     // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
-    // tiles, +1000 for the deep-issue form, +2000 for the 2-way phase-C split
-    const int c_split = choice >= 2000 ? 2 : 0;
+    // tiles, +1000 for the deep-issue form, +2000 x (s - 1) for the s-way
+    // phase-C split
+    const int c_split = choice >= 2000 ? choice / 2000 + 1 : 0;
     choice %= 2000;
     const int deep = choice >= 1000 ? 1 : 0;
     choice %= 1000;

@@ -222,15 +222,15 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
 
 @pytest.mark.parametrize("h,ce,s,cout,res,ce2", [c for c in MNV2_CHAINS if c[5]])
 def test_chain_split_phase_c(gpu_lib, h, ce, s, cout, res, ce2):
-    """the second 1x1's channel tiles split over 2 / 3 workgroups per pixel
+    """the second 1x1's channel tiles split over 2 / 3 / 4 workgroups per pixel
     block (c_split, grid.y): every slice recomputes the depthwise and first
     1x1 and stores its channel range; the first 1x1's output (when stored)
-    comes from slice 0.  Batch 2, 4- and 8-wave and 2-block forms, both
+    comes from slice 0.  Batch 2, 4-, 8- and 16-wave and 2-block forms, both
     requant forms, bit-exact"""
     import ctypes
     rng = np.random.default_rng(h * 7 + ce + cout)
     c = ChainCase(rng, 2, h, h, ce, s, cout, res, ce2, store_pw1=True)
-    for px, waves, split in ((1, 4, 2), (1, 8, 2), (2, 4, 2), (1, 4, 3)):
+    for px, waves, split in ((1, 4, 2), (1, 8, 2), (2, 4, 2), (1, 16, 2), (1, 4, 3), (1, 8, 3), (1, 4, 4)):
         keep = []
         if gpu_lib.bh_chain_lds_bytes(ctypes.byref(c.params(gpu_lib, px, keep, waves, 0, 0, 0, split))) == 0:
             continue

@@ -4,6 +4,7 @@
 #include <time.h>
 
 #include "backend/hip/affinity.h"
+#include "backend/hip/completion.h"
 
 #include <algorithm>
 #include <chrono>
@@ -88,7 +89,7 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
   if (const char* sy = std::getenv("BAND_HIP_SYNC")) {
     const std::string m(sy);
-    sync_mode_ = m == "block" ? kSyncBlock : (m == "poll" ? kSyncPoll : kSyncSpin);
+    sync_mode_ = m == "block" ? kSyncBlock : m == "poll" ? kSyncPoll : m == "poller" ? kSyncPoller : kSyncSpin;
   }
   block_sync_ = sync_mode_ == kSyncBlock;
   if (const char* d = std::getenv("BAND_HIP_DIRECT_IO")) direct_io_ = d[0] != '0';
@@ -2883,6 +2884,10 @@ absl::Status HipModelExecutor::WaitPass(PreparedSubgraph* sg) {
     return HipErr(1, "event create");
   rc = bh_event_record(done_event_, stream_);
   if (rc) return HipErr(rc, "event record");
+  if (sync_mode_ == kSyncPoller) {  // this GPU's poller thread waits for it (completion.h)
+    rc = CompletionPoller::ForDevice(ordinal_).Wait(done_event_);
+    return rc ? HipErr(rc, "event query") : absl::OkStatus();
+  }
   if (sync_mode_ == kSyncBlock) {
     rc = bh_event_sync(done_event_);
     return rc ? HipErr(rc, "event sync") : absl::OkStatus();

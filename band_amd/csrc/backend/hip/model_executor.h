@@ -292,7 +292,11 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // (WaitPass).  On the C3 mix poll frees ~7 cores but the late wake-ups
   // cost 15-20 % of throughput, and block still spins inside HIP
   // (profiles/r04e_*: spin 83 / 94 k, poll 76 / 78 k, block 79 / 80 k).
-  enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2 };
+  // poller (BAND_HIP_SYNC=poller): the thread parks on a condition variable
+  // and the GPU's CompletionPoller thread (completion.h) wakes it when the
+  // pass's event completes - one polling core per GPU instead of one per
+  // waiting thread.
+  enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2, kSyncPoller = 3 };
   int sync_mode_ = kSyncSpin;
   bool block_sync_ = false;  // sync_mode_ == kSyncBlock
   // waits for everything enqueued on stream_ (the pass of `sg`)

@@ -115,6 +115,8 @@ def parse():
     p.add_argument("--single-engine", action="store_true",
                    help="headline = one process, one Band engine, GPU workers over all --gpus GPUs")
     p.add_argument("--no-single-engine", action="store_true", help="N>1: skip the single-engine line")
+    p.add_argument("--per-process-headline", action="store_true",
+                   help="N>1: keep the per-process line (one engine per GPU) as the headline")
     p.add_argument("--single-engine-wpg", type=int, default=0,
                    help="--single-engine: GPU workers per GPU (default --workers-per-gpu; 1 = one Worker per GPU)")
     p.add_argument("--profile-only", action="store_true",
@@ -864,11 +866,15 @@ def main():
         # N = 1: the headline engine IS the single engine; north_star's one
         # GPU worker per GPU (worker_device_queue) is measured beside it
         single_1wpg = single_engine_line(args, D, paths, sched, 1, 1, n_warm, n_timed)
-    if D.world > 1 and not args.no_single_engine and not poisson and on_gpu:
+    if D.world > 1 and not args.no_single_engine and not poisson:
         D.barrier()  # every rank has closed its engines
         if D.rank == 0:
-            single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world)
-            if W != 1:
+            try:
+                single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world)
+            except Exception as ex:  # the per-process line stays the headline
+                single = {"error": repr(ex)}
+                print("bench: single-engine line failed: %r" % (ex,), file=sys.stderr, flush=True)
+            if W != 1 and "error" not in single:
                 single_1wpg = single_engine_line(args, D, paths, sched, 1, D.world, n_warm, n_timed * D.world)
         D.barrier()
 
@@ -897,6 +903,20 @@ def main():
         total_jobs = n_timed * n_ranks
         value = total_jobs / elapsed if not args.single_engine else single["value"]
         lat_ms = np.array(all_lat) * 1e3 if all_lat else None
+        # N > 1: the headline is C3's own shape - ONE Band engine (one planner
+        # thread, round_robin) whose GPU workers span the N GPUs; the
+        # per-process line (N engines, one per GPU) is reported beside it
+        per_process = None
+        if D.world > 1 and single and "error" not in single and not args.per_process_headline:
+            per_process = {"value": value, "unit": "inferences/s", "engines": D.world, "jobs": total_jobs,
+                           "ms_per_step": elapsed * 1e3 / args.steps,
+                           "p50_job_latency_ms": float(np.percentile(lat_ms, 50)) if lat_ms is not None else None,
+                           "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else None}
+            value = single["value"]
+            elapsed = single["jobs"] / single["value"]
+            total_jobs = single["jobs"]
+            lat_ms = None
+        one_engine = args.single_engine or per_process is not None
         line = {
             "metric": "multi-DNN inferences/sec + p99 job latency, 4-model int8 mix @1/2/4/8 GPU",
             "value": value,
@@ -916,8 +936,8 @@ def main():
             "config": {"workload": workload_label(args, models, n_cpu, W, poisson) + (
                            "; each GPU worker runs up to %d queued jobs of one model as one batched pass "
                            "(job batching)" % args.job_batch if args.job_batch > 1 else ""),
-                       "harness": ("ONE native Band engine over %d GPUs (single planner)" % max(1, args.gpus)
-                                   if args.single_engine else
+                       "harness": ("ONE native Band engine over %d GPUs (single planner)" % max(1, args.gpus, n_ranks)
+                                   if one_engine else
                                    "native Band engine per GPU (planner + workers + %s)" % args.scheduler) +
                                   ", %d requests in flight per engine" % inflight,
                        "step": "%d jobs (%d of each model), round-robin over the models" % (jps, jps // M),
@@ -926,7 +946,7 @@ def main():
                        "max_job_batch": args.job_batch,
                        "share_profiles": bool(args.share_profiles),
                        "model": args.model, "global_batch": n_ranks * W * max(1, args.job_batch), "seq_len": None,
-                       "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus)) if args.single_engine
+                       "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus, n_ranks)) if one_engine
                        else "job-sharded x%d (no collective)" % n_ranks,
                        "hipgraph": not args.no_graph,
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
@@ -940,6 +960,7 @@ def main():
             "device_us_per_model": dev["device_us"] if dev else None,
             "band_one_job_per_pass": batch1,
             "single_engine": single,
+            "per_process": per_process,
             "single_engine_one_worker_per_gpu": single_1wpg,
             "roofline": roof,
             "cpu_baseline": cpu,

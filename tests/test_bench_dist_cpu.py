@@ -2,7 +2,9 @@
 
 The N>1 bench is one process per GPU with no data-path collective: each
 rank serves its own job stream, a gloo group provides only the barrier,
-the max-over-ranks time and the latency gather (bench.py `Dist`).  With
+the max-over-ranks time and the latency gather (bench.py `Dist`); then
+rank 0 runs the headline, ONE engine whose workers span every GPU (C3's
+one-planner shape).  With
 `--device cpu` the same code runs its engine on Band CPU workers, so the
 whole launch / barrier / reduction / JSON contract is exercised here
 without a GPU.
@@ -44,16 +46,25 @@ def test_bench_two_ranks_gloo():
     assert r.returncode == 0, r.stderr[-3000:]
     line = _json_line(r.stdout)
     assert line["n_gpus"] == 2 and line["steps"] == steps and line["scaling"] == "weak"
-    # value = all ranks' jobs / max-over-ranks time; ms_per_step is that time / steps
+    # headline: ONE engine (one planner) whose workers span both devices -
+    # C3's shape; value = its jobs / its time, ms_per_step that time / steps
     elapsed_s = line["ms_per_step"] * steps / 1e3
-    # (a step = --jobs-per-step jobs: 4, one of each mix model)
+    # (a step = --jobs-per-step jobs: 4, one of each mix model, per device)
     assert line["jobs_per_step"] == 4 and line["jobs_timed"] == 2 * 4 * steps
     assert abs(line["value"] - 2 * 4 * steps / elapsed_s) < 1e-6 * line["value"]
-    assert sum(line["config"]["jobs_per_worker_rank0"]) == 4 * steps
+    assert line["single_engine"]["value"] == line["value"] and line["single_engine"]["n_gpus"] == 2
+    assert sum(line["single_engine"]["jobs_per_gpu"]) == 2 * 4 * steps
     assert line["p99_job_latency_ms"] >= line["p50_job_latency_ms"] > 0
+    assert "one engine" in line["config"]["parallelism"]
+    # beside it, the per-process line: each rank's own engine, all ranks'
+    # jobs / max-over-ranks time (gloo barrier + reduction)
+    pp = line["per_process"]
+    assert pp["engines"] == 2 and pp["jobs"] == 2 * 4 * steps and pp["value"] > 0
+    assert abs(pp["value"] - pp["jobs"] / (pp["ms_per_step"] * steps / 1e3)) < 1e-6 * pp["value"]
+    assert pp["p99_job_latency_ms"] >= pp["p50_job_latency_ms"] > 0
+    assert sum(line["config"]["jobs_per_worker_rank0"]) == 4 * steps
     assert line["cpu_baseline"] is None  # rank 0 at N=1 only
     assert line["roofline"] is None  # no GPU kernels on CPU workers
-    assert "no collective" in line["config"]["parallelism"]
 
 
 def test_bench_c1_cpu_worker_line():

@@ -737,14 +737,18 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
     return stem && !std::getenv("BH_CONV_NO_STEM") ? kStem : kDirect;
   }
   const bool aligned = (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.input) & 3) == 0;
-  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0 && aligned && p.kernel_hint == 0) {
-    if (K <= 320 && M >= XsMinM()) return kXs;
-    if (RowsMinM() >= 0 && M >= RowsMinM()) return kRows;
-  }
   // LDS-staged GEMM: int8 activations (glds cannot apply the uint8 XOR),
   // symmetric filters (no row sums), 16-byte K chunks
   const bool gemm_ok = is1x1 && p.stride_h == 1 && p.stride_w == 1 && p.in_xor == 0 && p.w_zp == 0 &&
                        K % 16 == 0 && aligned && ((uintptr_t)p.input & 15) == 0;
+  // (the 256-row GEMM tiles go first where K and N are both wide: there the
+  // layer is MFMA work, not an activation stream)
+  const bool big_first = gemm_ok && GemmMode() > 0 && K >= 128 && N >= 128 && bh_conv_gemm_big_config(M, N) != 0;
+  if (is1x1 && p.stride_h == 1 && p.stride_w == 1 && N % 4 == 0 && K % 4 == 0 && aligned && p.kernel_hint == 0 &&
+      !big_first) {
+    if (K <= 320 && M >= XsMinM()) return kXs;
+    if (RowsMinM() >= 0 && M >= RowsMinM()) return kRows;
+  }
   if (p.kernel_hint == BH_CONV_MFMA) return kMfma;
   if (p.kernel_hint == BH_CONV_GEMM) return gemm_ok ? kGemm : kMfma;
   if (p.kernel_hint == BH_CONV_GEMM_BIG) return gemm_ok ? kGemmBig : kMfma;

@@ -69,12 +69,15 @@ def test_conv1x1_gemm_big_routed(gpu_lib, b, spatial, ic, oc):
     ref = c.oracle()
     keep = []
     p = c.params(gpu_lib, keep)
-    assert gpu_lib.bh_conv2d_i8_kernel(ctypes.byref(p)).decode() == (
-        "conv_gemm_big_kernel" if gpu_lib.bh_conv_gemm_big_config(b * spatial * spatial, oc) else "conv_gemm_kernel")
+    routed = gpu_lib.bh_conv2d_i8_kernel(ctypes.byref(p)).decode()
+    if ic >= 128 and oc >= 128:  # wide K and N: the big tiles (else the activation-stream kernels may win)
+        assert routed == "conv_gemm_big_kernel", routed
     del keep
-    for fast in (None, False):
-        c.requant_fast = fast
-        np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="fast %s" % fast)
+    for hint in (0, 3):  # the routed kernel, then the big GEMM forced
+        c.kernel_hint = hint
+        for fast in (None, False):
+            c.requant_fast = fast
+            np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="hint %d fast %s" % (hint, fast))
 
 
 # the big GEMM's folded residual ADD and 8-bit output table, applied per byte

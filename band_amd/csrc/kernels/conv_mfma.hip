@@ -685,6 +685,8 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  
 int bh_conv_rows_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);  // conv_rows.hip
 int bh_conv_xs_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t s);    // conv_rows.hip
 int bh_conv_gemm_big_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  // conv_gemm_big.hip
+int bh_conv_stem_mfma_ok(const bh_conv_params& p);                                  // conv_stem_mfma.hip
+int bh_conv_stem_mfma_launch(const bh_conv_params& p, int M, hipStream_t s);       // conv_stem_mfma.hip
 
 namespace {
 // batched 1x1 layers (K <= 320) at or above this many output pixels take the
@@ -726,7 +728,7 @@ double GemmMinOps() {
   return v;
 }
 
-enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm, kGemmBig };
+enum Route { kDirect, kStem, kXs, kRows, kMfma, kGemm, kGemmBig, kStemMfma };
 
 Route route(const bh_conv_params& p, long M, int K, int N) {
   const bool is1x1 = p.k_h == 1 && p.k_w == 1 && p.pad_h == 0 && p.pad_w == 0;
@@ -734,7 +736,10 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
   // RGB-stem-like layers (tiny K, byte-granular gather): direct VALU kernel
   if (!is1x1 && K <= 64 && p.in_c < 8) {
     const bool stem = p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && N % 8 == 0 && !p.residual;
-    return stem && !std::getenv("BH_CONV_NO_STEM") ? kStem : kDirect;
+    if (!stem || std::getenv("BH_CONV_NO_STEM")) return kDirect;
+    // the window x filter contraction on MFMA (conv_stem_mfma.hip); the VALU
+    // form when forced (BH_CONV_STEM_VALU) or outside the MFMA form's range
+    return p.kernel_hint != BH_CONV_STEM_VALU && bh_conv_stem_mfma_ok(p) ? kStemMfma : kStem;
   }
   const bool aligned = (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.input) & 3) == 0;
   // LDS-staged GEMM: int8 activations (glds cannot apply the uint8 XOR),
@@ -763,7 +768,7 @@ extern "C" const char* bh_conv2d_i8_kernel(const bh_conv_params* p) {
   if (!p) return "";
   static const char* const names[] = {"conv_direct_kernel", "conv_stem_kernel", "conv_xs_kernel",
                                       "conv_rows_kernel", "conv_mfma_kernel", "conv_gemm_kernel",
-                                      "conv_gemm_big_kernel"};
+                                      "conv_gemm_big_kernel", "conv_stem_mfma_kernel"};
   return names[route(*p, (long)p->batch * p->out_h * p->out_w, p->k_h * p->k_w * p->in_c, p->out_c)];
 }
 
@@ -894,6 +899,7 @@ extern "C" int bh_conv2d_i8(const bh_conv_params* pp, bh_stream_t stream) {
     case kRows: return bh_conv_rows_launch(p, M, K, N, s);
     case kGemm: return bh::launch_gemm_shape(p, M, K, s);
     case kGemmBig: return bh_conv_gemm_big_launch(p, M, K, s);
+    case kStemMfma: return bh_conv_stem_mfma_launch(p, M, s);
     case kMfma: break;
   }
   if (is1x1 && c % 16 == 0) return bh::launch_shape<true, 16>(p, M, K, N, s);

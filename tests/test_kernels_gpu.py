@@ -125,14 +125,19 @@ def test_conv1x1_gemm_big_residual_table(gpu_lib, b, spatial, ch):
 # requantisation paths
 @pytest.mark.parametrize("b,h,w,oc,stride,same,dtype", [
     (2, 224, 224, 32, 2, True, np.int8), (3, 37, 41, 16, 2, True, np.uint8), (1, 15, 13, 24, 1, True, np.int8),
+    (5, 31, 29, 32, 1, True, np.uint8), (24, 224, 224, 32, 2, True, np.int8), (2, 11, 10, 64, 2, False, np.uint8),
     (2, 20, 23, 8, 1, False, np.uint8), (4, 9, 9, 48, 2, False, np.int8), (1, 224, 224, 64, 2, True, np.uint8)])
 def test_conv_stem(gpu_lib, b, h, w, oc, stride, same, dtype):
     rng = np.random.default_rng(5000 + b * h * w + oc + stride)
     c = ConvCase(rng, b, h, w, 3, oc, 3, 3, stride=(stride, stride), same=same, dtype=dtype, act=3)
     ref = c.oracle()
-    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
-    c.requant_fast = False
-    np.testing.assert_array_equal(c.gpu(gpu_lib), ref)
+    # the routed form (conv_stem_mfma_kernel for out_c % 16 == 0, <= 64), then
+    # the VALU form forced (BH_CONV_STEM_VALU = 4); both requantisation paths
+    for hint in (0, 4):
+        c.kernel_hint = hint
+        for fast in (None, False):
+            c.requant_fast = fast
+            np.testing.assert_array_equal(c.gpu(gpu_lib), ref, err_msg="hint %d fast %s" % (hint, fast))
 
 
 def test_conv_first_layer_3x3_s2_int8(gpu_lib):

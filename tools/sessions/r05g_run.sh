@@ -7,11 +7,13 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/r05g
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py -k "stem" tests/test_chain_gpu.py -k "stem or split" > $O/tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_kernels_gpu.py tests/test_chain_gpu.py -k "stem or split" > $O/tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_coalescer_gpu.py > $O/tests_coalescer.log 2>&1 || exit 1
 for r in 1 2; do
   BAND_HIP_FUSION=nosplit timeout -k 10 300 python -u tools/mix_breakdown.py --batch 24 > $O/breakdown_nosplit_r$r.txt 2>&1 || exit 2
   timeout -k 10 300 python -u tools/mix_breakdown.py --batch 24 > $O/breakdown_split_r$r.txt 2>&1 || exit 3
 done
+timeout -k 10 300 python -u tools/mix_breakdown.py --batch 1 --models mobilenet_v2 --top 30 > $O/breakdown_mnv2_b1.txt 2>&1 || exit 9
 B="--no-cpu-baseline --no-roofline --no-batch1 --no-single-engine"
 for r in 1 2; do
   BAND_HIP_FUSION=nosplit timeout -k 10 300 python bench.py $B > $O/bench_nosplit_r$r.json 2> $O/bench_nosplit_r$r.err || exit 4

@@ -401,6 +401,11 @@ def profile_roofline(args, D, models, paths):
     # device-side floor of one job: each model's passes replayed back to back
     # (graph incl. H2D/D2H), no host gaps; the rest of the job latency is
     # host launch + sync wakeup
+    # (one untimed round first: the first replay after an idle GPU runs at a
+    # lower clock - the first model timed read ~2x its eager time,
+    # profiles/r04o_breakdown_b24.txt)
+    for ex, key in execs:
+        ex.TimeSubgraph(key, iters=20)
     device_us = {name: ex.TimeSubgraph(key, iters=100) / B for (name, _), (ex, key) in zip(models, execs)}
     total_us = sum(k["us"] for k in by_k.values())
     ranked = sorted(by_k.items(), key=lambda kv: -kv[1]["us"])

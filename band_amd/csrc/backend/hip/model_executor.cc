@@ -584,6 +584,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
   if (f && std::strcmp(f, "nosplit") == 0) no_split_chain_ = true;  // A-B: without the phase-C split forms
+  if (f && std::strcmp(f, "novalu") == 0) no_valu_chain_ = true;  // A-B: depthwise phase on MFMA only
+  if (f && std::strcmp(f, "forcevalu") == 0) force_chain_ = force_valu_chain_ = true;  // parity: ... VALU depthwise
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
@@ -1314,7 +1316,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 8;
+constexpr int kChainTuneVersion = 9;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -1576,15 +1578,22 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // = px_blocks of the 2-launch form (the second conv stays a launch),
     // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
-    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d", kChainTuneVersion, ordinal_,
+    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d", kChainTuneVersion, ordinal_,
                   tune_batch_ > 0 ? tune_batch_ : D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
-                  ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0);
+                  ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0, no_tile_chain_, no_deep_chain_,
+                  no_split_chain_, no_valu_chain_);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
     if (force_tile_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
       q.tile = tile_pipe_ ? 2 : 1;
       if (bh_chain_lds_bytes(&q) > 0) choice += tile_pipe_ ? 500 : 400;
+    }
+    if (force_valu_chain_) {
+      bh_chain_params q = ok3 ? c3 : c2;
+      q.px_blocks = 4;
+      q.dw_valu = 1;
+      if (bh_chain_lds_bytes(&q) > 0) choice += 8000;
     }
     if (force_deep_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
@@ -1621,15 +1630,22 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // block staged once per run
         // {.., split}: the second 1x1's channel tiles over 2..4 workgroups
         // per pixel block (3-launch form only; BAND_HIP_FUSION=nosplit: none)
-        const int forms[19][6] = {{4, 4, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0},
-                                  {1, 16, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0}, {4, 4, 0, 1, 0, 0}, {4, 4, 0, 3, 0, 0},
-                                  {4, 4, 0, 4, 0, 0}, {2, 4, 0, 0, 1, 0}, {1, 4, 0, 0, 1, 0}, {1, 8, 0, 0, 1, 0},
-                                  {1, 4, 0, 0, 0, 2}, {1, 8, 0, 0, 0, 2}, {2, 4, 0, 0, 0, 2}, {1, 16, 0, 0, 0, 2},
-                                  {1, 4, 0, 0, 0, 3}, {1, 8, 0, 0, 0, 3}, {1, 4, 0, 0, 0, 4}};
+        // {.., valu}: the depthwise phase on VALU (v_dot4 over the tap
+        // table) instead of the block-diagonal MFMA tile (raster forms;
+        // BAND_HIP_FUSION=novalu: none)
+        const int forms[25][7] = {
+            {4, 4, 0, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0, 0},
+            {1, 16, 0, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0, 0}, {4, 4, 0, 1, 0, 0, 0}, {4, 4, 0, 3, 0, 0, 0},
+            {4, 4, 0, 4, 0, 0, 0}, {2, 4, 0, 0, 1, 0, 0}, {1, 4, 0, 0, 1, 0, 0}, {1, 8, 0, 0, 1, 0, 0},
+            {1, 4, 0, 0, 0, 2, 0}, {1, 8, 0, 0, 0, 2, 0}, {2, 4, 0, 0, 0, 2, 0}, {1, 16, 0, 0, 0, 2, 0},
+            {1, 4, 0, 0, 0, 3, 0}, {1, 8, 0, 0, 0, 3, 0}, {1, 4, 0, 0, 0, 4, 0},
+            {4, 4, 0, 0, 0, 0, 1}, {2, 4, 0, 0, 0, 0, 1}, {1, 4, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 0, 1},
+            {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
           if (pw[5] && no_split_chain_) continue;
+          if (pw[6] && no_valu_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;
@@ -1639,6 +1655,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             q.tile = pw[3];
             q.deep = pw[4];
             q.c_split = pw[5];
+            q.dw_valu = pw[6];
             if (pw[5] > 1 && form != 0) continue;
             if (bh_chain_lds_bytes(&q) == 0) continue;
             if (q.tile && !PackChainTile(&q, sg)) continue;
@@ -1652,7 +1669,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
                        (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
                        (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) +
-                       (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0);
+                       (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0) + (pw[6] ? 8000 : 0);
             }
           }
         }
@@ -1668,7 +1685,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
     // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
     // tiles, +1000 for the deep-issue form, +2000 x (s - 1) for the s-way
-    // phase-C split
+    // phase-C split, +8000 for the VALU depthwise phase
+    const int dw_valu = choice >= 8000 ? 1 : 0;
+    choice %= 8000;
     const int c_split = choice >= 2000 ? choice / 2000 + 1 : 0;
     choice %= 2000;
     const int deep = choice >= 1000 ? 1 : 0;
@@ -1688,6 +1707,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.tile = choice >= 400 && choice < 800 ? choice / 100 - 3 : 0;
     F.chain.deep = deep;
     F.chain.c_split = c_split;
+    F.chain.dw_valu = dw_valu;
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then
     if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {

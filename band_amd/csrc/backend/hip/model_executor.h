@@ -270,6 +270,8 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   bool no_tile_chain_ = false;     // BAND_HIP_FUSION=notile: the tuner skips the tile form
   bool no_deep_chain_ = false;     // BAND_HIP_FUSION=nodeep: the tuner skips the deep-issue forms
   bool no_split_chain_ = false;    // BAND_HIP_FUSION=nosplit: the tuner skips the phase-C split forms
+  bool no_valu_chain_ = false;     // BAND_HIP_FUSION=novalu: ... the VALU depthwise forms
+  bool force_valu_chain_ = false;  // BAND_HIP_FUSION=forcevalu: every feasible chain, VALU depthwise (parity)
   bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;

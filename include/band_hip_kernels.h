@@ -402,6 +402,10 @@ typedef struct bh_chain_params {
    * channel slice - more, shorter workgroups for the few-pixel 14x14 / 7x7
    * layers.  2..4 */
   int c_split;
+  /* raster forms (not persistent / tile / deep): the depthwise phase on VALU
+   * (v_dot4 over the tap table, 4 channels of one pixel per item) instead of
+   * the block-diagonal MFMA tile; MFMA then runs only the 1x1 contractions */
+  int dw_valu;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */

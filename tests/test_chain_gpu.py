@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split)
+    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split, dw_valu)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -175,7 +175,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param
@@ -237,6 +237,28 @@ def test_chain_split_phase_c(gpu_lib, h, ce, s, cout, res, ce2):
         _check(c, gpu_lib, px, waves, c_split=split)
     c.fast = False
     _check(c, gpu_lib, 1, 4, c_split=2)
+
+
+@pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)
+def test_chain_valu_depthwise(gpu_lib, h, ce, s, cout, res, ce2):
+    """the depthwise phase on VALU (dw_valu: v_dot4 over the tap table, 4
+    channels of one pixel per item; MFMA only on the 1x1 contractions) in
+    every raster form that admits it, with and without the phase-C split,
+    both requant forms, bit-exact"""
+    import ctypes
+    rng = np.random.default_rng(h * 11 + ce + cout + 5)
+    c = ChainCase(rng, 2, h, h, ce, s, cout, res, ce2, store_pw1=True)
+    for px, waves, split in ((4, 4, 0), (2, 4, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 8, 2)):
+        keep = []
+        q = c.params(gpu_lib, px, keep, waves, 0, 0, 0, split, 1)
+        if gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
+            continue
+        _check(c, gpu_lib, px, waves, c_split=split, dw_valu=1)
+    c.fast = False
+    _check(c, gpu_lib, 4, 4, dw_valu=1)
+    keep = []
+    q = c.params(gpu_lib, 4, keep, 4, 1, 0, 0, 0, 1)  # persistent: no VALU form
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
 
 
 def test_chain_split_rejects(gpu_lib):

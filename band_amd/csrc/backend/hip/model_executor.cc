@@ -585,6 +585,7 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
   if (f && std::strcmp(f, "nosplit") == 0) no_split_chain_ = true;  // A-B: without the phase-C split forms
   if (f && std::strcmp(f, "novalu") == 0) no_valu_chain_ = true;  // A-B: depthwise phase on MFMA only
+  if (f && std::strcmp(f, "r4forms") == 0) no_split_chain_ = no_valu_chain_ = true;  // A-B: round 4's form set
   if (f && std::strcmp(f, "forcevalu") == 0) force_chain_ = force_valu_chain_ = true;  // parity: ... VALU depthwise
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");

@@ -1,71 +1,33 @@
+// HipModelExecutor: the IModelExecutor of the HIP backend (model_executor.h):
+// construction, the op-set support checks, InvestigateModelSpec,
+// PrepareSubgraph, the metadata getters and views, and execution (graph
+// capture / replay, host copies, waits, profiling).  The lowering lives in
+// lower.cc, the fusion passes in fusion.cc, job batching in job_batch.cc.
 #include "backend/hip/model_executor.h"
 
 #include <sys/prctl.h>
 #include <time.h>
 
-#include "backend/hip/affinity.h"
-#include "backend/hip/completion.h"
-
-#include <algorithm>
 #include <chrono>
 #include <limits>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
 #include <mutex>
 #include <unordered_map>
 
-#include "backend/hip/quant.h"
-
-#define RETURN_STATUS_IF(expr)      \
-  do {                              \
-    absl::Status _st = (expr);      \
-    if (!_st.ok()) return _st;      \
-  } while (0)
+#include "backend/hip/affinity.h"
+#include "backend/hip/completion.h"
+#include "backend/hip/executor_internal.h"
 
 namespace band {
 namespace hip {
 
-namespace {
-// set while PrepareJobBatches constructs a variant executor: a kCPU variant
-// then makes no host pool of its own
+using namespace ex;
+
+namespace ex {
 thread_local bool t_variant_ctor = false;
-}  // namespace
+}  // namespace ex
+
 
 const std::vector<int> HipModelExecutor::kEmpty;
-
-namespace {
-
-constexpr size_t kAlign = 256;
-
-bool IsQ8(DataType t) { return t == DataType::kInt8 || t == DataType::kUInt8; }
-
-// zero point in the kernels' int8 domain (uint8 values are XOR 0x80 = x-128)
-int32_t Dom(const TflTensor& t) {
-  const int32_t zp = t.zero_point.empty() ? 0 : static_cast<int32_t>(t.zero_point[0]);
-  return t.type == DataType::kUInt8 ? zp - 128 : zp;
-}
-int32_t Zp(const TflTensor& t) { return t.zero_point.empty() ? 0 : static_cast<int32_t>(t.zero_point[0]); }
-float Scale(const TflTensor& t) { return t.scale.empty() ? 0.0f : t.scale[0]; }
-bool HasQ(const TflTensor& t) { return !t.scale.empty(); }
-
-std::string Hex(uint64_t v) {
-  char b[32];
-  std::snprintf(b, sizeof(b), "%llx", static_cast<unsigned long long>(v));
-  return b;
-}
-
-void Shape4(const std::vector<int>& s, int* out) {
-  const int pad = 4 - static_cast<int>(s.size());
-  for (int i = 0; i < 4; ++i) out[i] = i < pad ? 1 : s[i - pad];
-}
-
-absl::Status HipErr(int rc, const char* what) {
-  return absl::InternalError(std::string("HIP Error: ") + what + " (" + std::to_string(rc) + "): " + bh_last_error());
-}
-
-}  // namespace
 
 HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceFlag device_flag,
                                    CpuSet mask, int num_threads)
@@ -131,221 +93,6 @@ std::unique_ptr<HipModelExecutor> HipModelExecutor::MakeLane() {
   return lane;
 }
 
-namespace {
-// "<conv kernel>+add": a conv launch with the following ADD in its epilogue
-const char* WithAdd(const char* k) {
-  static const char* const names[][2] = {{"conv_mfma_kernel", "conv_mfma_kernel+add"},
-                                         {"conv_xs_kernel", "conv_xs_kernel+add"},
-                                         {"conv_rows_kernel", "conv_rows_kernel+add"},
-                                         {"conv_direct_kernel", "conv_direct_kernel+add"},
-                                         {"conv_stem_kernel", "conv_stem_kernel+add"}};
-  for (const auto& n : names)
-    if (std::strcmp(k, n[0]) == 0) return n[1];
-  return k;
-}
-
-int64_t MaxAbs(const int32_t* v, int n) {
-  int64_t m = 0;
-  for (int i = 0; v && i < n; ++i) m = std::max<int64_t>(m, v[i] < 0 ? -(int64_t)v[i] : (int64_t)v[i]);
-  return m;
-}
-
-// TFLite fp16 post-training quantization keeps constants in float16 behind
-// DEQUANTIZE ops; such a tensor is a constant of the float graph
-const TflOperator* ProducerOf(const TflModel& m, int t) {
-  for (const TflOperator& op : m.ops)
-    for (int o : op.outputs)
-      if (o == t) return &op;
-  return nullptr;
-}
-bool FoldableF16(const TflModel& m, int t) {
-  if (t < 0 || m.tensors[t].type != DataType::kFloat32) return false;
-  const TflOperator* p = ProducerOf(m, t);
-  return p && p->builtin == kTflDequantize && !p->inputs.empty() && p->inputs[0] >= 0 &&
-         m.tensors[p->inputs[0]].is_const() && m.tensors[p->inputs[0]].type == DataType::kFloat16;
-}
-bool ConstFloat(const TflModel& m, int t) {
-  return t >= 0 && ((m.tensors[t].is_const() && m.tensors[t].type == DataType::kFloat32) || FoldableF16(m, t));
-}
-float HalfToFloat(uint16_t h) {
-  const uint32_t sign = (h & 0x8000u) << 16;
-  uint32_t exp = (h >> 10) & 0x1fu, man = h & 0x3ffu, bits;
-  if (exp == 0) {
-    if (man == 0) {
-      bits = sign;
-    } else {  // subnormal: renormalise
-      exp = 127 - 15 + 1;
-      while (!(man & 0x400u)) {
-        man <<= 1;
-        --exp;
-      }
-      bits = sign | (exp << 23) | ((man & 0x3ffu) << 13);
-    }
-  } else if (exp == 31) {
-    bits = sign | 0x7f800000u | (man << 13);
-  } else {
-    bits = sign | ((exp + 127 - 15) << 23) | (man << 13);
-  }
-  float f;
-  std::memcpy(&f, &bits, 4);
-  return f;
-}
-// float values of a ConstFloat tensor
-std::vector<float> FloatData(const TflModel& m, int t) {
-  const TflTensor* src = &m.tensors[t];
-  if (!src->is_const()) src = &m.tensors[ProducerOf(m, t)->inputs[0]];
-  const size_t n = src->num_elements();
-  std::vector<float> v(n);
-  if (src->type == DataType::kFloat32) {
-    std::memcpy(v.data(), src->data, 4 * n);
-  } else {
-    for (size_t i = 0; i < n; ++i) {
-      uint16_t h;
-      std::memcpy(&h, src->data + 2 * i, 2);
-      v[i] = HalfToFloat(h);
-    }
-  }
-  return v;
-}
-// fused activation bounds of a float op (kernels/kernel_util.h
-// CalculateActivationRange)
-void FloatActRange(int act, float* lo, float* hi) {
-  const float inf = std::numeric_limits<float>::infinity();
-  *lo = act == 1 || act == 3 ? 0.f : (act == 2 ? -1.f : -inf);
-  *hi = act == 3 ? 6.f : (act == 2 ? 1.f : inf);
-}
-bool IsFloatOp(const TflModel& m, const TflOperator& op) {
-  if (op.inputs.empty() || op.inputs[0] < 0) return false;
-  const DataType t = m.tensors[op.inputs[0]].type;
-  switch (op.builtin) {
-    case kTflConv2D: case kTflDepthwiseConv2D: case kTflFullyConnected: case kTflAdd: case kTflSub: case kTflMul:
-    case kTflAveragePool2D: case kTflMaxPool2D: case kTflRelu: case kTflRelu6: case kTflReluN1To1:
-    case kTflLogistic: case kTflSoftmax: case kTflSquaredDifference: case kTflRsqrt:
-      return t == DataType::kFloat32;
-    case kTflDequantize:
-      return t == DataType::kFloat16;
-    default:
-      return false;
-  }
-}
-// the float32 op set (fp16-weight models)
-bool FloatSupports(const TflModel& m, const TflOperator& op, std::string* why) {
-  auto no = [&](const char* w) {
-    if (why) *why = w;
-    return false;
-  };
-  const TflTensor& in = m.tensors[op.inputs[0]];
-  const TflTensor& out = m.tensors[op.outputs[0]];
-  if (op.builtin == kTflDequantize)
-    return in.is_const() && out.type == DataType::kFloat32 ? true : no("float16 DEQUANTIZE of a constant only");
-  if (out.type != DataType::kFloat32) return no("float32 output expected");
-  switch (op.builtin) {
-    case kTflConv2D:
-    case kTflDepthwiseConv2D:
-    case kTflFullyConnected: {
-      if (op.inputs.size() < 2 || !ConstFloat(m, op.inputs[1])) return no("filter must be a float constant");
-      if (op.inputs.size() > 2 && op.inputs[2] >= 0 && !ConstFloat(m, op.inputs[2]))
-        return no("bias must be a float constant");
-      const TflTensor& w = m.tensors[op.inputs[1]];
-      if (op.builtin == kTflFullyConnected)
-        return w.shape.size() == 2 && w.shape[1] > 0 && in.num_elements() % w.shape[1] == 0 ? true
-                                                                                          : no("FC weights");
-      if (in.shape.size() != 4 || w.shape.size() != 4 || out.shape.size() != 4) return no("conv needs 4-D");
-      if (op.builtin == kTflConv2D && w.shape[3] != in.shape[3]) return no("grouped conv unsupported");
-      if (op.builtin == kTflDepthwiseConv2D && (in.shape[3] == 0 || w.shape[3] % in.shape[3] != 0))
-        return no("bad depth multiplier");
-      return true;
-    }
-    case kTflAdd:
-    case kTflSub:
-    case kTflMul:
-    case kTflSquaredDifference: {
-      if (op.inputs.size() != 2 || op.inputs[1] < 0) return no("binary op needs 2 inputs");
-      const TflTensor& b = m.tensors[op.inputs[1]];
-      if (b.type != DataType::kFloat32 || in.shape.size() > 4 || b.shape.size() > 4 || out.shape.size() > 4)
-        return no("float32, rank <= 4");
-      int sa[4], sb[4], so[4];
-      Shape4(in.shape, sa);
-      Shape4(b.shape, sb);
-      Shape4(out.shape, so);
-      for (int d = 0; d < 4; ++d)
-        if ((sa[d] != so[d] && sa[d] != 1) || (sb[d] != so[d] && sb[d] != 1)) return no("bad broadcast");
-      return true;
-    }
-    case kTflAveragePool2D:
-    case kTflMaxPool2D:
-      return in.shape.size() == 4 ? true : no("4-D only");
-    case kTflSoftmax:
-      return !in.shape.empty() ? true : no("rank >= 1");
-    default:
-      return true;  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC / RSQRT
-  }
-}
-
-// MIRROR_PAD paddings (constant [rank][2] int32 / int64) and mode
-// (MirrorPadOptions.mode: 0 REFLECT, 1 SYMMETRIC -> bh_pad_params.mode 1 / 2)
-bool MirrorPadArgs(const TflModel& m, const TflOperator& op, std::vector<int64_t>* pads, int* mode) {
-  if (op.inputs.size() < 2 || op.inputs[1] < 0) return false;
-  const TflTensor& in = m.tensors[op.inputs[0]];
-  const TflTensor& pt = m.tensors[op.inputs[1]];
-  if (!pt.is_const() || (pt.type != DataType::kInt32 && pt.type != DataType::kInt64)) return false;
-  const int rank = static_cast<int>(in.shape.size());
-  const size_t eb = pt.type == DataType::kInt64 ? 8 : 4;
-  if (rank < 1 || rank > 4 || pt.data_size < 2 * rank * eb) return false;
-  pads->assign(2 * static_cast<size_t>(rank), 0);
-  for (int i = 0; i < 2 * rank; ++i) {
-    if (eb == 8) {
-      int64_t v;
-      std::memcpy(&v, pt.data + 8 * i, 8);
-      (*pads)[i] = v;
-    } else {
-      int32_t v;
-      std::memcpy(&v, pt.data + 4 * i, 4);
-      (*pads)[i] = v;
-    }
-  }
-  *mode = op.options.valid() && op.options.Int8(0, 0) == 1 ? 2 : 1;
-  for (int dd = 0; dd < rank; ++dd) {
-    const int64_t lim = in.shape[dd] - (*mode == 1 ? 1 : 0);
-    if ((*pads)[2 * dd] < 0 || (*pads)[2 * dd + 1] < 0 || (*pads)[2 * dd] > lim || (*pads)[2 * dd + 1] > lim)
-      return false;
-  }
-  return true;
-}
-
-// MEAN: the reduced axes (constant int32, negatives resolved) must be one
-// contiguous run; 8-bit tensors only in the form TFLite 2.9.2 runs through
-// optimized_integer_ops::Mean / optimized_ops::Mean (4-D, keep_dims, axes
-// {1, 2}), the one restated by CpuMean.
-bool MeanArgs(const TflModel& m, const TflOperator& op, long* outer, long* reduce, long* inner) {
-  if (op.builtin != kTflMean || op.inputs.size() < 2 || op.inputs[1] < 0 || op.outputs.empty()) return false;
-  const TflTensor& in = m.tensors[op.inputs[0]];
-  const TflTensor& out = m.tensors[op.outputs[0]];
-  const TflTensor& ax = m.tensors[op.inputs[1]];
-  if (!ax.is_const() || ax.type != DataType::kInt32 || out.type != in.type) return false;
-  const int rank = static_cast<int>(in.shape.size());
-  std::set<int> axes;
-  for (size_t i = 0; i * 4 < ax.data_size; ++i) {
-    int32_t v;
-    std::memcpy(&v, ax.data + 4 * i, 4);
-    if (v < 0) v += rank;
-    if (v < 0 || v >= rank) return false;
-    axes.insert(v);
-  }
-  if (axes.empty() || *axes.rbegin() - *axes.begin() + 1 != static_cast<int>(axes.size())) return false;
-  if (in.type != DataType::kFloat32) {
-    const bool keep = op.options.valid() && op.options.Int8(0, 0) != 0;
-    if (!IsQ8(in.type) || !HasQ(in) || !HasQ(out) || rank != 4 || !keep || axes != std::set<int>{1, 2}) return false;
-  }
-  *outer = *reduce = *inner = 1;
-  for (int dd = 0; dd < rank; ++dd) {
-    if (dd < *axes.begin()) *outer *= in.shape[dd];
-    else if (dd > *axes.rbegin()) *inner *= in.shape[dd];
-    else *reduce *= in.shape[dd];
-  }
-  return *reduce > 0 && out.num_elements() == static_cast<size_t>(*outer * *inner);
-}
-}  // namespace
 
 bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   auto no = [&](const char* w) {
@@ -501,44 +248,6 @@ bool HipModelExecutor::GpuSupports(const TflModel& m, const TflOperator& op, std
   }
 }
 
-namespace {
-// TFLite_Detection_PostProcess in the form the host kernel implements
-bool DetectionSupported(const TflModel& m, const TflOperator& op, CpuDetectionParams* p) {
-  if (op.builtin != kTflCustom || op.custom_code != "TFLite_Detection_PostProcess") return false;
-  if (op.inputs.size() != 3 || op.outputs.size() != 4) return false;
-  for (int t : op.inputs)
-    if (t < 0) return false;
-  const TflTensor& be = m.tensors[op.inputs[0]];
-  const TflTensor& cs = m.tensors[op.inputs[1]];
-  const TflTensor& an = m.tensors[op.inputs[2]];
-  if (be.type != DataType::kFloat32 || cs.type != DataType::kFloat32 || an.type != DataType::kFloat32 ||
-      !an.is_const())
-    return false;
-  FlexMap f;
-  if (!f.Parse(op.custom_options, op.custom_options_size)) return false;
-  if (f.Number("use_regular_nms", 0) != 0 || f.Number("max_classes_per_detection", 1) != 1) return false;
-  const int n = an.shape.empty() ? 0 : an.shape[0];
-  if (n <= 0 || be.num_elements() != static_cast<size_t>(n) * 4 || cs.num_elements() % n) return false;
-  CpuDetectionParams d{};
-  d.num_boxes = n;
-  d.num_classes = static_cast<int>(f.Number("num_classes", 0));
-  d.num_classes_with_background = static_cast<int>(cs.num_elements() / n);
-  d.max_detections = static_cast<int>(f.Number("max_detections", 0));
-  // options are read with AsFloat (float), detection_postprocess.cc Init()
-  d.score_threshold = static_cast<float>(f.Number("nms_score_threshold", 0));
-  d.iou_threshold = static_cast<float>(f.Number("nms_iou_threshold", 0));
-  d.scale_y = static_cast<float>(f.Number("y_scale", 0));
-  d.scale_x = static_cast<float>(f.Number("x_scale", 0));
-  d.scale_h = static_cast<float>(f.Number("h_scale", 0));
-  d.scale_w = static_cast<float>(f.Number("w_scale", 0));
-  if (d.num_classes <= 0 || d.num_classes > d.num_classes_with_background || d.max_detections <= 0) return false;
-  for (int k = 0; k < 4; ++k)
-    if (m.tensors[op.outputs[k]].type != DataType::kFloat32) return false;
-  if (m.tensors[op.outputs[0]].num_elements() != static_cast<size_t>(d.max_detections) * 4) return false;
-  if (p) *p = d;
-  return true;
-}
-}  // namespace
 
 bool HipModelExecutor::CpuSupports(const TflModel& m, const TflOperator& op, std::string* why) {
   if (GpuSupports(m, op, nullptr)) return true;
@@ -661,1774 +370,6 @@ absl::StatusOr<ModelSpec> HipModelExecutor::InvestigateModelSpec(interface::IMod
                  std::set<int>(d.outputs.begin(), d.outputs.end()), op_in, op_out, unsupported, unavailable);
   spec.path = hm->GetPath();
   return spec;
-}
-
-absl::Status HipModelExecutor::DevicePtr(const HipModel& model, int t, PreparedSubgraph* sg, void** ptr) {
-  const TflTensor& tt = model.desc().tensors[t];
-  if (!tt.is_const()) {
-    auto it = sg->offset.find(t);
-    if (it == sg->offset.end()) return absl::InternalError("tensor without arena slot");
-    *ptr = static_cast<char*>(sg->arena->ptr()) + it->second;
-    return absl::OkStatus();
-  }
-  const std::string key = "m" + Hex(model.serial()) + "/t" + std::to_string(t);
-  auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
-  if (!blob) {
-    blob = std::make_shared<DeviceBlob>(ordinal_, tt.data_size);
-    if (!blob->ok() || !blob->Upload(0, tt.data, tt.data_size))
-      return HipErr(1, "upload constant");
-    DeviceRegistry::Get().PutConst(ordinal_, key, blob);
-  }
-  sg->consts.push_back(blob);
-  *ptr = blob->ptr();
-  return absl::OkStatus();
-}
-
-absl::Status HipModelExecutor::UploadConst(const std::string& key, const void* data, size_t bytes,
-                                           PreparedSubgraph* sg, const void** dev) {
-  auto blob = DeviceRegistry::Get().FindConst(ordinal_, key);
-  if (!blob) {
-    blob = std::make_shared<DeviceBlob>(ordinal_, bytes);
-    if (!blob->ok() || !blob->Upload(0, data, bytes)) return HipErr(1, "upload table");
-    DeviceRegistry::Get().PutConst(ordinal_, key, blob);
-  }
-  sg->consts.push_back(blob);
-  *dev = blob->ptr();
-  return absl::OkStatus();
-}
-
-// TRANSPOSE_CONV (int8; reference_integer_ops::TransposeConv scatters
-// (x - zp) * w into an int32 scratch).  MI355X form: a transpose conv is a
-// stride-1 CONV_2D over the zero-inserted input U (U[y*s][x*s] = x, the input
-// zero point elsewhere, so inserted positions contribute exactly 0) with
-// spatially flipped filters and top/left padding k-1-pad; integer sums are
-// order-free, so the result is bit-identical.  Two launches: zero insertion
-// into a per-subgraph scratch buffer, then the MFMA conv.
-absl::Status HipModelExecutor::LowerTransposeConv(const HipModel& model, int oi, void* out_ptr,
-                                                  const std::string& ckey, PreparedSubgraph* sg, Launch* L) {
-  const TflModel& d = model.desc();
-  const TflOperator& op = d.ops[oi];
-  const TflTensor& w = d.tensors[op.inputs[1]];
-  const TflTensor& x = d.tensors[op.inputs[2]];
-  const TflTensor& out = d.tensors[op.outputs[0]];
-  void* x_ptr = nullptr;
-  RETURN_STATUS_IF(DevicePtr(model, op.inputs[2], sg, &x_ptr));
-  const int32_t* bias = nullptr;
-  if (op.inputs.size() > 3 && op.inputs[3] >= 0) bias = reinterpret_cast<const int32_t*>(d.tensors[op.inputs[3]].data);
-  const FbTable& o = op.options;
-  const bool same = !o.valid() || o.Int8(0, 0) == 0;
-  const int sw = o.valid() ? o.Int(1, 1) : 1, sh = o.valid() ? o.Int(2, 1) : 1;
-  const int b = x.shape[0], ih = x.shape[1], iw = x.shape[2], ic = x.shape[3];
-  const int oc = w.shape[0], kh = w.shape[1], kw = w.shape[2];
-  const int oh = out.shape[1], ow = out.shape[2];
-  if (out.shape[0] != b || out.shape[3] != oc) return absl::InternalError("TRANSPOSE_CONV shape mismatch");
-  // transpose_conv.cc: padding computed as for a conv whose input is the output
-  const int ph = ComputePadding(sh, 1, oh, kh, ComputeOutSize(same, oh, kh, sh, 1));
-  const int pw = ComputePadding(sw, 1, ow, kw, ComputeOutSize(same, ow, kw, sw, 1));
-  const int uh = (ih - 1) * sh + 1, uw = (iw - 1) * sw + 1;
-  // zero-inserted input in a scratch buffer owned by this subgraph
-  auto scratch = std::make_shared<DeviceBlob>(ordinal_, static_cast<size_t>(b) * uh * uw * ic);
-  if (!scratch->ok()) return absl::InternalError("HBM scratch allocation failed");
-  sg->consts.push_back(scratch);
-  Launch Z;
-  Z.kind = Launch::kZeroInsert;
-  Z.op_index = oi;
-  Z.kernel = "zero_insert_kernel";
-  Z.zi = bh_zero_insert_params{};
-  Z.zi.batch = b; Z.zi.in_h = ih; Z.zi.in_w = iw; Z.zi.channels = ic;
-  Z.zi.stride_h = sh; Z.zi.stride_w = sw; Z.zi.out_h = uh; Z.zi.out_w = uw;
-  Z.zi.fill = static_cast<uint32_t>(Zp(x)) & 0xffu;
-  Z.zi.input = x_ptr;
-  Z.zi.output = scratch->ptr();
-  Z.alg_bytes = static_cast<double>(x.num_elements()) + static_cast<double>(b) * uh * uw * ic;
-  sg->launches.push_back(Z);
-  // flipped, packed filters + folded bias (int8 filters: zero point 0)
-  const int K = kh * kw * ic;
-  int kp = 0, np = 0;
-  bh_conv_packed_geometry(oc, K, &kp, &np);
-  const size_t wbytes = static_cast<size_t>(kp) * np;
-  const size_t tbytes = 12ull * oc;
-  std::vector<int32_t> mult, shift;
-  ConvMultipliers(Scale(x), w.scale, oc, Scale(out), false, &mult, &shift);
-  auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
-  if (!blob) {
-    std::vector<int8_t> flipped(static_cast<size_t>(oc) * K);
-    for (int co = 0; co < oc; ++co)
-      for (int fy = 0; fy < kh; ++fy)
-        for (int fx = 0; fx < kw; ++fx)
-          for (int ci = 0; ci < ic; ++ci)
-            flipped[((static_cast<size_t>(co) * kh + fy) * kw + fx) * ic + ci] = static_cast<int8_t>(
-                w.data[((static_cast<size_t>(co) * kh + (kh - 1 - fy)) * kw + (kw - 1 - fx)) * ic + ci]);
-    std::vector<int8_t> packed(wbytes);
-    std::vector<int32_t> tables(3ull * oc);
-    if (bh_pack_conv_weights(flipped.data(), 1, oc, K, kp, np, bias, Zp(x), 0, packed.data(), tables.data()) != 0)
-      return absl::InternalError("weight packing failed");
-    std::copy(mult.begin(), mult.end(), tables.begin() + oc);
-    std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
-    blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-    if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
-        !blob->Upload(wbytes, tables.data(), tbytes))
-      return HipErr(1, "upload transpose-conv operands");
-    DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
-  }
-  sg->consts.push_back(blob);
-  const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
-  bh_conv_params& p = L->conv;
-  p = bh_conv_params{};
-  p.batch = b; p.in_h = uh; p.in_w = uw; p.in_c = ic;
-  p.out_h = oh; p.out_w = ow; p.out_c = oc; p.k_h = kh; p.k_w = kw;
-  p.stride_h = 1; p.stride_w = 1; p.dil_h = 1; p.dil_w = 1;
-  p.pad_h = kh - 1 - ph; p.pad_w = kw - 1 - pw;
-  p.k_pad = kp; p.n_pad = np; p.in_xor = 0;
-  p.in_zp = Zp(x); p.w_zp = 0; p.out_zp = Zp(out); p.act_min = -128; p.act_max = 127;
-  p.input = scratch->ptr(); p.output = out_ptr;
-  p.weights = static_cast<const int8_t*>(blob->ptr());
-  p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
-  p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, K, MaxAbs(bias, oc));
-  L->kind = Launch::kConv;
-  L->kernel = bh_conv2d_i8_kernel(&p);
-  const double M = static_cast<double>(b) * oh * ow;
-  L->alg_ops = 2.0 * M * oc * K;
-  L->alg_bytes = static_cast<double>(b) * uh * uw * ic + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
-  return absl::OkStatus();
-}
-
-// Glue ops.  Every 8-bit unary op becomes a 256-entry
-// table built here with TFLite's formula (quant.cc), so the device does a
-// byte gather; index maps TFLite computes in float are tabulated here too.
-absl::Status HipModelExecutor::LowerGlue(const HipModel& model, int oi, void* in_ptr, void* out_ptr,
-                                         const std::string& ckey, PreparedSubgraph* sg, Launch* L) {
-  const TflModel& d = model.desc();
-  const TflOperator& op = d.ops[oi];
-  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
-  const TflTensor& in = T(op.inputs[0]);
-  const TflTensor& out = T(op.outputs[0]);
-  const bool i8 = in.type == DataType::kInt8;
-  const double in_bytes = static_cast<double>(meta_[op.inputs[0]]->bytes);
-  const double out_bytes = static_cast<double>(meta_[op.outputs[0]]->bytes);
-  L->alg_bytes = in_bytes + out_bytes;
-  switch (op.builtin) {
-    case kTflQuantize:
-    case kTflRelu:
-    case kTflRelu6:
-    case kTflReluN1To1:
-    case kTflLogistic:
-    case kTflHardSwish: {
-      L->src = in_ptr;
-      L->dst = out_ptr;
-      L->count = static_cast<long>(out.num_elements());
-      if (op.builtin == kTflQuantize && in.type == DataType::kFloat32) {
-        L->kind = Launch::kQuantF32;
-        L->kernel = "quantize_f32_kernel";
-        L->q_scale = Scale(out);
-        L->q_zp = Zp(out);
-        L->q_signed = out.type == DataType::kInt8 ? 1 : 0;
-        return absl::OkStatus();
-      }
-      uint8_t table[256];
-      if (op.builtin == kTflQuantize) {
-        RequantizeTable(i8, Scale(in), Zp(in), out.type == DataType::kInt8, Scale(out), Zp(out), table);
-      } else if (op.builtin == kTflLogistic) {
-        LogisticTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), table);
-      } else if (op.builtin == kTflHardSwish) {
-        if (!HardSwishTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), table))
-          return absl::InternalError("HARD_SWISH: output multiplier exponent > 0");
-      } else {
-        const float lo = op.builtin == kTflReluN1To1 ? -1.0f : 0.0f;
-        const float hi = op.builtin == kTflRelu6 ? 6.0f : 1.0f;
-        ReluTable(i8, Scale(in), Zp(in), Scale(out), Zp(out), lo, hi, op.builtin == kTflRelu, table);
-      }
-      RETURN_STATUS_IF(UploadConst(ckey + "/lut", table, sizeof(table), sg, &L->table));
-      L->kind = Launch::kLutU8;
-      L->kernel = "lut_u8_kernel";
-      return absl::OkStatus();
-    }
-    case kTflDequantize: {
-      float table[256];
-      DequantizeTable(i8, Scale(in), Zp(in), table);
-      RETURN_STATUS_IF(UploadConst(ckey + "/lut", table, sizeof(table), sg, &L->table));
-      L->kind = Launch::kLutF32;
-      L->kernel = "lut_f32_kernel";
-      L->src = in_ptr;
-      L->dst = out_ptr;
-      L->count = static_cast<long>(out.num_elements());
-      return absl::OkStatus();
-    }
-    case kTflSoftmax: {
-      const float beta = op.options.valid() ? op.options.Float(0, 1.0f) : 1.0f;
-      float table[256];
-      SoftmaxExpTable(Scale(in), beta, table);
-      const void* dt = nullptr;
-      RETURN_STATUS_IF(UploadConst(ckey + "/exp", table, sizeof(table), sg, &dt));
-      bh_softmax_params& p = L->softmax;
-      p = bh_softmax_params{};
-      p.depth = in.shape.back();
-      p.rows = static_cast<long>(in.num_elements() / std::max(p.depth, 1));
-      p.is_signed = i8 ? 1 : 0;
-      p.table = static_cast<const float*>(dt);
-      p.out_scale = Scale(out);
-      p.out_zp = Zp(out);
-      p.input = in_ptr;
-      p.output = out_ptr;
-      L->kind = Launch::kSoftmax;
-      L->kernel = "softmax_kernel";
-      return absl::OkStatus();
-    }
-    case kTflConcatenation: {
-      const int rank = static_cast<int>(out.shape.size());
-      int axis = op.options.valid() ? op.options.Int(0, 0) : 0;
-      if (axis < 0) axis += rank;
-      if (axis < 0 || axis >= rank) return absl::InternalError("CONCATENATION axis out of range");
-      long outer = 1, inner = static_cast<long>(GetDataTypeBytes(out.type));
-      for (int i = 0; i < axis; ++i) outer *= out.shape[i];
-      for (int i = axis + 1; i < rank; ++i) inner *= out.shape[i];
-      bh_concat_params& p = L->concat;
-      p = bh_concat_params{};
-      p.n_inputs = static_cast<int>(op.inputs.size());
-      p.outer = outer;
-      p.output = out_ptr;
-      L->alg_bytes = out_bytes;
-      for (int k = 0; k < p.n_inputs; ++k) {
-        const TflTensor& x = T(op.inputs[k]);
-        void* xp = nullptr;
-        RETURN_STATUS_IF(DevicePtr(model, op.inputs[k], sg, &xp));
-        p.input[k] = xp;
-        p.row[k] = static_cast<long>(x.shape[axis]) * inner;
-        L->alg_bytes += static_cast<double>(meta_.size() > static_cast<size_t>(op.inputs[k]) && meta_[op.inputs[k]]
-                                                ? meta_[op.inputs[k]]->bytes
-                                                : 0);
-        if (out.type == DataType::kUInt8 && (Zp(x) != Zp(out) || Scale(x) != Scale(out))) {
-          uint8_t table[256];
-          ConcatRescaleTable(Scale(x), Zp(x), Scale(out), Zp(out), table);
-          RETURN_STATUS_IF(UploadConst(ckey + "/lut" + std::to_string(k), table, sizeof(table), sg, &p.table[k]));
-        }
-      }
-      L->kind = Launch::kConcat;
-      L->kernel = "concat_kernel";
-      return absl::OkStatus();
-    }
-    case kTflPad:
-    case kTflPadV2:
-    case kTflMirrorPad: {
-      const TflTensor& pt = T(op.inputs[1]);
-      const int rank = static_cast<int>(in.shape.size());
-      std::vector<int64_t> pads(2 * static_cast<size_t>(rank), 0);
-      int mirror = 0;
-      if (op.builtin == kTflMirrorPad && !MirrorPadArgs(d, op, &pads, &mirror))
-        return absl::InternalError("MIRROR_PAD arguments");
-      for (size_t i = 0; !mirror && i < pads.size() && i * (pt.type == DataType::kInt64 ? 8 : 4) < pt.data_size;
-           ++i) {
-        if (pt.type == DataType::kInt64) {
-          int64_t v;
-          std::memcpy(&v, pt.data + 8 * i, 8);
-          pads[i] = v;
-        } else {
-          int32_t v;
-          std::memcpy(&v, pt.data + 4 * i, 4);
-          pads[i] = v;
-        }
-      }
-      bh_pad_params& p = L->pad;
-      p = bh_pad_params{};
-      p.elem_bytes = static_cast<int>(GetDataTypeBytes(in.type));
-      Shape4(in.shape, p.in_shape);
-      const int lead = 4 - rank;
-      for (int dd = 0; dd < rank; ++dd) {
-        p.pad_before[lead + dd] = static_cast<int>(pads[2 * dd]);
-        p.pad_after[lead + dd] = static_cast<int>(pads[2 * dd + 1]);
-      }
-      uint32_t value = 0;
-      if (op.builtin == kTflPadV2 && op.inputs.size() > 2 && op.inputs[2] >= 0) {
-        const TflTensor& cv = T(op.inputs[2]);
-        std::memcpy(&value, cv.data, std::min<size_t>(cv.data_size, p.elem_bytes));
-      } else if (IsQ8(in.type)) {
-        value = static_cast<uint32_t>(Zp(out)) & 0xffu;  // quantized PAD pads with the output zero point
-      }
-      p.value = value;
-      p.mode = mirror;
-      p.input = in_ptr;
-      p.output = out_ptr;
-      L->kind = Launch::kPad;
-      L->kernel = "pad_kernel";
-      return absl::OkStatus();
-    }
-    case kTflResizeNearestNeighbor:
-    case kTflResizeBilinear: {
-      const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], c = in.shape[3];
-      const int oh = out.shape[1], ow = out.shape[2];
-      const bool nearest = op.builtin == kTflResizeNearestNeighbor;
-      const bool ac = op.options.valid() && op.options.Bool(nearest ? 0 : 2, false);
-      const bool hp = op.options.valid() && op.options.Bool(nearest ? 1 : 3, false);
-      if (nearest) {
-        std::vector<int32_t> tab(static_cast<size_t>(oh) + ow);
-        for (int y = 0; y < oh; ++y) tab[y] = NearestNeighborIndex(y, ih, oh, ac, hp);
-        for (int x = 0; x < ow; ++x) tab[oh + x] = NearestNeighborIndex(x, iw, ow, ac, hp);
-        const void* dt = nullptr;
-        RETURN_STATUS_IF(UploadConst(ckey + "/idx", tab.data(), tab.size() * 4, sg, &dt));
-        bh_resize_nearest_params& p = L->rnear;
-        p = bh_resize_nearest_params{};
-        p.batch = b; p.in_h = ih; p.in_w = iw; p.out_h = oh; p.out_w = ow;
-        p.row_bytes = c * static_cast<int>(GetDataTypeBytes(in.type));
-        p.y_index = static_cast<const int32_t*>(dt);
-        p.x_index = static_cast<const int32_t*>(dt) + oh;
-        p.input = in_ptr;
-        p.output = out_ptr;
-        L->kind = Launch::kResizeNearest;
-        L->kernel = "resize_nearest_kernel";
-      } else if (in.type == DataType::kUInt8) {
-        // uint8: optimized_ops::ResizeBilinear's float path
-        std::vector<int32_t> iy, ix;
-        std::vector<float> fy, fx;
-        BilinearFloatTable(ih, oh, ac, hp, &iy, &fy);
-        BilinearFloatTable(iw, ow, ac, hp, &ix, &fx);
-        // one upload: {y_idx, x_idx} int32 then {y_frac, x_frac} float
-        std::vector<int32_t> blob(iy);
-        blob.insert(blob.end(), ix.begin(), ix.end());
-        blob.resize(blob.size() + fy.size() + fx.size());
-        std::memcpy(blob.data() + iy.size() + ix.size(), fy.data(), fy.size() * 4);
-        std::memcpy(blob.data() + iy.size() + ix.size() + fy.size(), fx.data(), fx.size() * 4);
-        const void* dt = nullptr;
-        RETURN_STATUS_IF(UploadConst(ckey + "/tab8", blob.data(), blob.size() * 4, sg, &dt));
-        const int32_t* t32 = static_cast<const int32_t*>(dt);
-        bh_resize_bilinear_u8_params& p = L->rbil8;
-        p = bh_resize_bilinear_u8_params{};
-        p.batch = b; p.in_h = ih; p.in_w = iw; p.channels = c; p.out_h = oh; p.out_w = ow;
-        p.y_idx = t32;
-        p.x_idx = t32 + 2 * oh;
-        p.y_frac = reinterpret_cast<const float*>(t32 + 2 * oh + 2 * ow);
-        p.x_frac = reinterpret_cast<const float*>(t32 + 3 * oh + 2 * ow);
-        p.input = in_ptr;
-        p.output = out_ptr;
-        L->kind = Launch::kResizeBilinearU8;
-        L->kernel = "resize_bilinear_u8_kernel";
-      } else {
-        std::vector<int32_t> ty, tx;
-        BilinearIntegerTable(ih, oh, ac, hp, &ty);
-        BilinearIntegerTable(iw, ow, ac, hp, &tx);
-        ty.insert(ty.end(), tx.begin(), tx.end());
-        const void* dt = nullptr;
-        RETURN_STATUS_IF(UploadConst(ckey + "/tab", ty.data(), ty.size() * 4, sg, &dt));
-        bh_resize_bilinear_params& p = L->rbil;
-        p = bh_resize_bilinear_params{};
-        p.batch = b; p.in_h = ih; p.in_w = iw; p.channels = c; p.out_h = oh; p.out_w = ow;
-        p.y_tab = static_cast<const int32_t*>(dt);
-        p.x_tab = static_cast<const int32_t*>(dt) + 3 * oh;
-        p.input = in_ptr;
-        p.output = out_ptr;
-        L->kind = Launch::kResizeBilinear;
-        L->kernel = "resize_bilinear_kernel";  // (row forms resize_bilinear_rows_kernel / resize_bilinear_cols_kernel when the rows fit LDS)
-      }
-      return absl::OkStatus();
-    }
-    default:
-      return absl::InternalError(std::string("no lowering for ") + TflBuiltinName(op.builtin));
-  }
-}
-
-absl::Status HipModelExecutor::BuildLaunches(const HipModel& model, PreparedSubgraph* sg) {
-  sg->launches.clear();
-  sg->fused_ops.clear();
-  sg->fused_tensors.clear();
-  for (int i : sg->ops) {
-    if (sg->fused_ops.count(i)) continue;
-    RETURN_STATUS_IF(Lower(model, i, sg));
-  }
-  // fused chains / blocks are GPU kernels picked by on-device timing; chains
-  // first (they cut more launches), blocks over what the chains left
-  if (allow_fusion_ && allow_chain_ && device_flag_ == DeviceFlag::kGPU) FuseChains(model, sg);
-  if (allow_fusion_ && allow_irb_ && device_flag_ == DeviceFlag::kGPU) FuseBlocks(model, sg);
-  if (allow_fusion_) FuseGlue(model, sg);
-  if (allow_fusion_ && allow_group_ && device_flag_ == DeviceFlag::kGPU) RETURN_STATUS_IF(GroupConvs(sg));
-  return absl::OkStatus();
-}
-
-namespace {
-// Device pointers a launch reads and writes (tensor bases or slices inside
-// the arena; constants are filtered out by the caller).  false: a launch kind
-// not analysed here - grouping treats it as a barrier.
-bool LaunchIo(const Launch& l, std::vector<const void*>* rd, std::vector<const void*>* wr) {
-  switch (l.kind) {
-    case Launch::kConv:
-      *rd = {l.conv.input, l.conv.residual};
-      *wr = {l.conv.output};
-      return true;
-    case Launch::kDwConv:
-      *rd = {l.dw.input};
-      *wr = {l.dw.output};
-      return true;
-    case Launch::kChain:
-      *rd = {l.chain.dw.input, l.chain.pw1.residual};
-      *wr = {l.chain.pw1.output, l.chain.has_pw2 ? l.chain.pw2.output : nullptr};
-      return true;
-    case Launch::kIrb:
-      *rd = {l.irb.input};
-      *wr = {l.irb.output};
-      return true;
-    case Launch::kFc:
-      *rd = {l.fc.input};
-      *wr = {l.fc.output};
-      return true;
-    case Launch::kEltwise:
-      *rd = {l.elt.a, l.elt.b};
-      *wr = {l.elt.out};
-      return true;
-    case Launch::kPool:
-      *rd = {l.pool.input};
-      *wr = {l.pool.output};
-      return true;
-    case Launch::kLutU8:
-    case Launch::kCopy:
-      *rd = {l.src};
-      *wr = {l.dst};
-      return true;
-    case Launch::kConcat:
-      rd->assign(l.concat.input, l.concat.input + l.concat.n_inputs);
-      *wr = {l.concat.output};
-      return true;
-    case Launch::kConvGroup:
-      rd->clear();
-      wr->clear();
-      for (const bh_conv_params& m : l.members) {
-        rd->push_back(m.input);
-        rd->push_back(m.residual);
-        wr->push_back(m.output);
-      }
-      return true;
-    default:
-      return false;
-  }
-}
-}  // namespace
-
-// Detector and pose heads are many small convs that read feature maps
-// produced long before and write tensors read only at the end (SSD's 12
-// box / class predictors feed two CONCATENATIONs; PoseNet's four heads are
-// the outputs).  Each alone is a dispatch at the ~4 us empty-kernel floor.
-// Walking the launches in order, a conv that routes to the general MFMA
-// kernel joins a pending set instead of being emitted; a later launch that
-// reads or overwrites a pending conv's output, or writes a pending conv's
-// input, first flushes that conv (alone); a launch kind not analysed here
-// flushes everything.  What stays pending to the end of a run is emitted as
-// one conv_group launch at the position of the first launch that needs any
-// of it - every member then still runs after its producers and before its
-// consumers.  Members of a group never read each other's outputs.
-absl::Status HipModelExecutor::GroupConvs(PreparedSubgraph* sg) {
-  // accesses by arena slot (the tensor slot, aliases excluded, holding the
-  // pointer) and byte interval within it: [lo, hi) in every image at
-  // `stride` (0: one interval).  Only conv outputs are known exactly (heads
-  // writing per-image slices of one concatenated tensor must not conflict
-  // with each other); anything else covers its whole slot.
-  std::vector<std::pair<uintptr_t, uintptr_t>> slots;
-  {
-    const uintptr_t base = reinterpret_cast<uintptr_t>(sg->arena->ptr());
-    std::map<size_t, size_t> by_off;
-    for (const auto& kv : sg->offset) {
-      size_t& b = by_off[kv.second];
-      b = std::max(b, meta_[kv.first]->bytes);
-    }
-    for (const auto& kv : by_off) slots.emplace_back(base + kv.first, base + kv.first + kv.second);
-  }
-  struct Acc {
-    int slot;
-    long lo, hi, stride;
-  };
-  constexpr long kAll = std::numeric_limits<long>::max();
-  auto acc_of = [&](const void* p, long bytes, long stride) -> Acc {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    auto it = std::upper_bound(slots.begin(), slots.end(), std::make_pair(a, ~uintptr_t(0)));
-    if (!p || it == slots.begin()) return Acc{-1, 0, 0, 0};
-    --it;
-    if (a >= it->second) return Acc{-1, 0, 0, 0};
-    const long lo = static_cast<long>(a - it->first);
-    return Acc{static_cast<int>(it - slots.begin()), bytes > 0 ? lo : 0, bytes > 0 ? lo + bytes : kAll, stride};
-  };
-  auto accesses = [&](const std::vector<const void*>& ps) {
-    std::vector<Acc> out;
-    for (const void* p : ps) {
-      const Acc a = acc_of(p, 0, 0);
-      if (a.slot >= 0) out.push_back(a);
-    }
-    return out;
-  };
-  auto conv_write = [&](const bh_conv_params& c) {
-    const long hwn = static_cast<long>(c.out_h) * c.out_w * c.out_c;
-    return c.out_img_stride ? acc_of(c.output, hwn, c.out_img_stride) : acc_of(c.output, hwn * c.batch, 0);
-  };
-  auto overlap = [&](const Acc& a, const Acc& b) {
-    if (a.slot != b.slot) return false;
-    if (a.stride != b.stride) return true;  // (per-image vs whole-tensor: conservative)
-    return a.lo < b.hi && b.lo < a.hi;
-  };
-  auto intersects = [&](const std::vector<Acc>& x, const std::vector<Acc>& y) {
-    for (const Acc& a : x)
-      for (const Acc& b : y)
-        if (overlap(a, b)) return true;
-    return false;
-  };
-  struct Pending {
-    Launch l;
-    std::vector<Acc> rd, wr;
-  };
-  std::vector<Launch> out;
-  std::vector<Pending> pending;
-  // emits `set` (mutually independent convs) as one group per window type
-  auto emit = [&](std::vector<Pending>& set) -> absl::Status {
-    for (int one = 1; one >= 0; --one) {
-      std::vector<const Launch*> ms;
-      for (const Pending& p : set) {
-        const bh_conv_params& c = p.l.conv;
-        const int is1 = c.k_h == 1 && c.k_w == 1 && c.pad_h == 0 && c.pad_w == 0;
-        if (is1 == one) ms.push_back(&p.l);
-      }
-      if (ms.empty()) continue;
-      if (ms.size() == 1) {
-        out.push_back(*ms[0]);
-        continue;
-      }
-      Launch G;
-      G.kind = Launch::kConvGroup;
-      G.op_index = ms[0]->op_index;
-      G.out_tensor = ms[0]->out_tensor;
-      G.kernel = "conv_group_kernel";
-      for (const Launch* m : ms) {
-        G.members.push_back(m->conv);
-        G.alg_bytes += m->alg_bytes;
-        G.alg_ops += m->alg_ops;
-      }
-      std::vector<char> host(bh_conv_group_table_bytes(static_cast<int>(ms.size())));
-      if (host.empty() || bh_conv_group_plan(G.members.data(), static_cast<int>(ms.size()), host.data(),
-                                             &G.cgroup) != 0) {
-        for (const Launch* m : ms) out.push_back(*m);  // not groupable after all: keep them
-        continue;
-      }
-      auto blob = std::make_shared<DeviceBlob>(ordinal_, host.size());
-      if (!blob->ok() || !blob->Upload(0, host.data(), host.size())) return HipErr(1, "upload conv group table");
-      sg->consts.push_back(blob);
-      G.cgroup.table = blob->ptr();
-      out.push_back(std::move(G));
-    }
-    set.clear();
-    return absl::OkStatus();
-  };
-  const size_t max_members = 32;
-  for (Launch& l : sg->launches) {
-    std::vector<const void*> rdp, wrp;
-    if (!LaunchIo(l, &rdp, &wrp)) {
-      RETURN_STATUS_IF(emit(pending));
-      out.push_back(std::move(l));
-      continue;
-    }
-    const std::vector<Acc> rd = accesses(rdp);
-    std::vector<Acc> wr = accesses(wrp);
-    if (l.kind == Launch::kConv) {
-      const Acc w = conv_write(l.conv);
-      wr.clear();
-      if (w.slot >= 0) wr.push_back(w);
-    }
-    const bool groupable = l.kind == Launch::kConv && bh_conv_group_ok(&l.conv) && !rd.empty() && !wr.empty();
-    // pending convs this launch depends on (reads or overwrites their
-    // output) or that depend on it (it overwrites their input)
-    std::vector<Pending> hit, keep;
-    for (Pending& p : pending)
-      (intersects(rd, p.wr) || intersects(wr, p.wr) || intersects(wr, p.rd) ? hit : keep).push_back(std::move(p));
-    pending = std::move(keep);
-    if (!hit.empty()) {
-      if (groupable) {
-        // a conv consuming pending ones (a detector's next extra layer):
-        // only those go now, the rest keep waiting for more members
-        RETURN_STATUS_IF(emit(hit));
-      } else {
-        // a consumer of the group (CONCATENATION, ...): everything pending
-        // runs here, as one launch
-        for (Pending& p : hit) pending.push_back(std::move(p));
-        RETURN_STATUS_IF(emit(pending));
-      }
-    }
-    if (groupable && pending.size() < max_members) {
-      pending.push_back(Pending{std::move(l), rd, wr});
-      continue;
-    }
-    // a launch that stays put: pending convs it does not touch are deferred
-    // past it
-    out.push_back(std::move(l));
-  }
-  RETURN_STATUS_IF(emit(pending));
-  sg->launches = std::move(out);
-  return absl::OkStatus();
-}
-
-namespace {
-bool Is1x1S1(const bh_conv_params& c) {
-  return c.k_h == 1 && c.k_w == 1 && c.stride_h == 1 && c.stride_w == 1 && c.pad_h == 0 && c.pad_w == 0;
-}
-
-// Static latency model for a fused block's tile (used when it cannot be
-// measured): (workgroup rounds over 256 CUs) x (MFMA tiles + depthwise /
-// epilogue work per workgroup) / waves - halo recompute of small tiles
-// against too few workgroups of large ones.
-double IrbModelCost(const bh_irb_params& q, int t, size_t lds) {
-  const int R = ((t - 1) * q.stride + 3) * ((t - 1) * q.stride + 3);
-  const double mt1 = (R + 15) / 16, mt3 = (t * t + 15) / 16;
-  const double ks1 = (q.in_c + 63) / 64, ks3 = (q.exp_c + 63) / 64;
-  const double work = (q.has_expand ? mt1 * (q.exp_c / 16) * (1.0 + ks1) : 0.0) +  // +1: epilogue
-                      mt3 * 16 * q.exp_c / 256.0 * 3.0 +                          // depthwise
-                      mt3 * ((q.out_c + 15) / 16) * ks3 + t * t * q.out_c / 64.0;
-  const int nw = lds > 80 * 1024 ? 16 : 8;
-  const double per_cu = lds > 80 * 1024 ? 1 : 2;
-  const long wg = static_cast<long>(q.batch) * ((q.out_h + t - 1) / t) * ((q.out_w + t - 1) / t);
-  const double rounds = std::ceil(static_cast<double>(wg) / (256.0 * per_cu));
-  return rounds * (work / nw + 8.0);  // + fixed per-workgroup latency
-}
-
-// Measured choices, shared by every executor of the process: one block
-// geometry is timed once per device.  Value: tile edge, or 0 = keep unfused.
-std::mutex g_tune_mu;
-std::unordered_map<std::string, int> g_tune;
-
-// BAND_HIP_TUNE_FILE: decisions persist across processes ("<key> <tile>"
-// lines), so a profiled run replays exactly the launch sequence a timed run
-// chose (the profiler's per-dispatch overhead would otherwise bias a fresh
-// measurement).  Loaded once; new decisions are appended.
-const char* TuneFile() {
-  const char* f = std::getenv("BAND_HIP_TUNE_FILE");
-  return f && f[0] ? f : nullptr;
-}
-void LoadTuneFileLocked() {
-  static bool loaded = false;
-  if (loaded) return;
-  loaded = true;
-  const char* path = TuneFile();
-  if (!path) return;
-  if (FILE* fp = std::fopen(path, "r")) {
-    char key[256];
-    int tile = 0;
-    while (std::fscanf(fp, "%255s %d", key, &tile) == 2) g_tune[key] = tile;
-    std::fclose(fp);
-  }
-}
-void AppendTuneFileLocked(const std::string& key, int tile) {
-  const char* path = TuneFile();
-  if (!path) return;
-  if (FILE* fp = std::fopen(path, "a")) {
-    std::fprintf(fp, "%s %d\n", key.c_str(), tile);
-    std::fclose(fp);
-  }
-}
-
-// bumped whenever a chain form's LDS layout or parameter rules change, so a
-// tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 9;
-
-std::string IrbKey(int ordinal, const bh_irb_params& q) {
-  char buf[256];
-  std::snprintf(buf, sizeof(buf), "%d:%d:%dx%dx%d:%d:%d:%dx%d:%d:%d:%d", ordinal, q.batch, q.in_h, q.in_w, q.in_c,
-                q.exp_c, q.out_c, q.out_h, q.out_w, q.stride, q.has_expand, q.has_residual);
-  return buf;
-}
-}  // namespace
-
-double HipModelExecutor::TimeLaunches(const std::vector<const Launch*>& ls, int iters) {
-  if (device_flag_ != DeviceFlag::kGPU || !stream_ || ls.empty()) return -1.0;
-  bh_event_t e0 = nullptr, e1 = nullptr;
-  if (bh_event_create(&e0) != 0) return -1.0;
-  if (bh_event_create(&e1) != 0) {
-    bh_event_destroy(e0);
-    return -1.0;
-  }
-  double us = -1.0;
-  bool ok = true;
-  for (int w = 0; w < 2 && ok; ++w)
-    for (const Launch* l : ls) ok = ok && EnqueueLaunch(*l).ok();
-  // head start: the whole timed sequence is queued before the GPU reaches
-  // it, so the events see back-to-back execution (as in a replayed graph),
-  // not host submission gaps
-  ok = ok && bh_spin_us(stream_, 300 + 40 * iters * static_cast<int>(ls.size())) == 0;
-  if (ok && bh_event_record(e0, stream_) == 0) {
-    for (int it = 0; it < iters && ok; ++it)
-      for (const Launch* l : ls) ok = ok && EnqueueLaunch(*l).ok();
-    float ms = 0.f;
-    if (ok && bh_event_record(e1, stream_) == 0 && bh_stream_sync(stream_) == 0 &&
-        bh_event_elapsed_ms(e0, e1, &ms) == 0)
-      us = 1e3 * ms / iters;
-  }
-  bh_stream_sync(stream_);
-  bh_event_destroy(e0);
-  bh_event_destroy(e1);
-  return us;
-}
-
-// Rewrites [conv1x1 ->] dw3x3 -> conv1x1 [+fused ADD] launch runs into one
-// bh_irb_i8 launch when the intermediates are private to the run.
-void HipModelExecutor::FuseBlocks(const HipModel& model, PreparedSubgraph* sg) {
-  const TflModel& d = model.desc();
-  auto private_tensor = [&](int t, int only_consumer) {
-    if (consumers_[t].size() != 1 || consumers_[t][0] != only_consumer) return false;
-    if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
-    if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
-    return std::find(d.outputs.begin(), d.outputs.end(), t) == d.outputs.end();
-  };
-  std::vector<Launch> out;
-  const auto& L = sg->launches;
-  for (size_t i = 0; i < L.size(); ++i) {
-    // candidate run: [E] D P
-    const Launch* E = nullptr;
-    size_t j = i;
-    if (L[i].kind == Launch::kConv && i + 2 < L.size() && L[i + 1].kind == Launch::kDwConv &&
-        L[i + 2].kind == Launch::kConv) {
-      E = &L[i];
-      j = i + 1;
-    } else if (!(L[i].kind == Launch::kDwConv && i + 1 < L.size() && L[i + 1].kind == Launch::kConv)) {
-      out.push_back(L[i]);
-      continue;
-    }
-    const Launch& D = L[j];
-    const Launch& P = L[j + 1];
-    const bh_dwconv_params& dw = D.dw;
-    const bh_conv_params& pc = P.conv;
-    bool ok = dw.in_xor == 0 && dw.w_zp == 0 && dw.depth_multiplier == 1 && dw.k_h == 3 && dw.k_w == 3 &&
-              dw.dil_h == 1 && dw.dil_w == 1 && dw.stride_h == dw.stride_w && pc.in_xor == 0 && pc.w_zp == 0 &&
-              Is1x1S1(pc) && pc.input == dw.output &&
-              private_tensor(d.ops[D.op_index].outputs[0], P.op_index);
-    if (ok && E) {
-      const bh_conv_params& ec = E->conv;
-      ok = ec.in_xor == 0 && ec.w_zp == 0 && Is1x1S1(ec) && !ec.residual && ec.output == dw.input &&
-           private_tensor(d.ops[E->op_index].outputs[0], D.op_index);
-    }
-    if (ok && pc.residual) {
-      const void* x = E ? E->conv.input : dw.input;
-      ok = pc.residual == x;
-    }
-    bh_irb_params q{};
-    if (ok) {
-      const bh_conv_params* ec = E ? &E->conv : nullptr;
-      q.batch = dw.batch;
-      q.in_h = dw.in_h; q.in_w = dw.in_w;
-      q.in_c = ec ? ec->in_c : dw.in_c;
-      q.exp_c = dw.in_c;
-      q.out_h = dw.out_h; q.out_w = dw.out_w; q.out_c = pc.out_c;
-      q.stride = dw.stride_h; q.pad_h = dw.pad_h; q.pad_w = dw.pad_w;
-      q.has_expand = ec ? 1 : 0;
-      if (ec) {
-        q.exp_w = ec->weights; q.exp_k_pad = ec->k_pad;
-        q.exp_bias_eff = ec->bias_eff; q.exp_mult = ec->mult; q.exp_shift = ec->shift;
-        q.x_zp = ec->in_zp;
-        q.e_zp = ec->out_zp; q.e_act_min = ec->act_min; q.e_act_max = ec->act_max;
-      }
-      q.dw_w = dw.weights; q.dw_bias = dw.bias; q.dw_mult = dw.mult; q.dw_shift = dw.shift;
-      if (!ec) q.e_zp = dw.in_zp;
-      q.d_zp = dw.out_zp; q.d_act_min = dw.act_min; q.d_act_max = dw.act_max;
-      q.proj_w = pc.weights; q.proj_k_pad = pc.k_pad;
-      q.proj_bias_eff = pc.bias_eff; q.proj_mult = pc.mult; q.proj_shift = pc.shift;
-      q.p_zp = pc.out_zp; q.p_act_min = pc.act_min; q.p_act_max = pc.act_max;
-      q.has_residual = pc.residual ? 1 : 0;
-      q.add_p_off = pc.add_y_off; q.add_x_off = pc.add_r_off; q.add_o_off = pc.add_o_off;
-      q.add_left_shift = pc.add_left_shift;
-      q.add_p_mult = pc.add_y_mult; q.add_p_shift = pc.add_y_shift;
-      q.add_x_mult = pc.add_r_mult; q.add_x_shift = pc.add_r_shift;
-      q.add_o_mult = pc.add_o_mult; q.add_o_shift = pc.add_o_shift;
-      q.add_act_min = pc.add_act_min; q.add_act_max = pc.add_act_max;
-      q.requant_fast = (ec && ec->requant_fast ? 1 : 0) | (dw.requant_fast ? 2 : 0) | (pc.requant_fast ? 4 : 0);
-      q.input = ec ? ec->input : dw.input;
-      q.output = pc.output;
-      // Tile edge: measured on this device when possible (each feasible
-      // tile, and the unfused launches, timed on the real buffers; the
-      // winner is cached per block geometry), else the static model.
-      int tile = 0;
-      bh_irb_params kq = q;
-      if (tune_batch_ > 0) kq.batch = tune_batch_;  // a job-batch variant reuses its anchor's choice
-      const std::string key = IrbKey(ordinal_, kq);
-      bool cached = false;
-      if (autotune_) {
-        std::lock_guard<std::mutex> lk(g_tune_mu);
-        LoadTuneFileLocked();
-        auto it = g_tune.find(key);
-        if (it != g_tune.end()) {
-          tile = it->second;
-          cached = true;
-        }
-      }
-      if (!cached) {
-        double best_model = 1e300, best_us = 1e300;
-        int model_tile = 0;
-        bool measured = autotune_;
-        if (measured) {
-          std::vector<const Launch*> unfused;
-          if (E) unfused.push_back(E);
-          unfused.push_back(&D);
-          unfused.push_back(&P);
-          const double u = TimeLaunches(unfused, 10);
-          measured = u > 0;
-          best_us = u * 0.98;  // fusion must win by > 2% to be taken
-        }
-        for (int t = 8; t >= 1; --t) {
-          q.tile_h = q.tile_w = t;
-          const size_t lds = bh_irb_lds_bytes(&q);
-          if (lds == 0) continue;
-          const double est = IrbModelCost(q, t, lds);
-          if (est < best_model * 0.97) {
-            best_model = est;
-            model_tile = t;
-          }
-          if (measured) {
-            Launch F;
-            F.kind = Launch::kIrb;
-            F.irb = q;
-            const double us = TimeLaunches({&F}, 10);
-            if (us > 0 && us < best_us) {
-              best_us = us;
-              tile = t;
-            }
-          }
-        }
-        if (!measured) tile = model_tile;
-        if (autotune_ && measured) {
-          std::lock_guard<std::mutex> lk(g_tune_mu);
-          if (!g_tune.count(key)) AppendTuneFileLocked(key, tile);
-          g_tune[key] = tile;
-        }
-      }
-      q.tile_h = q.tile_w = tile;
-      ok = tile > 0 && bh_irb_lds_bytes(&q) > 0;
-    }
-    if (!ok) {
-      out.push_back(L[i]);
-      continue;
-    }
-    Launch F;
-    F.kind = Launch::kIrb;
-    F.op_index = E ? E->op_index : D.op_index;
-    F.out_tensor = P.out_tensor;
-    F.irb = q;
-    F.kernel = "irb_kernel";
-    // algorithmic bytes: block input + block output + all filters/tables
-    const double x_bytes = static_cast<double>(q.batch) * q.in_h * q.in_w * q.in_c;
-    const double y_bytes = static_cast<double>(q.batch) * q.out_h * q.out_w * q.out_c;
-    F.alg_bytes = x_bytes + y_bytes + 12.0 * (q.exp_c + q.out_c) + 9.0 * q.exp_c +
-                  static_cast<double>(q.exp_c) * q.out_c + (E ? static_cast<double>(q.exp_c) * q.in_c + 12.0 * q.exp_c : 0);
-    F.alg_ops = (E ? E->alg_ops : 0) + D.alg_ops + P.alg_ops;
-    out.push_back(F);
-    // intermediates now live only in LDS; a later view of one re-lowers
-    sg->fused_tensors.insert(d.ops[D.op_index].outputs[0]);
-    if (E) sg->fused_tensors.insert(d.ops[E->op_index].outputs[0]);
-    i = j + 1;  // consumed [E] D P
-  }
-  sg->launches.swap(out);
-}
-
-// Rewrites dw3x3 -> conv1x1 [+fused ADD] [-> conv1x1] launch runs into one
-// bh_chain_i8 launch (a block's depthwise + project and the next block's
-// expand) when the depthwise output is private to the first conv.  The
-// first conv's output is stored only when something besides the second conv
-// reads it (the next block's residual, a subgraph output).  Taken per run
-// geometry by on-device timing against the unfused launches, as FuseBlocks.
-// The tile form's constant block (bh_chain_tile_pack): built on the device
-// from the chain's filter / table pointers, owned by the subgraph.
-bool HipModelExecutor::PackChainTile(bh_chain_params* q, PreparedSubgraph* sg) {
-  const size_t nb = bh_chain_tile_blob_bytes(q);
-  if (nb == 0 || ordinal_ < 0) return false;
-  auto blob = std::make_shared<DeviceBlob>(ordinal_, nb);
-  if (!blob->ok() || bh_chain_tile_pack(q, blob->ptr(), stream_) != 0 || bh_stream_sync(stream_) != 0) return false;
-  q->tile_blob = blob->ptr();
-  sg->consts.push_back(blob);
-  return true;
-}
-
-void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
-  const TflModel& d = model.desc();
-  auto private_tensor = [&](int t, int only_consumer) {
-    if (t < 0 || consumers_[t].size() != 1 || consumers_[t][0] != only_consumer) return false;
-    if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
-    if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
-    return std::find(d.outputs.begin(), d.outputs.end(), t) == d.outputs.end();
-  };
-  std::vector<Launch> out;
-  const auto& L = sg->launches;
-  for (size_t i = 0; i < L.size(); ++i) {
-    const bool head = L[i].kind == Launch::kDwConv && i + 1 < L.size() && L[i + 1].kind == Launch::kConv &&
-                      L[i + 1].conv.input == L[i].dw.output && !L[i].dw.out_table &&
-                      private_tensor(L[i].out_tensor, L[i + 1].op_index);
-    if (!head) {
-      out.push_back(L[i]);
-      continue;
-    }
-    const Launch& D = L[i];
-    const Launch& P1 = L[i + 1];
-    const Launch* P2 = nullptr;
-    if (i + 2 < L.size() && L[i + 2].kind == Launch::kConv && L[i + 2].conv.input == P1.conv.output &&
-        Is1x1S1(L[i + 2].conv) && !L[i + 2].conv.residual)
-      P2 = &L[i + 2];
-    bh_chain_params c{};
-    c.dw = D.dw;
-    c.pw1 = P1.conv;
-    c.px_blocks = 4;
-    // the two candidate forms: with the second conv, and without it
-    bh_chain_params c3 = c, c2 = c;
-    bool ok3 = false;
-    if (P2) {
-      c3.has_pw2 = 1;
-      c3.pw2 = P2->conv;
-      if (private_tensor(P1.out_tensor, P2->op_index)) c3.pw1.output = nullptr;
-      ok3 = bh_chain_lds_bytes(&c3) > 0;
-    }
-    const bool ok2 = bh_chain_lds_bytes(&c2) > 0;
-    if (!ok2 && !ok3) {
-      out.push_back(L[i]);
-      continue;
-    }
-    // choice: 0 = unfused, 1/2/4 = px_blocks of the 3-launch form, 11/12/14
-    // = px_blocks of the 2-launch form (the second conv stays a launch),
-    // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
-    char key[256];
-    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d", kChainTuneVersion, ordinal_,
-                  tune_batch_ > 0 ? tune_batch_ : D.dw.batch, D.dw.in_h,
-                  D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
-                  ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0, no_tile_chain_, no_deep_chain_,
-                  no_split_chain_, no_valu_chain_);
-    int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
-    if (force_tile_chain_) {
-      bh_chain_params q = ok3 ? c3 : c2;
-      q.tile = tile_pipe_ ? 2 : 1;
-      if (bh_chain_lds_bytes(&q) > 0) choice += tile_pipe_ ? 500 : 400;
-    }
-    if (force_valu_chain_) {
-      bh_chain_params q = ok3 ? c3 : c2;
-      q.px_blocks = 4;
-      q.dw_valu = 1;
-      if (bh_chain_lds_bytes(&q) > 0) choice += 8000;
-    }
-    if (force_deep_chain_) {
-      bh_chain_params q = ok3 ? c3 : c2;
-      q.px_blocks = 1;
-      q.deep = 1;
-      choice = bh_chain_lds_bytes(&q) > 0 ? (ok3 ? 1001 : 1011) : (ok3 ? 4 : 14);
-    }
-    if (autotune_ && choice < 0) {
-      std::lock_guard<std::mutex> lk(g_tune_mu);
-      LoadTuneFileLocked();
-      auto it = g_tune.find(key);
-      if (it != g_tune.end()) choice = it->second;
-    }
-    if (choice < 0) {
-      choice = 0;
-      bool measured = autotune_;
-      if (measured) {
-        std::vector<const Launch*> base = {&D, &P1};
-        if (ok3) base.push_back(P2);
-        const double u = TimeLaunches(base, 10);
-        const double u_p2 = ok3 ? TimeLaunches({P2}, 10) : 0.0;
-        measured = u > 0 && u_p2 >= 0;
-        double best = u * 0.98;  // fusion must win by > 2% to be taken
-        // (px_blocks, waves): 64 / 32 / 16 pixels per 4-wave workgroup, or
-        // 16 pixels over 16 waves (few-pixel, many-channel layers)
-        // {px_blocks, waves, persist}: the last is the persistent form
-        // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
-        // {.., tile}: the 2-D tile form (8 x 8 pixels, one LDS-DMA burst)
-        // {.., deep}: the deep-issue raster forms
-        // (the persistent tile form, tile 2, measured slower than the
-        // one-tile workgroups on every MobileNetV2 chain,
-        // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
-        // {.., tile 3 / 4}: runs of 2 / 4 tiles per workgroup, the constant
-        // block staged once per run
-        // {.., split}: the second 1x1's channel tiles over 2..4 workgroups
-        // per pixel block (3-launch form only; BAND_HIP_FUSION=nosplit: none)
-        // {.., valu}: the depthwise phase on VALU (v_dot4 over the tap
-        // table) instead of the block-diagonal MFMA tile (raster forms;
-        // BAND_HIP_FUSION=novalu: none)
-        const int forms[25][7] = {
-            {4, 4, 0, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0, 0},
-            {1, 16, 0, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0, 0}, {4, 4, 0, 1, 0, 0, 0}, {4, 4, 0, 3, 0, 0, 0},
-            {4, 4, 0, 4, 0, 0, 0}, {2, 4, 0, 0, 1, 0, 0}, {1, 4, 0, 0, 1, 0, 0}, {1, 8, 0, 0, 1, 0, 0},
-            {1, 4, 0, 0, 0, 2, 0}, {1, 8, 0, 0, 0, 2, 0}, {2, 4, 0, 0, 0, 2, 0}, {1, 16, 0, 0, 0, 2, 0},
-            {1, 4, 0, 0, 0, 3, 0}, {1, 8, 0, 0, 0, 3, 0}, {1, 4, 0, 0, 0, 4, 0},
-            {4, 4, 0, 0, 0, 0, 1}, {2, 4, 0, 0, 0, 0, 1}, {1, 4, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 0, 1},
-            {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}};
-        for (const auto& pw : forms) {
-          if (pw[3] && no_tile_chain_) continue;
-          if (pw[4] && no_deep_chain_) continue;
-          if (pw[5] && no_split_chain_) continue;
-          if (pw[6] && no_valu_chain_) continue;
-          for (int form = 0; form < 2 && measured; ++form) {
-            bh_chain_params q = form == 0 ? c3 : c2;
-            if (form == 0 ? !ok3 : !ok2) continue;
-            q.px_blocks = pw[0];
-            q.waves = pw[1];
-            q.persist = pw[2];
-            q.tile = pw[3];
-            q.deep = pw[4];
-            q.c_split = pw[5];
-            q.dw_valu = pw[6];
-            if (pw[5] > 1 && form != 0) continue;
-            if (bh_chain_lds_bytes(&q) == 0) continue;
-            if (q.tile && !PackChainTile(&q, sg)) continue;
-            Launch F;
-            F.kind = Launch::kChain;
-            F.chain = q;
-            const double us = TimeLaunches({&F}, 10);
-            const double total = us + (form == 1 && ok3 ? u_p2 : 0.0);
-            if (us > 0 && total < best) {
-              best = total;
-              choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
-                       (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) +
-                       (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0) + (pw[6] ? 8000 : 0);
-            }
-          }
-        }
-      }
-      if (!measured) choice = ok3 ? 4 : 14;  // no device timing: the 3-launch form when it applies
-      if (autotune_ && measured) {
-        std::lock_guard<std::mutex> lk(g_tune_mu);
-        if (!g_tune.count(key)) AppendTuneFileLocked(key, choice);
-        g_tune[key] = choice;
-      }
-    }
-    // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
-    // +200 for the persistent form, +300 for 8 waves, +400 for the tile
-    // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
-    // tiles, +1000 for the deep-issue form, +2000 x (s - 1) for the s-way
-    // phase-C split, +8000 for the VALU depthwise phase
-    const int dw_valu = choice >= 8000 ? 1 : 0;
-    choice %= 8000;
-    const int c_split = choice >= 2000 ? choice / 2000 + 1 : 0;
-    choice %= 2000;
-    const int deep = choice >= 1000 ? 1 : 0;
-    choice %= 1000;
-    const bool three = choice > 0 && choice % 100 < 10;
-    if (choice == 0 || (three && !ok3) || (!three && !ok2)) {
-      out.push_back(L[i]);
-      continue;
-    }
-    Launch F;
-    F.kind = Launch::kChain;
-    F.op_index = D.op_index;
-    F.chain = three ? c3 : c2;
-    F.chain.px_blocks = choice % 10;
-    F.chain.waves = choice >= 300 && choice < 400 ? 8 : (choice >= 100 && choice < 200 ? 16 : 4);
-    F.chain.persist = choice >= 200 && choice < 300 ? 1 : 0;
-    F.chain.tile = choice >= 400 && choice < 800 ? choice / 100 - 3 : 0;
-    F.chain.deep = deep;
-    F.chain.c_split = c_split;
-    F.chain.dw_valu = dw_valu;
-    // a choice read from a tune file written by another kernel tree may name
-    // a form these parameters do not admit: keep the unfused launches then
-    if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {
-      out.push_back(L[i]);
-      continue;
-    }
-    F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
-    F.kernel = F.chain.tile ? "chain_tile_kernel" : "chain_kernel";
-    const bh_dwconv_params& dw = F.chain.dw;
-    const bh_conv_params& a = F.chain.pw1;
-    const double px = static_cast<double>(dw.batch) * dw.out_h * dw.out_w;
-    F.alg_bytes = static_cast<double>(dw.batch) * dw.in_h * dw.in_w * dw.in_c + 9.0 * dw.out_c + 28.0 * dw.out_c +
-                  (a.residual ? px * a.out_c : 0.0) + (a.output ? px * a.out_c : 0.0) +
-                  static_cast<double>(a.out_c) * a.in_c + 12.0 * a.out_c;
-    F.alg_ops = D.alg_ops + P1.alg_ops;
-    if (three) {
-      const bh_conv_params& b = F.chain.pw2;
-      F.alg_bytes += px * b.out_c + static_cast<double>(b.out_c) * b.in_c + 12.0 * b.out_c;
-      F.alg_ops += P2->alg_ops;
-      if (!a.output) sg->fused_tensors.insert(P1.out_tensor);
-    }
-    out.push_back(F);
-    sg->fused_tensors.insert(D.out_tensor);
-    i += three ? 2 : 1;
-  }
-  sg->launches.swap(out);
-}
-
-namespace {
-void** OutSlot(Launch& l) {
-  switch (l.kind) {
-    case Launch::kChain: return l.chain.has_pw2 ? &l.chain.pw2.output : &l.chain.pw1.output;
-    case Launch::kConv: return &l.conv.output;
-    case Launch::kDwConv: return &l.dw.output;
-    case Launch::kFc: return &l.fc.output;
-    case Launch::kEltwise: return &l.elt.out;
-    case Launch::kPool: return &l.pool.output;
-    case Launch::kIrb: return &l.irb.output;
-    case Launch::kLutU8: return &l.dst;
-    default: return nullptr;
-  }
-}
-const void** TableSlot(Launch& l) {
-  switch (l.kind) {
-    case Launch::kConv: return l.conv.residual ? nullptr : &l.conv.out_table;  // + ADD epilogue: keep apart
-    case Launch::kDwConv: return &l.dw.out_table;
-    case Launch::kFc: return &l.fc.out_table;
-    default: return nullptr;
-  }
-}
-}  // namespace
-
-void HipModelExecutor::FuseGlue(const HipModel& model, PreparedSubgraph* sg) {
-  const TflModel& d = model.desc();
-  auto in_outputs = [&](int t) {
-    return std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end() ||
-           std::find(d.outputs.begin(), d.outputs.end(), t) != d.outputs.end();
-  };
-  // t reaches op `to` through RESHAPE / SQUEEZE aliases only, every tensor on
-  // the way read by nothing else and needed by nobody outside; collects them
-  auto private_chain = [&](int t, int to, std::vector<int>* chain) {
-    while (t >= 0) {
-      if (consumers_[t].size() != 1 || in_outputs(t) || sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
-      chain->push_back(t);
-      const int c = consumers_[t][0];
-      if (c == to) return true;
-      const TflOperator& op = d.ops[c];
-      if ((op.builtin != kTflReshape && op.builtin != kTflSqueeze) ||
-          !std::binary_search(sg->ops.begin(), sg->ops.end(), c))
-        return false;
-      t = op.outputs[0];
-    }
-    return false;
-  };
-  auto producer_of = [&](size_t i, const void* ptr) -> int {
-    for (size_t j = i; j-- > 0;) {
-      void** o = OutSlot(sg->launches[j]);
-      if (o && *o == ptr) return static_cast<int>(j);
-    }
-    return -1;
-  };
-  std::vector<bool> dead(sg->launches.size(), false);
-  // (1) byte tables into the producer's epilogue; a CONCATENATION without
-  // rescale tables takes the table as every input's copy table (and may
-  // hand it on to its producers in (2))
-  for (size_t i = 0; i < sg->launches.size(); ++i) {
-    Launch& L = sg->launches[i];
-    if (L.kind != Launch::kLutU8) continue;
-    const int j = producer_of(i, L.src);
-    if (j < 0 || dead[j]) continue;
-    Launch& P = sg->launches[j];
-    std::vector<int> chain;
-    if (P.kind == Launch::kConcat) {
-      bool plain = P.concat.output == L.src;
-      for (int k = 0; k < P.concat.n_inputs && plain; ++k) plain = P.concat.table[k] == nullptr;
-      if (!plain || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
-      for (int k = 0; k < P.concat.n_inputs; ++k) P.concat.table[k] = L.table;
-      P.concat.output = L.dst;
-    } else {
-      const void** ts = TableSlot(P);
-      if (!ts || *ts || !private_chain(P.out_tensor, L.op_index, &chain)) continue;
-      *ts = L.table;
-      *OutSlot(P) = L.dst;
-    }
-    P.out_tensor = L.out_tensor;
-    P.alg_bytes += 0;  // same bytes: the table gather happens on the stored value
-    for (int t : chain) sg->fused_tensors.insert(t);
-    sg->fused_ops.insert(L.op_index);
-    dead[i] = true;
-  }
-  // (2) CONCATENATION whose inputs are slices of the output: contiguous
-  // ones (outer size 1) from any producer; per-image slices (outer = batch
-  // > 1, a detector's per-anchor concat) from convs, which store each image
-  // at the concat's row stride (bh_conv_params.out_img_stride); an input
-  // copy table moves into the producer's epilogue table
-  for (size_t i = 0; i < sg->launches.size(); ++i) {
-    Launch& C = sg->launches[i];
-    if (C.kind != Launch::kConcat) continue;
-    const bool strided = C.concat.outer != 1;
-    if (strided && device_flag_ != DeviceFlag::kGPU) continue;  // (the host conv stores dense images)
-    long total_row = 0;
-    for (int k = 0; k < C.concat.n_inputs; ++k) total_row += C.concat.row[k];
-    bool ok = true;
-    std::vector<int> prod(C.concat.n_inputs, -1);
-    std::vector<int> chain;
-    for (int k = 0; k < C.concat.n_inputs && ok; ++k) {
-      const int j = producer_of(i, C.concat.input[k]);
-      ok = j >= 0 && !dead[j] && OutSlot(sg->launches[j]) &&
-           private_chain(sg->launches[j].out_tensor, C.op_index, &chain);
-      if (ok && C.concat.table[k]) {
-        const void** ts = TableSlot(sg->launches[j]);
-        ok = ts && *ts == nullptr;
-      }
-      if (ok && strided) {
-        const Launch& P = sg->launches[j];
-        ok = P.kind == Launch::kConv && P.conv.out_img_stride == 0 && P.conv.batch == C.concat.outer &&
-             static_cast<long>(P.conv.out_h) * P.conv.out_w * P.conv.out_c == C.concat.row[k];
-      }
-      if (ok) prod[k] = j;
-      for (int kk = 0; kk < k && ok; ++kk) ok = prod[kk] != j;  // one producer per slice
-    }
-    if (!ok) continue;
-    long off = 0;
-    for (int k = 0; k < C.concat.n_inputs; ++k) {
-      Launch& P = sg->launches[prod[k]];
-      *OutSlot(P) = static_cast<char*>(C.concat.output) + off;
-      if (C.concat.table[k]) *TableSlot(P) = C.concat.table[k];
-      if (strided) P.conv.out_img_stride = total_row;
-      off += C.concat.row[k];
-    }
-    for (int t : chain) sg->fused_tensors.insert(t);
-    sg->fused_ops.insert(C.op_index);
-    dead[i] = true;
-  }
-  std::vector<Launch> out;
-  for (size_t i = 0; i < sg->launches.size(); ++i)
-    if (!dead[i]) out.push_back(sg->launches[i]);
-  sg->launches.swap(out);
-}
-
-// Folds `conv -> ADD/SUB(conv_out, residual)` into the conv epilogue when the
-// conv output has no other reader and nobody needs it materialised.  The
-// epilogue reproduces both TFLite ops exactly (conv requant + clamp to the
-// conv's 8-bit output, then add.cc's arithmetic), so the result is
-// bit-identical to running the two ops.
-bool HipModelExecutor::TryFuseResidualAdd(const HipModel& model, int oi, PreparedSubgraph* sg, Launch* L) {
-  if (!allow_fusion_ || !allow_add_) return false;
-  const TflModel& d = model.desc();
-  const int t = d.ops[oi].outputs[0];
-  if (consumers_[t].size() != 1) return false;
-  const int j = consumers_[t][0];
-  if (j <= oi || !std::binary_search(sg->ops.begin(), sg->ops.end(), j)) return false;
-  const TflOperator& add = d.ops[j];
-  if ((add.builtin != kTflAdd && add.builtin != kTflSub) || add.inputs.size() != 2) return false;
-  if (!GpuSupports(d, add, nullptr)) return false;
-  if (sg->no_fuse.count(t) || sg->extra_d2h.count(t)) return false;
-  if (std::find(sg->outputs.begin(), sg->outputs.end(), t) != sg->outputs.end()) return false;
-  if (std::find(d.outputs.begin(), d.outputs.end(), t) != d.outputs.end()) return false;
-  const bool conv_is_first = add.inputs[0] == t;
-  const int other = conv_is_first ? add.inputs[1] : add.inputs[0];
-  if (other == t) return false;
-  // the epilogue reads the other operand while the conv runs, so it must
-  // already exist then: produced by an earlier op (an FPN's ADD of a lateral
-  // conv and an upsampled map produced later must stay unfused)
-  if (other < 0 || producer_[other] > oi) return false;
-  const TflTensor& tc = d.tensors[t];
-  const TflTensor& tr = d.tensors[other];
-  const TflTensor& to = d.tensors[add.outputs[0]];
-  if (tr.shape != tc.shape || to.shape != tc.shape || tr.type != tc.type || to.type != tc.type) return false;
-  void* rptr = nullptr;
-  void* optr = nullptr;
-  if (!DevicePtr(model, other, sg, &rptr).ok() || !DevicePtr(model, add.outputs[0], sg, &optr).ok()) return false;
-  const TflTensor& t1 = d.tensors[add.inputs[0]];
-  const TflTensor& t2 = d.tensors[add.inputs[1]];
-  const AddParams ap = AddSubParams(Scale(t1), Scale(t2), Scale(to), add.builtin == kTflSub);
-  bh_conv_params& p = L->conv;
-  p.residual = rptr;
-  p.output = optr;
-  p.add_left_shift = ap.left_shift;
-  p.add_y_off = -Zp(tc);
-  p.add_r_off = -Zp(tr);
-  p.add_o_off = Zp(to);
-  p.add_y_mult = conv_is_first ? ap.m1 : ap.m2;
-  p.add_y_shift = conv_is_first ? ap.s1 : ap.s2;
-  p.add_r_mult = conv_is_first ? ap.m2 : ap.m1;
-  p.add_r_shift = conv_is_first ? ap.s2 : ap.s1;
-  p.add_o_mult = ap.mo;
-  p.add_o_shift = ap.so;
-  const int act = add.options.valid() ? add.options.Int8(0, 0) : 0;
-  ActivationRangeQuantized(act, Scale(to), Zp(to), to.type == DataType::kInt8, &p.add_act_min, &p.add_act_max);
-  L->alg_bytes += static_cast<double>(tr.num_elements());  // residual read; y never stored
-  L->kernel = WithAdd(L->kernel);
-  sg->fused_ops.insert(j);
-  L->out_tensor = add.outputs[0];
-  sg->fused_tensors.insert(t);
-  return true;
-}
-
-// float32 graphs (fp16-weight models): constants (fp16 behind DEQUANTIZE,
-// or float32) are folded on the host into the layouts the bh_*_f32 kernels
-// read; a DEQUANTIZE whose consumers all fold it emits nothing.
-absl::Status HipModelExecutor::LowerFloat(const HipModel& model, int oi, void* in_ptr, void* out_ptr,
-                                          const std::string& ckey, PreparedSubgraph* sg, Launch* L, bool* emit) {
-  const TflModel& d = model.desc();
-  const TflOperator& op = d.ops[oi];
-  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
-  const TflTensor& in = T(op.inputs[0]);
-  const TflTensor& out = T(op.outputs[0]);
-  const double io_bytes = 4.0 * (static_cast<double>(in.num_elements()) + out.num_elements());
-  L->alg_bytes = io_bytes;
-  auto upload = [&](const std::string& key, const std::vector<float>& v, const void** dev) {
-    return UploadConst(key, v.data(), v.size() * sizeof(float), sg, dev);
-  };
-  switch (op.builtin) {
-    case kTflDequantize: {
-      const int t = op.outputs[0];
-      bool all_fold = true;
-      for (int c : consumers_[t]) {
-        const TflOperator& co = d.ops[c];
-        const bool folds = (co.builtin == kTflConv2D || co.builtin == kTflDepthwiseConv2D ||
-                            co.builtin == kTflFullyConnected) &&
-                           co.inputs[0] != t;
-        all_fold = all_fold && folds;
-      }
-      std::set<int> subgraph_outputs(sg->outputs.begin(), sg->outputs.end());
-      if (all_fold && !subgraph_outputs.count(t) && !sg->no_fuse.count(t)) {
-        *emit = false;
-        return absl::OkStatus();
-      }
-      const void* dev = nullptr;
-      RETURN_STATUS_IF(upload(ckey + "/f32", FloatData(d, t), &dev));
-      L->kind = Launch::kCopy;
-      L->kernel = "copy";
-      L->src = dev;
-      L->dst = out_ptr;
-      L->bytes = 4 * out.num_elements();
-      L->alg_bytes = 2.0 * L->bytes;
-      return absl::OkStatus();
-    }
-    case kTflConv2D:
-    case kTflDepthwiseConv2D: {
-      const bool dw = op.builtin == kTflDepthwiseConv2D;
-      const TflTensor& w = T(op.inputs[1]);
-      const FbTable& o = op.options;
-      const bool same = o.Int8(0, 0) == 0;
-      const int sw = o.Int(1, 1), sh = o.Int(2, 1);
-      const int act = dw ? o.Int8(4, 0) : o.Int8(3, 0);
-      const int dlw = dw ? o.Int(5, 1) : o.Int(4, 1);
-      const int dlh = dw ? o.Int(6, 1) : o.Int(5, 1);
-      const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], ic = in.shape[3];
-      const int oc = dw ? w.shape[3] : w.shape[0];
-      const int kh = w.shape[1], kw = w.shape[2];
-      const int oh = ComputeOutSize(same, ih, kh, sh, dlh), ow = ComputeOutSize(same, iw, kw, sw, dlw);
-      if (out.shape != std::vector<int>{b, oh, ow, oc}) return absl::InternalError("conv output shape mismatch");
-      std::vector<float> wf = FloatData(d, op.inputs[1]);
-      std::vector<float> laid(wf.size());
-      if (dw) {
-        laid = wf;  // [1][kh][kw][oc] is already [kh*kw][oc]
-      } else {
-        const int K = kh * kw * ic;  // OHWI -> [K][oc]
-        for (int c = 0; c < oc; ++c)
-          for (int k = 0; k < K; ++k) laid[static_cast<size_t>(k) * oc + c] = wf[static_cast<size_t>(c) * K + k];
-      }
-      bh_conv_f32_params& p = L->convf;
-      p = bh_conv_f32_params{};
-      const void* wdev = nullptr;
-      RETURN_STATUS_IF(upload(ckey + "/w", laid, &wdev));
-      p.weights = static_cast<const float*>(wdev);
-      if (op.inputs.size() > 2 && op.inputs[2] >= 0) {
-        const void* bdev = nullptr;
-        RETURN_STATUS_IF(upload(ckey + "/b", FloatData(d, op.inputs[2]), &bdev));
-        p.bias = static_cast<const float*>(bdev);
-      }
-      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic; p.out_h = oh; p.out_w = ow; p.out_c = oc;
-      p.k_h = kh; p.k_w = kw; p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw;
-      p.pad_h = ComputePadding(sh, dlh, ih, kh, oh);
-      p.pad_w = ComputePadding(sw, dlw, iw, kw, ow);
-      p.depthwise = dw ? 1 : 0;
-      p.depth_multiplier = dw ? oc / ic : 1;
-      FloatActRange(act, &p.act_min, &p.act_max);
-      p.input = static_cast<const float*>(in_ptr);
-      p.output = static_cast<float*>(out_ptr);
-      L->kind = Launch::kConvF32;
-      L->kernel = dw ? "dwconv_f32_kernel" : "conv_f32_kernel";
-      L->alg_ops = 2.0 * b * oh * ow * oc * kh * kw * (dw ? 1 : ic);
-      L->alg_bytes = io_bytes + 4.0 * laid.size() + 4.0 * oc;
-      return absl::OkStatus();
-    }
-    case kTflFullyConnected: {
-      const TflTensor& w = T(op.inputs[1]);
-      const int units = w.shape[0], depth = w.shape[1];
-      bh_fc_f32_params& p = L->fcf;
-      p = bh_fc_f32_params{};
-      const void* wdev = nullptr;
-      RETURN_STATUS_IF(upload(ckey + "/w", FloatData(d, op.inputs[1]), &wdev));
-      p.weights = static_cast<const float*>(wdev);
-      if (op.inputs.size() > 2 && op.inputs[2] >= 0) {
-        const void* bdev = nullptr;
-        RETURN_STATUS_IF(upload(ckey + "/b", FloatData(d, op.inputs[2]), &bdev));
-        p.bias = static_cast<const float*>(bdev);
-      }
-      p.rows = static_cast<int>(in.num_elements() / depth);
-      p.depth = depth;
-      p.units = units;
-      FloatActRange(op.options.valid() ? op.options.Int8(0, 0) : 0, &p.act_min, &p.act_max);
-      p.input = static_cast<const float*>(in_ptr);
-      p.output = static_cast<float*>(out_ptr);
-      L->kind = Launch::kFcF32;
-      L->kernel = "fc_f32_kernel";
-      L->alg_ops = 2.0 * p.rows * units * depth;
-      L->alg_bytes = io_bytes + 4.0 * units * depth;
-      return absl::OkStatus();
-    }
-    case kTflAdd:
-    case kTflSub:
-    case kTflMul:
-    case kTflSquaredDifference: {
-      const TflTensor& bt = T(op.inputs[1]);
-      void* b_ptr = nullptr;
-      RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
-      bh_eltwise_f32_params& p = L->eltf;
-      p = bh_eltwise_f32_params{};
-      p.kind = op.builtin == kTflAdd   ? BH_ELTF_ADD
-               : op.builtin == kTflSub ? BH_ELTF_SUB
-               : op.builtin == kTflMul ? BH_ELTF_MUL
-                                       : BH_ELTF_SQDIFF;
-      Shape4(in.shape, p.shape_a);
-      Shape4(bt.shape, p.shape_b);
-      Shape4(out.shape, p.shape_o);
-      FloatActRange(op.options.valid() ? op.options.Int8(0, 0) : 0, &p.act_min, &p.act_max);
-      p.a = static_cast<const float*>(in_ptr);
-      p.b = static_cast<const float*>(b_ptr);
-      p.out = static_cast<float*>(out_ptr);
-      L->kind = Launch::kEltwiseF32;
-      L->kernel = "eltwise_f32_kernel";
-      L->alg_bytes += 4.0 * bt.num_elements();
-      return absl::OkStatus();
-    }
-    case kTflAveragePool2D:
-    case kTflMaxPool2D: {
-      const FbTable& o = op.options;
-      const bool same = o.Int8(0, 0) == 0;
-      const int sw = o.Int(1, 1), sh = o.Int(2, 1), fw = o.Int(3, 1), fh = o.Int(4, 1);
-      bh_pool_f32_params& p = L->poolf;
-      p = bh_pool_f32_params{};
-      p.kind = op.builtin == kTflAveragePool2D ? BH_POOL_AVG : BH_POOL_MAX;
-      p.batch = in.shape[0]; p.in_h = in.shape[1]; p.in_w = in.shape[2]; p.channels = in.shape[3];
-      p.out_h = ComputeOutSize(same, p.in_h, fh, sh, 1);
-      p.out_w = ComputeOutSize(same, p.in_w, fw, sw, 1);
-      p.f_h = fh; p.f_w = fw; p.stride_h = sh; p.stride_w = sw;
-      p.pad_h = ComputePadding(sh, 1, p.in_h, fh, p.out_h);
-      p.pad_w = ComputePadding(sw, 1, p.in_w, fw, p.out_w);
-      FloatActRange(o.Int8(5, 0), &p.act_min, &p.act_max);
-      p.input = static_cast<const float*>(in_ptr);
-      p.output = static_cast<float*>(out_ptr);
-      L->kind = Launch::kPoolF32;
-      L->kernel = "pool_f32_kernel";
-      return absl::OkStatus();
-    }
-    case kTflSoftmax:
-      L->kind = Launch::kSoftmaxF32;
-      L->kernel = "softmax_f32_kernel";
-      L->beta = op.options.valid() ? op.options.Float(0, 1.0f) : 1.0f;
-      L->depth = in.shape.back();
-      L->count = static_cast<long>(in.num_elements() / std::max(L->depth, 1));
-      L->src = in_ptr;
-      L->dst = out_ptr;
-      return absl::OkStatus();
-    default: {  // RELU / RELU6 / RELU_N1_TO_1 / LOGISTIC / RSQRT
-      L->kind = Launch::kUnaryF32;
-      L->kernel = "unary_f32_kernel";
-      L->unary_kind = op.builtin == kTflLogistic ? BH_UNARY_LOGISTIC
-                      : op.builtin == kTflRsqrt  ? BH_UNARY_RSQRT
-                                                 : BH_UNARY_CLAMP;
-      L->lo = op.builtin == kTflReluN1To1 ? -1.f : 0.f;
-      L->hi = op.builtin == kTflRelu6 ? 6.f : (op.builtin == kTflReluN1To1 ? 1.f : std::numeric_limits<float>::infinity());
-      L->count = static_cast<long>(in.num_elements());
-      L->src = in_ptr;
-      L->dst = out_ptr;
-      return absl::OkStatus();
-    }
-  }
-}
-
-absl::Status HipModelExecutor::Lower(const HipModel& model, int oi, PreparedSubgraph* sg) {
-  const TflModel& d = model.desc();
-  const TflOperator& op = d.ops[oi];
-  std::string why;
-  const bool cpu = device_flag_ == DeviceFlag::kCPU;
-  if (!(cpu ? CpuSupports(d, op, &why) : GpuSupports(d, op, &why)))
-    return absl::InternalError("HIP backend cannot run op " + std::to_string(oi) + " (" +
-                               TflBuiltinName(op.builtin) + ") on " + ToString(device_flag_) + ": " + why);
-  auto T = [&](int i) -> const TflTensor& { return d.tensors[i]; };
-  const TflTensor& in = T(op.inputs[0]);
-  const TflTensor& out = T(op.outputs[0]);
-  void* in_ptr = nullptr;
-  void* out_ptr = nullptr;
-  RETURN_STATUS_IF(DevicePtr(model, op.inputs[0], sg, &in_ptr));
-  RETURN_STATUS_IF(DevicePtr(model, op.outputs[0], sg, &out_ptr));
-  const bool i8 = in.type == DataType::kInt8;
-  const std::string ckey = "m" + Hex(model.serial()) + "/op" + std::to_string(oi);
-  Launch L;
-  L.op_index = oi;
-  L.out_tensor = op.outputs[0];
-
-  if (IsFloatOp(d, op)) {
-    bool emit = true;
-    RETURN_STATUS_IF(LowerFloat(model, oi, in_ptr, out_ptr, ckey, sg, &L, &emit));
-    if (emit) sg->launches.push_back(L);
-    return absl::OkStatus();
-  }
-  if (op.builtin == kTflConv2D || op.builtin == kTflDepthwiseConv2D) {
-    const bool dw = op.builtin == kTflDepthwiseConv2D;
-    const TflTensor& w = T(op.inputs[1]);
-    const int32_t* bias = nullptr;
-    if (op.inputs.size() > 2 && op.inputs[2] >= 0) bias = reinterpret_cast<const int32_t*>(T(op.inputs[2]).data);
-    const FbTable& o = op.options;
-    const bool same = o.Int8(0, 0) == 0;
-    const int sw = o.Int(1, 1), sh = o.Int(2, 1);
-    const int act = dw ? o.Int8(4, 0) : o.Int8(3, 0);
-    const int dlw = dw ? o.Int(5, 1) : o.Int(4, 1);
-    const int dlh = dw ? o.Int(6, 1) : o.Int(5, 1);
-    const int b = in.shape[0], ih = in.shape[1], iw = in.shape[2], ic = in.shape[3];
-    const int oc = dw ? w.shape[3] : w.shape[0];
-    const int kh = w.shape[1], kw = w.shape[2];
-    const int oh = ComputeOutSize(same, ih, kh, sh, dlh);
-    const int ow = ComputeOutSize(same, iw, kw, sw, dlw);
-    if (out.shape != std::vector<int>{b, oh, ow, oc}) return absl::InternalError("conv output shape mismatch");
-    const int ph = ComputePadding(sh, dlh, ih, kh, oh);
-    const int pw = ComputePadding(sw, dlw, iw, kw, ow);
-    std::vector<int32_t> mult, shift;
-    ConvMultipliers(Scale(in), w.scale, oc, Scale(out), !i8, &mult, &shift);
-    int32_t amin, amax;
-    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &amin, &amax);
-    const int32_t in_zp = Dom(in);
-    const int32_t w_zp = i8 ? 0 : Dom(w);  // int8 kernels ignore the filter zero point
-    const double M = static_cast<double>(b) * oh * ow;
-    if (!dw) {
-      const int K = kh * kw * ic;
-      int kp = 0, np = 0;
-      bh_conv_packed_geometry(oc, K, &kp, &np);
-      const size_t wbytes = static_cast<size_t>(kp) * np;
-      const size_t tbytes = 12ull * oc;
-      auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
-      if (!blob) {
-        std::vector<int8_t> packed(wbytes);
-        std::vector<int32_t> tables(3ull * oc);
-        if (bh_pack_conv_weights(w.data, i8 ? 1 : 0, oc, K, kp, np, bias, in_zp, w_zp, packed.data(), tables.data()) != 0)
-          return absl::InternalError("weight packing failed");
-        std::copy(mult.begin(), mult.end(), tables.begin() + oc);
-        std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
-        blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-        if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
-            !blob->Upload(wbytes, tables.data(), tbytes))
-          return HipErr(1, "upload conv operands");
-        DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
-      }
-      sg->consts.push_back(blob);
-      const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
-      bh_conv_params& p = L.conv;
-      p = bh_conv_params{};
-      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic;
-      p.out_h = oh; p.out_w = ow; p.out_c = oc; p.k_h = kh; p.k_w = kw;
-      p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw; p.pad_h = ph; p.pad_w = pw;
-      p.k_pad = kp; p.n_pad = np; p.in_xor = i8 ? 0 : 0x80;
-      p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out); p.act_min = amin; p.act_max = amax;
-      p.input = in_ptr; p.output = out_ptr;
-      p.weights = static_cast<const int8_t*>(blob->ptr());
-      p.bias_eff = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
-      p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, K, MaxAbs(bias, oc));
-      L.kind = Launch::kConv;
-      L.kernel = bh_conv2d_i8_kernel(&p);  // the kernel bh_conv2d_i8 dispatches to
-      L.alg_ops = 2.0 * M * oc * K;
-      L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(oc) * K + 12.0 * oc;
-    } else {
-      const int dm = oc / ic;
-      const size_t wbytes = static_cast<size_t>(kh) * kw * oc;
-      const size_t wpad = (wbytes + 15) / 16 * 16;
-      const size_t tbytes = 12ull * oc;
-      // 3x3 / dm 1 layers also get the dot4 kernel's tap table (bh_pack_dw_taps)
-      const bool dot = kh == 3 && kw == 3 && dm == 1 && oc % 4 == 0;
-      const size_t pbytes = dot ? 16ull * oc : 0;
-      auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
-      if (!blob) {
-        std::vector<uint8_t> wd(wpad, 0);
-        for (size_t i = 0; i < wbytes; ++i) wd[i] = i8 ? w.data[i] : static_cast<uint8_t>(w.data[i] ^ 0x80);
-        std::vector<int32_t> tables(3ull * oc, 0);
-        for (int c = 0; c < oc; ++c) tables[c] = bias ? bias[c] : 0;
-        std::copy(mult.begin(), mult.end(), tables.begin() + oc);
-        std::copy(shift.begin(), shift.end(), tables.begin() + 2 * oc);
-        std::vector<int32_t> taps(pbytes / 4);
-        if (dot && bh_pack_dw_taps(reinterpret_cast<const int8_t*>(wd.data()), oc, tables.data(), in_zp, w_zp,
-                                   taps.data()) != 0)
-          return absl::InternalError("depthwise tap packing failed");
-        blob = std::make_shared<DeviceBlob>(ordinal_, wpad + tbytes + pbytes);
-        if (!blob->ok() || !blob->Upload(0, wd.data(), wpad) ||
-            !blob->Upload(wpad, tables.data(), tbytes) || (dot && !blob->Upload(wpad + tbytes, taps.data(), pbytes)))
-          return HipErr(1, "upload depthwise operands");
-        DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
-      }
-      sg->consts.push_back(blob);
-      const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wpad);
-      bh_dwconv_params& p = L.dw;
-      p = bh_dwconv_params{};
-      p.batch = b; p.in_h = ih; p.in_w = iw; p.in_c = ic;
-      p.out_h = oh; p.out_w = ow; p.out_c = oc; p.depth_multiplier = dm; p.k_h = kh; p.k_w = kw;
-      p.stride_h = sh; p.stride_w = sw; p.dil_h = dlh; p.dil_w = dlw; p.pad_h = ph; p.pad_w = pw;
-      p.in_xor = i8 ? 0 : 0x80; p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out);
-      p.act_min = amin; p.act_max = amax; p.input = in_ptr; p.output = out_ptr;
-      p.weights = static_cast<const int8_t*>(blob->ptr());
-      p.bias = tab; p.mult = tab + oc; p.shift = tab + 2 * oc;
-      if (dot && !blob->host()) p.taps = tab + 3 * oc;
-      p.requant_fast = bh_conv_requant_fast_ok(mult.data(), shift.data(), oc, kh * kw, MaxAbs(bias, oc));
-      L.kind = Launch::kDwConv;
-      L.kernel = bh_dwconv2d_i8_kernel(&p);  // the kernel bh_dwconv2d_i8 dispatches to
-      L.alg_ops = 2.0 * M * oc * kh * kw;
-      L.alg_bytes = static_cast<double>(in.num_elements()) + M * oc + static_cast<double>(wbytes) + 12.0 * oc;
-    }
-  } else if (op.builtin == kTflFullyConnected) {
-    const TflTensor& w = T(op.inputs[1]);
-    const int32_t* bias = nullptr;
-    if (op.inputs.size() > 2 && op.inputs[2] >= 0) bias = reinterpret_cast<const int32_t*>(T(op.inputs[2]).data);
-    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
-    const int units = w.shape[0], depth = w.shape[1];
-    const int rows = static_cast<int>(in.num_elements() / depth);
-    const int depth_pad = (depth + 15) / 16 * 16;
-    int32_t mult, shift, amin, amax;
-    FullyConnectedMultiplier(Scale(in), Scale(w), Scale(out), &mult, &shift);
-    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &amin, &amax);
-    const int32_t in_zp = Dom(in), w_zp = Dom(w);
-    const size_t wbytes = static_cast<size_t>(units) * depth_pad;
-    const size_t tbytes = 12ull * units;
-    auto blob = DeviceRegistry::Get().FindConst(ordinal_, ckey);
-    if (!blob) {
-      std::vector<int8_t> packed(wbytes, 0);
-      std::vector<int32_t> tables(3ull * units);
-      for (int u = 0; u < units; ++u) {
-        int64_t s = 0;
-        for (int k = 0; k < depth; ++k) {
-          const uint8_t raw = w.data[static_cast<size_t>(u) * depth + k];
-          const int v = i8 ? static_cast<int>(static_cast<int8_t>(raw)) : static_cast<int>(raw) - 128;
-          packed[static_cast<size_t>(u) * depth_pad + k] = static_cast<int8_t>(v);
-          s += v;
-        }
-        tables[u] = static_cast<int32_t>((bias ? bias[u] : 0) - static_cast<int64_t>(in_zp) * s +
-                                         static_cast<int64_t>(depth) * in_zp * w_zp);
-        tables[units + u] = mult;
-        tables[2 * units + u] = shift;
-      }
-      blob = std::make_shared<DeviceBlob>(ordinal_, wbytes + tbytes);
-      if (!blob->ok() || !blob->Upload(0, packed.data(), wbytes) ||
-          !blob->Upload(wbytes, tables.data(), tbytes))
-        return HipErr(1, "upload fc operands");
-      DeviceRegistry::Get().PutConst(ordinal_, ckey, blob);
-    }
-    sg->consts.push_back(blob);
-    const int32_t* tab = reinterpret_cast<const int32_t*>(static_cast<char*>(blob->ptr()) + wbytes);
-    bh_fc_params& p = L.fc;
-    p = bh_fc_params{};
-    p.rows = rows; p.depth = depth; p.depth_pad = depth_pad; p.units = units;
-    p.in_xor = i8 ? 0 : 0x80; p.in_zp = in_zp; p.w_zp = w_zp; p.out_zp = Zp(out);
-    p.act_min = amin; p.act_max = amax; p.input = in_ptr; p.output = out_ptr;
-    p.weights = static_cast<const int8_t*>(blob->ptr());
-    p.bias_eff = tab; p.mult = tab + units; p.shift = tab + 2 * units;
-    L.kind = Launch::kFc;
-    L.kernel = "fc_kernel";
-    L.alg_ops = 2.0 * rows * units * depth;
-    L.alg_bytes = static_cast<double>(rows) * depth + static_cast<double>(rows) * units +
-                  static_cast<double>(units) * depth + 12.0 * units;
-  } else if (op.builtin == kTflAdd || op.builtin == kTflSub || op.builtin == kTflMul) {
-    const TflTensor& b = T(op.inputs[1]);
-    void* b_ptr = nullptr;
-    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &b_ptr));
-    const int act = op.options.valid() ? op.options.Int8(0, 0) : 0;
-    bh_eltwise_params& p = L.elt;
-    p = bh_eltwise_params{};
-    p.in_signed = i8 ? 1 : 0;
-    Shape4(in.shape, p.shape_a);
-    Shape4(b.shape, p.shape_b);
-    Shape4(out.shape, p.shape_o);
-    p.a_off = -Zp(in);
-    p.b_off = -Zp(b);
-    p.o_off = Zp(out);
-    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &p.act_min, &p.act_max);
-    if (op.builtin == kTflMul) {
-      p.kind = BH_ELT_MUL;
-      MulMultiplier(Scale(in), Scale(b), Scale(out), &p.o_mult, &p.o_shift);
-    } else {
-      p.kind = BH_ELT_ADD;
-      const AddParams ap = AddSubParams(Scale(in), Scale(b), Scale(out), op.builtin == kTflSub);
-      p.left_shift = ap.left_shift;
-      p.a_mult = ap.m1; p.a_shift = ap.s1;
-      p.b_mult = ap.m2; p.b_shift = ap.s2;
-      p.o_mult = ap.mo; p.o_shift = ap.so;
-    }
-    p.a = in_ptr; p.b = b_ptr; p.out = out_ptr;
-    L.kind = Launch::kEltwise;
-    L.kernel = "eltwise_kernel";
-    L.alg_bytes = static_cast<double>(in.num_elements() + b.num_elements() + out.num_elements());
-  } else if (op.builtin == kTflAveragePool2D || op.builtin == kTflMaxPool2D) {
-    const FbTable& o = op.options;
-    const bool same = o.Int8(0, 0) == 0;
-    const int sw = o.Int(1, 1), sh = o.Int(2, 1), fw = o.Int(3, 1), fh = o.Int(4, 1);
-    const int act = o.Int8(5, 0);
-    bh_pool_params& p = L.pool;
-    p = bh_pool_params{};
-    p.kind = op.builtin == kTflAveragePool2D ? BH_POOL_AVG : BH_POOL_MAX;
-    p.in_signed = i8 ? 1 : 0;
-    p.batch = in.shape[0]; p.in_h = in.shape[1]; p.in_w = in.shape[2]; p.channels = in.shape[3];
-    p.out_h = ComputeOutSize(same, p.in_h, fh, sh, 1);
-    p.out_w = ComputeOutSize(same, p.in_w, fw, sw, 1);
-    p.f_h = fh; p.f_w = fw; p.stride_h = sh; p.stride_w = sw;
-    p.pad_h = ComputePadding(sh, 1, p.in_h, fh, p.out_h);
-    p.pad_w = ComputePadding(sw, 1, p.in_w, fw, p.out_w);
-    ActivationRangeQuantized(act, Scale(out), Zp(out), i8, &p.act_min, &p.act_max);
-    p.input = in_ptr; p.output = out_ptr;
-    L.kind = Launch::kPool;
-    L.kernel = "pool_kernel";
-    L.alg_bytes = static_cast<double>(in.num_elements() + out.num_elements());
-  } else if (op.builtin == kTflCustom) {
-    // TFLite_Detection_PostProcess (CPU worker only: CpuSupports)
-    CpuDetectionParams& p = L.det;
-    if (!DetectionSupported(d, op, &p)) return absl::InternalError("unsupported custom op " + op.custom_code);
-    void* scores = nullptr;
-    void* anchors = nullptr;
-    void* outs[4];
-    RETURN_STATUS_IF(DevicePtr(model, op.inputs[1], sg, &scores));
-    RETURN_STATUS_IF(DevicePtr(model, op.inputs[2], sg, &anchors));
-    for (int k = 0; k < 4; ++k) RETURN_STATUS_IF(DevicePtr(model, op.outputs[k], sg, &outs[k]));
-    p.box_encodings = static_cast<const float*>(in_ptr);
-    p.class_scores = static_cast<const float*>(scores);
-    p.anchors = static_cast<const float*>(anchors);
-    p.out_boxes = static_cast<float*>(outs[0]);
-    p.out_classes = static_cast<float*>(outs[1]);
-    p.out_scores = static_cast<float*>(outs[2]);
-    p.out_num = static_cast<float*>(outs[3]);
-    L.kind = Launch::kDetectionPost;
-    L.kernel = "detection_postprocess_host";
-  } else if (op.builtin == kTflMean) {
-    // MEAN: host kernel on a CPU worker, mean_kernel on the GPU
-    CpuMeanParams& p = L.mean;
-    p = CpuMeanParams{};
-    if (!MeanArgs(d, op, &p.outer, &p.reduce, &p.inner)) return absl::InternalError("unsupported MEAN");
-    p.type = in.type == DataType::kFloat32 ? 0 : (in.type == DataType::kInt8 ? 1 : 2);
-    if (p.type) {
-      // optimized_integer_ops::Mean (TFLite 2.9.2): the float products as
-      // written there, then QuantizeMultiplier of the float scale
-      const float in_scale = Scale(in), out_scale = Scale(out);
-      const float n = static_cast<float>(p.reduce);
-      p.bias = Zp(out) - static_cast<int32_t>(Zp(in) * in_scale / out_scale);
-      const float real_scale = in_scale / (n * out_scale);
-      int shift = 0;
-      QuantizeMultiplier(static_cast<double>(real_scale), &p.multiplier, &shift);
-      p.shift = shift;
-    }
-    p.input = in_ptr;
-    p.output = out_ptr;
-    L.kind = Launch::kMean;
-    L.kernel = device_flag_ == DeviceFlag::kGPU ? "mean_kernel" : "mean_host";
-    L.alg_bytes = static_cast<double>(meta_[op.inputs[0]]->bytes + meta_[op.outputs[0]]->bytes);
-  } else if (op.builtin == kTflTransposeConv) {
-    RETURN_STATUS_IF(LowerTransposeConv(model, oi, out_ptr, ckey, sg, &L));
-  } else if (op.builtin != kTflReshape && op.builtin != kTflSqueeze) {
-    RETURN_STATUS_IF(LowerGlue(model, oi, in_ptr, out_ptr, ckey, sg, &L));
-  } else {  // RESHAPE / SQUEEZE: same bytes, new dims
-    L.kind = Launch::kCopy;
-    L.kernel = "copy";
-    L.src = in_ptr;
-    L.dst = out_ptr;
-    L.bytes = meta_[op.outputs[0]]->bytes;
-    L.alg_bytes = 2.0 * L.bytes;
-    if (L.src == L.dst) return absl::OkStatus();  // aliased slot: nothing to move
-  }
-  if (L.kind == Launch::kConv) {
-    const bh_conv_params c = L.conv;
-    const long M = static_cast<long>(c.batch) * c.out_h * c.out_w;
-    if (c.k_h == 1 && c.k_w == 1 && c.stride_h == 1 && c.stride_w == 1 && M <= 4) {
-      // a 1x1 conv over a handful of pixels (the classifier at batch 1) is
-      // a GEMV: run it on the weight-streaming FC kernel with the same
-      // packed operands (Bt rows are K-contiguous, bias_eff identical)
-      Launch F;
-      F.kind = Launch::kFc;
-      F.op_index = oi;
-      F.out_tensor = L.out_tensor;
-      bh_fc_params& f = F.fc;
-      f = bh_fc_params{};
-      f.rows = static_cast<int>(M); f.depth = c.in_c; f.depth_pad = c.k_pad; f.units = c.out_c;
-      f.in_xor = c.in_xor; f.in_zp = c.in_zp; f.w_zp = c.w_zp; f.out_zp = c.out_zp;
-      f.act_min = c.act_min; f.act_max = c.act_max; f.input = c.input; f.output = c.output;
-      f.weights = c.weights; f.bias_eff = c.bias_eff; f.mult = c.mult; f.shift = c.shift;
-      F.kernel = "fc_kernel";
-      F.alg_bytes = L.alg_bytes;
-      F.alg_ops = L.alg_ops;
-      L = F;
-    } else {
-      TryFuseResidualAdd(model, oi, sg, &L);
-    }
-  }
-  sg->launches.push_back(L);
-  return absl::OkStatus();
 }
 
 absl::Status HipModelExecutor::PrepareSubgraph(interface::IModel* model, std::set<int> ops, std::set<int> unit_indices) {
@@ -2931,231 +872,6 @@ absl::Status HipModelExecutor::WaitPass(PreparedSubgraph* sg) {
     const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     sg->wait_us = sg->wait_us > 0 ? 0.9 * sg->wait_us + 0.1 * us : us;
   }
-  return absl::OkStatus();
-}
-
-absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const SubgraphKey& key, int max_batch) {
-  // kGPU: batched graphs on the device; kCPU: the same lowering at batch n
-  // run by the host kernels (one pass over n images instead of n passes)
-  if (device_flag_ != DeviceFlag::kGPU && device_flag_ != DeviceFlag::kCPU)
-    return absl::InternalError("job batching needs a kGPU or kCPU executor");
-  PreparedSubgraph* base = Find(key);
-  if (!base) return absl::InternalError("Cannot find subgraph");
-  auto* hm = dynamic_cast<HipModel*>(model);
-  if (!hm || hm != model_) return absl::InternalError("job batching: not the model this executor prepared");
-  job_batches_.erase(key);
-  // the harness batches this executor's jobs itself: no coalescing
-  if (coalescer_) {
-    coalescer_->Leave(this);
-    coalescer_.reset();
-  }
-  if (max_batch <= 1) return absl::OkStatus();
-  // anchors (2, 4, 8, .., max_batch) measure their fusion choices; every
-  // other size reuses the next anchor's.  Anchors are prepared first, the
-  // largest first of all: its arena and mirrors serve every variant.
-  int step = 1;
-  if (const char* e = std::getenv("BAND_HIP_BATCH_STEP")) step = std::max(1, std::atoi(e));
-  std::vector<int> anchors;
-  for (int b = 2; b < max_batch; b *= 2) anchors.push_back(b);
-  anchors.push_back(max_batch);
-  std::vector<int> order(anchors.rbegin(), anchors.rend());
-  for (int b = max_batch - 1; b >= 2; --b)
-    if ((b % step == 0) && std::find(anchors.begin(), anchors.end(), b) == anchors.end()) order.push_back(b);
-  // the base's op set, or {} when the base was prepared as the whole model
-  // (model-order I/O): the variants' I/O order is the base's
-  std::set<int> ops;
-  if (!base->model_order_io) ops.insert(base->ops.begin(), base->ops.end());
-  const std::set<int> units = key.GetUnitIndicesSet();
-  std::vector<JobBatchVariant> variants;
-  HipModelExecutor* largest = nullptr;
-  for (int b : order) {
-    JobBatchVariant v;
-    v.batch = b;
-    RETURN_STATUS_IF(hm->CloneWithJobBatch(b, &v.model));
-    t_variant_ctor = true;
-    v.exec = std::make_unique<HipModelExecutor>(model_id_, worker_id_, device_flag_, thread_affinity_mask_,
-                                                num_threads_);
-    t_variant_ctor = false;
-    v.exec->use_graph_ = use_graph_;
-    v.exec->stream_ = stream_;  // a lane's variants run on the lane's stream
-    v.exec->coalesce_ok_ = false;
-    // direct job I/O captures the variants' graphs without host copies
-    v.exec->io_mode_ = direct_io_ ? 1 : io_mode_;
-    v.exec->direct_io_ = direct_io_;
-    v.exec->block_sync_ = block_sync_;
-    v.exec->sync_mode_ = sync_mode_;
-    if (device_flag_ == DeviceFlag::kCPU) {  // one host pool per worker
-      if (!cpu_pool_)
-        cpu_pool_ = std::make_shared<CpuPool>(num_threads_ > 0 ? num_threads_ : 1,
-                                              PinnableCpus(thread_affinity_mask_));
-      v.exec->cpu_pool_ = cpu_pool_;
-    }
-    v.exec->io_stream_bytes_ = io_stream_bytes_;
-    if (largest) {
-      PreparedSubgraph* ls = largest->Find(key);
-      v.exec->shared_arena_ = ls ? ls->arena : nullptr;
-      v.exec->shared_host_from_ = ls;
-    }
-    if (std::find(anchors.begin(), anchors.end(), b) == anchors.end())
-      v.exec->tune_batch_ = *std::lower_bound(anchors.begin(), anchors.end(), b);
-    // the base subgraph's op set (a whole-model key prepares all ops)
-    RETURN_STATUS_IF(v.exec->PrepareSubgraph(v.model.get(), ops, units));
-    PreparedSubgraph* vs = v.exec->Find(key);
-    if (!vs || vs->inputs != base->inputs || vs->outputs != base->outputs)
-      return absl::InternalError("job batching: variant I/O differs from the subgraph's");
-    if (!largest) largest = v.exec.get();
-    variants.push_back(std::move(v));
-  }
-  // ascending batch (VariantFor takes the smallest >= n); the largest
-  // variant, whose arena / mirrors the others view, is destroyed last
-  std::sort(variants.begin(), variants.end(),
-            [](const JobBatchVariant& a, const JobBatchVariant& b) { return a.batch < b.batch; });
-  job_batches_[key] = std::move(variants);
-  return absl::OkStatus();
-}
-
-int HipModelExecutor::MaxJobBatch(const SubgraphKey& key) const {
-  auto it = job_batches_.find(key);
-  return it == job_batches_.end() || it->second.empty() ? 1 : it->second.back().batch;
-}
-
-const HipModelExecutor::JobBatchVariant* HipModelExecutor::VariantFor(const SubgraphKey& key, int n) const {
-  auto it = job_batches_.find(key);
-  if (it == job_batches_.end()) return nullptr;
-  for (const JobBatchVariant& v : it->second)
-    if (v.batch >= n) return &v;
-  return nullptr;
-}
-
-std::shared_ptr<interface::ITensorView> HipModelExecutor::GetJobSlotView(const SubgraphKey& key, int index, int n,
-                                                                          int slot) {
-  if (n == 1 && slot == 0) return GetTensorView(key, index);
-  const JobBatchVariant* v = VariantFor(key, n);
-  if (!v || n < 1 || slot < 0 || slot >= n || index < 0 || index >= static_cast<int>(meta_.size())) return nullptr;
-  PreparedSubgraph* vs = v->exec->Find(key);
-  auto h = vs ? vs->host.find(index) : decltype(vs->host.end()){};
-  if (!vs || h == vs->host.end()) return nullptr;  // slot views exist for boundary tensors only
-  TensorMeta* m = meta_[index].get();
-  return std::make_shared<HipTensorView>(m, h->second->data() + static_cast<size_t>(slot) * m->bytes);
-}
-
-absl::Status HipModelExecutor::ExecuteJobBatch(const SubgraphKey& key, int n) {
-  if (n == 1) return ExecuteSubgraph(key);
-  const JobBatchVariant* v = VariantFor(key, n);
-  if (!v || n < 1) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
-  return v->exec->ExecuteSubgraph(key);
-}
-
-absl::Status HipModelExecutor::ExecuteJobBatchDirect(const SubgraphKey& key, int n,
-                                                     const std::vector<const interface::ITensor*>& in,
-                                                     const std::vector<interface::ITensor*>& out) {
-  if (device_flag_ != DeviceFlag::kGPU || n < 1 || !direct_io_) return absl::UnimplementedError("direct job batch I/O");
-  PreparedSubgraph* base = Find(key);
-  if (n == 1) {
-    // one job: the captured graph's own copy nodes, pointed at the job's
-    // ring slots for this pass (back at the mirrors before any staged pass)
-    if (!base || !use_graph_ || !base->graph || !base->io_in_graph || base->io_nodes.empty() ||
-        !base->extra_d2h.empty() || in.size() != base->inputs.size() || out.size() != base->outputs.size())
-      return absl::UnimplementedError("direct job batch I/O");
-    for (size_t k = 0; k < in.size(); ++k)
-      if (!in[k] || in[k]->GetBytes() != meta_[base->inputs[k]]->bytes)
-        return absl::InternalError("direct job I/O: input size");
-    for (size_t k = 0; k < out.size(); ++k)
-      if (out[k] && out[k]->GetBytes() != meta_[base->outputs[k]]->bytes)
-        return absl::InternalError("direct job I/O: output size");
-    int rc = bh_set_device(ordinal_);
-    if (rc) return HipErr(rc, "hipSetDevice");
-    char* arena = static_cast<char*>(base->arena->ptr());
-    // set first: a retarget that fails part-way leaves the nodes already
-    // changed pointing at ring slots, and RestoreIoNodes must reset them all
-    base->io_retargeted = true;
-    for (const auto& nd : base->io_nodes) {
-      char* dev = arena + base->offset.at(nd.tensor);
-      const size_t bytes = meta_[nd.tensor]->bytes;
-      if (nd.h2d) {
-        const size_t k = std::find(base->inputs.begin(), base->inputs.end(), nd.tensor) - base->inputs.begin();
-        rc = bh_graph_exec_set_memcpy(base->graph, nd.node, dev, in[k]->GetData(), bytes, 1);
-      } else {
-        const size_t k = std::find(base->outputs.begin(), base->outputs.end(), nd.tensor) - base->outputs.begin();
-        char* host = out[k] ? out[k]->GetData() : base->host.at(nd.tensor)->data();
-        rc = bh_graph_exec_set_memcpy(base->graph, nd.node, host, dev, bytes, 0);
-      }
-      if (rc) return HipErr(rc, "graph copy node");
-    }
-    rc = bh_graph_launch(base->graph, stream_);
-    if (rc) return HipErr(rc, "graph launch");
-    RETURN_STATUS_IF(WaitPass(base));
-    ++base->runs;
-    return absl::OkStatus();
-  }
-
-  const JobBatchVariant* v = VariantFor(key, n);
-  if (!base || !v) return absl::InternalError("no job batch variant for " + std::to_string(n) + " jobs");
-  if (in.size() != base->inputs.size() * n || out.size() != base->outputs.size() * n)
-    return absl::InternalError("direct job batch I/O: tensor count mismatch");
-  std::vector<size_t> per_job;
-  for (int t : base->inputs) per_job.push_back(meta_[t]->bytes);
-  for (int t : base->outputs) per_job.push_back(meta_[t]->bytes);
-  PreparedSubgraph* vs = v->exec->Find(key);
-  if (!vs) return absl::InternalError("job batch variant lost its subgraph");
-  return v->exec->RunDirect(vs, n, per_job, in, out);
-}
-
-absl::Status HipModelExecutor::RunDirect(PreparedSubgraph* sg, int n, const std::vector<size_t>& per_job,
-                                         const std::vector<const interface::ITensor*>& in,
-                                         const std::vector<interface::ITensor*>& out) {
-  // a graph that already holds its host copies, or intermediates a later
-  // subgraph reads back, take the staged path
-  if (!sg->extra_d2h.empty() || (use_graph_ && sg->graph && sg->io_in_graph))
-    return absl::UnimplementedError("direct job batch I/O");
-  const size_t ni = sg->inputs.size();
-  for (size_t i = 0; i < in.size(); ++i)
-    if (!in[i] || in[i]->GetBytes() != per_job[i / n]) return absl::InternalError("direct job batch I/O: input size");
-  for (size_t i = 0; i < out.size(); ++i)
-    if (out[i] && out[i]->GetBytes() != per_job[ni + i / n]) return absl::InternalError("direct job batch I/O: output size");
-  int rc = bh_set_device(ordinal_);
-  if (rc) return HipErr(rc, "hipSetDevice");
-  if (use_graph_ && !sg->graph && sg->runs > 0) {  // kernels-only graph (variants stream their I/O)
-    RETURN_STATUS_IF(CaptureGraph(sg));
-    if (sg->io_in_graph) return absl::UnimplementedError("direct job batch I/O");
-  }
-  char* arena = static_cast<char*>(sg->arena->ptr());
-  // jobs whose host tensors are adjacent (consecutive ring slots of one
-  // page-locked block) go in one DMA: a run of slots s0..s1 of tensor k
-  for (size_t k = 0; k < ni; ++k)
-    for (int s0 = 0; s0 < n;) {
-      const char* h0 = in[k * n + s0]->GetData();
-      int s1 = s0 + 1;
-      while (s1 < n && in[k * n + s1]->GetData() == h0 + (s1 - s0) * per_job[k]) ++s1;
-      rc = bh_memcpy_h2d_async(arena + sg->offset.at(sg->inputs[k]) + s0 * per_job[k], h0, (s1 - s0) * per_job[k],
-                               stream_);
-      if (rc) return HipErr(rc, "H2D input");
-      s0 = s1;
-    }
-  if (use_graph_ && sg->graph) {
-    rc = bh_graph_launch(sg->graph, stream_);
-    if (rc) return HipErr(rc, "graph launch");
-  } else {
-    RETURN_STATUS_IF(EnqueueLaunches(sg));
-  }
-  for (size_t k = 0; k < sg->outputs.size(); ++k) {
-    const size_t pb = per_job[ni + k];
-    for (int s0 = 0; s0 < n;) {
-      interface::ITensor* o = out[k * n + s0];
-      if (!o) {
-        ++s0;
-        continue;
-      }
-      char* h0 = o->GetData();
-      int s1 = s0 + 1;
-      while (s1 < n && out[k * n + s1] && out[k * n + s1]->GetData() == h0 + (s1 - s0) * pb) ++s1;
-      rc = bh_memcpy_d2h_async(h0, arena + sg->offset.at(sg->outputs[k]) + s0 * pb, (s1 - s0) * pb, stream_);
-      if (rc) return HipErr(rc, "D2H output");
-      s0 = s1;
-    }
-  }
-  RETURN_STATUS_IF(WaitPass(sg));
-  ++sg->runs;
   return absl::OkStatus();
 }
 

@@ -165,16 +165,24 @@ __global__ __launch_bounds__(256) void conv_stem_mfma_kernel(bh_conv_params p, i
   }
 }
 
-template <int NB>
-static int launch_stem_mfma(const bh_conv_params& p, int M, hipStream_t s) {
-  constexpr int PB = 4;  // 16-pixel blocks per wave
-  StemDivs dv;
-  dv.out_w = FastDiv(p.out_w);
-  dv.out_h = FastDiv(p.out_h);
+template <int NB, int PB>
+static void launch_stem_pb(const bh_conv_params& p, int M, const StemDivs& dv, hipStream_t s) {
   const int waves = (M + PB * 16 - 1) / (PB * 16);
   const dim3 grid((unsigned)((waves + 3) / 4));
   if (p.requant_fast) BH_LAUNCH((conv_stem_mfma_kernel<NB, PB, true>), grid, dim3(256), 0, s, p, M, dv);
   else BH_LAUNCH((conv_stem_mfma_kernel<NB, PB, false>), grid, dim3(256), 0, s, p, M, dv);
+}
+
+// 16-pixel blocks per wave: 4 (all four blocks' gathers in flight) while
+// that still leaves >= 4096 waves, else fewer blocks and more waves
+template <int NB>
+static int launch_stem_mfma(const bh_conv_params& p, int M, hipStream_t s) {
+  StemDivs dv;
+  dv.out_w = FastDiv(p.out_w);
+  dv.out_h = FastDiv(p.out_h);
+  if (M >= 4096 * 64) launch_stem_pb<NB, 4>(p, M, dv, s);
+  else if (M >= 4096 * 32) launch_stem_pb<NB, 2>(p, M, dv, s);
+  else launch_stem_pb<NB, 1>(p, M, dv, s);
   return bh_check_launch("conv_stem_mfma_kernel");
 }
 
@@ -183,7 +191,15 @@ static int launch_stem_mfma(const bh_conv_params& p, int M, hipStream_t s) {
 // 3x3 stems over 3 channels, dilation-1 columns, out_c in {16, 32, 48, 64}
 // (4-byte aligned output), no residual: 1 when this kernel takes the layer
 int bh_conv_stem_mfma_ok(const bh_conv_params& p) {
-  return p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.k_pad == 64 && p.out_c % 16 == 0 &&
+  // batch-1 stems (12.5k pixels) keep the VALU form: one pixel per thread
+  // over every channel group is the wider grid there (8.9 vs ~5 us,
+  // profiles/r05h_breakdown_mnv2_b1.txt); BH_STEM_MFMA_MIN_M overrides
+  static const long min_m = [] {
+    const char* e = std::getenv("BH_STEM_MFMA_MIN_M");
+    return e ? std::atol(e) : 65536L;
+  }();
+  const long M = (long)p.batch * p.out_h * p.out_w;
+  return (M >= min_m || p.kernel_hint == BH_CONV_STEM_MFMA) && p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.k_pad == 64 && p.out_c % 16 == 0 &&
          p.out_c >= 16 && p.out_c <= 64 && !p.residual && !p.out_img_stride && (((uintptr_t)p.output) & 3) == 0;
 }
 

@@ -81,7 +81,12 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_big_kernel(bh
   constexpr int D = NB - 1;
   static_assert(D >= 1 && D <= 3, "1..3 K-steps in flight");
   constexpr int OPITCH = BN + 16;  // output staging row pitch (bank spread)
-  constexpr int LDS = NB * STAGE > BM * OPITCH ? NB * STAGE : BM * OPITCH;
+  constexpr int MAIN = NB * STAGE > BM * OPITCH ? NB * STAGE : BM * OPITCH;
+  // the tile's per-channel epilogue constants (bias_eff, mult, shift), staged
+  // once before the K loop so the epilogue reads them from LDS instead of
+  // paying a dependent global round trip per channel group
+  constexpr int CONST = MAIN;
+  constexpr int LDS = MAIN + 3 * BN * 4;
   __shared__ __attribute__((aligned(16))) uint8_t lds[LDS];
 
   const int lane = threadIdx.x & 63;
@@ -134,6 +139,14 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_big_kernel(bh
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0;
 
+  {
+    int32_t* cst = (int32_t*)(lds + CONST);
+    for (int i = threadIdx.x; i < 3 * BN; i += T) {
+      const int a = i / BN, c = i - a * BN;
+      const int n = min(n0 + c, N - 1);
+      cst[i] = a == 0 ? p.bias_eff[n] : (a == 1 ? p.mult[n] : p.shift[n]);
+    }
+  }
 #pragma unroll
   for (int d = 0; d < D; ++d)
     if (d < ksteps) stage(d);
@@ -178,14 +191,16 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_big_kernel(bh
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int ch = wn0 + j * 32 + 8 * q + 4 * h;  // tile-local, 4 consecutive channels
-      const int nb = n0 + ch;
+      const int32_t* cst = (const int32_t*)(lds + CONST);
+      const v4i b4 = *(const v4i*)(cst + ch);
+      const v4i m4 = *(const v4i*)(cst + BN + ch);
+      const v4i s4 = *(const v4i*)(cst + 2 * BN + ch);
       int32_t be[4], mu[4], sh[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int n = nb + r < N ? nb + r : 0;
-        be[r] = p.bias_eff[n];
-        mu[r] = p.mult[n];
-        sh[r] = p.shift[n];
+        be[r] = b4[r];
+        mu[r] = m4[r];
+        sh[r] = s4[r];
       }
       ChanQ cq[4];
 #pragma unroll
@@ -251,6 +266,9 @@ static long big_wgs(long M, long N, int tm, int tn) { return ((M + tm - 1) / tm)
 // Tile rule (BH_GEMM_BIG_CFG for A-B runs): 256x256 tiles over 8 waves
 // (128 x 64 per wave) from one round of workgroups up; 256 x 128 (4 x 2
 // waves, 64 x 64 per wave) where 256 x 256 leaves the chip under-filled.
+// Configurations: 1 = 256x256 with 3 K-steps in flight (4 LDS buffers),
+// 2 = 256x128 / 3 = 128x256 with 2 in flight (2 workgroups per CU),
+// 4 = 256x256 with 2 in flight, 5 = 256x128 with 3 in flight.
 // Returns 0 when the layer is too small for this kernel.
 extern "C" int bh_conv_gemm_big_config(long M, int N) {
   static const int cfg = [] {
@@ -267,7 +285,8 @@ int bh_conv_gemm_big_launch(const bh_conv_params& p, int M, int K, hipStream_t s
   switch (bh_conv_gemm_big_config(M, p.out_c)) {
     case 2: return bh::launch_big<256, 128, 4, 2, 3>(p, M, K, s);
     case 3: return bh::launch_big<128, 256, 2, 4, 3>(p, M, K, s);
-    case 4: return bh::launch_big<256, 256, 2, 4, 2>(p, M, K, s);
-    default: return bh::launch_big<256, 256, 2, 4, 3>(p, M, K, s);
+    case 4: return bh::launch_big<256, 256, 2, 4, 3>(p, M, K, s);
+    case 5: return bh::launch_big<256, 128, 4, 2, 4>(p, M, K, s);
+    default: return bh::launch_big<256, 256, 2, 4, 4>(p, M, K, s);
   }
 }

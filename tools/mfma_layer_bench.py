@@ -57,7 +57,7 @@ def main():
     ap.add_argument("--batches", default="1,32,256")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--hint", type=int, default=0, help="force a conv form (BH_CONV_*), 0 = routed")
-    ap.add_argument("--only", default="", help="substring filter on layer names")
+    ap.add_argument("--only", default="", help="substring filter on layer names ('a|b': either)")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     from band_amd import _abi
@@ -72,7 +72,7 @@ def main():
     rows = []
     for B in [int(b) for b in a.batches.split(",")]:
         for name, sp_in, ci, co, k, stride in LAYERS:
-            if a.only and a.only not in name:
+            if a.only and not any(o in name for o in a.only.split("|")):
                 continue
             c = ConvCase(rng, B, sp_in, sp_in, ci, co, k, k, stride=(stride, stride), act=3, kernel_hint=a.hint)
             keep = []

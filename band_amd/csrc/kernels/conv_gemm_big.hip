@@ -263,12 +263,10 @@ static int launch_big(const bh_conv_params& p, int M, int K, hipStream_t s) {
 
 static long big_wgs(long M, long N, int tm, int tn) { return ((M + tm - 1) / tm) * ((N + tn - 1) / tn); }
 
-// Tile rule (BH_GEMM_BIG_CFG for A-B runs): 256x256 tiles over 8 waves
-// (128 x 64 per wave) from one round of workgroups up; 256 x 128 (4 x 2
-// waves, 64 x 64 per wave) where 256 x 256 leaves the chip under-filled.
-// Configurations: 1 = 256x256 with 3 K-steps in flight (4 LDS buffers),
-// 2 = 256x128 / 3 = 128x256 with 2 in flight (2 workgroups per CU),
-// 4 = 256x256 with 2 in flight, 5 = 256x128 with 3 in flight.
+// Configurations (BH_GEMM_BIG_CFG forces one for A-B runs): 1 = 256x256
+// tiles (8 waves of 128 x 64) with 3 K-steps in flight (4 LDS buffers),
+// 2 = 256x128 / 3 = 128x256 (8 waves of 64 x 64) with 2 in flight (two
+// workgroups per CU), 4 = 256x256 with 2 in flight, 5 = 256x128 with 3.
 // Returns 0 when the layer is too small for this kernel.
 extern "C" int bh_conv_gemm_big_config(long M, int N) {
   static const int cfg = [] {
@@ -276,7 +274,13 @@ extern "C" int bh_conv_gemm_big_config(long M, int N) {
     return e ? std::atoi(e) : 0;
   }();
   if (cfg > 0) return cfg;
-  if (big_wgs(M, N, 256, 256) >= 192) return 1;
+  // two workgroups per CU (72 KB of LDS each) beat one 256 x 256 tile with a
+  // deeper pipeline on every layer measured: the second workgroup's K loop
+  // runs under the first one's barriers and epilogue (PoseNet 1024 -> 1024
+  // at B = 256: 92-95 vs 110 us; MobileNetV2 320 -> 1280: 18.3 vs 30.9 us,
+  // profiles/r05j_gemm_big_cfg.txt).  128 x 256 when N fills the 256
+  // columns, else 256 x 128; from one round of 256 workgroups.
+  if (N >= 256 && big_wgs(M, N, 128, 256) >= 256) return 3;
   if (big_wgs(M, N, 256, 128) >= 256) return 2;
   return 0;
 }
@@ -284,9 +288,9 @@ extern "C" int bh_conv_gemm_big_config(long M, int N) {
 int bh_conv_gemm_big_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   switch (bh_conv_gemm_big_config(M, p.out_c)) {
     case 2: return bh::launch_big<256, 128, 4, 2, 3>(p, M, K, s);
-    case 3: return bh::launch_big<128, 256, 2, 4, 3>(p, M, K, s);
     case 4: return bh::launch_big<256, 256, 2, 4, 3>(p, M, K, s);
     case 5: return bh::launch_big<256, 128, 4, 2, 4>(p, M, K, s);
-    default: return bh::launch_big<256, 256, 2, 4, 4>(p, M, K, s);
+    case 1: return bh::launch_big<256, 256, 2, 4, 4>(p, M, K, s);
+    default: return bh::launch_big<128, 256, 2, 4, 3>(p, M, K, s);
   }
 }

@@ -97,7 +97,7 @@ def main():
             ops = 2.0 * M * co * K
             byts = B * sp_in * sp_in * ci + M * co + co * K + 12 * co  # the input once, not its im2col
             tops = ops / us / 1e6
-            attain = min(PEAK_TOPS, ops / byts * HBM_TBS * 1e3)
+            attain = min(PEAK_TOPS, ops / byts * HBM_TBS)  # op/B x TB/s = TOPS
             r = dict(layer=name, batch=B, M=M, N=co, K=K, kernel=kern, us=round(us, 2), gop=round(ops / 1e9, 3),
                      tops=round(tops, 1), frac_peak=round(tops / PEAK_TOPS, 4), op_per_byte=round(ops / byts, 1),
                      attainable_tops=round(attain, 1), frac_attainable=round(tops / attain, 4),

@@ -586,6 +586,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         const double u = TimeLaunches(base, 10);
         const double u_p2 = ok3 ? TimeLaunches({P2}, 10) : 0.0;
         measured = u > 0 && u_p2 >= 0;
+        // BAND_HIP_TUNE_LOG=1: every measured form of every chain on stderr
+        static const bool tune_log = std::getenv("BAND_HIP_TUNE_LOG") != nullptr;
+        if (tune_log) std::fprintf(stderr, "[chain-tune] %s unfused %.2f (pw2 %.2f)\n", key, u, u_p2);
         double best = u * 0.98;  // fusion must win by > 2% to be taken
         // (px_blocks, waves): 64 / 32 / 16 pixels per 4-wave workgroup, or
         // 16 pixels over 16 waves (few-pixel, many-channel layers)
@@ -634,6 +637,9 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             F.chain = q;
             const double us = TimeLaunches({&F}, 10);
             const double total = us + (form == 1 && ok3 ? u_p2 : 0.0);
+            if (tune_log)
+              std::fprintf(stderr, "[chain-tune]   form%d px%d w%d persist%d tile%d deep%d split%d valu%d: %.2f\n", 3 - form,
+                           pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], total);
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
@@ -645,6 +651,7 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         }
       }
       if (!measured) choice = ok3 ? 4 : 14;  // no device timing: the 3-launch form when it applies
+      if (measured && std::getenv("BAND_HIP_TUNE_LOG")) std::fprintf(stderr, "[chain-tune] %s -> %d\n", key, choice);
       if (autotune_ && measured) {
         std::lock_guard<std::mutex> lk(g_tune_mu);
         if (!g_tune.count(key)) AppendTuneFileLocked(key, choice);

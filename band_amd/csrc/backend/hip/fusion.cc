@@ -286,7 +286,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 9;
+constexpr int kChainTuneVersion = 10;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];

@@ -74,6 +74,9 @@ class Engine : public IEngine {
   // read in the end-of-request callback stays usable after the planner's
   // 1000-record window has moved past the job)
   absl::Status GetOutputTensorsOf(const Job& job, Tensors outputs);
+  // restriction: the request's output slot is held while its callbacks run;
+  // a callback blocking on a newer request of the same model fails that
+  // request after BANDX_OUTPUT_HOLD_MS (TensorRingBuffer::AcquireForWrite)
   CallbackId SetOnEndRequest(std::function<void(int, absl::Status)> on_end_request);
   absl::Status UnsetOnEndRequest(CallbackId callback_id);
   // extension: one call per group of finished requests with their records

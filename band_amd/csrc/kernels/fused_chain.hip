@@ -290,7 +290,11 @@ __device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsig
 #else
 #define BH_CHAIN_OCC
 #endif
-template <int RB, bool FAST, int KX, int NW, bool AM, int DA = 2>
+// VAR: compile-time form variants, so the default instantiation carries no
+// code of the others (built as runtime branches they cost 1-3.6 us per
+// launch on every chain at batch 24, profiles/r05m_*): bit 0 = the VALU
+// depthwise phase (dw_valu), bit 1 = the phase-C channel split over grid.y
+template <int RB, bool FAST, int KX, int NW, bool AM, int DA = 2, int VAR = 0>
 __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     int off_add, ChainDivs dv) {
   typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -338,7 +342,8 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
   if (stamps && threadIdx.x == 0) stamps[7] = t_entry;
 
   // ---- phase A: depthwise 3x3 -> LDS -------------------------------------
-  if (cp.dw_valu) {
+  constexpr bool SPLIT = (VAR & 2) != 0;
+  if constexpr ((VAR & 1) != 0) {
     // VALU form (dw_valu): a thread takes (pixel, 4-channel quad) items; the
     // nine tap dwords of an item hold 4 CHANNELS of one tap, two 4x4 byte
     // transposes turn taps 0-3 / 4-7 into dwords of 4 TAPS of one channel
@@ -510,7 +515,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int KS1 = a.k_pad >> 6;
     const unsigned char* xrow = dl + prow * S1 + g * 16;
     const uint8_t* res = (const uint8_t*)a.residual;
-    const bool out1 = a.output != nullptr && blockIdx.y == 0;  // split: slice 0 stores it
+    const bool out1 = a.output != nullptr && (!SPLIT || blockIdx.y == 0);  // split: slice 0 stores it
     auto epi = [&](int t, int n, v4i acc, int mu, int sh) {
       if (n >= N1) return;
       const ChanQ q = chan_q(mu, sh, a.out_zp);
@@ -572,7 +577,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
   }
   __syncthreads();
   CHAIN_STAMP(2)
-  if (cp.pw1.output && blockIdx.y == 0)
+  if (cp.pw1.output && (!SPLIT || blockIdx.y == 0))
     copy_out(o1, (uint8_t*)cp.pw1.output + (long)m0 * cp.pw1.out_c, rows * cp.pw1.out_c);
   CHAIN_STAMP(3)
   if (!cp.has_pw2) return;
@@ -583,35 +588,39 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int N2 = b.out_c;
     const int KS2 = b.k_pad >> 6;
     const unsigned char* xrow = pl + prow * S2 + g * 16;
-    // split (grid.y > 1): this workgroup's channel tiles [t_lo, t_hi)
-    const int T2 = (N2 + 15) >> 4;
-    const int t_lo = (int)blockIdx.y * T2 / (int)gridDim.y, t_hi = ((int)blockIdx.y + 1) * T2 / (int)gridDim.y;
-    if (AM) {
-      gemm_xs4_nt<KX>(b, pl, S2, KS2, wave, r16, g, [&](int n, const v4i* acc, int mu, int sh) {
-        if (n >= N2) return;
-        const ChanQ q = chan_q(mu, sh, b.out_zp);
+    auto epi4 = [&](int n, const v4i* acc, int mu, int sh) {
+      if (n >= N2) return;
+      const ChanQ q = chan_q(mu, sh, b.out_zp);
 #pragma unroll
-        for (int pb4 = 0; pb4 < 4; ++pb4) {
-          int32_t v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
-          stage4(dl, N2, pb4 * 16 + 4 * g, n, v);
-        }
-      }, t_lo, t_hi);
-    } else {
-      gemm_xs_nt<KX, TTC>(b, xrow, KS2, t_lo + wsub, WPB, r16, g, [&](int t, int n, v4i acc, int mu, int sh) {
-        if (n >= N2) return;
-        const ChanQ q = chan_q(mu, sh, b.out_zp);
+      for (int pb4 = 0; pb4 < 4; ++pb4) {
         int32_t v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
-        stage4(dl, N2, orow, n, v);
-      }, t_hi);
+        for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[pb4][r], q, b.out_zp, b.act_min, b.act_max);
+        stage4(dl, N2, pb4 * 16 + 4 * g, n, v);
+      }
+    };
+    auto epi1 = [&](int t, int n, v4i acc, int mu, int sh) {
+      if (n >= N2) return;
+      const ChanQ q = chan_q(mu, sh, b.out_zp);
+      int32_t v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = requant_out<FAST>(acc[r], q, b.out_zp, b.act_min, b.act_max);
+      stage4(dl, N2, orow, n, v);
+    };
+    if constexpr (SPLIT) {
+      // this workgroup's channel tiles [t_lo, t_hi) (grid.y slices)
+      const int T2 = (N2 + 15) >> 4;
+      const int t_lo = (int)blockIdx.y * T2 / (int)gridDim.y, t_hi = ((int)blockIdx.y + 1) * T2 / (int)gridDim.y;
+      if constexpr (AM) gemm_xs4_nt<KX>(b, pl, S2, KS2, wave, r16, g, epi4, t_lo, t_hi);
+      else gemm_xs_nt<KX, TTC>(b, xrow, KS2, t_lo + wsub, WPB, r16, g, epi1, t_hi);
+    } else {
+      if constexpr (AM) gemm_xs4_nt<KX>(b, pl, S2, KS2, wave, r16, g, epi4);
+      else gemm_xs_nt<KX, TTC>(b, xrow, KS2, wsub, WPB, r16, g, epi1);
     }
   }
   __syncthreads();
   CHAIN_STAMP(4)
-  if (gridDim.y == 1) {
+  if constexpr (!SPLIT) {
     copy_out(dl, (uint8_t*)cp.pw2.output + (long)m0 * cp.pw2.out_c, rows * cp.pw2.out_c);
   } else {
     const int N2 = cp.pw2.out_c;
@@ -933,15 +942,15 @@ __global__ __launch_bounds__(256) void chain_persist_kernel(bh_chain_params cp, 
   }
 }
 
-template <int RB, bool FAST, int KX, int NW = 4, bool AM = false, int DA = 2>
-static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
+template <int RB, bool FAST, int KX, int NW, bool AM, int DA, int VAR>
+static void launch_chain_v(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
   if (lds > 64 * 1024) {
     // opt in to the CU's full 160 KiB of LDS for this instantiation (once per device)
     static thread_local int opted_device = -1;
     int dev = 0;
     (void)hipGetDevice(&dev);
     if (opted_device != dev) {
-      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW, AM, DA>, hipFuncAttributeMaxDynamicSharedMemorySize,
+      (void)hipFuncSetAttribute((const void*)chain_kernel<RB, FAST, KX, NW, AM, DA, VAR>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
       opted_device = dev;
     }
@@ -951,9 +960,25 @@ static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, siz
   dv.out_h = FastDiv(p.dw.out_h);
   dv.quads = FastDiv(p.dw.out_c / 4);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
-  const int split = p.has_pw2 && p.c_split > 1 ? p.c_split : 1;
-  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA>), dim3(blocks, split), dim3(NW * 64), lds, s, p, P, L.S1, L.S2,
-            L.off_pl, L.off_o1, L.off_add, dv);
+  const int split = (VAR & 2) ? p.c_split : 1;
+  BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA, VAR>), dim3(blocks, split), dim3(NW * 64), lds, s, p, P, L.S1,
+            L.S2, L.off_pl, L.off_o1, L.off_add, dv);
+}
+
+// the variant instantiations: VALU phase A on the DA = 2 forms; the split on
+// the one- / two-block forms without the amortised GEMMs (bh_chain_lds_bytes
+// admits nothing else)
+template <int RB, bool FAST, int KX, int NW = 4, bool AM = false, int DA = 2>
+static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
+  const int var = (p.dw_valu ? 1 : 0) | (p.has_pw2 && p.c_split > 1 ? 2 : 0);
+  if constexpr (DA == 2) {
+    if constexpr (!AM && RB <= 2) {
+      if (var == 3) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 3>(p, P, L, lds, s);
+      if (var == 2) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 2>(p, P, L, lds, s);
+    }
+    if (var == 1) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 1>(p, P, L, lds, s);
+  }
+  launch_chain_v<RB, FAST, KX, NW, AM, DA, 0>(p, P, L, lds, s);
 }
 
 template <bool FAST, int KX>
@@ -1023,7 +1048,9 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   if (p.c_split < 0 || p.c_split > 4) return 0;
   // the VALU depthwise phase: raster forms (not persistent / tile / deep)
   if (p.dw_valu && (p.tile || p.persist || p.deep)) return 0;
-  if (p.c_split > 1 && (p.tile || p.persist || !p.has_pw2 || (p.pw2.out_c + 15) / 16 < p.c_split)) return 0;
+  if (p.c_split > 1 && (p.tile || p.persist || p.deep || p.px_blocks > 2 || !p.has_pw2 ||
+                        (p.pw2.out_c + 15) / 16 < p.c_split))
+    return 0;
   if (p.tile) return bh_chain_tile_lds_bytes(pp);
   if (p.deep && (p.persist || !((p.px_blocks == 1 && (p.waves == 0 || p.waves == 4 || p.waves == 8)) ||
                                 (p.px_blocks == 2 && (p.waves == 0 || p.waves == 4)))))

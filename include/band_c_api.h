@@ -173,6 +173,12 @@ BAND_CAPI_EXPORT BandRequestHandle BandEngineRequestAsyncOptions(BandEngine* eng
                                                                  BandTensor** input_tensors);
 BAND_CAPI_EXPORT BandStatus BandEngineWait(BandEngine* engine, BandRequestHandle handle, BandTensor** output_tensors,
                                            size_t num_outputs);
+// The finished request's output slot stays held until its callbacks
+// return.  A callback that blocks on a newer request of the same model
+// (BandEngineRequestSync / BandEngineWait) may need that slot: the worker
+// writing it waits at most BANDX_OUTPUT_HOLD_MS (default 2000) and then
+// fails that request (kBandErr) instead of deadlocking.  Callbacks should
+// return promptly and not wait on the same model's requests.
 BAND_CAPI_EXPORT BandCallbackHandle BandEngineSetOnEndRequest(BandEngine* engine,
                                                               void (*on_end_invoke)(void* user_data,
                                                                                     BandRequestHandle job_id,

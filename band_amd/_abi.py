@@ -169,6 +169,7 @@ KERNEL_SYMBOLS = {
     "bh_stream_create": (c_int, [ctypes.POINTER(c_void_p)]),
     "bh_stream_destroy": (c_int, [c_void_p]),
     "bh_stream_sync": (c_int, [c_void_p]),
+    "bh_stream_query": (c_int, [c_void_p]),
     "bh_malloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),
     "bh_free": (c_int, [c_void_p]),
     "bh_host_alloc": (c_int, [ctypes.POINTER(c_void_p), c_size_t]),

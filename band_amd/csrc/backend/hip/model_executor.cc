@@ -51,8 +51,13 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
   if (const char* b = std::getenv("BAND_HIP_IO_STREAM_BYTES")) io_stream_bytes_ = std::strtoull(b, nullptr, 10);
   if (const char* sy = std::getenv("BAND_HIP_SYNC")) {
     const std::string m(sy);
-    sync_mode_ = m == "block" ? kSyncBlock : m == "poll" ? kSyncPoll : m == "poller" ? kSyncPoller : kSyncSpin;
+    sync_mode_ = m == "block"    ? kSyncBlock
+                 : m == "poll"     ? kSyncPoll
+                 : m == "poller"   ? kSyncPoller
+                 : m == "adaptive" ? kSyncAdaptive
+                                   : kSyncSpin;
   }
+  if (const char* f = std::getenv("BAND_HIP_SYNC_SLEEP")) sleep_frac_ = std::min(0.95, std::max(0.0, std::atof(f)));
   block_sync_ = sync_mode_ == kSyncBlock;
   if (const char* d = std::getenv("BAND_HIP_DIRECT_IO")) direct_io_ = d[0] != '0';
   if (const char* c = std::getenv("BAND_HIP_COALESCE")) coalesce_max_ = std::atoi(c);
@@ -837,9 +842,32 @@ absl::Status HipModelExecutor::RunPass(PreparedSubgraph* sg) {
 
 absl::Status HipModelExecutor::WaitPass(PreparedSubgraph* sg) {
   int rc = 0;
-  if (sync_mode_ == kSyncSpin) {
+  if (sync_mode_ == kSyncSpin || (sync_mode_ == kSyncAdaptive && !sg)) {
     rc = bh_stream_sync(stream_);
     return rc ? HipErr(rc, "stream sync") : absl::OkStatus();
+  }
+  if (sync_mode_ == kSyncAdaptive) {
+    // sleep through sleep_frac_ of the pass's expected wait, then spin in
+    // hipStreamSynchronize: the thread holds a core only for the tail of the
+    // pass, and it is already running (no wake-up from an idle core, the
+    // cost of the blocking forms) when the pass ends.  A wake-up that finds
+    // the pass already done shortens the next sleep.
+    thread_local bool slack = [] { return prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0) == 0; }();
+    (void)slack;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double sleep = sleep_frac_ * sg->wait_us;
+    bool overslept = false;
+    if (sleep >= 20.0) {
+      timespec ts{0, static_cast<long>(sleep * 1000.0)};
+      nanosleep(&ts, nullptr);
+      overslept = bh_stream_query(stream_) == 0;
+    }
+    rc = bh_stream_sync(stream_);
+    if (rc) return HipErr(rc, "stream sync");
+    const double us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+    if (overslept) sg->wait_us *= 0.85;
+    else sg->wait_us = sg->wait_us > 0 ? 0.9 * sg->wait_us + 0.1 * us : us;
+    return absl::OkStatus();
   }
   if (!done_event_ && (sync_mode_ == kSyncBlock ? bh_event_create_blocking(&done_event_)
                                                 : bh_event_create_untimed(&done_event_)) != 0)

@@ -298,8 +298,11 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // and the GPU's CompletionPoller thread (completion.h) wakes it when the
   // pass's event completes - one polling core per GPU instead of one per
   // waiting thread.
-  enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2, kSyncPoller = 3 };
+  // adaptive (BAND_HIP_SYNC=adaptive): sleep through BAND_HIP_SYNC_SLEEP
+  // (default 0.7) of the pass's expected wait, then spin (WaitPass).
+  enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2, kSyncPoller = 3, kSyncAdaptive = 4 };
   int sync_mode_ = kSyncSpin;
+  double sleep_frac_ = 0.7;
   bool block_sync_ = false;  // sync_mode_ == kSyncBlock
   // waits for everything enqueued on stream_ (the pass of `sg`)
   absl::Status WaitPass(PreparedSubgraph* sg);

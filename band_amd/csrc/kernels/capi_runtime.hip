@@ -79,6 +79,11 @@ extern "C" int bh_stream_create(bh_stream_t* stream) {
 }
 extern "C" int bh_stream_destroy(bh_stream_t s) { return ck(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy"); }
 extern "C" int bh_stream_sync(bh_stream_t s) { return ck(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize"); }
+extern "C" int bh_stream_query(bh_stream_t s) {
+  const hipError_t e = hipStreamQuery((hipStream_t)s);
+  if (e == hipErrorNotReady) return BH_ENOTREADY;
+  return ck(e, "hipStreamQuery");
+}
 
 extern "C" int bh_malloc(void** p, size_t bytes) { return ck(hipMalloc(p, bytes ? bytes : 16), "hipMalloc"); }
 extern "C" int bh_free(void* p) { return p ? ck(hipFree(p), "hipFree") : 0; }

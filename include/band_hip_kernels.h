@@ -71,6 +71,8 @@ int bh_device_pci_bus_id(int ordinal, char* buf, int cap);
 int bh_stream_create(bh_stream_t* stream);
 int bh_stream_destroy(bh_stream_t stream);
 int bh_stream_sync(bh_stream_t stream);
+/* 0 when all work on the stream is done, BH_ENOTREADY while some is not */
+int bh_stream_query(bh_stream_t stream);
 int bh_malloc(void** ptr, size_t bytes);
 int bh_free(void* ptr);
 int bh_host_alloc(void** ptr, size_t bytes); /* pinned, portable */

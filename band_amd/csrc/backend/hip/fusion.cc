@@ -26,7 +26,7 @@ bool LaunchIo(const Launch& l, std::vector<const void*>* rd, std::vector<const v
       *wr = {l.dw.output};
       return true;
     case Launch::kChain:
-      *rd = {l.chain.dw.input, l.chain.pw1.residual};
+      *rd = {l.chain_stem ? l.conv.input : l.chain.dw.input, l.chain.pw1.residual};
       *wr = {l.chain.pw1.output, l.chain.has_pw2 ? l.chain.pw2.output : nullptr};
       return true;
     case Launch::kIrb:
@@ -706,11 +706,70 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       F.alg_ops += P2->alg_ops;
       if (!a.output) sg->fused_tensors.insert(P1.out_tensor);
     }
+    // the RGB stem into the tile form: the launch just before the chain
+    // produces the depthwise input and nothing else reads it
+    if (F.chain.tile == 1 && !no_stem_chain_ && !out.empty() && out.back().kind == Launch::kConv &&
+        out.back().conv.k_h == 3 && out.back().conv.k_w == 3 && out.back().conv.in_c == 3 &&
+        out.back().conv.output == F.chain.dw.input && private_tensor(out.back().out_tensor, D.op_index))
+      TryFuseStem(&out, &F, sg);
     out.push_back(F);
     sg->fused_tensors.insert(D.out_tensor);
     i += three ? 2 : 1;
   }
   sg->launches.swap(out);
+}
+
+// The RGB stem (out->back()) computed inside the tile chain F's workgroups
+// (bh_chain_params.stem): taken by on-device timing against the two
+// launches (> 2 %), cached per geometry; BAND_HIP_FUSION=forcestem always,
+// nostem never.
+void HipModelExecutor::TryFuseStem(std::vector<Launch>* out, Launch* F, PreparedSubgraph* sg) {
+  const Launch& S = out->back();
+  Launch Q = *F;
+  Q.chain_stem = true;
+  Q.conv = S.conv;
+  {
+    bh_chain_params q = Q.chain;
+    q.stem = &Q.conv;
+    if (bh_chain_lds_bytes(&q) == 0) return;
+  }
+  const bh_conv_params& st = S.conv;
+  char key[160];
+  std::snprintf(key, sizeof(key), "cs%d:%d:%d:%dx%d:s%d:%d:%d:%d", kChainTuneVersion, ordinal_,
+                tune_batch_ > 0 ? tune_batch_ : st.batch, st.in_h, st.in_w, st.stride_h, st.out_c, F->chain.pw1.out_c,
+                F->chain.has_pw2 ? F->chain.pw2.out_c : 0);
+  int fuse = force_stem_chain_ ? 1 : -1;
+  if (fuse < 0 && autotune_) {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    LoadTuneFileLocked();
+    auto it = g_tune.find(key);
+    if (it != g_tune.end()) fuse = it->second;
+  }
+  if (fuse < 0) {
+    fuse = 0;
+    if (autotune_) {
+      const double u = TimeLaunches({&S, F}, 10);
+      const double f = TimeLaunches({&Q}, 10);
+      if (u > 0 && f > 0 && f < 0.98 * u) fuse = 1;
+      if (std::getenv("BAND_HIP_TUNE_LOG"))
+        std::fprintf(stderr, "[chain-tune] %s stem + chain %.2f, fused %.2f -> %d\n", key, u, f, fuse);
+      std::lock_guard<std::mutex> lk(g_tune_mu);
+      if (!g_tune.count(key)) AppendTuneFileLocked(key, fuse);
+      g_tune[key] = fuse;
+    }
+  }
+  if (!fuse) return;
+  // algorithmic bytes: the image and the stem's filter / tables instead of
+  // the depthwise input
+  const bh_dwconv_params& dw = F->chain.dw;
+  Q.alg_bytes = F->alg_bytes - static_cast<double>(dw.batch) * dw.in_h * dw.in_w * dw.in_c +
+                static_cast<double>(st.batch) * st.in_h * st.in_w * st.in_c +
+                static_cast<double>(st.out_c) * st.k_pad + 12.0 * st.out_c;
+  Q.alg_ops = F->alg_ops + S.alg_ops;
+  Q.op_index = S.op_index;
+  sg->fused_tensors.insert(S.out_tensor);
+  out->pop_back();
+  *F = Q;
 }
 
 namespace {

@@ -54,8 +54,8 @@ HipModelExecutor::HipModelExecutor(ModelId model_id, WorkerId worker_id, DeviceF
     sync_mode_ = m == "block"    ? kSyncBlock
                  : m == "poll"     ? kSyncPoll
                  : m == "poller"   ? kSyncPoller
-                 : m == "adaptive" ? kSyncAdaptive
-                                   : kSyncSpin;
+                 : m == "spin"     ? kSyncSpin
+                                   : kSyncAdaptive;
   }
   if (const char* f = std::getenv("BAND_HIP_SYNC_SLEEP")) sleep_frac_ = std::min(0.95, std::max(0.0, std::atof(f)));
   block_sync_ = sync_mode_ == kSyncBlock;
@@ -302,6 +302,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "r4forms") == 0) no_split_chain_ = no_valu_chain_ = true;  // A-B: round 4's form set
   if (f && std::strcmp(f, "forcevalu") == 0) force_chain_ = force_valu_chain_ = true;  // parity: ... VALU depthwise
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
+  if (f && std::strcmp(f, "nostem") == 0) no_stem_chain_ = true;  // A-B: the stem stays its own launch
+  if (f && std::strcmp(f, "forcestem") == 0) force_chain_ = force_tile_chain_ = force_stem_chain_ = true;  // parity
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();
@@ -579,7 +581,15 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kEltwise: rc = bh_eltwise_i8(&l.elt, stream_); break;
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
-    case Launch::kChain: rc = bh_chain_i8(&l.chain, stream_); break;
+    case Launch::kChain:
+      if (l.chain_stem) {
+        bh_chain_params q = l.chain;
+        q.stem = &l.conv;
+        rc = bh_chain_i8(&q, stream_);
+      } else {
+        rc = bh_chain_i8(&l.chain, stream_);
+      }
+      break;
     case Launch::kConvGroup: rc = bh_conv_group_i8(&l.cgroup, stream_); break;
     case Launch::kCopy: {
       // a kernel copy, not a blit: graphs replayed under rocprofv3's kernel

@@ -48,6 +48,9 @@ struct Launch {
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
+  // kChain with the RGB stem fused into its tile form: `conv` holds the
+  // stem (bh_chain_params.stem points at it for the launch)
+  bool chain_stem = false;
   bh_conv_params conv{};
   bh_dwconv_params dw{};
   bh_fc_params fc{};
@@ -203,6 +206,7 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
   // dw3x3 -> conv1x1 [+ADD] [-> conv1x1] runs into one bh_chain_i8 launch
   bool PackChainTile(bh_chain_params* q, PreparedSubgraph* sg);
+  void TryFuseStem(std::vector<Launch>* out, Launch* F, PreparedSubgraph* sg);
   void FuseChains(const HipModel& model, PreparedSubgraph* sg);
   // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
   // CONCATENATION with outer size 1 elided (producers write their slices)
@@ -273,6 +277,8 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   bool no_valu_chain_ = false;     // BAND_HIP_FUSION=novalu: ... the VALU depthwise forms
   bool force_valu_chain_ = false;  // BAND_HIP_FUSION=forcevalu: every feasible chain, VALU depthwise (parity)
   bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form
+  bool no_stem_chain_ = false;     // BAND_HIP_FUSION=nostem: the RGB stem stays its own launch
+  bool force_stem_chain_ = false;  // BAND_HIP_FUSION=forcestem: tile chains, the stem fused wherever it fits
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;
@@ -286,7 +292,7 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // stream | auto (default: stream from io_stream_bytes_ of host I/O per
   // pass, BAND_HIP_IO_STREAM_BYTES)
   int io_mode_ = 2;  // 0 graph, 1 stream, 2 auto
-  // How a pass is waited for.  spin (default): hipStreamSynchronize, which
+  // How a pass is waited for.  spin (BAND_HIP_SYNC=spin): hipStreamSynchronize, which
   // busy-polls - a core per GPU worker for the whole pass, and the lowest
   // completion latency.  block (BAND_HIP_SYNC=block): a blocking-sync event.
   // poll (BAND_HIP_SYNC=poll): the thread sleeps through most of the pass's
@@ -298,11 +304,15 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   // and the GPU's CompletionPoller thread (completion.h) wakes it when the
   // pass's event completes - one polling core per GPU instead of one per
   // waiting thread.
-  // adaptive (BAND_HIP_SYNC=adaptive): sleep through BAND_HIP_SYNC_SLEEP
-  // (default 0.7) of the pass's expected wait, then spin (WaitPass).
+  // adaptive (default since round 5; BAND_HIP_SYNC=spin restores spinning):
+  // sleep through BAND_HIP_SYNC_SLEEP (default 0.85) of the pass's expected
+  // wait, then spin (WaitPass).  C3 headline, interleaved on one box
+  // (profiles/r05p_*): spin 109.8k / 103.4k inf/s at 8.9 / 8.7 process
+  // cores; adaptive 0.7 109.1k / 110.0k at 4.5 / 4.2; 0.85 108.4k / 109.6k
+  // at 4.1 / 4.0 (one of them the request driver's submitter thread).
   enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2, kSyncPoller = 3, kSyncAdaptive = 4 };
-  int sync_mode_ = kSyncSpin;
-  double sleep_frac_ = 0.7;
+  int sync_mode_ = kSyncAdaptive;
+  double sleep_frac_ = 0.85;
   bool block_sync_ = false;  // sync_mode_ == kSyncBlock
   // waits for everything enqueued on stream_ (the pass of `sg`)
   absl::Status WaitPass(PreparedSubgraph* sg);

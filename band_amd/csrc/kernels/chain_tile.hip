@@ -45,8 +45,10 @@
 // fall on distinct LDS banks (the DMA writes LDS linearly; no padding).
 #include <algorithm>
 #include <cstring>
+#include <type_traits>
 
 #include "common.hpp"
+#include "stem_window.hpp"
 
 namespace bh {
 
@@ -204,6 +206,7 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
 
 struct TileDivs {
   FastDiv tiles_x, txy, patch_ru, res_ru4;
+  FastDiv pw;  // STEM: patch pixels per row
   int per;     // PIPE: consecutive tiles per workgroup
   int ntiles;  // batch x tiles
 };
@@ -283,8 +286,19 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
 // constant block is staged once per workgroup instead of once per tile (for
 // the 112x112 x 32 chain it is 9.2 KB against a 3.2 KB patch), and each
 // further tile's patch is DMA'd after the previous tile is done
-template <int TH, int TW, bool FAST, int KX, int PIPE>
-__global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv) {
+// STEM (bh_chain_params.stem, tile 1): the depthwise input is the RGB stem's
+// output, and the workgroup computes its patch from the image instead of
+// reading it: wave w takes patch pixels (w & 1) + 2k and output channels
+// [(w >> 1) C/2, (w >> 1 + 1) C/2) - the stem's window gather and v_dot4
+// over filter dwords read through the scalar cache, as conv_stem_kernel -
+// and writes each channel quad to the patch at its swizzled chunk.  Pixels
+// outside the image are skipped (phase A masks those taps).  The stem's
+// output never reaches HBM; halo pixels are computed by both neighbouring
+// tiles (1.56x the stem's arithmetic for 8 x 8 tiles at stride 1).
+struct NoStem {};
+template <int TH, int TW, bool FAST, int KX, int PIPE, typename ST = NoStem>
+__global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv, ST st) {
+  constexpr bool STEM = !std::is_same<ST, NoStem>::value;
   static_assert(TH * TW == 64, "4 pixel blocks of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_entry = __builtin_amdgcn_s_memtime();  // before any kernarg load
@@ -324,9 +338,47 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
     int n, oy0, ox0;
     tile_xy(t, n, oy0, ox0);
     const int C = d.out_c;
+    const int y0 = oy0 * d.stride_h - d.pad_h;  // image coords of patch (0, 0)
+    if constexpr (STEM) {
+      const int xs = ox0 * d.stride_w - d.pad_w;
+      const int npix = G.PH * G.PW;
+      const int half = C >> 1;
+      const int cbeg = (wave >> 1) * half;  // uniform per wave: scalar filter loads
+      const long img = (long)st.in_h * st.in_w * 3;
+      const uint8_t* im = (const uint8_t*)st.input + n * img;
+      const uint8_t* end = (const uint8_t*)st.input + st.batch * img;
+      const cst_ptr<int32_t> wts = as_const((const int32_t*)st.weights);
+      const cst_ptr<int32_t> sbias = as_const(st.bias_eff), smult = as_const(st.mult), sshift = as_const(st.shift);
+      const int kpw = st.k_pad >> 2;
+      for (int pix = (wave & 1) * 64 + lane; pix < npix; pix += 128) {
+        const int r = dv.pw.div(pix);
+        const int px = pix - r * G.PW;
+        const int y = y0 + r, x = xs + px;
+        if (y < 0 || y >= d.in_h || x < 0 || x >= d.in_w) continue;
+        uint32_t xw[7];
+        stem_window(im, end, y * st.stride_h - st.pad_h, x * st.stride_w - st.pad_w, st.dil_h, st.in_h, st.in_w,
+                    (uint32_t)st.in_xor, (uint32_t)st.in_zp, xw);
+        const int f = (3 * r + px) & G.pmask;
+        unsigned char* dst = buf + (r * G.patch_ru + px * (C >> 4)) * 16;
+        for (int c0 = cbeg; c0 < cbeg + half; c0 += 4) {
+          uint32_t packed = 0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const int oc = c0 + c;
+            const cst_ptr<int32_t> wrow = wts + oc * kpw;
+            int acc = sbias[oc];
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc = __builtin_amdgcn_sdot4((int)xw[j], wrow[j], acc, false);
+            const int32_t v =
+                requant_out<FAST>(acc, chan_q(smult[oc], sshift[oc], st.out_zp), st.out_zp, st.act_min, st.act_max);
+            packed |= ((uint32_t)v & 0xffu) << (8 * c);
+          }
+          *(uint32_t*)(dst + ((((c0 >> 4) ^ f)) << 4) + (c0 & 15)) = packed;
+        }
+      }
+    } else {
     const uint8_t* in = (const uint8_t*)d.input;
     const long in_last = (long)d.batch * d.in_h * d.in_w * C - 16;
-    const int y0 = oy0 * d.stride_h - d.pad_h;  // image coords of patch (0, 0)
     const long row0 = (long)n * d.in_h;
     const long xoff = (long)(ox0 * d.stride_w - d.pad_w) * C;
     for (int base = wave * 64; base < G.u_patch; base += 256) {
@@ -341,6 +393,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
         dma16(in + off, buf + base * 16);
       }
     }
+    }  // patch DMA
     if (a.residual) {
       const int N1 = a.out_c;
       const uint8_t* res = (const uint8_t*)a.residual;
@@ -586,13 +639,13 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
 #undef TILE_STAMP
 }
 
-template <int TH, int TW, bool FAST, int KX, int PIPE>
-static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s) {
+template <int TH, int TW, bool FAST, int KX, int PIPE, typename ST = NoStem>
+static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s, ST st = ST{}) {
   static thread_local int opted_device = -1;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (opted_device != dev) {
-    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX, PIPE>,
+    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     opted_device = dev;
   }
@@ -601,6 +654,7 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
   dv.txy = FastDiv(G.tiles_x * G.tiles_y);
   dv.patch_ru = FastDiv(G.patch_ru);
   dv.res_ru4 = FastDiv(G.res_ru4 > 0 ? G.res_ru4 : 1);
+  dv.pw = FastDiv(G.PW);
   dv.ntiles = p.dw.batch * G.tiles_y * G.tiles_x;
   dv.per = 1;
   int blocks = dv.ntiles;
@@ -615,7 +669,7 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
     static thread_local int cached_per_cu = 1;
     if (cached_lds != G.bytes) {
       int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_tile_kernel<TH, TW, FAST, KX, PIPE>, 256, G.bytes) !=
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>, 256, G.bytes) !=
           hipSuccess)
         nb = 1;
       cached_per_cu = std::max(1, std::min(4, nb));
@@ -625,7 +679,7 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
     dv.per = (dv.ntiles + slots - 1) / slots;
     blocks = (dv.ntiles + dv.per - 1) / dv.per;
   }
-  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX, PIPE>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv);
+  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv, st);
 }
 
 }  // namespace bh
@@ -639,6 +693,17 @@ extern "C" size_t bh_chain_tile_lds_bytes(const bh_chain_params* pp) {
   // 2: the persistent pipelined form; 3 / 4: runs of 2 / 4 tiles per
   // workgroup through one buffer
   if (p.tile < 1 || p.tile > 4) return 0;
+  if (p.stem) {
+    // the fused RGB stem: a 3x3 CONV_2D over 3 channels whose output (int8,
+    // no table / residual) is the depthwise input; one tile per workgroup
+    const bh_conv_params& st = *(const bh_conv_params*)p.stem;
+    if (p.tile != 1 || st.k_h != 3 || st.k_w != 3 || st.in_c != 3 || st.dil_w != 1 || st.dil_h < 1 ||
+        st.out_c != d.in_c || d.in_c % 8 || st.w_zp != 0 || st.residual || st.out_table || st.k_pad < 28 ||
+        st.k_pad % 4 || st.out_img_stride || !st.input || !st.weights || !st.bias_eff || !st.mult || !st.shift ||
+        st.batch != d.batch || st.out_h != d.in_h || st.out_w != d.in_w || st.output != d.input ||
+        st.act_min < -128 || st.act_max > 127 || st.stride_h < 1 || st.stride_w < 1)
+      return 0;
+  }
   if (d.stride_h < 1 || d.stride_h > 2 || d.stride_w < 1 || d.stride_w > 2 || d.dil_h < 1 || d.dil_h > 2 ||
       d.dil_w < 1 || d.dil_w > 2)
     return 0;
@@ -679,9 +744,21 @@ extern "C" int bh_chain_tile_launch(const bh_chain_params* pp, bh_stream_t strea
   }
   const bool pipe = p.tile == 2;
   const bh::TileGeom G = bh::tile_geom(p, 8, 8, pipe);
-  const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast);
+  const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast) &&
+                    (!p.stem || ((const bh_conv_params*)p.stem)->requant_fast);
   const bool k2 = !p.has_pw2 || p.pw2.k_pad <= 128;
   hipStream_t s = (hipStream_t)stream;
+  if (p.stem) {  // tile 1 (bh_chain_tile_lds_bytes)
+    const bh_conv_params st = *(const bh_conv_params*)p.stem;
+    if (k2) {
+      if (fast) bh::launch_tile<8, 8, true, 2, 0>(p, G, s, st);
+      else bh::launch_tile<8, 8, false, 2, 0>(p, G, s, st);
+    } else {
+      if (fast) bh::launch_tile<8, 8, true, 5, 0>(p, G, s, st);
+      else bh::launch_tile<8, 8, false, 5, 0>(p, G, s, st);
+    }
+    return bh_check_launch("chain_tile_kernel");
+  }
 #define BH_TILE(PIPE)                                                  \
   if (k2) {                                                            \
     if (fast) bh::launch_tile<8, 8, true, 2, PIPE>(p, G, s);           \

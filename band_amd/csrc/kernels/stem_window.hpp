@@ -1,0 +1,60 @@
+// The RGB stem's 3x3 x 3-channel window of one output pixel as the
+// k-ordered byte stream k = (fy*3 + fx)*3 + ci (27 bytes in seven dwords,
+// one zero byte of tail), int8 domain, padding taps = the input zero point:
+// three aligned dword loads + v_alignbyte per window row, the byte path
+// where the window leaves the image horizontally or the aligned loads
+// would run past the tensor.  The gather conv_stem_kernel (conv_direct.hip)
+// does inline; chain_tile_kernel's fused-stem prologue uses this copy.
+#pragma once
+#include "common.hpp"
+
+namespace bh {
+
+// img: this image's first byte; end: one past the tensor; (y0, x0): the
+// window's top-left input pixel (may be negative); in_h / in_w: image size
+__device__ __forceinline__ void stem_window(const uint8_t* img, const uint8_t* end, int y0, int x0, int dil_h,
+                                            int in_h, int in_w, uint32_t in_xor, uint32_t in_zp, uint32_t xw[7]) {
+  const uint32_t xorw = splat_byte(in_xor);
+  const uint32_t padw = splat_byte(in_zp);
+  uint32_t r[3][3];  // row fy: window bytes 0-3, 4-7, 8
+  const bool colok = x0 >= 0 && x0 + 3 <= in_w;
+#pragma unroll
+  for (int fy = 0; fy < 3; ++fy) {
+    const int y = y0 + fy * dil_h;
+    const bool rowok = y >= 0 && y < in_h;
+    const uint8_t* a = img + ((long)y * in_w + x0) * 3;
+    const uintptr_t ai = (uintptr_t)a;
+    const uint32_t* base = (const uint32_t*)(ai & ~(uintptr_t)3);
+    if (rowok && colok && (const uint8_t*)(base + 3) <= end) {
+      const uint32_t o = (uint32_t)(ai & 3);
+      const uint32_t d0 = base[0], d1 = base[1], d2 = base[2];
+      r[fy][0] = __builtin_amdgcn_alignbyte(d1, d0, o) ^ xorw;
+      r[fy][1] = __builtin_amdgcn_alignbyte(d2, d1, o) ^ xorw;
+      r[fy][2] = ((d2 >> (8 * o)) ^ xorw) & 0xffu;
+    } else if (!rowok) {
+      r[fy][0] = padw;
+      r[fy][1] = padw;
+      r[fy][2] = padw & 0xffu;
+    } else {
+      uint32_t b[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int x = x0 + k / 3;
+        b[k] = (x >= 0 && x < in_w) ? (uint32_t)(a[k] ^ (uint8_t)in_xor) : (padw & 0xffu);
+      }
+      r[fy][0] = b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24;
+      r[fy][1] = b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24;
+      r[fy][2] = b[8];
+    }
+  }
+  xw[0] = r[0][0];
+  xw[1] = r[0][1];
+  xw[2] = __builtin_amdgcn_perm(r[1][0], r[0][2], 0x06050400u);  // R0[8] R1[0..2]
+  xw[3] = __builtin_amdgcn_alignbyte(r[1][1], r[1][0], 3);        // R1[3..6]
+  const uint32_t u = __builtin_amdgcn_perm(r[1][2], r[1][1], 0x0c0c0403u);  // R1[7] R1[8] 0 0
+  xw[4] = u | (r[2][0] << 16);                                             // .. R2[0] R2[1]
+  xw[5] = __builtin_amdgcn_alignbyte(r[2][1], r[2][0], 2);                 // R2[2..5]
+  xw[6] = __builtin_amdgcn_alignbyte(r[2][2], r[2][1], 2);                 // R2[6..8] 0
+}
+
+}  // namespace bh

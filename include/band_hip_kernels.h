@@ -409,6 +409,13 @@ typedef struct bh_chain_params {
    * (v_dot4 over the tap table, 4 channels of one pixel per item) instead of
    * the block-diagonal MFMA tile; MFMA then runs only the 1x1 contractions */
   int dw_valu;
+  /* tile form 1 only: when non-NULL, a const bh_conv_params* of the RGB stem
+   * (CONV_2D 3x3 over 3 channels, int8 symmetric filters, no residual /
+   * table, out_c == dw.in_c) whose output is dw.input.  Each workgroup then
+   * computes its depthwise input patch from the image instead of reading
+   * the stem's output: the stem launch and its output tensor go away.
+   * Read during the bh_chain_i8 / bh_chain_lds_bytes call only. */
+  const void* stem;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */

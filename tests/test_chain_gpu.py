@@ -175,7 +175,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu", "forcestem"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param
@@ -201,8 +201,10 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
     key = SubgraphKey(41, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
     assert "chain_kernel" in kernels or "chain_tile_kernel" in kernels, kernels
-    if forcechain in ("forcetile", "forcetilepipe"):
+    if forcechain in ("forcetile", "forcetilepipe", "forcestem"):
         assert "chain_tile_kernel" in kernels, kernels
+    if forcechain == "forcestem":  # the RGB stem computed inside the first chain's tiles
+        assert kernels[0] == "chain_tile_kernel" and not any(k.startswith("conv_stem") for k in kernels), kernels
     for rep in range(2):  # eager, then graph replay
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
         assert ex.ExecuteSubgraph(key).ok()
@@ -274,3 +276,41 @@ def test_chain_split_rejects(gpu_lib):
     q.c_split = 2
     q.persist = 1  # raster forms only
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
+
+
+@pytest.mark.parametrize("arch,size", [("mobilenet_v2", 100), ("mobilenet_v2", 57), ("posenet_mobilenet_v1", 90),
+                                       ("ssd_mobilenet_v2", 72)])
+def test_chain_stem_fused_ragged(gpu_lib, monkeypatch, arch, size):
+    """the RGB stem fused into the first tile chain (BAND_HIP_FUSION=
+    forcestem) on image sizes whose stem output is not a multiple of the
+    8 x 8 tile (ragged right / bottom tiles, odd sizes: SAME padding with a
+    one-sided pad); one-job and job-batched passes bit-exact vs the oracle"""
+    monkeypatch.setenv("BAND_HIP_FUSION", "forcestem")
+    buf = getattr(S, arch)(np.int8, size=size)
+    om = OModel(buf)
+    t = om.tensors[om.inputs[0]]
+    rng = np.random.default_rng(size + len(arch))
+    xs = [rng.integers(-128, 128, t.shape).astype(np.int8) for _ in range(3)]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x}) for x in xs]
+    m = HipModel(43)
+    assert m.FromBuffer(buf).ok()
+    ex = HipModelExecutor(43, 1, DeviceFlag.kGPU)
+    assert ex.PrepareSubgraph(m).ok()
+    key = SubgraphKey(43, 1)
+    kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
+    assert kernels[0] == "chain_tile_kernel" and not any(k.startswith("conv_stem") for k in kernels), kernels
+    for rep in range(2):
+        ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
+        assert ex.ExecuteSubgraph(key).ok()
+        for o in om.outputs:
+            got = ex.GetTensorView(key, o).GetData()
+            np.testing.assert_array_equal(got, refs[0][o].reshape(got.shape), err_msg="%s run %d" % (arch, rep))
+    assert ex.PrepareJobBatches(m, key, 3).ok()
+    for s_, x in enumerate(xs):
+        ex.GetJobSlotView(key, om.inputs[0], 3, s_).GetData()[...] = x
+    assert ex.ExecuteJobBatch(key, 3).ok()
+    for s_ in range(3):
+        for o in om.outputs:
+            got = ex.GetJobSlotView(key, o, 3, s_).GetData()
+            np.testing.assert_array_equal(got, refs[s_][o].reshape(got.shape), err_msg="%s slot %d" % (arch, s_))
+    ex._model_ref = m

@@ -100,13 +100,15 @@ def test_single_executor_does_not_build_lanes(gpu_lib):
     assert ex.Coalescer() == (1, False)
 
 
-@pytest.mark.parametrize("sync", ["spin", "poller"])
+@pytest.mark.parametrize("sync", ["adaptive", "spin", "poller"])
 def test_engine_one_job_per_pass_coalesced_bit_exact(gpu_lib, monkeypatch, sync):
     """Band's own contract (max_job_batch 1: the engine calls only
     band/interface) with 6 GPU workers under round_robin: a burst of
     requests from several submitter threads; every request's outputs equal
     the oracle's, and the backend coalesced some of the jobs.  sync=poller:
-    the waiting threads sleep and the GPU's CompletionPoller wakes them."""
+    the waiting threads sleep and the GPU's CompletionPoller wakes them;
+    adaptive (the default): sleep through most of the expected wait, then
+    spin."""
     monkeypatch.setenv("BAND_HIP_COALESCE", "6")
     monkeypatch.setenv("BAND_HIP_SYNC", sync)
     buf = tflite_synth.mobilenet_v2(np.int8, size=96)

@@ -278,8 +278,9 @@ def test_chain_split_rejects(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
 
 
-@pytest.mark.parametrize("arch,size", [("mobilenet_v2", 100), ("mobilenet_v2", 57), ("posenet_mobilenet_v1", 90),
-                                       ("ssd_mobilenet_v2", 72)])
+@pytest.mark.parametrize("arch,size", [("deeplab_v3_mobilenet_v2", 100), ("deeplab_v3_mobilenet_v2", 57),
+                                       ("posenet_mobilenet_v1", 90), ("posenet_mobilenet_v1", 57),
+                                       ("ssd_mobilenet_v2", 100)])
 def test_chain_stem_fused_ragged(gpu_lib, monkeypatch, arch, size):
     """the RGB stem fused into the first tile chain (BAND_HIP_FUSION=
     forcestem) on image sizes whose stem output is not a multiple of the

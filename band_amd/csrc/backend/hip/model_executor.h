@@ -313,6 +313,7 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   enum SyncMode { kSyncSpin = 0, kSyncBlock = 1, kSyncPoll = 2, kSyncPoller = 3, kSyncAdaptive = 4 };
   int sync_mode_ = kSyncAdaptive;
   double sleep_frac_ = 0.85;
+  double sleep_min_us_ = 500.0;  // BAND_HIP_SYNC_MIN_US: expected waits below this spin
   bool block_sync_ = false;  // sync_mode_ == kSyncBlock
   // waits for everything enqueued on stream_ (the pass of `sg`)
   absl::Status WaitPass(PreparedSubgraph* sg);

@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,tp,1d,1w8d,2d",
                     help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form, "
                          "tp = its persistent double-buffered variant, t3 / t4 = runs of 2 / 4 tiles per workgroup; "
-                         "sN suffix = the phase-C split over N workgroups")
+                         "sN suffix = the phase-C split over N workgroups; v suffix = the VALU depthwise phase")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
@@ -42,6 +42,8 @@ def main():
         row = []
         for form in a.px.split(","):
             split = 0
+            valu = int(form.endswith("v"))
+            form = form[:-1] if valu else form
             if "s" in form and not form.startswith("t"):  # "1s2": the phase-C split over 2 workgroups
                 form, split = form.split("s")[0], int(form.split("s")[1])
             tile = {"t": 1, "tp": 2, "t3": 3, "t4": 4}.get(form, 0)
@@ -50,7 +52,7 @@ def main():
             f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves, persist, tile, deep, split)
+            q = c.params(lib, px, keep, waves, persist, tile, deep, split, valu)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue
@@ -65,7 +67,7 @@ def main():
             ms = ctypes.c_float()
             lib.bh_event_elapsed_ms(e0, e1, ctypes.byref(ms))
             us = 1e3 * ms.value / a.iters
-            total[form] = total.get(form, 0.0) + us
+            total[form + ("v" if valu else "")] = total.get(form + ("v" if valu else ""), 0.0) + us
             row.append("%7.2f" % us)
         print("%3dx%-3d ce %4d s%d -> %3d%s -> %4d   %s" % (h, h, ce, s, cout, "+res" if res else "    ", ce2,
                                                            "  ".join(row)), flush=True)

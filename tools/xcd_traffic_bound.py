@@ -69,7 +69,8 @@ def main():
         print("%-24s %3d %-18s in %-20s out %-20s k%d  alg %6.2f MB  bound %6.2f MB  %.2fx (%d XCDs)" % (
             r["model"], r["op"], r["kernel"], r["inp"], r["out"], r["k"], alg / 1e6, tb / 1e6, tb / alg, X))
     for k, (n, alg, tb) in tot.items():
-        print("%-20s %2d launches: bound / algorithmic over the launches = %.2fx" % (k, n, tb / alg))
+        print("%-20s %2d launches: mean algorithmic %.3f MB, mean bound %.3f MB per launch; bound / algorithmic = %.2fx"
+              % (k, n, alg / n / 1e6, tb / n / 1e6, tb / alg))
 
 
 if __name__ == "__main__":

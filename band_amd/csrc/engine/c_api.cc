@@ -438,19 +438,26 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // results out (DeepLab's are 1 MB), each into output tensors of its own.
   int lanes = 1;
   if (const char* lv = std::getenv("BANDX_DRIVER_LANES")) lanes = std::max(1, std::atoi(lv));
-  // one submitter lane per shard of the models (below), so at most one per model
-  lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight, n_models}));
+  // a shard of the models per lane up to one model per shard (below); more
+  // lanes than models share a shard: its runs are dealt to them in turn
+  // (one engine over several GPUs needs several submitters per model)
+  lanes = std::max(1, std::min({lanes, n_jobs > 0 ? n_jobs : 1, max_inflight}));
+  const int n_shards = std::min(lanes, std::max(1, n_models));
+  // submitter lanes of a model's shard: each can hold a run's slots reserved
+  // but not yet allocated in the ring
+  const int lanes_per_shard = (lanes + n_shards - 1) / n_shards;
   // requests of one model submitted per RequestAsync call (closed loop:
   // the job -> model order is run-major, `burst` jobs per model in turn)
   int burst = burst_hint > 0 ? burst_hint : 1;
   if (const char* bv = std::getenv("BANDX_DRIVER_BURST")) burst = std::max(1, std::atoi(bv));
   burst = std::max(1, std::min(burst, max_inflight / std::max(1, lanes)));
   for (int m = 0; m < n_models; ++m)
-    burst = std::max(1, std::min(burst, e.RequestRingSize(models[m]->impl->GetId()) / (2 * lanes)));
+    burst = std::max(1, std::min(burst, e.RequestRingSize(models[m]->impl->GetId()) /
+                                            (2 * std::max(n_shards, lanes_per_shard + 1))));
   int readers = 6;
   if (const char* rv = std::getenv("BANDX_DRIVER_READERS")) readers = std::max(1, std::atoi(rv));
   readers = std::max(1, std::min(readers, n_jobs > 0 ? n_jobs : 1));
-  readers = std::max(readers, lanes);  // every shard has a reader
+  readers = std::max(readers, n_shards);  // every shard has a reader
   std::vector<std::vector<std::vector<std::unique_ptr<band::Tensor>>>> reader_outs(readers);
   std::vector<std::vector<band::Tensors>> reader_out_ptrs(readers);
   for (int r = 0; r < readers; ++r) {
@@ -498,7 +505,6 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
       last_tick = now;
     }
   };
-  const int n_shards = lanes;
   std::vector<std::unique_ptr<Shard>> shards;
   for (int i = 0; i < n_shards; ++i) shards.emplace_back(new Shard());
   // a model's shard follows its engine id (a model listed twice shares one)
@@ -620,19 +626,25 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
   // benchmark tool uses with batch_size >= 2), up to `burst` requests: one
   // ring allocation, one planner enqueue and one wake-up per run instead of
   // per request.  Lane l takes the runs of its shard's models, in order.
-  std::vector<std::vector<std::pair<int, int>>> runs(n_shards);  // (first job, length) per lane
-  for (int j = 0; j < n_jobs;) {
-    int k = j + 1;
-    while (k < n_jobs && k - j < burst && arrivals[k].second == arrivals[j].second &&
-           arrivals[k].first == arrivals[j].first)
-      ++k;
-    runs[shard_of[arrivals[j].second]].emplace_back(j, k - j);
-    j = k;
+  // lane l serves shard l % n_shards; a shard's runs go to its lanes in turn
+  std::vector<std::vector<std::pair<int, int>>> runs(lanes);  // (first job, length) per lane
+  {
+    std::vector<int> dealt(n_shards, 0);
+    for (int j = 0; j < n_jobs;) {
+      int k = j + 1;
+      while (k < n_jobs && k - j < burst && arrivals[k].second == arrivals[j].second &&
+             arrivals[k].first == arrivals[j].first)
+        ++k;
+      const int sh = shard_of[arrivals[j].second];
+      const int in_shard = (lanes - sh + n_shards - 1) / n_shards;  // lanes sh, sh + n_shards, ...
+      runs[sh + n_shards * (dealt[sh]++ % in_shard)].emplace_back(j, k - j);
+      j = k;
+    }
   }
   for (int l = 0; l < lanes; ++l) {
     threads.emplace_back([&, l] {
       pthread_setname_np(pthread_self(), "bandx-submit");
-      Shard& sh = *shards[l];
+      Shard& sh = *shards[l % n_shards];
       std::vector<band::ModelId> ids;
       std::vector<band::RequestOption> opts;
       std::vector<band::Tensors> ins;
@@ -643,9 +655,11 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
         const int64_t now = band::time::NowMicros() - t0;
         if (arrival.first > now) band::time::SleepForMicros(arrival.first - now);
         const int m = arrival.second;
-        // one submitter per model: a run is < ring - burst submissions ahead
-        // of the model's oldest unread request, so its ring slots are free
-        const long span = std::max(1, ring[m] - burst);
+        // a run is < ring - (lanes of the shard) x burst submissions ahead of
+        // the model's oldest unread request: the runs other lanes of the
+        // shard have reserved but not yet allocated (their ring handles may
+        // come before this run's) still leave this run's ring slots free
+        const long span = std::max(1, ring[m] - lanes_per_shard * burst);
         const int64_t w0 = band::time::NowMicros();
         seqs.clear();
         {

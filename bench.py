@@ -719,14 +719,37 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
     # --device cpu: Band CPU workers stand in for the GPUs (CPU tests of this
     # path); the worker -> device mapping is the same
     flag = DeviceFlag.kGPU if args.device == "gpu" else DeviceFlag.kCPU
-    e, bm, ins = make_engine(args, D, paths, sched, [flag] * n_workers, 0, n_workers, args.job_batch)
-    inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
-    el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
-    e.close()
+    # the request driver of N GPUs' job stream: 2 submitter lanes per GPU
+    # (lanes beyond the model count share a model's shard) and 6 readers per
+    # GPU, free to run on every CPU of the process (the GPU workers pin
+    # themselves to their own GPU's NUMA node); the N = 1 settings otherwise
+    saved = {k: os.environ.get(k) for k in ("BANDX_DRIVER_LANES", "BANDX_DRIVER_READERS")}
+    if n_gpus > 1:
+        os.environ.setdefault("BANDX_DRIVER_LANES", str(2 * n_gpus))
+        os.environ.setdefault("BANDX_DRIVER_READERS", str(6 * n_gpus))
+        if flag == DeviceFlag.kGPU and _START_AFFINITY:
+            from band_amd import backend as _backend
+            _backend.PinProcessToCpus(sorted(_START_AFFINITY))
+    try:
+        e, bm, ins = make_engine(args, D, paths, sched, [flag] * n_workers, 0, n_workers, args.job_batch)
+        inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
+        el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
+        e.close()
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+        if n_gpus > 1 and flag == DeviceFlag.kGPU and _START_AFFINITY and os.environ.get("BANDX_NUMA_PIN") != "0":
+            from band_amd import backend as _backend
+            _backend.PinProcessToGpu(D.local_rank)
     per_gpu = np.bincount(np.asarray(wid) % n_gpus, minlength=n_gpus).tolist()
     for w in range(n_workers):  # back to the per-process mapping
         band_amd.SetWorkerDevice(w, D.local_rank)
     return {"value": n_timed / el, "unit": "inferences/s", "n_gpus": n_gpus, "jobs": n_timed,
+            "driver": {"lanes": int(os.environ.get("BANDX_DRIVER_LANES", 2 * n_gpus if n_gpus > 1 else 1)),
+                       "readers": int(os.environ.get("BANDX_DRIVER_READERS", 6 * n_gpus if n_gpus > 1 else 6))},
             "ms_per_step": el * 1e3 / max(1, n_timed // args.jobs_per_step),
             "workers": n_workers, "worker_to_gpu": "w %% %d" % n_gpus, "jobs_per_gpu": per_gpu,
             "p50_job_latency_ms": float(np.percentile(lat * 1e-3, 50)),

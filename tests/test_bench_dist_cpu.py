@@ -100,6 +100,23 @@ def test_bench_single_engine_cpu_stand_ins():
     assert line["value"] == se["value"] and "single planner" in line["config"]["harness"]
 
 
+def test_bench_single_engine_two_submitters_per_model():
+    """the single engine's request driver with more submitter lanes than
+    models (8 lanes over the 4-model mix: two per model shard, sharing its
+    ring-slot accounting): every job completes, on both devices"""
+    env = _env()
+    env["BANDX_DRIVER_LANES"] = "8"
+    env["BANDX_DRIVER_READERS"] = "5"
+    cmd = [sys.executable, "bench.py", "--single-engine", "--gpus", "2", "--device", "cpu", "--model", "mix_c3",
+           "--size", "64", "--workers-per-gpu", "2", "--cpu-threads", "1", "--steps", "6", "--warmup", "2",
+           "--jobs-per-step", "16", "--job-batch", "2", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    se = _json_line(r.stdout)["single_engine"]
+    assert se["driver"] == {"lanes": 8, "readers": 5}
+    assert se["jobs"] == 6 * 16 and sum(se["jobs_per_gpu"]) == 6 * 16 and min(se["jobs_per_gpu"]) > 0
+
+
 def test_worker_device_mapping():
     """DeviceRegistry (backend/hip/device.cc): an explicit worker -> ordinal
     mapping is returned as set and can be changed (bench.py remaps workers for

@@ -9,6 +9,7 @@
 // byte of the window is loaded at once (one memory round trip) and the dot
 // products are v_dot4_i32_i8.
 #include "common.hpp"
+#include "stem_window.hpp"
 
 namespace bh {
 
@@ -190,6 +191,94 @@ __global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M,
   }
 }
 
+// conv_stem_lds_kernel: the same stem with every channel's constants staged
+// in LDS once per workgroup - filter dwords, folded bias and the
+// requantisation constants (ChanQ precomputed) in one 64-byte record per
+// channel - instead of read through the scalar cache per wave.  The scalar
+// form issues ~200 s_load per wave in SGPR-bounded batches, each a full
+// round trip (PMC at B = 24: waves resident from start to end, 50 % of their
+// cycles parked on those waits, profiles/r05t_stem_pmc.txt); here a channel
+// is four broadcast ds_read_b128 (every lane reads the same record).
+// Channel ranges of up to 64 (grid.y splits wider layers).
+struct StemChan {
+  int32_t w[8];  // filter dwords 0..6 (k-ordered window), 0
+  int32_t bias, mu, sh, e, emask, zpe, c0lo, c0hi;
+};
+static_assert(sizeof(StemChan) == 64, "one 64-byte record per channel");
+
+template <bool FAST>
+__global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, int M, DirectDivs dv, int ch_per_y) {
+  __shared__ __attribute__((aligned(16))) StemChan sc[64];
+  const int cb = blockIdx.y * ch_per_y;
+  const int ce = min(p.out_c, cb + ch_per_y);
+  const int nc = ce - cb;
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  const int mm = m < M ? m : M - 1;
+  // the window first: its loads are in flight while the constants stage
+  const int t = dv.out_w.div(mm);
+  const int ox = mm - t * p.out_w;
+  const int n = dv.out_h.div(t);
+  const int oy = t - n * p.out_h;
+  const long img = (long)p.in_h * p.in_w * 3;
+  uint32_t xw[7];
+  stem_window((const uint8_t*)p.input + n * img, (const uint8_t*)p.input + p.batch * img, oy * p.stride_h - p.pad_h,
+              ox * p.stride_w - p.pad_w, p.dil_h, p.in_h, p.in_w, (uint32_t)p.in_xor, (uint32_t)p.in_zp, xw);
+  {
+    const int kpw = p.k_pad >> 2;
+    const int32_t* wts = (const int32_t*)p.weights;
+    for (int i = threadIdx.x; i < nc * 16; i += 256) {
+      const int c = i >> 4, j = i & 15, oc = cb + c;
+      int32_t v = 0;
+      if (j < 7) {
+        v = wts[(long)oc * kpw + j];
+      } else if (j >= 8) {
+        const ChanQ q = chan_q(p.mult[oc], p.shift[oc], p.out_zp);
+        v = j == 8 ? p.bias_eff[oc] : j == 9 ? q.mu : j == 10 ? q.sh : j == 11 ? q.e : j == 12 ? q.emask
+            : j == 13 ? q.zpe : j == 14 ? (int32_t)(uint32_t)(uint64_t)q.c0 : (int32_t)(q.c0 >> 32);
+      }
+      ((int32_t*)sc)[i] = v;
+    }
+  }
+  __syncthreads();
+  if (m >= M) return;
+  int rowsum = 0;
+  if (p.w_zp != 0) {
+#pragma unroll
+    for (int j = 0; j < 7; ++j) rowsum = __builtin_amdgcn_sdot4((int)xw[j], 0x01010101, rowsum, false);
+  }
+  uint8_t* out = (uint8_t*)p.output + (long)m * p.out_c;
+  const uint8_t* tab = (const uint8_t*)p.out_table;
+  for (int c0 = 0; c0 < nc; c0 += 4) {
+    uint32_t packed = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const StemChan& k = sc[c0 + c];
+      const v4i w0 = *(const v4i*)k.w, w1 = *(const v4i*)(k.w + 4);
+      const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
+      int acc = q0.x;
+      acc = __builtin_amdgcn_sdot4((int)xw[0], w0.x, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[1], w0.y, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[2], w0.z, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[3], w0.w, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[4], w1.x, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[5], w1.y, acc, false);
+      acc = __builtin_amdgcn_sdot4((int)xw[6], w1.z, acc, false);
+      if (p.w_zp != 0) acc -= p.w_zp * rowsum;
+      ChanQ q;
+      q.mu = q0.y;
+      q.sh = q0.z;
+      q.e = q0.w;
+      q.emask = q1.x;
+      q.zpe = q1.y;
+      q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
+      const int32_t v = requant_out<FAST>(acc, q, p.out_zp, p.act_min, p.act_max);
+      const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
+      packed |= byte << (8 * c);
+    }
+    *(uint32_t*)(out + cb + c0) = packed;
+  }
+}
+
 }  // namespace bh
 
 // Launched by bh_conv2d_i8 for small-K layers (conv_mfma.hip); returns
@@ -225,6 +314,20 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const int ch_per_y = (groups + gy - 1) / gy * 8;
   gy = (p.out_c + ch_per_y - 1) / ch_per_y;
   const dim3 grid((unsigned)gx, (unsigned)gy);
+  // the LDS-staged constants (default; channel ranges of <= 64, out_c % 4 ==
+  // 0 for its dword stores, aligned output) or the scalar-cache form
+  // (BH_CONV_STEM_SCALAR, or BH_STEM_SCALAR=1 for A-B runs)
+  static const bool scalar_env = [] {
+    const char* e = std::getenv("BH_STEM_SCALAR");
+    return e && e[0] == '1';
+  }();
+  const bool lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && ch_per_y <= 64 && p.out_c % 4 == 0 &&
+                   (((uintptr_t)p.output) & 3) == 0;
+  if (lds) {
+    if (p.requant_fast) BH_LAUNCH(bh::conv_stem_lds_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+    else BH_LAUNCH(bh::conv_stem_lds_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+    return bh_check_launch("conv_stem_kernel");
+  }
   if (p.requant_fast) BH_LAUNCH(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
   else BH_LAUNCH(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
   return bh_check_launch("conv_stem_kernel");

@@ -131,10 +131,11 @@ def test_conv_stem(gpu_lib, b, h, w, oc, stride, same, dtype):
     rng = np.random.default_rng(5000 + b * h * w + oc + stride)
     c = ConvCase(rng, b, h, w, 3, oc, 3, 3, stride=(stride, stride), same=same, dtype=dtype, act=3)
     ref = c.oracle()
-    # the routed form, then the VALU form (BH_CONV_STEM_VALU = 4) and the MFMA
-    # form (BH_CONV_STEM_MFMA = 5, out_c % 16 == 0, <= 64) forced; both
-    # requantisation paths
-    for hint in (0, 4, 5):
+    # the routed form (LDS-staged VALU stem), then the VALU form
+    # (BH_CONV_STEM_VALU = 4), the MFMA form (BH_CONV_STEM_MFMA = 5, out_c %
+    # 16 == 0, <= 64) and the scalar-cache VALU form (BH_CONV_STEM_SCALAR =
+    # 6) forced; both requantisation paths
+    for hint in (0, 4, 5, 6):
         c.kernel_hint = hint
         for fast in (None, False):
             c.requant_fast = fast

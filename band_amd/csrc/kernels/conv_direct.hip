@@ -321,8 +321,10 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
     const char* e = std::getenv("BH_STEM_SCALAR");
     return e && e[0] == '1';
   }();
+  // from 256 workgroups (batched passes): at batch 1 the LDS staging is
+  // not repaid (5.05 vs 4.87 us; B = 24: 13.6 vs 14.6 us, r05u_stem_*)
   const bool lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && ch_per_y <= 64 && p.out_c % 4 == 0 &&
-                   (((uintptr_t)p.output) & 3) == 0;
+                   (((uintptr_t)p.output) & 3) == 0 && (gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
   if (lds) {
     if (p.requant_fast) BH_LAUNCH(bh::conv_stem_lds_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
     else BH_LAUNCH(bh::conv_stem_lds_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);

@@ -206,23 +206,29 @@ struct StemChan {
 };
 static_assert(sizeof(StemChan) == 64, "one 64-byte record per channel");
 
-template <bool FAST>
+// PX pixels per thread (m, m + 256, ...: stores stay lane-consecutive): the
+// channel records' LDS reads serve PX pixels and their dot / requant chains
+// interleave
+template <bool FAST, int PX>
 __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, int M, DirectDivs dv, int ch_per_y) {
   __shared__ __attribute__((aligned(16))) StemChan sc[64];
   const int cb = blockIdx.y * ch_per_y;
   const int ce = min(p.out_c, cb + ch_per_y);
   const int nc = ce - cb;
-  const int m = blockIdx.x * 256 + threadIdx.x;
-  const int mm = m < M ? m : M - 1;
-  // the window first: its loads are in flight while the constants stage
-  const int t = dv.out_w.div(mm);
-  const int ox = mm - t * p.out_w;
-  const int n = dv.out_h.div(t);
-  const int oy = t - n * p.out_h;
+  const int m0 = blockIdx.x * 256 * PX + threadIdx.x;
   const long img = (long)p.in_h * p.in_w * 3;
-  uint32_t xw[7];
-  stem_window((const uint8_t*)p.input + n * img, (const uint8_t*)p.input + p.batch * img, oy * p.stride_h - p.pad_h,
-              ox * p.stride_w - p.pad_w, p.dil_h, p.in_h, p.in_w, (uint32_t)p.in_xor, (uint32_t)p.in_zp, xw);
+  // the windows first: their loads are in flight while the constants stage
+  uint32_t xw[PX][7];
+#pragma unroll
+  for (int u = 0; u < PX; ++u) {
+    const int mm = min(m0 + 256 * u, M - 1);
+    const int t = dv.out_w.div(mm);
+    const int ox = mm - t * p.out_w;
+    const int n = dv.out_h.div(t);
+    const int oy = t - n * p.out_h;
+    stem_window((const uint8_t*)p.input + n * img, (const uint8_t*)p.input + p.batch * img, oy * p.stride_h - p.pad_h,
+                ox * p.stride_w - p.pad_w, p.dil_h, p.in_h, p.in_w, (uint32_t)p.in_xor, (uint32_t)p.in_zp, xw[u]);
+  }
   {
     const int kpw = p.k_pad >> 2;
     const int32_t* wts = (const int32_t*)p.weights;
@@ -240,30 +246,26 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
     }
   }
   __syncthreads();
-  if (m >= M) return;
-  int rowsum = 0;
-  if (p.w_zp != 0) {
+  if (m0 >= M) return;
+  int rowsum[PX];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) rowsum = __builtin_amdgcn_sdot4((int)xw[j], 0x01010101, rowsum, false);
+  for (int u = 0; u < PX; ++u) {
+    rowsum[u] = 0;
+    if (p.w_zp != 0) {
+#pragma unroll
+      for (int j = 0; j < 7; ++j) rowsum[u] = __builtin_amdgcn_sdot4((int)xw[u][j], 0x01010101, rowsum[u], false);
+    }
   }
-  uint8_t* out = (uint8_t*)p.output + (long)m * p.out_c;
   const uint8_t* tab = (const uint8_t*)p.out_table;
   for (int c0 = 0; c0 < nc; c0 += 4) {
-    uint32_t packed = 0;
+    uint32_t packed[PX];
+#pragma unroll
+    for (int u = 0; u < PX; ++u) packed[u] = 0;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const StemChan& k = sc[c0 + c];
       const v4i w0 = *(const v4i*)k.w, w1 = *(const v4i*)(k.w + 4);
       const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
-      int acc = q0.x;
-      acc = __builtin_amdgcn_sdot4((int)xw[0], w0.x, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[1], w0.y, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[2], w0.z, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[3], w0.w, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[4], w1.x, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[5], w1.y, acc, false);
-      acc = __builtin_amdgcn_sdot4((int)xw[6], w1.z, acc, false);
-      if (p.w_zp != 0) acc -= p.w_zp * rowsum;
       ChanQ q;
       q.mu = q0.y;
       q.sh = q0.z;
@@ -271,11 +273,27 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
       q.emask = q1.x;
       q.zpe = q1.y;
       q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
-      const int32_t v = requant_out<FAST>(acc, q, p.out_zp, p.act_min, p.act_max);
-      const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
-      packed |= byte << (8 * c);
+#pragma unroll
+      for (int u = 0; u < PX; ++u) {
+        int acc = q0.x;
+        acc = __builtin_amdgcn_sdot4((int)xw[u][0], w0.x, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][1], w0.y, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][2], w0.z, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][3], w0.w, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][4], w1.x, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][5], w1.y, acc, false);
+        acc = __builtin_amdgcn_sdot4((int)xw[u][6], w1.z, acc, false);
+        if (p.w_zp != 0) acc -= p.w_zp * rowsum[u];
+        const int32_t v = requant_out<FAST>(acc, q, p.out_zp, p.act_min, p.act_max);
+        const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
+        packed[u] |= byte << (8 * c);
+      }
     }
-    *(uint32_t*)(out + cb + c0) = packed;
+#pragma unroll
+    for (int u = 0; u < PX; ++u) {
+      const int m = m0 + 256 * u;
+      if (m < M) *(uint32_t*)((uint8_t*)p.output + (long)m * p.out_c + cb + c0) = packed[u];
+    }
   }
 }
 
@@ -326,8 +344,21 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const bool lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && ch_per_y <= 64 && p.out_c % 4 == 0 &&
                    (((uintptr_t)p.output) & 3) == 0 && (gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
   if (lds) {
-    if (p.requant_fast) BH_LAUNCH(bh::conv_stem_lds_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
-    else BH_LAUNCH(bh::conv_stem_lds_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+    // pixels per thread: BH_STEM_PX (A-B runs), default 2 from 1024
+    // workgroups of one pixel per thread
+    static const int px_env = [] {
+      const char* e = std::getenv("BH_STEM_PX");
+      return e ? std::atoi(e) : 0;
+    }();
+    const int px = px_env == 1 || px_env == 2 ? px_env : (gx >= 1024 ? 2 : 1);
+    const dim3 g2((unsigned)((M + 256 * px - 1) / (256 * px)), (unsigned)gy);
+    if (px == 2) {
+      if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 2>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
+      else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 2>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
+    } else {
+      if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
+      else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
+    }
     return bh_check_launch("conv_stem_kernel");
   }
   if (p.requant_fast) BH_LAUNCH(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);

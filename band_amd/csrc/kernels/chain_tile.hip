@@ -343,13 +343,18 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
       const int xs = ox0 * d.stride_w - d.pad_w;
       const int npix = G.PH * G.PW;
       const int half = C >> 1;
-      const int cbeg = (wave >> 1) * half;  // uniform per wave: scalar filter loads
+      const int cbeg = (wave >> 1) * half;
       const long img = (long)st.in_h * st.in_w * 3;
       const uint8_t* im = (const uint8_t*)st.input + n * img;
       const uint8_t* end = (const uint8_t*)st.input + st.batch * img;
-      const cst_ptr<int32_t> wts = as_const((const int32_t*)st.weights);
-      const cst_ptr<int32_t> sbias = as_const(st.bias_eff), smult = as_const(st.mult), sshift = as_const(st.shift);
-      const int kpw = st.k_pad >> 2;
+      // the stem's channel records (filter dwords, bias, ChanQ) in the
+      // depthwise-output region, unused until phase A (C x 64 bytes <= the
+      // region's 64 x (k_pad + 32))
+      StemChan* rec = (StemChan*)(smem + G.off_dl);
+      for (int i = tid; i < C * 16; i += 256)
+        ((int32_t*)rec)[i] = stem_chan_word((const int32_t*)st.weights, st.k_pad >> 2, st.bias_eff, st.mult,
+                                            st.shift, st.out_zp, i >> 4, i & 15);
+      __syncthreads();
       for (int pix = (wave & 1) * 64 + lane; pix < npix; pix += 128) {
         const int r = dv.pw.div(pix);
         const int px = pix - r * G.PW;
@@ -364,13 +369,7 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
           uint32_t packed = 0;
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            const int oc = c0 + c;
-            const cst_ptr<int32_t> wrow = wts + oc * kpw;
-            int acc = sbias[oc];
-#pragma unroll
-            for (int j = 0; j < 7; ++j) acc = __builtin_amdgcn_sdot4((int)xw[j], wrow[j], acc, false);
-            const int32_t v =
-                requant_out<FAST>(acc, chan_q(smult[oc], sshift[oc], st.out_zp), st.out_zp, st.act_min, st.act_max);
+            const int32_t v = stem_chan_eval<FAST>(rec[c0 + c], xw, false, 0, st.out_zp, st.act_min, st.act_max);
             packed |= ((uint32_t)v & 0xffu) << (8 * c);
           }
           *(uint32_t*)(dst + ((((c0 >> 4) ^ f)) << 4) + (c0 & 15)) = packed;

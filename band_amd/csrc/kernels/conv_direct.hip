@@ -200,11 +200,6 @@ __global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M,
 // cycles parked on those waits, profiles/r05t_stem_pmc.txt); here a channel
 // is four broadcast ds_read_b128 (every lane reads the same record).
 // Channel ranges of up to 64 (grid.y splits wider layers).
-struct StemChan {
-  int32_t w[8];  // filter dwords 0..6 (k-ordered window), 0
-  int32_t bias, mu, sh, e, emask, zpe, c0lo, c0hi;
-};
-static_assert(sizeof(StemChan) == 64, "one 64-byte record per channel");
 
 // PX pixels per thread (m, m + 256, ...: stores stay lane-consecutive): the
 // channel records' LDS reads serve PX pixels and their dot / requant chains
@@ -233,16 +228,7 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
     const int kpw = p.k_pad >> 2;
     const int32_t* wts = (const int32_t*)p.weights;
     for (int i = threadIdx.x; i < nc * 16; i += 256) {
-      const int c = i >> 4, j = i & 15, oc = cb + c;
-      int32_t v = 0;
-      if (j < 7) {
-        v = wts[(long)oc * kpw + j];
-      } else if (j >= 8) {
-        const ChanQ q = chan_q(p.mult[oc], p.shift[oc], p.out_zp);
-        v = j == 8 ? p.bias_eff[oc] : j == 9 ? q.mu : j == 10 ? q.sh : j == 11 ? q.e : j == 12 ? q.emask
-            : j == 13 ? q.zpe : j == 14 ? (int32_t)(uint32_t)(uint64_t)q.c0 : (int32_t)(q.c0 >> 32);
-      }
-      ((int32_t*)sc)[i] = v;
+      ((int32_t*)sc)[i] = stem_chan_word(wts, kpw, p.bias_eff, p.mult, p.shift, p.out_zp, cb + (i >> 4), i & 15);
     }
   }
   __syncthreads();
@@ -264,27 +250,9 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const StemChan& k = sc[c0 + c];
-      const v4i w0 = *(const v4i*)k.w, w1 = *(const v4i*)(k.w + 4);
-      const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
-      ChanQ q;
-      q.mu = q0.y;
-      q.sh = q0.z;
-      q.e = q0.w;
-      q.emask = q1.x;
-      q.zpe = q1.y;
-      q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
 #pragma unroll
       for (int u = 0; u < PX; ++u) {
-        int acc = q0.x;
-        acc = __builtin_amdgcn_sdot4((int)xw[u][0], w0.x, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][1], w0.y, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][2], w0.z, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][3], w0.w, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][4], w1.x, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][5], w1.y, acc, false);
-        acc = __builtin_amdgcn_sdot4((int)xw[u][6], w1.z, acc, false);
-        if (p.w_zp != 0) acc -= p.w_zp * rowsum[u];
-        const int32_t v = requant_out<FAST>(acc, q, p.out_zp, p.act_min, p.act_max);
+        const int32_t v = stem_chan_eval<FAST>(k, xw[u], p.w_zp != 0, p.w_zp * rowsum[u], p.out_zp, p.act_min, p.act_max);
         const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
         packed[u] |= byte << (8 * c);
       }

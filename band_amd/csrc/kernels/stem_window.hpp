@@ -57,4 +57,54 @@ __device__ __forceinline__ void stem_window(const uint8_t* img, const uint8_t* e
   xw[6] = __builtin_amdgcn_alignbyte(r[2][2], r[2][1], 2);                 // R2[6..8] 0
 }
 
+// One output channel of the stem as a 64-byte LDS record: the filter dwords
+// 0..6 of the k-ordered window (and a zero), the folded bias and the
+// requantisation constants (ChanQ precomputed).  Every lane of a wave reads
+// the same record: four broadcast ds_read_b128.
+struct StemChan {
+  int32_t w[8];
+  int32_t bias, mu, sh, e, emask, zpe, c0lo, c0hi;
+};
+static_assert(sizeof(StemChan) == 64, "one 64-byte record per channel");
+
+// word j of channel oc's record (weights: the layer's [n_pad][k_pad] filter
+// rows; kpw = k_pad / 4)
+__device__ __forceinline__ int32_t stem_chan_word(const int32_t* weights, int kpw, const int32_t* bias,
+                                                  const int32_t* mult, const int32_t* shift, int32_t out_zp, int oc,
+                                                  int j) {
+  if (j < 7) return weights[(long)oc * kpw + j];
+  if (j == 7) return 0;
+  if (j == 8) return bias[oc];
+  const ChanQ q = chan_q(mult[oc], shift[oc], out_zp);
+  return j == 9 ? q.mu : j == 10 ? q.sh : j == 11 ? q.e : j == 12 ? q.emask : j == 13 ? q.zpe
+       : j == 14 ? (int32_t)(uint32_t)(uint64_t)q.c0 : (int32_t)(q.c0 >> 32);
+}
+
+// acc = bias + window . filter of one channel record (minus w_zp x the
+// window's byte sum for uint8 filters: wzp is wave-uniform), then the
+// requantised output value (int8 domain)
+template <bool FAST>
+__device__ __forceinline__ int32_t stem_chan_eval(const StemChan& k, const uint32_t xw[7], bool wzp,
+                                                  int32_t wzp_rowsum, int32_t out_zp, int32_t lo, int32_t hi) {
+  const v4i w0 = *(const v4i*)k.w, w1 = *(const v4i*)(k.w + 4);
+  const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
+  int acc = q0.x;
+  acc = __builtin_amdgcn_sdot4((int)xw[0], w0.x, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[1], w0.y, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[2], w0.z, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[3], w0.w, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[4], w1.x, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[5], w1.y, acc, false);
+  acc = __builtin_amdgcn_sdot4((int)xw[6], w1.z, acc, false);
+  if (wzp) acc -= wzp_rowsum;
+  ChanQ q;
+  q.mu = q0.y;
+  q.sh = q0.z;
+  q.e = q0.w;
+  q.emask = q1.x;
+  q.zpe = q1.y;
+  q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
+  return requant_out<FAST>(acc, q, out_zp, lo, hi);
+}
+
 }  // namespace bh

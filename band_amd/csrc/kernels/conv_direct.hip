@@ -312,13 +312,15 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const bool lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && ch_per_y <= 64 && p.out_c % 4 == 0 &&
                    (((uintptr_t)p.output) & 3) == 0 && (gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
   if (lds) {
-    // pixels per thread: BH_STEM_PX (A-B runs), default 2 from 1024
-    // workgroups of one pixel per thread
+    // pixels per thread: 1; BH_STEM_PX=2 (A-B runs) gives each thread two
+    // pixels sharing the channel records' LDS reads - slower, 17.5 vs 14.7
+    // us at B = 24 (interleaved, profiles/r05x_stem_px{1,2}.txt): half the
+    // waves, each with twice the dependent VALU chains
     static const int px_env = [] {
       const char* e = std::getenv("BH_STEM_PX");
       return e ? std::atoi(e) : 0;
     }();
-    const int px = px_env == 1 || px_env == 2 ? px_env : (gx >= 1024 ? 2 : 1);
+    const int px = px_env == 2 ? 2 : 1;
     const dim3 g2((unsigned)((M + 256 * px - 1) / (256 * px)), (unsigned)gy);
     if (px == 2) {
       if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 2>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);

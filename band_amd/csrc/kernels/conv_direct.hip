@@ -282,35 +282,57 @@ int bh_conv_direct_launch(const bh_conv_params& p, int M, int K, hipStream_t s) 
 
 // 3x3 / in_c 3 / dil_w 1 stems, out_c % 8 == 0, no residual (conv_mfma.hip
 // routes them here); anything else takes conv_direct_kernel
-int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
-  if (p.k_h != 3 || p.k_w != 3 || p.in_c != 3 || p.dil_w != 1 || p.out_c % 8 || p.residual || p.k_pad < 28)
-    return bh_conv_direct_launch(p, M, K, s);
-  bh::DirectDivs dv;
-  dv.out_w = bh::FastDiv(p.out_w);
-  dv.out_h = bh::FastDiv(p.out_h);
-  // >= ~min_wg workgroups: split the output channels over grid.y (8 at a time)
+namespace {
+// the stem's grid (channels split over grid.y to reach ~min_wg workgroups,
+// 8 at a time) and form: the LDS-staged constants (default; channel ranges
+// of <= 64, out_c % 4 == 0 for its dword stores, aligned output, from 256
+// workgroups - at batch 1 the staging is not repaid: 5.05 vs 4.87 us; B = 24:
+// 13.6 vs 14.6 us, r05u_stem_*) or the scalar-cache form
+// (BH_CONV_STEM_SCALAR, or BH_STEM_SCALAR=1 for A-B runs)
+struct StemPlan {
+  int gx, gy, ch_per_y;
+  bool lds;
+};
+StemPlan stem_plan(const bh_conv_params& p, int M) {
   static const int min_wg = [] {
     const char* e = std::getenv("BH_STEM_MIN_WG");  // A-B runs
     return e ? std::atoi(e) : 512;
   }();
-  const int gx = (M + 255) / 256;
-  const int groups = p.out_c / 8;
-  int gy = (min_wg + gx - 1) / gx;
-  gy = gy < 1 ? 1 : (gy > groups ? groups : gy);
-  const int ch_per_y = (groups + gy - 1) / gy * 8;
-  gy = (p.out_c + ch_per_y - 1) / ch_per_y;
-  const dim3 grid((unsigned)gx, (unsigned)gy);
-  // the LDS-staged constants (default; channel ranges of <= 64, out_c % 4 ==
-  // 0 for its dword stores, aligned output) or the scalar-cache form
-  // (BH_CONV_STEM_SCALAR, or BH_STEM_SCALAR=1 for A-B runs)
   static const bool scalar_env = [] {
     const char* e = std::getenv("BH_STEM_SCALAR");
     return e && e[0] == '1';
   }();
-  // from 256 workgroups (batched passes): at batch 1 the LDS staging is
-  // not repaid (5.05 vs 4.87 us; B = 24: 13.6 vs 14.6 us, r05u_stem_*)
-  const bool lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && ch_per_y <= 64 && p.out_c % 4 == 0 &&
-                   (((uintptr_t)p.output) & 3) == 0 && (gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
+  StemPlan sp;
+  sp.gx = (M + 255) / 256;
+  const int groups = p.out_c / 8;
+  int gy = (min_wg + sp.gx - 1) / sp.gx;
+  gy = gy < 1 ? 1 : (gy > groups ? groups : gy);
+  sp.ch_per_y = (groups + gy - 1) / gy * 8;
+  sp.gy = (p.out_c + sp.ch_per_y - 1) / sp.ch_per_y;
+  sp.lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && sp.ch_per_y <= 64 && p.out_c % 4 == 0 &&
+           (((uintptr_t)p.output) & 3) == 0 && (sp.gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
+  return sp;
+}
+bool stem_shape_ok(const bh_conv_params& p) {
+  return p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.out_c % 8 == 0 && !p.residual && p.k_pad >= 28;
+}
+}  // namespace
+
+// the kernel symbol conv_stem routing lands on (profiling attribution)
+const char* bh_conv_stem_kernel_name(const bh_conv_params& p, int M) {
+  if (!stem_shape_ok(p)) return "conv_direct_kernel";
+  return stem_plan(p, M).lds ? "conv_stem_lds_kernel" : "conv_stem_kernel";
+}
+
+int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
+  if (!stem_shape_ok(p)) return bh_conv_direct_launch(p, M, K, s);
+  bh::DirectDivs dv;
+  dv.out_w = bh::FastDiv(p.out_w);
+  dv.out_h = bh::FastDiv(p.out_h);
+  const StemPlan sp = stem_plan(p, M);
+  const int gx = sp.gx, gy = sp.gy, ch_per_y = sp.ch_per_y;
+  const dim3 grid((unsigned)gx, (unsigned)gy);
+  const bool lds = sp.lds;
   if (lds) {
     // pixels per thread: 1; BH_STEM_PX=2 (A-B runs) gives each thread two
     // pixels sharing the channel records' LDS reads - slower, 17.5 vs 14.7
@@ -329,7 +351,7 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
       if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
       else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
     }
-    return bh_check_launch("conv_stem_kernel");
+    return bh_check_launch("conv_stem_lds_kernel");
   }
   if (p.requant_fast) BH_LAUNCH(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);
   else BH_LAUNCH(bh::conv_stem_kernel<false>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);

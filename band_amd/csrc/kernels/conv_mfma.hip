@@ -687,6 +687,7 @@ int bh_conv_xs_launch(const bh_conv_params& p, int M, int K, int N, hipStream_t 
 int bh_conv_gemm_big_launch(const bh_conv_params& p, int M, int K, hipStream_t s);  // conv_gemm_big.hip
 int bh_conv_stem_mfma_ok(const bh_conv_params& p);                                  // conv_stem_mfma.hip
 int bh_conv_stem_mfma_launch(const bh_conv_params& p, int M, hipStream_t s);       // conv_stem_mfma.hip
+const char* bh_conv_stem_kernel_name(const bh_conv_params& p, int M);           // conv_direct.hip
 
 namespace {
 // batched 1x1 layers (K <= 320) at or above this many output pixels take the
@@ -769,7 +770,10 @@ extern "C" const char* bh_conv2d_i8_kernel(const bh_conv_params* p) {
   static const char* const names[] = {"conv_direct_kernel", "conv_stem_kernel", "conv_xs_kernel",
                                       "conv_rows_kernel", "conv_mfma_kernel", "conv_gemm_kernel",
                                       "conv_gemm_big_kernel", "conv_stem_mfma_kernel"};
-  return names[route(*p, (long)p->batch * p->out_h * p->out_w, p->k_h * p->k_w * p->in_c, p->out_c)];
+  const long M = (long)p->batch * p->out_h * p->out_w;
+  const Route r = route(*p, M, p->k_h * p->k_w * p->in_c, p->out_c);
+  if (r == kStem) return bh_conv_stem_kernel_name(*p, (int)M);
+  return names[r];
 }
 
 extern "C" int bh_conv_packed_geometry(int out_c, int k, int* k_pad, int* n_pad) {

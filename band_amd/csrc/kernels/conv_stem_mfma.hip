@@ -80,20 +80,16 @@ __global__ __launch_bounds__(256) void conv_stem_mfma_kernel(bh_conv_params p, i
   v4i wf[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) wf[b] = *(const v4i*)(p.weights + (long)(16 * b + r16) * p.k_pad + 16 * g);
-  // this lane's output channels: 16b + 4g + r, r = 0..3
-  int32_t be[NB][4];
-  ChanQ cq[NB][4];
+  // D = X W^T: lane (r16, g) gets pixels 4g .. 4g+3 of channel 16b + r16, so
+  // one set of requantisation constants per channel block serves every
+  // value the lane produces (the transposed form derived them per value)
+  int32_t be[NB];
+  ChanQ cq[NB];
 #pragma unroll
   for (int b = 0; b < NB; ++b) {
-    const int c0 = 16 * b + 4 * g;
-    const v4i b4 = *(const v4i*)(p.bias_eff + c0);
-    const v4i m4 = *(const v4i*)(p.mult + c0);
-    const v4i s4 = *(const v4i*)(p.shift + c0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      be[b][r] = b4[r];
-      cq[b][r] = chan_q(m4[r], s4[r], p.out_zp);
-    }
+    const int c = 16 * b + r16;
+    be[b] = p.bias_eff[c];
+    cq[b] = chan_q(p.mult[c], p.shift[c], p.out_zp);
   }
 
   // gather: the PB blocks' window fragments, every load issued first
@@ -129,38 +125,44 @@ __global__ __launch_bounds__(256) void conv_stem_mfma_kernel(bh_conv_params p, i
       }
     }
   }
-  // uint8 filters: the window row sum of each pixel (lane groups 0 and 1
-  // hold its two halves)
-  int rsum[PB];
+  // uint8 filters: the window byte sum of each of this lane's 4 pixels (the
+  // pixel's two halves sit in lane groups 0 and 1 at lane r16 = pixel)
+  int rsum[PB][4];
 #pragma unroll
-  for (int pb = 0; pb < PB; ++pb) {
-    rsum[pb] = 0;
-    if (p.w_zp != 0) {
+  for (int pb = 0; pb < PB; ++pb)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) rsum[pb][i] = 0;
+  if (p.w_zp != 0) {
+#pragma unroll
+    for (int pb = 0; pb < PB; ++pb) {
       int s = 0;
       s = __builtin_amdgcn_sdot4(xf[pb].x, 0x01010101, s, false);
       s = __builtin_amdgcn_sdot4(xf[pb].y, 0x01010101, s, false);
       s = __builtin_amdgcn_sdot4(xf[pb].z, 0x01010101, s, false);
       s = __builtin_amdgcn_sdot4(xf[pb].w, 0x01010101, s, false);
-      rsum[pb] = __shfl(s, r16) + __shfl(s, r16 + 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rsum[pb][i] = __shfl(s, 4 * g + i) + __shfl(s, 4 * g + i + 16);
     }
   }
   const uint8_t* tab = (const uint8_t*)p.out_table;
+  const int qi = lane & 3, qj = (lane >> 2) & 3;  // after the quad transpose: pixel 4g + qi, channels 4qj..4qj+3
 #pragma unroll
   for (int pb = 0; pb < PB; ++pb) {
-    const int m = m_base + pb * 16 + r16;
+    const int m = m_base + pb * 16 + 4 * g + qi;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(wf[b], xf[pb], (v4i){0, 0, 0, 0}, 0, 0, 0);
-      uint32_t packed = 0;
+      const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf[pb], wf[b], (v4i){0, 0, 0, 0}, 0, 0, 0);
+      int32_t v[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int32_t a = acc[r] + be[b][r];
-        if (p.w_zp != 0) a -= p.w_zp * rsum[pb];
-        const int32_t v = requant_out<FAST>(a, cq[b][r], p.out_zp, p.act_min, p.act_max);
-        const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
-        packed |= byte << (8 * r);
+      for (int i = 0; i < 4; ++i) {
+        int32_t a = acc[i] + be[b];
+        if (p.w_zp != 0) a -= p.w_zp * rsum[pb][i];
+        v[i] = requant_out<FAST>(a, cq[b], p.out_zp, p.act_min, p.act_max);
+        if (tab) v[i] = tab[(uint8_t)v[i]];
       }
-      if (m < M) *(uint32_t*)((uint8_t*)p.output + (long)m * p.out_c + 16 * b + 4 * g) = packed;
+      // lane 4qj + qi of the r16 group: channels 16b + 4qj .. +3 of its pixel
+      const uint32_t packed = quad_transpose8(pack4_bytes(v));
+      if (m < M) *(uint32_t*)((uint8_t*)p.output + (long)m * p.out_c + 16 * b + 4 * qj) = packed;
     }
   }
 }

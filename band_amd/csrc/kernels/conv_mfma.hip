@@ -740,7 +740,7 @@ Route route(const bh_conv_params& p, long M, int K, int N) {
     if (!stem || std::getenv("BH_CONV_NO_STEM")) return kDirect;
     // the window x filter contraction on MFMA (conv_stem_mfma.hip); the VALU
     // form when forced (BH_CONV_STEM_VALU) or outside the MFMA form's range
-    return p.kernel_hint != BH_CONV_STEM_VALU && bh_conv_stem_mfma_ok(p) ? kStemMfma : kStem;
+    return bh_conv_stem_mfma_ok(p) ? kStemMfma : kStem;
   }
   const bool aligned = (((uintptr_t)p.output | (uintptr_t)p.residual | (uintptr_t)p.input) & 3) == 0;
   // LDS-staged GEMM: int8 activations (glds cannot apply the uint8 XOR),

@@ -193,19 +193,22 @@ static int launch_stem_mfma(const bh_conv_params& p, int M, hipStream_t s) {
 // 3x3 stems over 3 channels, dilation-1 columns, out_c in {16, 32, 48, 64}
 // (4-byte aligned output), no residual: 1 when this kernel takes the layer
 int bh_conv_stem_mfma_ok(const bh_conv_params& p) {
-  // opt-in (BH_CONV_STEM_MFMA, or BH_STEM_MFMA_MIN_M pixels and up): the
-  // VALU conv_stem_kernel is faster on the same box at every batch measured
-  // - 15.1 vs 17.2 us at B = 24, 18.5 vs 20.3 us at B = 32 (interleaved,
-  // profiles/r05l_stem_ab.txt), 5.0 vs 8.9 us at B = 1 (r05h).  The stem's
-  // 27-deep contraction fills one K-step of 64 at 42 %, and two of the four
-  // lane groups gather nothing, so the MFMA form issues as many loads and
-  // epilogue VALU per pixel as the dot4 form while adding the MFMA latency.
-  static const long min_m = [] {
-    const char* e = std::getenv("BH_STEM_MFMA_MIN_M");
-    return e ? std::atol(e) : -1L;
+  // small grids (batch-1 stems, below 65,536 output pixels; BH_STEM_MFMA_MAX_M
+  // overrides), or forced (BH_CONV_STEM_MFMA).  With the untransposed
+  // epilogue (a lane requantises 4 pixels of one channel) it is the fastest
+  // stem at batch 1: 4.2-4.3 us against 4.9 for the scalar-cache VALU form
+  // and 5.2-5.6 for the LDS-staged one; at B = 24 the LDS-staged VALU form
+  // wins, 14.0 vs 14.6-14.9 us (interleaved, profiles/r05z2_stem_h{4,5}_r*).
+  // The round-4 transposed epilogue derived the requantisation constants
+  // per value and lost everywhere (r05l_stem_ab.txt).
+  static const long max_m = [] {
+    const char* e = std::getenv("BH_STEM_MFMA_MAX_M");
+    return e ? std::atol(e) : 65535L;
   }();
   const long M = (long)p.batch * p.out_h * p.out_w;
-  return ((min_m >= 0 && M >= min_m) || p.kernel_hint == BH_CONV_STEM_MFMA) && p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.k_pad == 64 && p.out_c % 16 == 0 &&
+  const bool want = p.kernel_hint == BH_CONV_STEM_MFMA ||
+                    (p.kernel_hint != BH_CONV_STEM_VALU && p.kernel_hint != BH_CONV_STEM_SCALAR && M <= max_m);
+  return want && p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.k_pad == 64 && p.out_c % 16 == 0 &&
          p.out_c >= 16 && p.out_c <= 64 && !p.residual && !p.out_img_stride && (((uintptr_t)p.output) & 3) == 0;
 }
 

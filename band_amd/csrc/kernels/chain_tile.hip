@@ -288,13 +288,13 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
 // further tile's patch is DMA'd after the previous tile is done
 // STEM (bh_chain_params.stem, tile 1): the depthwise input is the RGB stem's
 // output, and the workgroup computes its patch from the image instead of
-// reading it: wave w takes patch pixels (w & 1) + 2k and output channels
-// [(w >> 1) C/2, (w >> 1 + 1) C/2) - the stem's window gather and v_dot4
-// over filter dwords read through the scalar cache, as conv_stem_kernel -
-// and writes each channel quad to the patch at its swizzled chunk.  Pixels
-// outside the image are skipped (phase A masks those taps).  The stem's
-// output never reaches HBM; halo pixels are computed by both neighbouring
-// tiles (1.56x the stem's arithmetic for 8 x 8 tiles at stride 1).
+// reading it, on MFMA as conv_stem_mfma_kernel does (16-pixel blocks, the
+// channel's bias and requantisation constants from LDS records), writing
+// each pixel's channel quads to the patch at their swizzled chunks.  Pixels
+// outside the image get values phase A never reads (it masks those taps).
+// The stem's output never reaches HBM; halo pixels are computed by both
+// neighbouring tiles (1.56x the stem's arithmetic for 8 x 8 tiles at
+// stride 1).
 struct NoStem {};
 template <int TH, int TW, bool FAST, int KX, int PIPE, typename ST = NoStem>
 __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv, ST st) {
@@ -342,8 +342,6 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
     if constexpr (STEM) {
       const int xs = ox0 * d.stride_w - d.pad_w;
       const int npix = G.PH * G.PW;
-      const int half = C >> 1;
-      const int cbeg = (wave >> 1) * half;
       const long img = (long)st.in_h * st.in_w * 3;
       const uint8_t* im = (const uint8_t*)st.input + n * img;
       const uint8_t* end = (const uint8_t*)st.input + st.batch * img;
@@ -355,24 +353,50 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
         ((int32_t*)rec)[i] = stem_chan_word((const int32_t*)st.weights, st.k_pad >> 2, st.bias_eff, st.mult,
                                             st.shift, st.out_zp, i >> 4, i & 15);
       __syncthreads();
-      for (int pix = (wave & 1) * 64 + lane; pix < npix; pix += 128) {
-        const int r = dv.pw.div(pix);
-        const int px = pix - r * G.PW;
-        const int y = y0 + r, x = xs + px;
-        if (y < 0 || y >= d.in_h || x < 0 || x >= d.in_w) continue;
-        uint32_t xw[7];
-        stem_window(im, end, y * st.stride_h - st.pad_h, x * st.stride_w - st.pad_w, st.dil_h, st.in_h, st.in_w,
-                    (uint32_t)st.in_xor, (uint32_t)st.in_zp, xw);
-        const int f = (3 * r + px) & G.pmask;
-        unsigned char* dst = buf + (r * G.patch_ru + px * (C >> 4)) * 16;
-        for (int c0 = cbeg; c0 < cbeg + half; c0 += 4) {
-          uint32_t packed = 0;
+      // the patch on v_mfma_i32_16x16x64_i8, as conv_stem_mfma_kernel: wave w
+      // takes 16-pixel blocks w, w + 4, ...; lane groups 0 / 1 gather the
+      // pixel's window bytes 0-15 / 16-26 (k-ordered), D = X W^T gives a lane
+      // 4 pixels of channel 16b + r16 (one record per lane and block), and a
+      // quad byte-transpose turns them into 4 channels of one pixel for one
+      // dword into the patch at its swizzled chunk
+      const int nblk = (npix + 15) >> 4;
+      const int nbc = C >> 4;
+      const int qi = lane & 3, qj = (lane >> 2) & 3;
+      for (int blk = wave; blk < nblk; blk += 4) {
+        v4i xf = (v4i){0, 0, 0, 0};
+        if (g < 2) {
+          const int pc = min(blk * 16 + r16, npix - 1);
+          const int r = dv.pw.div(pc);
+          const int px = pc - r * G.PW;
+          uint32_t xw[7];
+          stem_window(im, end, (y0 + r) * st.stride_h - st.pad_h, (xs + px) * st.stride_w - st.pad_w, st.dil_h,
+                      st.in_h, st.in_w, (uint32_t)st.in_xor, (uint32_t)st.in_zp, xw);
+          xf = g == 0 ? (v4i){(int)xw[0], (int)xw[1], (int)xw[2], (int)xw[3]}
+                      : (v4i){(int)xw[4], (int)xw[5], (int)xw[6], 0};
+        }
+        const int p2 = blk * 16 + 4 * g + qi;  // this lane's pixel after the transpose
+        const int r2 = dv.pw.div(min(p2, npix - 1));
+        const int px2 = min(p2, npix - 1) - r2 * G.PW;
+        const bool wr = p2 < npix;
+        const int f2 = (3 * r2 + px2) & G.pmask;
+        unsigned char* dst = buf + (r2 * G.patch_ru + px2 * nbc) * 16 + 4 * qj;
+        for (int b = 0; b < nbc; ++b) {
+          const v4i wf = *(const v4i*)(st.weights + (long)(16 * b + r16) * st.k_pad + 16 * g);
+          const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, wf, (v4i){0, 0, 0, 0}, 0, 0, 0);
+          const StemChan& k = rec[16 * b + r16];
+          const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
+          ChanQ q;
+          q.mu = q0.y;
+          q.sh = q0.z;
+          q.e = q0.w;
+          q.emask = q1.x;
+          q.zpe = q1.y;
+          q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
+          int32_t v[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const int32_t v = stem_chan_eval<FAST>(rec[c0 + c], xw, false, 0, st.out_zp, st.act_min, st.act_max);
-            packed |= ((uint32_t)v & 0xffu) << (8 * c);
-          }
-          *(uint32_t*)(dst + ((((c0 >> 4) ^ f)) << 4) + (c0 & 15)) = packed;
+          for (int t = 0; t < 4; ++t) v[t] = requant_out<FAST>(acc[t] + q0.x, q, st.out_zp, st.act_min, st.act_max);
+          const uint32_t packed = quad_transpose8(pack4_bytes(v));
+          if (wr) *(uint32_t*)(dst + ((b ^ f2) << 4)) = packed;
         }
       }
     } else {

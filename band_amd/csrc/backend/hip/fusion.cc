@@ -286,7 +286,7 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 11;
+constexpr int kChainTuneVersion = 10;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -606,14 +606,14 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // {.., valu}: the depthwise phase on VALU (v_dot4 over the tap
         // table) instead of the block-diagonal MFMA tile (raster forms;
         // BAND_HIP_FUSION=novalu: none)
-        const int forms[26][7] = {
+        const int forms[25][7] = {
             {4, 4, 0, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0, 0},
             {1, 16, 0, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0, 0}, {4, 4, 0, 1, 0, 0, 0}, {4, 4, 0, 3, 0, 0, 0},
             {4, 4, 0, 4, 0, 0, 0}, {2, 4, 0, 0, 1, 0, 0}, {1, 4, 0, 0, 1, 0, 0}, {1, 8, 0, 0, 1, 0, 0},
             {1, 4, 0, 0, 0, 2, 0}, {1, 8, 0, 0, 0, 2, 0}, {2, 4, 0, 0, 0, 2, 0}, {1, 16, 0, 0, 0, 2, 0},
             {1, 4, 0, 0, 0, 3, 0}, {1, 8, 0, 0, 0, 3, 0}, {1, 4, 0, 0, 0, 4, 0},
             {4, 4, 0, 0, 0, 0, 1}, {2, 4, 0, 0, 0, 0, 1}, {1, 4, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 0, 1},
-            {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}, {4, 4, 0, 0, 1, 0, 0}};
+            {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}};
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;

@@ -1053,7 +1053,7 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
     return 0;
   if (p.tile) return bh_chain_tile_lds_bytes(pp);
   if (p.deep && (p.persist || !((p.px_blocks == 1 && (p.waves == 0 || p.waves == 4 || p.waves == 8)) ||
-                                ((p.px_blocks == 2 || p.px_blocks == 4) && (p.waves == 0 || p.waves == 4)))))
+                                (p.px_blocks == 2 && (p.waves == 0 || p.waves == 4)))))
     return 0;
   if (p.persist) {
     if (p.px_blocks != 4 || (p.waves != 0 && p.waves != 4)) return 0;
@@ -1097,7 +1097,7 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
     }
     return bh_check_launch("chain_persist_kernel");
   }
-  if (p.deep) {  // deep-issue forms (DA = 6): px_blocks 1 with 4 or 8 waves, px_blocks 2 / 4 with 4
+  if (p.deep) {  // deep-issue forms (DA = 6): px_blocks 1 with 4 or 8 waves, px_blocks 2 with 4
 #define BH_DEEP(RB, NW)                                                                      \
   if (k2) {                                                                                  \
     if (fast) bh::launch_chain<RB, true, 2, NW, false, 6>(p, P, L, lds, s);                  \
@@ -1106,13 +1106,7 @@ extern "C" int bh_chain_i8(const bh_chain_params* pp, bh_stream_t stream) {
     if (fast) bh::launch_chain<RB, true, bh::kXsMax, NW, false, 6>(p, P, L, lds, s);         \
     else bh::launch_chain<RB, false, bh::kXsMax, NW, false, 6>(p, P, L, lds, s);             \
   }
-    const int t_deep = p.has_pw2 ? (p.pw2.out_c + 15) / 16 : (p.pw1.out_c + 15) / 16;
-    if (p.px_blocks == 4 && k2 && t_deep >= 8) {  // the amortised 64-pixel form, deep phase A
-      if (fast) bh::launch_chain<4, true, 2, 4, true, 6>(p, P, L, lds, s);
-      else bh::launch_chain<4, false, 2, 4, true, 6>(p, P, L, lds, s);
-    } else if (p.px_blocks == 4) {
-      BH_DEEP(4, 4)
-    } else if (p.px_blocks == 2) {
+    if (p.px_blocks == 2) {
       BH_DEEP(2, 4)
     } else if (p.waves == 8) {
       BH_DEEP(1, 8)

@@ -398,7 +398,7 @@ typedef struct bh_chain_params {
   void* debug_stamps;
   /* 1: deep-issue form - each wave issues the loads of 6 depthwise channel
    * groups per round (instead of 2) and the x-stationary 1x1 GEMMs take 3-6
-   * channel tiles per round; px_blocks 1 (4 or 8 waves), 2 or 4 (4 waves) */
+   * channel tiles per round; px_blocks 1 (4 or 8 waves) or 2 (4 waves) */
   int deep;
   /* raster forms with a second 1x1 (0 / 1: off): the second 1x1's channel
    * tiles are split over c_split workgroups per pixel block (grid.y); each

@@ -38,14 +38,13 @@ def test_chain_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
     _check(c, gpu_lib, 1, waves=8)
-    for px, w in ((1, 4), (1, 8), (2, 4), (4, 4)):  # the deep-issue forms
+    for px, w in ((1, 4), (1, 8), (2, 4)):  # the deep-issue forms
         _check(c, gpu_lib, px, waves=w, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
     c.fast = False  # TFLite's two-step requantisation in every stage
     _check(c, gpu_lib, 4)
     _check(c, gpu_lib, 1, deep=1)
-    _check(c, gpu_lib, 4, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
 
@@ -70,7 +69,7 @@ def test_chain_general(gpu_lib, args):
         _check(c, gpu_lib, px)
     _check(c, gpu_lib, 1, waves=16)
     _check(c, gpu_lib, 1, waves=8)
-    for px, w in ((1, 4), (1, 8), (2, 4), (4, 4)):
+    for px, w in ((1, 4), (1, 8), (2, 4)):
         _check(c, gpu_lib, px, waves=w, deep=1)
     if _persist_fits(c, gpu_lib):
         _check(c, gpu_lib, 4, persist=1)
@@ -160,9 +159,9 @@ def test_chain_rejects_unsupported(gpu_lib):
     c = ChainCase(rng, 1, 8, 8, 32, 1, 16, False, 48).params(gpu_lib, 4, keep)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0
     c.deep = 1
-    c.persist = 1  # the deep forms are raster forms (16, 32 or 64 pixels per workgroup), not persistent
+    c.px_blocks = 4  # the deep forms take 16 or 32 pixels per workgroup
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
-    c.deep, c.persist, c.px_blocks = 0, 0, 4
+    c.deep, c.px_blocks = 0, 4
     for field, bad in (("px_blocks", 3), ("waves", 12)):
         old = getattr(c, field)
         setattr(c, field, bad)

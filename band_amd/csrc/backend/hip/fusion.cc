@@ -286,7 +286,8 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
-constexpr int kChainTuneVersion = 10;
+// (11: column-reuse depthwise phase, every raster form re-measured)
+constexpr int kChainTuneVersion = 11;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];

@@ -438,16 +438,25 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int n = dv.out_h.div(t);
     const int oy = t - n * d.out_h;
     const int iy = oy * d.stride_h, ix = ox * d.stride_w, row0 = n * d.in_h;
-    // this lane's tap of each K-step (taps 4s..4s+3; lane group g = tap % 4)
+    // K-step s takes filter row s and lane group g filter column g (group
+    // 3 idles: zero filter bytes, so its operand bytes do not matter).
+    // Column reuse: lane (p, g) reads input column ix + g*dil_w, which is
+    // lane (p + dd, 0)'s column when dd = g*dil_w / stride_w is whole and
+    // pixel p + dd lies in the same 16-pixel block and output row; such a
+    // lane takes that lane's filled tap dwords by ds_bpermute instead of
+    // loading them, so only group 0 and the block's edge lanes issue tap
+    // loads (a quarter of the texture-path lane accesses at stride 1)
+    const int gx = g * d.dil_w;
+    const int dd = (g == 1 || g == 2) && gx % d.stride_w == 0 ? gx / d.stride_w : 0;
+    const bool borrow = dd > 0 && r16 + dd < 16 && ox + dd < d.out_w;
+    const bool need = g < 3 && !borrow;
+    const int src4 = (borrow ? r16 + dd : lane) << 2;
     int off[3];
     bool ok[3];
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      const int tap = 4 * s + g;
-      const int fy = (tap * 11) >> 5;  // tap / 3 for tap < 12
-      const int fx = tap - 3 * fy;
-      const int y = iy + fy * d.dil_h - d.pad_h, x = ix + fx * d.dil_w - d.pad_w;
-      ok[s] = mval && tap < 9 && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
+      const int y = iy + s * d.dil_h - d.pad_h, x = ix + gx - d.pad_w;
+      ok[s] = mval && g < 3 && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
       off[s] = ok[s] ? ((row0 + y) * d.in_w + x) * C : 0;
     }
     const __amdgpu_buffer_rsrc_t rsrc =
@@ -455,33 +464,49 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
     const int zfill = (int)splat_byte(d.in_zp);
     const int dsel = r16 >> 2;
     const int bsh = 8 * (r16 & 3);
+    // this lane's filter byte of K-step s, tap 3s + g, in the tap table
+    // row (bh_pack_dw_taps): dword tsel[s], bit offset tbit[s]; tap 8
+    // sits in byte c % 4 of dword 2
+    const int tsel1 = g == 0 ? 0 : 1, tbit1 = g == 0 ? 24 : 8 * (g - 1);
+    const int tbit2 = g < 2 ? 8 * (2 + g) : bsh;
     // two channel groups per iteration: both items' loads (input taps,
-    // filter bytes, epilogue operands) are issued before either's MFMAs
+    // the channel's tap-table row, requantisation operands) are issued
+    // before either's MFMAs
     struct DwItem {
       v4i xf[3];
-      uint32_t wb[3];
-      int32_t be, mu, sh;
+      v4i tw;
+      int32_t mu, sh;
     };
     auto dw_load = [&](int cg, DwItem& it) {
       const int c0 = cg * 16;
+      v4u v[3] = {};
+      if (need) {
 #pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[s] + c0, 0, 0);
-        it.xf[s] = (v4i){ok[s] ? (int)v.x : zfill, ok[s] ? (int)v.y : zfill, ok[s] ? (int)v.z : zfill,
-                         ok[s] ? (int)v.w : zfill};
-        const int tap = 4 * s + g;
-        it.wb[s] = tap < 9 ? (uint32_t)(uint8_t)d.weights[tap * C + c0 + r16] : 0u;
+        for (int s = 0; s < 3; ++s) v[s] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off[s] + c0, 0, 0);
       }
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+        it.xf[s] = (v4i){ok[s] ? (int)v[s].x : zfill, ok[s] ? (int)v[s].y : zfill, ok[s] ? (int)v[s].z : zfill,
+                         ok[s] ? (int)v[s].w : zfill};
       const int c = c0 + r16;  // this lane's result channel
-      it.be = d.taps[4 * c + 3];
+      it.tw = *(const v4i*)(d.taps + 4 * c);
       it.mu = d.mult[c];
       it.sh = d.shift[c];
     };
-    auto dw_finish = [&](int cg, const DwItem& it) {
-      v4i acc = (v4i){it.be, it.be, it.be, it.be};
+    auto dw_finish = [&](int cg, DwItem& it) {
+#pragma unroll
+      for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) it.xf[s][j] = __builtin_amdgcn_ds_bpermute(src4, it.xf[s][j]);
+      const uint32_t t0 = (uint32_t)it.tw.x, t1 = (uint32_t)it.tw.y, t2 = (uint32_t)it.tw.z;
+      uint32_t wb[3];
+      wb[0] = (t0 >> (8 * g)) & 0xffu;
+      wb[1] = ((tsel1 ? t1 : t0) >> tbit1) & 0xffu;
+      wb[2] = ((g < 2 ? t1 : t2) >> tbit2) & 0xffu;
+      v4i acc = (v4i){it.tw.w, it.tw.w, it.tw.w, it.tw.w};
 #pragma unroll
       for (int s = 0; s < 3; ++s) {
-        const int w = (int)(it.wb[s] << bsh);
+        const int w = g < 3 ? (int)(wb[s] << bsh) : 0;
         const v4i wf = (v4i){dsel == 0 ? w : 0, dsel == 1 ? w : 0, dsel == 2 ? w : 0, dsel == 3 ? w : 0};
         acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(it.xf[s], wf, acc, 0, 0, 0);
       }

@@ -204,6 +204,10 @@ __global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M,
 // PX pixels per thread (m, m + 256, ...: stores stay lane-consecutive): the
 // channel records' LDS reads serve PX pixels and their dot / requant chains
 // interleave
+// BH_STEM_STORE16 (build-time A-B switch, default on): 16-byte output stores
+#ifndef BH_STEM_STORE16
+#define BH_STEM_STORE16 1
+#endif
 template <bool FAST, int PX>
 __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, int M, DirectDivs dv, int ch_per_y) {
   __shared__ __attribute__((aligned(16))) StemChan sc[64];
@@ -243,6 +247,38 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
     }
   }
   const uint8_t* tab = (const uint8_t*)p.out_table;
+#if BH_STEM_STORE16
+  // 16 channels per store (one 16-byte store per pixel instead of four
+  // dword stores) when the channel range and the row pitch allow it
+  if ((nc & 15) == 0 && (p.out_c & 15) == 0 && (cb & 15) == 0) {
+    for (int c0 = 0; c0 < nc; c0 += 16) {
+      uint32_t packed[PX][4];
+#pragma unroll
+      for (int u = 0; u < PX; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) packed[u][j] = 0;
+#pragma unroll
+      for (int c = 0; c < 16; ++c) {
+        const StemChan& k = sc[c0 + c];
+#pragma unroll
+        for (int u = 0; u < PX; ++u) {
+          const int32_t v =
+              stem_chan_eval<FAST>(k, xw[u], p.w_zp != 0, p.w_zp * rowsum[u], p.out_zp, p.act_min, p.act_max);
+          const uint32_t byte = tab ? tab[(uint8_t)v] : ((uint32_t)v & 0xffu);
+          packed[u][c >> 2] |= byte << (8 * (c & 3));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < PX; ++u) {
+        const int m = m0 + 256 * u;
+        if (m < M)
+          *(uint4*)((uint8_t*)p.output + (long)m * p.out_c + cb + c0) =
+              make_uint4(packed[u][0], packed[u][1], packed[u][2], packed[u][3]);
+      }
+    }
+    return;
+  }
+#endif
   for (int c0 = 0; c0 < nc; c0 += 4) {
     uint32_t packed[PX];
 #pragma unroll

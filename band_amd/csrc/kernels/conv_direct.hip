@@ -204,6 +204,11 @@ __global__ __launch_bounds__(256) void conv_stem_kernel(bh_conv_params p, int M,
 // PX pixels per thread (m, m + 256, ...: stores stay lane-consecutive): the
 // channel records' LDS reads serve PX pixels and their dot / requant chains
 // interleave
+// BH_STEM_ROWS (build-time A-B switch, default on): input rows staged in LDS
+#ifndef BH_STEM_ROWS
+#define BH_STEM_ROWS 1
+#endif
+constexpr int kStemRowWords = 3072;  // 12 KB: nine 224-pixel RGB rows
 // BH_STEM_STORE16 (build-time A-B switch, default on): 16-byte output stores
 #ifndef BH_STEM_STORE16
 #define BH_STEM_STORE16 1
@@ -216,17 +221,67 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
   const int nc = ce - cb;
   const int m0 = blockIdx.x * 256 * PX + threadIdx.x;
   const long img = (long)p.in_h * p.in_w * 3;
-  // the windows first: their loads are in flight while the constants stage
   uint32_t xw[PX][7];
+  // staged rows (BH_STEM_ROWS, one pixel per thread): when the workgroup's
+  // 256 pixels lie in one image and their input rows fit kStemRowWords,
+  // the rows come in as 16-byte loads into LDS (one load per 16 bytes of
+  // the image instead of nine dword loads per pixel) and each window is read
+  // from there after the barrier
+  bool staged = false;
+  int iy_lo = 0, rw = 0, n_img = 0;
+#if BH_STEM_ROWS
+  __shared__ __attribute__((aligned(16))) uint32_t rows[kStemRowWords];
+  if constexpr (PX == 1) {
+    const int mf = blockIdx.x * 256, ml = min(mf + 255, M - 1);
+    const int tf = dv.out_w.div(mf), tl = dv.out_w.div(ml);
+    const int nf = dv.out_h.div(tf), nl = dv.out_h.div(tl);
+    rw = (((15 + p.in_w * 3) >> 2) + 4) & ~3;
+    const int nrows = (tl - nf * p.out_h - (tf - nf * p.out_h)) * p.stride_h + 2 * p.dil_h + 1;
+    if (nf == nl && (((uintptr_t)p.input) & 15) == 0 && nrows * rw <= kStemRowWords && p.batch * img < INT32_MAX) {
+      staged = true;
+      n_img = nf;
+      iy_lo = (tf - nf * p.out_h) * p.stride_h - p.pad_h;
+      typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+      const int total = (int)(p.batch * img);
+      const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)p.input, (short)0, total, 0x00020000);
+      const int cpr = rw >> 2;  // 16-byte chunks per staged row
+      for (int i = threadIdx.x; i < nrows * cpr; i += 256) {
+        const int r = i / cpr;
+        const int k = i - r * cpr;
+        const int y = iy_lo + r;
+        if (y >= 0 && y < p.in_h) {
+          const int rel = n_img * (int)img + y * p.in_w * 3;
+          const int g = (rel & ~15) + 16 * k;
+          v4u v;
+          if (g + 16 <= total) {
+            v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, g, 0, 0);
+          } else {
+            // the chunk that runs past the tensor's end (a range-checked
+            // 16-byte load would drop its valid bytes too): bytewise
+            uint32_t wv[4] = {0, 0, 0, 0};
+            for (int j = 0; j < 16 && g + j < total; ++j)
+              wv[j >> 2] |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rsrc, g + j, 0, 0) << (8 * (j & 3));
+            v = (v4u){wv[0], wv[1], wv[2], wv[3]};
+          }
+          *(v4u*)(rows + r * rw + 4 * k) = v;
+        }
+      }
+    }
+  }
+#endif
+  if (!staged) {
+    // the windows first: their loads are in flight while the constants stage
 #pragma unroll
-  for (int u = 0; u < PX; ++u) {
-    const int mm = min(m0 + 256 * u, M - 1);
-    const int t = dv.out_w.div(mm);
-    const int ox = mm - t * p.out_w;
-    const int n = dv.out_h.div(t);
-    const int oy = t - n * p.out_h;
-    stem_window((const uint8_t*)p.input + n * img, (const uint8_t*)p.input + p.batch * img, oy * p.stride_h - p.pad_h,
-                ox * p.stride_w - p.pad_w, p.dil_h, p.in_h, p.in_w, (uint32_t)p.in_xor, (uint32_t)p.in_zp, xw[u]);
+    for (int u = 0; u < PX; ++u) {
+      const int mm = min(m0 + 256 * u, M - 1);
+      const int t = dv.out_w.div(mm);
+      const int ox = mm - t * p.out_w;
+      const int n = dv.out_h.div(t);
+      const int oy = t - n * p.out_h;
+      stem_window((const uint8_t*)p.input + n * img, (const uint8_t*)p.input + p.batch * img,
+                  oy * p.stride_h - p.pad_h, ox * p.stride_w - p.pad_w, p.dil_h, p.in_h, p.in_w, (uint32_t)p.in_xor,
+                  (uint32_t)p.in_zp, xw[u]);
+    }
   }
   {
     const int kpw = p.k_pad >> 2;
@@ -236,6 +291,16 @@ __global__ __launch_bounds__(256) void conv_stem_lds_kernel(bh_conv_params p, in
     }
   }
   __syncthreads();
+#if BH_STEM_ROWS
+  if (staged) {
+    const int mm = min(m0, M - 1);
+    const int t = dv.out_w.div(mm);
+    const int ox = mm - t * p.out_w;
+    const int oy = t - n_img * p.out_h;
+    stem_window_lds(rows, rw, iy_lo, n_img * (int)img, oy * p.stride_h - p.pad_h, ox * p.stride_w - p.pad_w, p.dil_h,
+                    p.in_h, p.in_w, (uint32_t)p.in_xor, (uint32_t)p.in_zp, xw[0]);
+  }
+#endif
   if (m0 >= M) return;
   int rowsum[PX];
 #pragma unroll

@@ -57,6 +57,59 @@ __device__ __forceinline__ void stem_window(const uint8_t* img, const uint8_t* e
   xw[6] = __builtin_amdgcn_alignbyte(r[2][2], r[2][1], 2);                 // R2[6..8] 0
 }
 
+// The same window read from input rows staged in LDS (conv_stem_lds_kernel
+// with BH_STEM_ROWS): staged row r holds image row iy_lo + r from the
+// 16-byte-aligned global address below its first byte, rw words apart, so
+// pixel x of row y starts at byte (y - iy_lo) * 4 * rw + (rel_y & 15) + 3x,
+// rel_y = the row's byte offset in the tensor (img_rel + y * in_w * 3).
+__device__ __forceinline__ void stem_window_lds(const uint32_t* rows, int rw, int iy_lo, int img_rel, int y0, int x0,
+                                                int dil_h, int in_h, int in_w, uint32_t in_xor, uint32_t in_zp,
+                                                uint32_t xw[7]) {
+  const uint32_t xorw = splat_byte(in_xor);
+  const uint32_t padw = splat_byte(in_zp);
+  const uint8_t* bytes = (const uint8_t*)rows;
+  uint32_t r[3][3];
+  const bool colok = x0 >= 0 && x0 + 3 <= in_w;
+#pragma unroll
+  for (int fy = 0; fy < 3; ++fy) {
+    const int y = y0 + fy * dil_h;
+    if (y < 0 || y >= in_h) {
+      r[fy][0] = padw;
+      r[fy][1] = padw;
+      r[fy][2] = padw & 0xffu;
+      continue;
+    }
+    const int rel = img_rel + y * in_w * 3;
+    const int b = (y - iy_lo) * 4 * rw + (rel & 15) + x0 * 3;
+    if (colok) {
+      const uint32_t* w = rows + (b >> 2);
+      const uint32_t o = (uint32_t)(b & 3);
+      const uint32_t d0 = w[0], d1 = w[1], d2 = w[2];
+      r[fy][0] = __builtin_amdgcn_alignbyte(d1, d0, o) ^ xorw;
+      r[fy][1] = __builtin_amdgcn_alignbyte(d2, d1, o) ^ xorw;
+      r[fy][2] = ((d2 >> (8 * o)) ^ xorw) & 0xffu;
+    } else {
+      uint32_t bb[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) {
+        const int x = x0 + k / 3;
+        bb[k] = (x >= 0 && x < in_w) ? (uint32_t)(bytes[b + k] ^ (uint8_t)in_xor) : (padw & 0xffu);
+      }
+      r[fy][0] = bb[0] | bb[1] << 8 | bb[2] << 16 | bb[3] << 24;
+      r[fy][1] = bb[4] | bb[5] << 8 | bb[6] << 16 | bb[7] << 24;
+      r[fy][2] = bb[8];
+    }
+  }
+  xw[0] = r[0][0];
+  xw[1] = r[0][1];
+  xw[2] = __builtin_amdgcn_perm(r[1][0], r[0][2], 0x06050400u);
+  xw[3] = __builtin_amdgcn_alignbyte(r[1][1], r[1][0], 3);
+  const uint32_t u = __builtin_amdgcn_perm(r[1][2], r[1][1], 0x0c0c0403u);
+  xw[4] = u | (r[2][0] << 16);
+  xw[5] = __builtin_amdgcn_alignbyte(r[2][1], r[2][0], 2);
+  xw[6] = __builtin_amdgcn_alignbyte(r[2][2], r[2][1], 2);
+}
+
 // One output channel of the stem as a 64-byte LDS record: the filter dwords
 // 0..6 of the k-ordered window (and a zero), the folded bias and the
 // requantisation constants (ChanQ precomputed).  Every lane of a wave reads

@@ -82,6 +82,21 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
     if (!largest) largest = v.exec.get();
     variants.push_back(std::move(v));
   }
+  // every variant's graph is captured here (one eager pass first, as
+  // RunPass's second-run rule does): captured lazily, the first passes of a
+  // rarely used size (a few jobs) captured inside the serving path, a
+  // stall of that worker's lane of ~ms while its jobs wait.
+  // BAND_HIP_PRECAPTURE=0 keeps the lazy capture (A-B runs).
+  static const bool precapture = [] {
+    const char* e = std::getenv("BAND_HIP_PRECAPTURE");
+    return !(e && e[0] == '0');
+  }();
+  if (device_flag_ == DeviceFlag::kGPU && use_graph_ && precapture) {
+    for (JobBatchVariant& v : variants) {
+      PreparedSubgraph* vs = v.exec->Find(key);
+      if (vs) RETURN_STATUS_IF(v.exec->PrecaptureGraph(vs));
+    }
+  }
   // ascending batch (VariantFor takes the smallest >= n); the largest
   // variant, whose arena / mirrors the others view, is destroyed last
   std::sort(variants.begin(), variants.end(),

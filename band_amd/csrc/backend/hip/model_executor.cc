@@ -740,6 +740,16 @@ absl::Status HipModelExecutor::CaptureGraph(PreparedSubgraph* sg) {
   return absl::OkStatus();
 }
 
+absl::Status HipModelExecutor::PrecaptureGraph(PreparedSubgraph* sg) {
+  if (!use_graph_ || sg->graph) return absl::OkStatus();
+  const int rc = bh_set_device(ordinal_);
+  if (rc) return HipErr(rc, "hipSetDevice");
+  RETURN_STATUS_IF(EnqueueLaunches(sg));
+  if (bh_stream_sync(stream_) != 0) return HipErr(1, "stream sync");
+  ++sg->runs;
+  return CaptureGraph(sg);
+}
+
 absl::Status HipModelExecutor::EnqueuePass(PreparedSubgraph* sg) {
   if (!use_graph_ || !sg->graph) return Enqueue(sg);
   RETURN_STATUS_IF(RestoreIoNodes(sg));

@@ -238,6 +238,9 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   absl::Status EnqueuePass(PreparedSubgraph* sg);
   // captures sg's pass into its graph (host copies inside when io_in_graph)
   absl::Status CaptureGraph(PreparedSubgraph* sg);
+  // one eager pass of the kernels, then the graph capture a second pass
+  // would do (PrepareJobBatches: no variant captures in the serving path)
+  absl::Status PrecaptureGraph(PreparedSubgraph* sg);
   // drops sg's graph (and its captured template / copy nodes)
   void DropGraph(PreparedSubgraph* sg);
   // points sg's graph copy nodes at the host mirrors again

@@ -96,6 +96,7 @@ absl::Status HipModelExecutor::PrepareJobBatches(interface::IModel* model, const
       PreparedSubgraph* vs = v.exec->Find(key);
       if (vs) RETURN_STATUS_IF(v.exec->PrecaptureGraph(vs));
     }
+    RETURN_STATUS_IF(PrecaptureGraph(base));  // one-job passes
   }
   // ascending batch (VariantFor takes the smallest >= n); the largest
   // variant, whose arena / mirrors the others view, is destroyed last

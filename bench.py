@@ -756,6 +756,23 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
             "p99_job_latency_ms": float(np.percentile(lat * 1e-3, 99))}
 
 
+def per_model_latency(lat_us, names, n_models, burst=4):
+    """rank 0's p50 / p99 job latency per model of the closed loop: job j is
+    a request for model (j / burst) % n_models (BandxEngineRunClosedLoop,
+    band_amd/csrc/engine/c_api.cc)"""
+    lat = np.asarray(lat_us) * 1e-3
+    if n_models < 1 or lat.size == 0:
+        return None
+    mid = (np.arange(lat.size) // burst) % n_models
+    out = {}
+    for m in range(n_models):
+        v = lat[mid == m]
+        if v.size:
+            key = names[m] if m < len(names) else str(m)
+            out[key] = {"p50": round(float(np.percentile(v, 50)), 3), "p99": round(float(np.percentile(v, 99)), 3)}
+    return out
+
+
 def main():
     args = parse()
     global SAMPLE_THREADS
@@ -982,6 +999,8 @@ def main():
             single["p50_job_latency_ms"],
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
             single["p99_job_latency_ms"],
+            "job_latency_ms_per_model": per_model_latency(lat_us, [m[0] for m in models], M)
+            if lat_us is not None and not poisson else None,
             "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
             "gpu_kernel_us_per_inference_at_mean_pass": dev.get("gpu_us_per_inference_at_mean_pass") if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,

@@ -548,10 +548,12 @@ def PinProcessToCpus(cpus):
 
 def CoalescerStats(reset=False):
     """process-wide job coalescing totals: calls, solo passes, group passes,
-    jobs in group passes, largest group (coalescer.h)"""
-    arr = (ctypes.c_longlong * 5)()
+    jobs in group passes, largest group, calls run with coalescing off (no
+    lanes) and the most of those at once (coalescer.h)"""
+    arr = (ctypes.c_longlong * 7)()
     _abi.check(_abi.load().bhx_coalescer_stats(arr, int(bool(reset))), "coalescer_stats")
-    keys = ("calls", "solo_passes", "group_passes", "group_jobs", "max_group")
+    keys = ("calls", "solo_passes", "group_passes", "group_jobs", "max_group", "bypass_calls",
+            "max_bypass_inflight")
     return {k: int(v) for k, v in zip(keys, arr)}
 
 

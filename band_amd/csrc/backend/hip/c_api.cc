@@ -392,6 +392,8 @@ int bhx_coalescer_stats(long long* out, int reset) {
   out[2] = s.group_passes;
   out[3] = s.group_jobs;
   out[4] = s.max_group;
+  out[5] = s.bypass_calls;
+  out[6] = s.max_bypass_inflight;
   if (reset) band::hip::JobCoalescer::ResetTotals();
   return 0;
 }

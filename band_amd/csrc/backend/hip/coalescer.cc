@@ -45,6 +45,8 @@ std::shared_ptr<JobCoalescer> JobCoalescer::Join(HipModelExecutor* e, interface:
       for (int l = 0; l < c->num_lanes_; ++l) c->free_lanes_.push_back(l);
       if (const char* io = std::getenv("BAND_HIP_COALESCE_IO")) c->dma_io_ = std::string(io) == "dma";
       if (const char* w = std::getenv("BAND_HIP_COALESCE_WAIT_US")) c->wait_us_ = std::max(0, std::atoi(w));
+      // test hook: the lane build fails as it would out of device memory
+      if (const char* f = std::getenv("BAND_HIP_COALESCE_FAIL_BUILD")) c->fail_build_ = std::atoi(f) != 0;
       slot = c;
     }
   }
@@ -74,6 +76,7 @@ std::shared_ptr<JobCoalescer> JobCoalescer::Join(HipModelExecutor* e, interface:
 }
 
 absl::Status JobCoalescer::BuildLanes(HipModelExecutor* e, interface::IModel* model, const SubgraphKey& key) {
+  if (fail_build_) return absl::InternalError("coalescer: lane build failed (BAND_HIP_COALESCE_FAIL_BUILD)");
   PreparedSubgraph* base = e->Find(key);
   if (!base) return absl::InternalError("coalescer: no prepared subgraph");
   std::vector<size_t> in_bytes, out_bytes;
@@ -160,6 +163,16 @@ void JobCoalescer::Account(int n) {
   g_totals.calls += n;
 }
 
+void JobCoalescer::AccountBypass(int inflight) {
+  ++stats_.calls;
+  ++stats_.bypass_calls;
+  stats_.max_bypass_inflight = std::max<int64_t>(stats_.max_bypass_inflight, inflight);
+  std::lock_guard<std::mutex> lock(g_totals_mu);
+  ++g_totals.calls;
+  ++g_totals.bypass_calls;
+  g_totals.max_bypass_inflight = std::max<int64_t>(g_totals.max_bypass_inflight, inflight);
+}
+
 int JobCoalescer::want() const {
   return lanes_ready_ && wait_us_ > 0 ? std::max(1, std::min(max_batch_, last_group_)) : 1;
 }
@@ -202,6 +215,18 @@ void JobCoalescer::Release(Group* g) {
 absl::Status JobCoalescer::Run(HipModelExecutor* e, PreparedSubgraph* sg) {
   Member me{e, sg};
   std::unique_lock<std::mutex> lock(mu_);
+  if (!lanes_ready_) {
+    // no lanes (not built yet, or the build failed): coalescing is off, so
+    // the call runs its own executor's pass at once, beside any others - it
+    // takes no lane token, which would cap the model's concurrent calls on
+    // this GPU at num_lanes_
+    AccountBypass(++bypass_inflight_);
+    lock.unlock();
+    absl::Status s = e->RunPass(sg);
+    lock.lock();
+    --bypass_inflight_;
+    return s;
+  }
   pending_.push_back(&me);
   Dispatch();
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(wait_us_);

@@ -60,6 +60,8 @@ class JobCoalescer {
     int64_t group_passes = 0; // lane passes (>= 2 jobs)
     int64_t group_jobs = 0;   // jobs in those passes
     int64_t max_group = 0;
+    int64_t bypass_calls = 0;         // calls that ran without lanes (none built: coalescing off)
+    int64_t max_bypass_inflight = 0;  // the most such calls running at once
   };
 
   // Registers `e`'s whole-model subgraph `key` of `model` on GPU `ordinal`;
@@ -118,6 +120,7 @@ class JobCoalescer {
   // releases a finished group's lane (mu_ held)
   void Release(Group* g);
   void Account(int n);
+  void AccountBypass(int inflight);
 
   mutable std::mutex mu_;
   std::vector<HipModelExecutor*> members_;
@@ -138,6 +141,8 @@ class JobCoalescer {
   // want() calls; 0 = dispatch whatever is queued at once
   int wait_us_ = 100;
   int last_group_ = 1;  // size of the group that released its lane last
+  int bypass_inflight_ = 0;  // calls running without lanes right now
+  bool fail_build_ = false;  // BAND_HIP_COALESCE_FAIL_BUILD (tests)
   int ordinal_ = -1;
   std::vector<size_t> in_bytes_, out_bytes_;  // per boundary tensor, one job
   Stats stats_;

@@ -742,14 +742,22 @@ BandStatus DriveRequests(BandEngine* engine, BandModel** models, BandTensor** in
 }
 }  // namespace
 
-BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
-                                    int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
-                                    double* wall_s) {
-  // closed loop: runs of `burst` requests per model, models in turn
+BandStatus BandxEngineRunClosedLoopEx(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
+                                      int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
+                                      int* model_index, double* wall_s) {
+  // closed loop: runs of `burst` requests per model, models in turn (the
+  // burst DriveRequests settles on, so model_index is the one to key on)
   return DriveRequests(
       engine, models, inputs, n_models, n_jobs, max_inflight, false,
       [&](int j, int burst) { return std::make_pair(int64_t(0), (j / burst) % std::max(n_models, 1)); },
-      latency_us, worker_ids, nullptr, wall_s, 4);
+      latency_us, worker_ids, model_index, wall_s, 4);
+}
+
+BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,
+                                    int n_jobs, int max_inflight, double* latency_us, int* worker_ids,
+                                    double* wall_s) {
+  return BandxEngineRunClosedLoopEx(engine, models, inputs, n_models, n_jobs, max_inflight, latency_us, worker_ids,
+                                    nullptr, wall_s);
 }
 
 BandStatus BandxEngineRunPoisson(BandEngine* engine, BandModel** models, BandTensor** inputs, int n_models,

@@ -842,9 +842,10 @@ absl::Status Engine::InvokeJobBatchDirect(const SubgraphKey& key, const std::vec
       // a subgraph output outside the output ring feeds a later subgraph:
       // it must reach the executor's own views
       if (!out_it->second->IsTensorIndexValid(outs[k])) return absl::UnimplementedError("intermediate output");
-    // as in CopyOutputs; a slot still held past the bound: the staged path
-    // fails that job's output copy alone
-    if (!out_it->second->AcquireForWrite(j.output_handle)) return absl::UnimplementedError("output slot held");
+    // as in CopyOutputs, but without waiting: a slot held right now sends
+    // the pass to the staged path at once, whose CopyOutputs waits (bounded,
+    // once) and fails that job's output copy alone if the hold outlasts it
+    if (!out_it->second->TryAcquireForWrite(j.output_handle)) return absl::UnimplementedError("output slot held");
     for (size_t k = 0; k < outs.size(); ++k) {
       Tensor* t = out_it->second->SlotTensor(outs[k], j.output_handle);
       if (!t || !t->IsRingMemory()) return absl::UnimplementedError("output slot not page-locked");

@@ -169,6 +169,10 @@ TensorRingBuffer::TensorRingBuffer(const std::vector<std::shared_ptr<interface::
       busy_(size_, 0),
       owner_(size_, -1),
       held_(size_, 0) {
+  // read per ring (not once per process), so an engine created after a
+  // change of the variable sees it
+  const char* hold = std::getenv("BANDX_OUTPUT_HOLD_MS");
+  hold_ms_ = hold ? std::max(0L, std::atol(hold)) : 2000L;
   std::vector<size_t> stride(tensors.size(), 0);
   if (a.alloc && a.free) {
     block_free_ = a.free;
@@ -238,12 +242,18 @@ void TensorRingBuffer::Release(int handle) {
   slot_cv_.notify_all();  // waiters may need different slot counts
 }
 
+bool TensorRingBuffer::TryAcquireForWrite(int handle) {
+  if (handle < 0) return true;
+  std::lock_guard<std::mutex> lock(head_mtx_);
+  const int s = Slot(handle);
+  if (held_[s] && owner_[s] != handle) return false;
+  owner_[s] = handle;
+  return true;
+}
+
 bool TensorRingBuffer::AcquireForWrite(int handle) {
   if (handle < 0) return true;
-  static const long hold_ms = [] {
-    const char* e = std::getenv("BANDX_OUTPUT_HOLD_MS");
-    return e ? std::max(0L, std::atol(e)) : 2000L;
-  }();
+  const long hold_ms = hold_ms_;
   std::unique_lock<std::mutex> lock(head_mtx_);
   const int s = Slot(handle);
   if (!slot_cv_.wait_for(lock, std::chrono::milliseconds(hold_ms),

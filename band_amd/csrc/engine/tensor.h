@@ -106,6 +106,8 @@ class TensorRingBuffer {
   // (false, a warning is logged) and the newer job fails its output copy;
   // the held outputs stay intact.
   bool AcquireForWrite(int handle);
+  // the same without waiting: false when the slot is held right now
+  bool TryAcquireForWrite(int handle);
   void Hold(int handle);
   void Unhold(int handle);
   int size() const { return size_; }
@@ -136,6 +138,7 @@ class TensorRingBuffer {
   std::vector<char> busy_;  // per slot: taken by AllocBlocking[N], not yet released
   std::vector<int> owner_;  // per slot: handle whose outputs it holds (-1: none)
   std::vector<char> held_;  // per slot: the owner's outputs are being read
+  long hold_ms_ = 2000;     // AcquireForWrite's bound (BANDX_OUTPUT_HOLD_MS at construction)
   // per tensor: one page-locked block holding every slot's bytes at a fixed
   // stride (consecutive handles are adjacent, so a batched pass copies a
   // run of them in one DMA); empty when the ring has no host allocator

@@ -142,6 +142,8 @@ _abi.BACKEND_SYMBOLS.update({
     "BandxBenchmarkRun": (c_size_t, [c_char_p, c_char_p, c_size_t]),
     "BandxEngineRunClosedLoop": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
                                          POINTER(c_double), POINTER(c_int), POINTER(c_double)]),
+    "BandxEngineRunClosedLoopEx": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_int,
+                                           POINTER(c_double), POINTER(c_int), POINTER(c_int), POINTER(c_double)]),
     "BandxEngineRunPoisson": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_void_p), c_int, c_int, c_double, c_uint64,
                                       c_int, POINTER(c_double), POINTER(c_int), POINTER(c_int), POINTER(c_double)]),
 })
@@ -428,22 +430,27 @@ class Engine:
     def GetExpectedLatency(self, model, worker_id, unit_mask):
         return int(self.lib.BandxEngineGetExpectedLatency(self.handle, model.handle, worker_id, unit_mask))
 
-    def RunClosedLoop(self, models, n_jobs, max_inflight, inputs=None):
-        """Native closed-loop driver (BandxEngineRunClosedLoop): n_jobs requests
-        round-robin over `models`, <= max_inflight outstanding.  Returns
-        (latency_us array, worker id array, wall seconds)."""
+    def RunClosedLoop(self, models, n_jobs, max_inflight, inputs=None, with_models=False):
+        """Native closed-loop driver (BandxEngineRunClosedLoopEx): n_jobs
+        requests round-robin over `models`, <= max_inflight outstanding.
+        Returns (latency_us array, worker id array, wall seconds), with the
+        model index of every job before the wall time when with_models."""
         ms = (c_void_p * len(models))(*[m.handle.value for m in models])
         ins = None
         if inputs is not None:
             ins = (c_void_p * len(models))(*[t.handle.value if t is not None else None for t in inputs])
         lat = np.zeros(max(n_jobs, 1), np.float64)
         wid = np.zeros(max(n_jobs, 1), np.int32)
+        mid = np.zeros(max(n_jobs, 1), np.int32)
         wall = c_double(0)
-        rc = self.lib.BandxEngineRunClosedLoop(self.handle, ms, ins, len(models), int(n_jobs), int(max_inflight),
-                                               lat.ctypes.data_as(POINTER(c_double)),
-                                               wid.ctypes.data_as(POINTER(c_int)), ctypes.byref(wall))
+        rc = self.lib.BandxEngineRunClosedLoopEx(self.handle, ms, ins, len(models), int(n_jobs), int(max_inflight),
+                                                 lat.ctypes.data_as(POINTER(c_double)),
+                                                 wid.ctypes.data_as(POINTER(c_int)),
+                                                 mid.ctypes.data_as(POINTER(c_int)), ctypes.byref(wall))
         if rc != kBandOk:
             raise _abi.BandHipError("BandxEngineRunClosedLoop: a job failed")
+        if with_models:
+            return lat[:n_jobs], wid[:n_jobs], mid[:n_jobs], wall.value
         return lat[:n_jobs], wid[:n_jobs], wall.value
 
     def RunPoisson(self, models, n_jobs, rate_per_s, seed=5489, max_inflight=64, inputs=None):

@@ -533,6 +533,7 @@ def thread_cpu():
 HOST_THREADS = {}
 HOST_THREAD_STATES = {}
 COALESCE = {}  # backend job coalescing over the last timed loop (coalescer.h)
+LAST_MODEL_IDX = []  # the model index of every job of the last timed closed loop (driver-reported)
 
 
 def cgroup_cpu_stat():
@@ -628,8 +629,10 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     except Exception:  # the CPU-only stand-in runs have no HIP library loaded
         coalesce = None
     t0 = time.perf_counter()
-    lat_us, worker_ids, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs)
+    lat_us, worker_ids, model_idx, _ = engine.RunClosedLoop(band_models, n_timed, inflight, inputs,
+                                                            with_models=True)
     t1 = time.perf_counter()
+    LAST_MODEL_IDX[:] = [int(v) for v in model_idx]
     COALESCE.clear()
     if coalesce:
         cs = coalesce()
@@ -699,7 +702,7 @@ def run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D):
     return D.max(t1 - t0), lat_us, worker_ids
 
 
-def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
+def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed, names=()):
     """ONE Band engine over n_gpus GPUs in this process: W GPU workers per GPU,
     worker w on GPU w % n_gpus (so round_robin's rotation alternates GPUs),
     one planner thread (band/engine.cc:681-713, band/planner.cc:268-293)"""
@@ -734,6 +737,7 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
         e, bm, ins = make_engine(args, D, paths, sched, [flag] * n_workers, 0, n_workers, args.job_batch)
         inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
         el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
+        per_model = per_model_latency(lat, list(names), len(bm), LAST_MODEL_IDX)
         e.close()
     finally:
         for k, v in saved.items():
@@ -753,17 +757,18 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed):
             "ms_per_step": el * 1e3 / max(1, n_timed // args.jobs_per_step),
             "workers": n_workers, "worker_to_gpu": "w %% %d" % n_gpus, "jobs_per_gpu": per_gpu,
             "p50_job_latency_ms": float(np.percentile(lat * 1e-3, 50)),
-            "p99_job_latency_ms": float(np.percentile(lat * 1e-3, 99))}
+            "p99_job_latency_ms": float(np.percentile(lat * 1e-3, 99)),
+            "job_latency_ms_per_model": per_model}
 
 
-def per_model_latency(lat_us, names, n_models, burst=4):
-    """rank 0's p50 / p99 job latency per model of the closed loop: job j is
-    a request for model (j / burst) % n_models (BandxEngineRunClosedLoop,
-    band_amd/csrc/engine/c_api.cc)"""
+def per_model_latency(lat_us, names, n_models, model_idx):
+    """rank 0's p50 / p99 job latency per model of the closed loop, keyed on
+    the model index the driver reports for every job
+    (BandxEngineRunClosedLoopEx, band_amd/csrc/engine/c_api.cc)"""
     lat = np.asarray(lat_us) * 1e-3
-    if n_models < 1 or lat.size == 0:
+    mid = np.asarray(model_idx)
+    if n_models < 1 or lat.size == 0 or mid.size != lat.size:
         return None
-    mid = (np.arange(lat.size) // burst) % n_models
     out = {}
     for m in range(n_models):
         v = lat[mid == m]
@@ -846,7 +851,7 @@ def main():
         # headline: one process, one engine over all --gpus GPUs
         assert D.world == 1, "--single-engine runs in one process (no torchrun)"
         single = single_engine_line(args, D, paths, sched, args.single_engine_wpg or W, max(1, args.gpus), n_warm,
-                                    n_timed)
+                                    n_timed, names=[m[0] for m in models])
         elapsed, lat_us, worker_ids = n_timed / single["value"], None, []
         jobs_per_worker = single["jobs_per_gpu"]
         subgraph_jobs = None
@@ -910,17 +915,19 @@ def main():
     if D.world == 1 and W != 1 and not args.no_single_engine and not poisson and on_gpu and batching:
         # N = 1: the headline engine IS the single engine; north_star's one
         # GPU worker per GPU (worker_device_queue) is measured beside it
-        single_1wpg = single_engine_line(args, D, paths, sched, 1, 1, n_warm, n_timed)
+        single_1wpg = single_engine_line(args, D, paths, sched, 1, 1, n_warm, n_timed, names=[m[0] for m in models])
     if D.world > 1 and not args.no_single_engine and not poisson:
         D.barrier()  # every rank has closed its engines
         if D.rank == 0:
             try:
-                single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world)
+                single = single_engine_line(args, D, paths, sched, W, D.world, n_warm, n_timed * D.world,
+                                            names=[m[0] for m in models])
             except Exception as ex:  # the per-process line stays the headline
                 single = {"error": repr(ex)}
                 print("bench: single-engine line failed: %r" % (ex,), file=sys.stderr, flush=True)
             if W != 1 and "error" not in single:
-                single_1wpg = single_engine_line(args, D, paths, sched, 1, D.world, n_warm, n_timed * D.world)
+                single_1wpg = single_engine_line(args, D, paths, sched, 1, D.world, n_warm, n_timed * D.world,
+                                                  names=[m[0] for m in models])
         D.barrier()
 
     roof, dev = None, None
@@ -999,8 +1006,9 @@ def main():
             single["p50_job_latency_ms"],
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
             single["p99_job_latency_ms"],
-            "job_latency_ms_per_model": per_model_latency(lat_us, [m[0] for m in models], M)
-            if lat_us is not None and not poisson else None,
+            "job_latency_ms_per_model": single.get("job_latency_ms_per_model") if single and "value" in single else
+            (per_model_latency(lat_us, [m[0] for m in models], M, LAST_MODEL_IDX)
+             if lat_us is not None and not poisson else None),
             "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
             "gpu_kernel_us_per_inference_at_mean_pass": dev.get("gpu_us_per_inference_at_mean_pass") if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,

@@ -262,6 +262,11 @@ BAND_CAPI_EXPORT BandStatus BandxEngineRequestsAsync(BandEngine* engine, BandMod
 BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoop(BandEngine* engine, BandModel** models, BandTensor** inputs,
                                                      int n_models, int n_jobs, int max_inflight, double* latency_us,
                                                      int* worker_ids, double* wall_s);
+/* the same, and model_index[j] = the index into `models` of job j (may be
+ * NULL): the per-model statistics key on it, not on an assumed burst */
+BAND_CAPI_EXPORT BandStatus BandxEngineRunClosedLoopEx(BandEngine* engine, BandModel** models, BandTensor** inputs,
+                                                       int n_models, int n_jobs, int max_inflight, double* latency_us,
+                                                       int* worker_ids, int* model_index, double* wall_s);
 
 /* Open-loop Poisson driver (BASELINE config C5): n_jobs arrivals with
  * exponential inter-arrival times at rate_per_s (all models together, seeded

@@ -100,7 +100,10 @@ int bhx_ring_page_nodes(long long* bytes_per_node, int cap);
  * concurrent ExecuteSubgraph calls of one model on one GPU run as job-batch
  * passes): out[0] calls, out[1] passes that ran one job alone, out[2]
  * passes of >= 2 jobs, out[3] jobs in those passes, out[4] the largest such
- * pass.  reset != 0 zeroes the totals after reading them. */
+ * pass, out[5] calls that ran with coalescing off (no lanes: a lone
+ * executor's model, or a failed lane build) and out[6] the most such calls
+ * running at once (out must hold 7).  reset != 0 zeroes the totals after
+ * reading them. */
 int bhx_coalescer_stats(long long* out, int reset);
 /* members and lanes-ready flag of the coalescer executor `e`'s whole-model
  * subgraph joined (0 / 0 when it joined none) */

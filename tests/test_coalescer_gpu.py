@@ -154,3 +154,61 @@ def test_engine_one_job_per_pass_coalesced_bit_exact(gpu_lib, monkeypatch, sync)
     assert s["calls"] >= n_sub * per, s
     assert s["group_jobs"] > 0, s
     e.close()
+
+
+def test_failed_lane_build_turns_coalescing_off(gpu_lib, monkeypatch):
+    """A lane build that fails (as out of device memory would) leaves
+    coalescing OFF: every call runs its own executor's pass at once, several
+    at a time (no lane token caps them), bit-exact with the oracle."""
+    monkeypatch.setenv("BAND_HIP_COALESCE", "4")
+    monkeypatch.setenv("BAND_HIP_COALESCE_FAIL_BUILD", "1")
+    buf = tflite_synth.mobilenet_v2(np.int8, size=96)
+    om = OModel(buf)
+    t_in = om.tensors[om.inputs[0]]
+    rng = np.random.default_rng(17)
+    xs = [rng.integers(-128, 128, t_in.shape).astype(np.int8) for _ in range(3)]
+    refs = [OracleInterpreter(om).run({om.inputs[0]: x}) for x in xs]
+    mid = 33
+    m = HipModel(mid)
+    assert m.FromBuffer(buf).ok()
+    W = 6
+    execs = []
+    for w in range(W):
+        SetWorkerDevice(140 + w, 0)
+        ex = HipModelExecutor(mid, 140 + w, DeviceFlag.kGPU)
+        assert ex.PrepareSubgraph(m).ok()
+        execs.append((ex, SubgraphKey(mid, 140 + w)))
+    for ex, _ in execs:
+        assert ex.Coalescer() == (W, False)
+    CoalescerStats(reset=True)
+    rounds = 6
+    barrier = threading.Barrier(W)
+    errors = []
+
+    def run(tid):
+        ex, key = execs[tid]
+        try:
+            for r in range(rounds):
+                k = (tid + r) % len(xs)
+                ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[k]
+                barrier.wait(timeout=60)
+                assert ex.ExecuteSubgraph(key).ok()
+                for o in om.outputs:
+                    got = ex.GetTensorView(key, o).GetData()
+                    np.testing.assert_array_equal(got, refs[k][o].reshape(got.shape))
+        except BaseException as e:  # noqa: BLE001 - reported below
+            errors.append(e)
+            barrier.abort()
+
+    ths = [threading.Thread(target=run, args=(t,)) for t in range(W)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in ths)
+    if errors:
+        raise errors[0]
+    s = CoalescerStats()
+    assert s["calls"] == W * rounds and s["bypass_calls"] == W * rounds, s
+    assert s["group_passes"] == 0, s
+    assert s["max_bypass_inflight"] >= 2, s

@@ -287,7 +287,9 @@ void AppendTuneFileLocked(const std::string& key, int tile) {
 // bumped whenever a chain form's LDS layout or parameter rules change, so a
 // tune file written by an older kernel tree is not replayed against this one
 // (11: column-reuse depthwise phase, every raster form re-measured)
-constexpr int kChainTuneVersion = 11;
+constexpr int kChainTuneVersion = 12;
+// chain choices from here up name a stage form (FuseChains)
+constexpr int kStageChoice = 100000;
 
 std::string IrbKey(int ordinal, const bh_irb_params& q) {
   char buf[256];
@@ -549,12 +551,22 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // = px_blocks of the 2-launch form (the second conv stays a launch),
     // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
-    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d", kChainTuneVersion, ordinal_,
+    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d%d", kChainTuneVersion, ordinal_,
                   tune_batch_ > 0 ? tune_batch_ : D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
                   ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0, no_tile_chain_, no_deep_chain_,
-                  no_split_chain_, no_valu_chain_);
+                  no_split_chain_, no_valu_chain_, no_stage_chain_);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
+    if (force_stage_chain_ && ok3) {
+      bh_chain_params q = c3;
+      q.px_blocks = 1;
+      q.waves = 8;
+      q.c_split = 2;
+      q.stage = 1;
+      if (bh_chain_lds_bytes(&q) > 0) choice = kStageChoice + 2 * 100 + 1 * 10 + 1;  // 1 block, 8 waves, 2 slices
+      q.stage = 2;
+      if (bh_chain_lds_bytes(&q) > 0) choice += 1000;  // ... with loader waves
+    }
     if (force_tile_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
       q.tile = tile_pipe_ ? 2 : 1;
@@ -615,6 +627,32 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             {1, 4, 0, 0, 0, 3, 0}, {1, 8, 0, 0, 0, 3, 0}, {1, 4, 0, 0, 0, 4, 0},
             {4, 4, 0, 0, 0, 0, 1}, {2, 4, 0, 0, 0, 0, 1}, {1, 4, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 0, 1},
             {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}};
+        // the stage forms (3-launch only): {px_blocks, waves, phase-C slices,
+        // stage (2: loader waves)}
+        const int stage_forms[16][4] = {{1, 4, 0, 1}, {1, 8, 0, 1}, {2, 4, 0, 1}, {2, 8, 0, 1}, {1, 8, 2, 1},
+                                        {2, 8, 2, 1}, {1, 8, 4, 1}, {1, 8, 8, 1}, {1, 8, 0, 2}, {2, 8, 0, 2},
+                                        {1, 4, 0, 2}, {1, 8, 2, 2}, {2, 8, 2, 2}, {1, 8, 3, 2}, {1, 8, 4, 2},
+                                        {1, 8, 8, 2}};
+        for (const auto& sf : stage_forms) {
+          if (no_stage_chain_ || !ok3 || !measured) break;
+          bh_chain_params q = c3;
+          q.px_blocks = sf[0];
+          q.waves = sf[1];
+          q.c_split = sf[2];
+          q.stage = sf[3];
+          if (bh_chain_lds_bytes(&q) == 0 || !PackChainTile(&q, sg)) continue;
+          Launch F;
+          F.kind = Launch::kChain;
+          F.chain = q;
+          const double us = TimeLaunches({&F}, 10);
+          if (tune_log)
+            std::fprintf(stderr, "[chain-tune]   form3 stage%d px%d w%d split%d: %.2f\n", sf[3], sf[0], sf[1], sf[2],
+                         us);
+          if (us > 0 && us < best) {
+            best = us;
+            choice = kStageChoice + (sf[3] - 1) * 1000 + sf[2] * 100 + sf[0] * 10 + (sf[1] == 8 ? 1 : 0);
+          }
+        }
         for (const auto& pw : forms) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
@@ -663,7 +701,19 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
     // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
     // tiles, +1000 for the deep-issue form, +2000 x (s - 1) for the s-way
-    // phase-C split, +8000 for the VALU depthwise phase
+    // phase-C split, +8000 for the VALU depthwise phase; the stage form is
+    // kStageChoice + 1000 x (stage - 1) + 100 x slices + 10 x px_blocks + (8 waves)
+    int stage = choice >= kStageChoice ? 1 : 0;
+    int stage_split = 0, stage_px = 1, stage_waves = 4;
+    if (stage) {
+      int c = choice - kStageChoice;
+      stage = 1 + c / 1000;
+      c %= 1000;
+      stage_split = c / 100;
+      stage_px = (c / 10) % 10;
+      stage_waves = c % 10 ? 8 : 4;
+      choice = 1;  // a 3-launch form
+    }
     const int dw_valu = choice >= 8000 ? 1 : 0;
     choice %= 8000;
     const int c_split = choice >= 2000 ? choice / 2000 + 1 : 0;
@@ -686,14 +736,20 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.deep = deep;
     F.chain.c_split = c_split;
     F.chain.dw_valu = dw_valu;
+    if (stage) {
+      F.chain.px_blocks = stage_px;
+      F.chain.waves = stage_waves;
+      F.chain.c_split = stage_split;
+      F.chain.stage = stage;
+    }
     // a choice read from a tune file written by another kernel tree may name
     // a form these parameters do not admit: keep the unfused launches then
-    if (bh_chain_lds_bytes(&F.chain) == 0 || (F.chain.tile && !PackChainTile(&F.chain, sg))) {
+    if (bh_chain_lds_bytes(&F.chain) == 0 || ((F.chain.tile || F.chain.stage) && !PackChainTile(&F.chain, sg))) {
       out.push_back(L[i]);
       continue;
     }
     F.out_tensor = three ? P2->out_tensor : P1.out_tensor;
-    F.kernel = F.chain.tile ? "chain_tile_kernel" : "chain_kernel";
+    F.kernel = F.chain.stage ? "chain_stage_kernel" : (F.chain.tile ? "chain_tile_kernel" : "chain_kernel");
     const bh_dwconv_params& dw = F.chain.dw;
     const bh_conv_params& a = F.chain.pw1;
     const double px = static_cast<double>(dw.batch) * dw.out_h * dw.out_w;

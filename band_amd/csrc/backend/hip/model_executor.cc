@@ -305,6 +305,8 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
   if (f && std::strcmp(f, "nostem") == 0) no_stem_chain_ = true;  // A-B: the stem stays its own launch
   if (f && std::strcmp(f, "forcestem") == 0) force_chain_ = force_tile_chain_ = force_stem_chain_ = true;  // parity
+  if (f && std::strcmp(f, "forcestage") == 0) force_chain_ = force_stage_chain_ = true;  // parity: ... stage form
+  if (f && std::strcmp(f, "nostage") == 0) no_stage_chain_ = true;  // A-B: without the stage forms
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
   if (at && at[0] == '0') autotune_ = false;
   return absl::OkStatus();

@@ -282,6 +282,8 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form
   bool no_stem_chain_ = false;     // BAND_HIP_FUSION=nostem: the RGB stem stays its own launch
   bool force_stem_chain_ = false;  // BAND_HIP_FUSION=forcestem: tile chains, the stem fused wherever it fits
+  bool force_stage_chain_ = false; // BAND_HIP_FUSION=forcestage: every chain the stage form takes, in it (parity)
+  bool no_stage_chain_ = false;    // BAND_HIP_FUSION=nostage: the tuner skips the stage forms
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model
   std::map<SubgraphKey, std::unique_ptr<PreparedSubgraph>> subgraphs_;
   int ordinal_ = -1;

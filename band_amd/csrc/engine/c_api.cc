@@ -100,6 +100,7 @@ absl::Status Validate(const band::RuntimeConfig& c) {
   for (int t : w.num_threads)
     if (t < 0) return absl::InvalidArgumentError("[WorkerConfigBuilder] num_threads_[i] >= 0");
   if (w.max_job_batch < 1) return absl::InvalidArgumentError("max_job_batch >= 1");
+  if (w.pass_target_us < 0) return absl::InvalidArgumentError("pass_target_us >= 0");
   if (w.availability_check_interval_ms <= 0)
     return absl::InvalidArgumentError("[WorkerConfigBuilder] availability_check_interval_ms_ > 0");
   if (c.subgraph_config.minimum_subgraph_size <= 0)
@@ -179,6 +180,7 @@ void BandAddConfig(BandConfigBuilder* b, int field, int count, ...) {
     case BAND_RESOURCE_MONITOR_INTERVAL_MS: (void)va_arg(vl, int); break;
     case BAND_RESOURCE_MONITOR_LOG_PATH: (void)va_arg(vl, const char*); break;
     case BANDX_WORKER_MAX_JOB_BATCH: c.worker_config.max_job_batch = va_arg(vl, int); break;
+    case BANDX_WORKER_PASS_TARGET_US: c.worker_config.pass_target_us = va_arg(vl, int); break;
     case BANDX_PROFILE_SHARE_IDENTICAL: c.profile_config.share_identical_workers = va_arg(vl, int) != 0; break;
     default: BAND_LOG(LogSeverity::kWarning, "unknown config field %d", field);
   }

@@ -44,6 +44,10 @@ struct WorkerConfig {
   // many queued whole-model jobs of one subgraph as one batched pass when
   // the executor implements interface::IJobBatching.  1 = Band's behaviour.
   int max_job_batch = 1;
+  // Extension: the pass-size policy of job batching (Engine::MaxJobBatch):
+  // a batched pass of a model takes at most the jobs whose expected pass
+  // time fits this target in microseconds (0 = off: up to max_job_batch).
+  int pass_target_us = 0;
 };
 
 struct SubgraphConfig {

@@ -60,6 +60,7 @@ absl::Status Engine::Init(const RuntimeConfig& config) {
   }
   const bool global = planner_->GetWorkerType() == static_cast<int>(WorkerType::kGlobalQueue);
   max_job_batch_ = std::max(1, config.worker_config.max_job_batch);
+  pass_target_us_ = std::max(0, config.worker_config.pass_target_us);
   rotate_ties_ = config.profile_config.share_identical_workers;
   for (DeviceFlag flag : config.worker_config.workers) {
     if (!valid.count(flag)) {
@@ -147,6 +148,18 @@ absl::Status Engine::RegisterModel(Model* model) {
           if (!bs.ok())
             BAND_LOG(LogSeverity::kWarning, "model %d runs unbatched on worker %d: %s", model_id, def.worker_id,
                      bs.message().c_str());
+          else if (pass_target_us_ > 0) {
+            bool have;
+            {
+              std::lock_guard<std::mutex> lock(pass_mu_);
+              have = pass_cap_.count(model_id) != 0;
+            }
+            if (!have) {
+              const int cap = PassCap(jb, key);
+              std::lock_guard<std::mutex> lock(pass_mu_);
+              pass_cap_[model_id] = cap;
+            }
+          }
         }
       }
       unit_subgraphs_to_subgraph_keys_[model_id][*def.unit_subgraph_indices.begin()]
@@ -794,7 +807,32 @@ absl::Status Engine::CopyOutputs(const Job& job, const ViewFn& view) {
 int Engine::MaxJobBatch(const SubgraphKey& key) const {
   if (max_job_batch_ <= 1) return 1;
   auto* jb = dynamic_cast<const hip::IJobBatching*>(GetModelExecutor(key));
-  return jb ? jb->MaxJobBatch(key) : 1;
+  const int n = jb ? jb->MaxJobBatch(key) : 1;
+  if (pass_target_us_ <= 0) return n;
+  std::lock_guard<std::mutex> lock(pass_mu_);
+  auto cap = pass_cap_.find(key.GetModelId());
+  return cap == pass_cap_.end() ? n : std::min(n, cap->second);
+}
+
+// The pass-size policy (WorkerConfig::pass_target_us): the model's largest
+// batch variant is timed once (best of 3 passes after one warm-up, inputs
+// whatever the slots hold), the pass time taken as linear in the jobs, and
+// the batch capped where it reaches the target.  A model whose full pass
+// is 2x the target then runs half-size passes: its jobs no longer wait
+// behind the longest pass of the mix, which sets the job-latency tail.
+int Engine::PassCap(hip::IJobBatching* jb, const SubgraphKey& key) {
+  const int b = jb->MaxJobBatch(key);
+  if (b <= 1 || !jb->ExecuteJobBatch(key, b).ok()) return b;
+  int64_t best = INT64_MAX;
+  for (int i = 0; i < 3; ++i) {
+    const int64_t t0 = time::NowMicros();
+    if (!jb->ExecuteJobBatch(key, b).ok()) return b;
+    best = std::min(best, time::NowMicros() - t0);
+  }
+  const int cap = static_cast<int>(std::max<int64_t>(1, std::min<int64_t>(b, pass_target_us_ * b / std::max<int64_t>(1, best))));
+  BAND_LOG(LogSeverity::kInfo, "model %d: %d-job pass %lld us, pass target %d us -> at most %d jobs per pass",
+           key.GetModelId(), b, static_cast<long long>(best), pass_target_us_, cap);
+  return cap;
 }
 
 absl::Status Engine::TryCopyInputTensorsToSlot(const Job& job, int n, int slot) {

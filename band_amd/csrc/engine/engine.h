@@ -33,6 +33,9 @@
 #include "engine/worker.h"
 
 namespace band {
+namespace hip {
+class IJobBatching;
+}  // namespace hip
 
 using Tensors = std::vector<interface::ITensor*>;
 
@@ -164,6 +167,11 @@ class Engine : public IEngine {
 
   SubgraphConfig subgraph_config_;
   int max_job_batch_ = 1;
+  // pass-size policy (WorkerConfig::pass_target_us): model -> jobs per pass
+  int pass_target_us_ = 0;
+  std::map<ModelId, int> pass_cap_;  // written at RegisterModel, read by the planner / workers
+  mutable std::mutex pass_mu_;
+  int PassCap(hip::IJobBatching* jb, const SubgraphKey& key);
   // share_identical_workers: equal expected latencies break round-robin
   bool rotate_ties_ = false;
   mutable std::atomic<size_t> tie_rotation_{0};

@@ -61,6 +61,7 @@ class ConfigField(enum.IntEnum):  # band/c/c_api_type.h:145-166
     BAND_CPU_MASK = 16
     BANDX_WORKER_MAX_JOB_BATCH = 1000  # extension (include/band_c_api.h)
     BANDX_PROFILE_SHARE_IDENTICAL = 1001  # extension
+    BANDX_WORKER_PASS_TARGET_US = 1002  # extension: pass-size policy of job batching
 
 
 class JobStatus(enum.IntEnum):  # band/common.h:185-200
@@ -200,7 +201,8 @@ class Config:
 
 def make_config(schedulers, workers, num_threads=None, cpu_masks=None, window_size=None, online=True,
                 num_warmups=1, num_runs=1, smoothing=0.1, profile_path=None, log_path=None,
-                subgraph_type=None, minimum_subgraph_size=None, max_job_batch=None, share_identical=None):
+                subgraph_type=None, minimum_subgraph_size=None, max_job_batch=None, share_identical=None,
+                pass_target_us=None):
     b = ConfigBuilder()
     b.add(ConfigField.BAND_PLANNER_SCHEDULERS, *[int(s) for s in schedulers])
     b.add(ConfigField.BAND_WORKER_WORKERS, *[int(w) for w in workers])
@@ -224,6 +226,8 @@ def make_config(schedulers, workers, num_threads=None, cpu_masks=None, window_si
         b.add(ConfigField.BANDX_WORKER_MAX_JOB_BATCH, max_job_batch)
     if share_identical is not None:
         b.add(ConfigField.BANDX_PROFILE_SHARE_IDENTICAL, int(bool(share_identical)))
+    if pass_target_us:
+        b.add(ConfigField.BANDX_WORKER_PASS_TARGET_US, int(pass_target_us))
     return b.build()
 
 

@@ -108,6 +108,9 @@ def parse():
     p.add_argument("--job-batch", type=int, default=24,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
+    p.add_argument("--pass-target-us", type=int, default=0,
+                   help="pass-size policy of job batching (BANDX_WORKER_PASS_TARGET_US): a model's pass takes at "
+                        "most the jobs whose expected pass time fits this many microseconds (0 = off)")
     p.add_argument("--share-profiles", type=int, default=-1, choices=[-1, 0, 1],
                    help="BANDX_PROFILE_SHARE_IDENTICAL: identical workers share latency estimates; -1 (default) = "
                         "on for the latency-driven schedulers (SEL / HEFT: C4, C5), 0 = the reference's "
@@ -466,7 +469,8 @@ def make_engine(args, D, paths, sched, workers, n_cpu, W, job_batch, seed_offset
                                 num_threads=[args.cpu_threads] * n_cpu + [1 if on_gpu else args.cpu_threads] * W,
                                 num_warmups=3, num_runs=5,
                                 max_job_batch=job_batch if job_batch > 1 else None,
-                                share_identical=(args.share_profiles > 0) if args.share_profiles >= 0 else None))
+                                share_identical=(args.share_profiles > 0) if args.share_profiles >= 0 else None,
+                                pass_target_us=args.pass_target_us if job_batch > 1 else None))
     band_models, inputs = [], []
     rng = np.random.default_rng(5489 + seed_offset)
     for path in paths:
@@ -995,7 +999,7 @@ def main():
                        "step": "%d jobs (%d of each model), round-robin over the models" % (jps, jps // M),
                        "jobs_per_worker_rank0": jobs_per_worker,
                        "subgraph_jobs_per_worker_rank0": subgraph_jobs,
-                       "max_job_batch": args.job_batch,
+                       "max_job_batch": args.job_batch, "pass_target_us": args.pass_target_us,
                        "share_profiles": bool(args.share_profiles),
                        "model": args.model, "global_batch": n_ranks * W * max(1, args.job_batch), "seq_len": None,
                        "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus, n_ranks)) if one_engine

@@ -98,6 +98,11 @@ typedef enum BandConfigField {
   /* int: 1 = workers of one device kind (same device flag, thread count and
    * CPU mask: e.g. several GPU workers of one node) share latency estimates */
   BANDX_PROFILE_SHARE_IDENTICAL = 1001,
+  /* int, microseconds (default 0 = off): pass-size policy of job batching -
+   * a model's batched pass takes at most the jobs whose expected pass time
+   * stays within this target (its largest batch variant timed once at
+   * registration, pass time taken as linear in the jobs), at least 1 */
+  BANDX_WORKER_PASS_TARGET_US = 1002,
 } BandConfigField;
 
 typedef struct BandRequestOption {

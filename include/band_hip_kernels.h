@@ -417,16 +417,29 @@ typedef struct bh_chain_params {
    * the stem's output: the stem launch and its output tensor go away.
    * Read during the bh_chain_i8 / bh_chain_lds_bytes call only. */
   const void* stem;
+  /* 1: raster form with staged filters (chain_stage_kernel) - a workgroup of
+   * px_blocks (1 / 2) x 16 pixels and `waves` (4 / 8) waves starts with one
+   * burst of LDS-DMA of the first 1x1's filter and tables, its c_split slice
+   * (0 / 1 .. 8, grid.y) of the second 1x1's and the residual rows from
+   * tile_blob (bh_chain_tile_pack), runs the depthwise from global memory
+   * and both 1x1 GEMMs from LDS; has_pw2 only, pw2 K <= 320.  2: the same
+   * with the burst issued by the upper half of the waves while the lower
+   * half runs the depthwise phase */
+  int stage;
 } bh_chain_params;
 
 /* LDS bytes one workgroup of bh_chain_i8 needs (0 if unsupported) */
 size_t bh_chain_lds_bytes(const bh_chain_params* p);
+/* the stage form's share of bh_chain_lds_bytes / bh_chain_i8 (stage != 0) */
+size_t bh_chain_stage_lds_bytes(const bh_chain_params* p);
+int bh_chain_stage_launch(const bh_chain_params* p, bh_stream_t s);
 /* the tile form's share of bh_chain_lds_bytes / bh_chain_i8 (tile != 0) */
 size_t bh_chain_tile_lds_bytes(const bh_chain_params* p);
 int bh_chain_tile_launch(const bh_chain_params* p, bh_stream_t s);
-/* the tile form's constant block: its size for these parameters (as if
- * tile == 1; 0 if the form does not apply) and a device pass that builds it
- * from the params' filter / table pointers into `blob` */
+/* the tile / stage forms' constant block: its size for these parameters (as
+ * if tile == 1, or for the stage form when stage != 0; 0 if the form does not
+ * apply) and a device pass that builds it from the params' filter / table
+ * pointers into `blob` */
 size_t bh_chain_tile_blob_bytes(const bh_chain_params* p);
 int bh_chain_tile_pack(const bh_chain_params* p, void* blob, bh_stream_t s);
 int bh_chain_i8(const bh_chain_params* p, bh_stream_t s);

@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0, stage=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split, dw_valu)
+    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split, dw_valu, stage)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -175,7 +175,8 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu", "forcestem"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu", "forcestem",
+                        "forcestage"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param
@@ -200,9 +201,11 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
     assert ex.PrepareSubgraph(m).ok()
     key = SubgraphKey(41, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
-    assert "chain_kernel" in kernels or "chain_tile_kernel" in kernels, kernels
+    assert any(k in kernels for k in ("chain_kernel", "chain_tile_kernel", "chain_stage_kernel")), kernels
     if forcechain in ("forcetile", "forcetilepipe", "forcestem"):
         assert "chain_tile_kernel" in kernels, kernels
+    if forcechain == "forcestage" and arch != "posenet_mobilenet_v1":  # MobileNetV1: pairs, no second 1x1
+        assert "chain_stage_kernel" in kernels, kernels
     if forcechain == "forcestem":  # the RGB stem computed inside the first chain's tiles
         assert kernels[0] == "chain_tile_kernel" and not any(k.startswith("conv_stem") for k in kernels), kernels
     for rep in range(2):  # eager, then graph replay
@@ -239,6 +242,78 @@ def test_chain_split_phase_c(gpu_lib, h, ce, s, cout, res, ce2):
         _check(c, gpu_lib, px, waves, c_split=split)
     c.fast = False
     _check(c, gpu_lib, 1, 4, c_split=2)
+
+
+def _stage_fits(c, lib, px, waves, split):
+    import ctypes
+    keep = []
+    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, px, keep, waves, 0, 0, 0, split, 0, 1))) > 0
+
+
+@pytest.mark.parametrize("h,ce,s,cout,res,ce2", [c for c in MNV2_CHAINS if c[5]])
+def test_chain_stage_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
+    """the stage form (chain_stage_kernel): the first 1x1's filter, the
+    workgroup's slice of the second's and the residual rows staged by one
+    LDS-DMA burst, both GEMMs from LDS; 1 / 2 pixel blocks, 4 / 8 waves, 1-8
+    phase-C slices, batch 1 and a ragged batch 3, both requant forms"""
+    for b in (1, 3):
+        rng = np.random.default_rng(h * 31 + ce + cout + b)
+        c = ChainCase(rng, b, h, h, ce, s, cout, res, ce2, store_pw1=True if b == 3 else None)
+        ran = 0
+        for px, waves, split in ((1, 4, 0), (1, 8, 0), (2, 4, 0), (2, 8, 0), (1, 8, 2), (1, 4, 3), (2, 8, 4),
+                                 (1, 8, 8)):
+            if not _stage_fits(c, gpu_lib, px, waves, split):
+                continue
+            _check(c, gpu_lib, px, waves, c_split=split, stage=1)
+            _check(c, gpu_lib, px, waves, c_split=split, stage=2)  # loader waves
+            ran += 1
+        # LDS holds the whole first filter: only the 7x7 x 960 chains do not fit
+        assert ran or ce >= 960, "stage form should cover the %dx%dx%d chain" % (h, h, ce)
+        if ran:
+            c.fast = False
+            for px, waves, split in ((1, 8, 2), (2, 4, 0)):
+                if _stage_fits(c, gpu_lib, px, waves, split):
+                    _check(c, gpu_lib, px, waves, c_split=split, stage=1)
+                    _check(c, gpu_lib, px, waves, c_split=split, stage=2)
+
+
+@pytest.mark.parametrize("args", [
+    dict(b=2, h=14, w=14, ce=192, stride=1, cout=64, residual=True, ce2=192, dil=2),  # dilated
+    dict(b=3, h=9, w=13, ce=48, stride=1, cout=24, residual=True, ce2=96),          # ragged pixel tail
+    dict(b=1, h=11, w=10, ce=64, stride=2, cout=40, residual=False, ce2=128),       # N2 % 16 != 0 slices
+    dict(b=2, h=5, w=7, ce=16, stride=1, cout=8, residual=True, ce2=48),
+    dict(b=1, h=3, w=2, ce=16, stride=2, cout=4, residual=False, ce2=20),           # one partial block
+    dict(b=1, h=20, w=20, ce=96, stride=1, cout=40, residual=True, ce2=320),        # pw2 K 320 (KX 5)
+    dict(b=24, h=14, w=14, ce=384, stride=1, cout=64, residual=True, ce2=384),      # a batch-24 pass
+])
+def test_chain_stage_general(gpu_lib, args):
+    rng = np.random.default_rng(11 + sum(v for v in args.values() if isinstance(v, int)))
+    c = ChainCase(rng, store_pw1=True, **args)
+    for px, waves, split in ((1, 4, 0), (2, 8, 0), (1, 8, 2), (2, 4, 3), (1, 8, 8)):
+        if _stage_fits(c, gpu_lib, px, waves, split):
+            _check(c, gpu_lib, px, waves, c_split=split, stage=1)
+            _check(c, gpu_lib, px, waves, c_split=split, stage=2)
+
+
+def test_chain_stage_rejects(gpu_lib):
+    import ctypes
+    keep = []
+    c = ChainCase(np.random.default_rng(3), 1, 14, 14, 64, 1, 32, False, 64)
+    q = c.params(gpu_lib, 1, keep, 8, 0, 0, 0, 2, 0, 1)
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) > 0
+    for field, bad in (("px_blocks", 4), ("waves", 16), ("c_split", 9), ("deep", 1), ("dw_valu", 1), ("stage", 3)):
+        old = getattr(q, field)
+        setattr(q, field, bad)
+        assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0, field
+        setattr(q, field, old)
+    q.c_split = 5  # 64 channels = 4 tiles < 5 slices
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
+    q.c_split = 2
+    q.has_pw2 = 0  # the stage form always has the second 1x1
+    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
+    q.has_pw2 = 1
+    q.tile_blob = None
+    assert gpu_lib.bh_chain_i8(ctypes.byref(q), None) != 0  # no constant block: refused, nothing launched
 
 
 @pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)

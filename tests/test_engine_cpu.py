@@ -641,3 +641,35 @@ def test_batched_request_runs_as_one_assignment(tmp_path):
     assert sorted(j for j, _ in done) == sorted(hs) and all(s == 0 for _, s in done)
     assert e.UnsetOnEndRequest(cb) == kBandOk
     e.close()
+
+
+def test_pass_target_caps_batched_passes(tmp_path):
+    """the pass-size policy (BANDX_WORKER_PASS_TARGET_US): the model's 8-job
+    pass is timed at registration and later passes take at most the jobs
+    that fit the target - a 1 us target leaves one job per pass; results
+    stay bit-exact"""
+    from oracle.runner import OracleInterpreter
+    from oracle.tflite_fb import Model as OModel
+    path, buf = _slow_cpu_model(tmp_path)
+    e = Engine(make_config([SchedulerType.kRoundRobin], [DeviceFlag.kCPU], num_threads=[2], max_job_batch=8,
+                           pass_target_us=1))
+    m = Model()
+    assert m.FromPath(path)
+    assert e.RegisterModel(m)
+    om = OModel(buf)
+    rng = np.random.default_rng(13)
+    xs = [rng.integers(-128, 128, om.tensors[om.inputs[0]].shape).astype(np.int8) for _ in range(8)]
+    ins = [e.CreateInputTensor(m, 0) for _ in xs]
+    for t, x in zip(ins, xs):
+        t.data()[...] = x
+    passes0 = e.GetWorkerPhaseTimes(0)["passes"]
+    hs = e.RequestsAsync([m] * 8, [[t] for t in ins])
+    assert hs is not None and len(hs) == 8
+    e.WaitAll()
+    assert e.GetWorkerPhaseTimes(0)["passes"] - passes0 == 8  # the same burst ran as ONE pass without the policy
+    o = e.CreateOutputTensor(m, 0)
+    for h, x in zip(hs, xs):
+        assert e.Wait(h, [o]) == kBandOk
+        ref = OracleInterpreter(om).run({om.inputs[0]: x})[om.outputs[0]].reshape(-1)
+        np.testing.assert_array_equal(o.data().reshape(-1), ref)
+    e.close()

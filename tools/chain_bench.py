@@ -24,7 +24,8 @@ def main():
     ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,tp,1d,1w8d,2d",
                     help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form, "
                          "tp = its persistent double-buffered variant, t3 / t4 = runs of 2 / 4 tiles per workgroup; "
-                         "sN suffix = the phase-C split over N workgroups; v suffix = the VALU depthwise phase")
+                         "sN suffix = the phase-C split over N workgroups; v suffix = the VALU depthwise phase; "
+                         "g prefix = the stage form (g1w8s2: 1 pixel block, 8 waves, 2 slices)")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
     from band_amd import _abi
@@ -41,7 +42,11 @@ def main():
         c = ChainCase(np.random.default_rng(1), a.batch, h, h, ce, s, cout, res, ce2)
         row = []
         for form in a.px.split(","):
+            label = form
             split = 0
+            # "g1w8s2": the stage form, 1 block, 8 waves, 2 slices; "G": with loader waves (stage 2)
+            stage = 1 if form.startswith("g") else (2 if form.startswith("G") else 0)
+            form = form[1:] if stage else form
             valu = int(form.endswith("v"))
             form = form[:-1] if valu else form
             if "s" in form and not form.startswith("t"):  # "1s2": the phase-C split over 2 workgroups
@@ -52,7 +57,7 @@ def main():
             f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves, persist, tile, deep, split, valu)
+            q = c.params(lib, px, keep, waves, persist, tile, deep, split, valu, stage)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue
@@ -67,7 +72,7 @@ def main():
             ms = ctypes.c_float()
             lib.bh_event_elapsed_ms(e0, e1, ctypes.byref(ms))
             us = 1e3 * ms.value / a.iters
-            total[form + ("v" if valu else "")] = total.get(form + ("v" if valu else ""), 0.0) + us
+            total[label] = total.get(label, 0.0) + us
             row.append("%7.2f" % us)
         print("%3dx%-3d ce %4d s%d -> %3d%s -> %4d   %s" % (h, h, ce, s, cout, "+res" if res else "    ", ce2,
                                                            "  ".join(row)), flush=True)

@@ -90,7 +90,7 @@ class ChainParams(ctypes.Structure):
     _fields_ = [("dw", DwConvParams), ("pw1", ConvParams), ("pw2", ConvParams), ("has_pw2", c_int),
                 ("px_blocks", c_int), ("waves", c_int), ("persist", c_int), ("tile", c_int),
                 ("tile_blob", c_void_p), ("debug_stamps", c_void_p), ("deep", c_int), ("c_split", c_int),
-                ("dw_valu", c_int), ("stem", c_void_p), ("stage", c_int)]
+                ("stage", c_int)]
 
 
 # symbol -> (restype, argtypes)

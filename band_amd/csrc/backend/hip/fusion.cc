@@ -26,7 +26,7 @@ bool LaunchIo(const Launch& l, std::vector<const void*>* rd, std::vector<const v
       *wr = {l.dw.output};
       return true;
     case Launch::kChain:
-      *rd = {l.chain_stem ? l.conv.input : l.chain.dw.input, l.chain.pw1.residual};
+      *rd = {l.chain.dw.input, l.chain.pw1.residual};
       *wr = {l.chain.pw1.output, l.chain.has_pw2 ? l.chain.pw2.output : nullptr};
       return true;
     case Launch::kIrb:
@@ -551,11 +551,11 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     // = px_blocks of the 2-launch form (the second conv stays a launch),
     // +100 = 16 waves per workgroup, +200 = persistent form, +300 = 8 waves
     char key[256];
-    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d%d", kChainTuneVersion, ordinal_,
+    std::snprintf(key, sizeof(key), "ch%d:%d:%d:%dx%dx%d:s%dd%d:%d:%d:%d:%d:f%d%d%d%d", kChainTuneVersion, ordinal_,
                   tune_batch_ > 0 ? tune_batch_ : D.dw.batch, D.dw.in_h,
                   D.dw.in_w, D.dw.in_c, D.dw.stride_h, D.dw.dil_h, P1.conv.out_c, P1.conv.residual ? 1 : 0,
                   ok3 ? c3.pw2.out_c : 0, ok3 && c3.pw1.output ? 1 : 0, no_tile_chain_, no_deep_chain_,
-                  no_split_chain_, no_valu_chain_, no_stage_chain_);
+                  no_split_chain_, no_stage_chain_);
     int choice = force_chain_ ? (ok3 ? 4 : 14) : -1;
     if (force_stage_chain_ && ok3) {
       bh_chain_params q = c3;
@@ -569,14 +569,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     }
     if (force_tile_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
-      q.tile = tile_pipe_ ? 2 : 1;
-      if (bh_chain_lds_bytes(&q) > 0) choice += tile_pipe_ ? 500 : 400;
-    }
-    if (force_valu_chain_) {
-      bh_chain_params q = ok3 ? c3 : c2;
-      q.px_blocks = 4;
-      q.dw_valu = 1;
-      if (bh_chain_lds_bytes(&q) > 0) choice += 8000;
+      q.tile = 1;
+      if (bh_chain_lds_bytes(&q) > 0) choice += 400;
     }
     if (force_deep_chain_) {
       bh_chain_params q = ok3 ? c3 : c2;
@@ -609,24 +603,16 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
         // (filters in LDS, 64-pixel blocks walked by one wave of workgroups)
         // {.., tile}: the 2-D tile form (8 x 8 pixels, one LDS-DMA burst)
         // {.., deep}: the deep-issue raster forms
-        // (the persistent tile form, tile 2, measured slower than the
-        // one-tile workgroups on every MobileNetV2 chain,
-        // profiles/r03an_chain_bench_b24.txt: not a candidate; forcetilepipe)
         // {.., tile 3 / 4}: runs of 2 / 4 tiles per workgroup, the constant
         // block staged once per run
         // {.., split}: the second 1x1's channel tiles over 2..4 workgroups
         // per pixel block (3-launch form only; BAND_HIP_FUSION=nosplit: none)
-        // {.., valu}: the depthwise phase on VALU (v_dot4 over the tap
-        // table) instead of the block-diagonal MFMA tile (raster forms;
-        // BAND_HIP_FUSION=novalu: none)
-        const int forms[25][7] = {
-            {4, 4, 0, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0, 0},
-            {1, 16, 0, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0, 0}, {4, 4, 0, 1, 0, 0, 0}, {4, 4, 0, 3, 0, 0, 0},
-            {4, 4, 0, 4, 0, 0, 0}, {2, 4, 0, 0, 1, 0, 0}, {1, 4, 0, 0, 1, 0, 0}, {1, 8, 0, 0, 1, 0, 0},
-            {1, 4, 0, 0, 0, 2, 0}, {1, 8, 0, 0, 0, 2, 0}, {2, 4, 0, 0, 0, 2, 0}, {1, 16, 0, 0, 0, 2, 0},
-            {1, 4, 0, 0, 0, 3, 0}, {1, 8, 0, 0, 0, 3, 0}, {1, 4, 0, 0, 0, 4, 0},
-            {4, 4, 0, 0, 0, 0, 1}, {2, 4, 0, 0, 0, 0, 1}, {1, 4, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 0, 1},
-            {1, 16, 0, 0, 0, 0, 1}, {1, 8, 0, 0, 0, 2, 1}};
+        const int forms[19][6] = {
+            {4, 4, 0, 0, 0, 0}, {2, 4, 0, 0, 0, 0}, {1, 4, 0, 0, 0, 0}, {1, 8, 0, 0, 0, 0},
+            {1, 16, 0, 0, 0, 0}, {4, 4, 1, 0, 0, 0}, {4, 4, 0, 1, 0, 0}, {4, 4, 0, 3, 0, 0},
+            {4, 4, 0, 4, 0, 0}, {2, 4, 0, 0, 1, 0}, {1, 4, 0, 0, 1, 0}, {1, 8, 0, 0, 1, 0},
+            {1, 4, 0, 0, 0, 2}, {1, 8, 0, 0, 0, 2}, {2, 4, 0, 0, 0, 2}, {1, 16, 0, 0, 0, 2},
+            {1, 4, 0, 0, 0, 3}, {1, 8, 0, 0, 0, 3}, {1, 4, 0, 0, 0, 4}};
         // the stage forms (3-launch only): {px_blocks, waves, phase-C slices,
         // stage (2: loader waves)}
         const int stage_forms[16][4] = {{1, 4, 0, 1}, {1, 8, 0, 1}, {2, 4, 0, 1}, {2, 8, 0, 1}, {1, 8, 2, 1},
@@ -657,7 +643,6 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
           if (pw[3] && no_tile_chain_) continue;
           if (pw[4] && no_deep_chain_) continue;
           if (pw[5] && no_split_chain_) continue;
-          if (pw[6] && no_valu_chain_) continue;
           for (int form = 0; form < 2 && measured; ++form) {
             bh_chain_params q = form == 0 ? c3 : c2;
             if (form == 0 ? !ok3 : !ok2) continue;
@@ -667,7 +652,6 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             q.tile = pw[3];
             q.deep = pw[4];
             q.c_split = pw[5];
-            q.dw_valu = pw[6];
             if (pw[5] > 1 && form != 0) continue;
             if (bh_chain_lds_bytes(&q) == 0) continue;
             if (q.tile && !PackChainTile(&q, sg)) continue;
@@ -677,14 +661,13 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
             const double us = TimeLaunches({&F}, 10);
             const double total = us + (form == 1 && ok3 ? u_p2 : 0.0);
             if (tune_log)
-              std::fprintf(stderr, "[chain-tune]   form%d px%d w%d persist%d tile%d deep%d split%d valu%d: %.2f\n", 3 - form,
-                           pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], pw[6], total);
+              std::fprintf(stderr, "[chain-tune]   form%d px%d w%d persist%d tile%d deep%d split%d: %.2f\n", 3 - form,
+                           pw[0], pw[1], pw[2], pw[3], pw[4], pw[5], total);
             if (us > 0 && total < best) {
               best = total;
               choice = (form == 0 ? 0 : 10) + pw[0] + (pw[1] == 16 ? 100 : 0) + (pw[1] == 8 ? 300 : 0) +
-                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 2 ? 500 : 0) +
-                       (pw[3] == 3 ? 600 : 0) + (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) +
-                       (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0) + (pw[6] ? 8000 : 0);
+                       (pw[2] ? 200 : 0) + (pw[3] == 1 ? 400 : 0) + (pw[3] == 3 ? 600 : 0) +
+                       (pw[3] == 4 ? 700 : 0) + (pw[4] ? 1000 : 0) + (pw[5] > 1 ? 2000 * (pw[5] - 1) : 0);
             }
           }
         }
@@ -699,9 +682,8 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     }
     // choice: px_blocks, +10 for the 2-launch form, +100 for 16 waves,
     // +200 for the persistent form, +300 for 8 waves, +400 for the tile
-    // form, +500 for the persistent tile form, +600 / +700 for runs of 2 / 4
-    // tiles, +1000 for the deep-issue form, +2000 x (s - 1) for the s-way
-    // phase-C split, +8000 for the VALU depthwise phase; the stage form is
+    // form, +600 / +700 for runs of 2 / 4 tiles, +1000 for the deep-issue
+    // form, +2000 x (s - 1) for the s-way phase-C split; the stage form is
     // kStageChoice + 1000 x (stage - 1) + 100 x slices + 10 x px_blocks + (8 waves)
     int stage = choice >= kStageChoice ? 1 : 0;
     int stage_split = 0, stage_px = 1, stage_waves = 4;
@@ -714,8 +696,6 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       stage_waves = c % 10 ? 8 : 4;
       choice = 1;  // a 3-launch form
     }
-    const int dw_valu = choice >= 8000 ? 1 : 0;
-    choice %= 8000;
     const int c_split = choice >= 2000 ? choice / 2000 + 1 : 0;
     choice %= 2000;
     const int deep = choice >= 1000 ? 1 : 0;
@@ -735,7 +715,6 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
     F.chain.tile = choice >= 400 && choice < 800 ? choice / 100 - 3 : 0;
     F.chain.deep = deep;
     F.chain.c_split = c_split;
-    F.chain.dw_valu = dw_valu;
     if (stage) {
       F.chain.px_blocks = stage_px;
       F.chain.waves = stage_waves;
@@ -763,70 +742,11 @@ void HipModelExecutor::FuseChains(const HipModel& model, PreparedSubgraph* sg) {
       F.alg_ops += P2->alg_ops;
       if (!a.output) sg->fused_tensors.insert(P1.out_tensor);
     }
-    // the RGB stem into the tile form: the launch just before the chain
-    // produces the depthwise input and nothing else reads it
-    if (F.chain.tile == 1 && !no_stem_chain_ && !out.empty() && out.back().kind == Launch::kConv &&
-        out.back().conv.k_h == 3 && out.back().conv.k_w == 3 && out.back().conv.in_c == 3 &&
-        out.back().conv.output == F.chain.dw.input && private_tensor(out.back().out_tensor, D.op_index))
-      TryFuseStem(&out, &F, sg);
     out.push_back(F);
     sg->fused_tensors.insert(D.out_tensor);
     i += three ? 2 : 1;
   }
   sg->launches.swap(out);
-}
-
-// The RGB stem (out->back()) computed inside the tile chain F's workgroups
-// (bh_chain_params.stem): taken by on-device timing against the two
-// launches (> 2 %), cached per geometry; BAND_HIP_FUSION=forcestem always,
-// nostem never.
-void HipModelExecutor::TryFuseStem(std::vector<Launch>* out, Launch* F, PreparedSubgraph* sg) {
-  const Launch& S = out->back();
-  Launch Q = *F;
-  Q.chain_stem = true;
-  Q.conv = S.conv;
-  {
-    bh_chain_params q = Q.chain;
-    q.stem = &Q.conv;
-    if (bh_chain_lds_bytes(&q) == 0) return;
-  }
-  const bh_conv_params& st = S.conv;
-  char key[160];
-  std::snprintf(key, sizeof(key), "cs%d:%d:%d:%dx%d:s%d:%d:%d:%d", kChainTuneVersion, ordinal_,
-                tune_batch_ > 0 ? tune_batch_ : st.batch, st.in_h, st.in_w, st.stride_h, st.out_c, F->chain.pw1.out_c,
-                F->chain.has_pw2 ? F->chain.pw2.out_c : 0);
-  int fuse = force_stem_chain_ ? 1 : -1;
-  if (fuse < 0 && autotune_) {
-    std::lock_guard<std::mutex> lk(g_tune_mu);
-    LoadTuneFileLocked();
-    auto it = g_tune.find(key);
-    if (it != g_tune.end()) fuse = it->second;
-  }
-  if (fuse < 0) {
-    fuse = 0;
-    if (autotune_) {
-      const double u = TimeLaunches({&S, F}, 10);
-      const double f = TimeLaunches({&Q}, 10);
-      if (u > 0 && f > 0 && f < 0.98 * u) fuse = 1;
-      if (std::getenv("BAND_HIP_TUNE_LOG"))
-        std::fprintf(stderr, "[chain-tune] %s stem + chain %.2f, fused %.2f -> %d\n", key, u, f, fuse);
-      std::lock_guard<std::mutex> lk(g_tune_mu);
-      if (!g_tune.count(key)) AppendTuneFileLocked(key, fuse);
-      g_tune[key] = fuse;
-    }
-  }
-  if (!fuse) return;
-  // algorithmic bytes: the image and the stem's filter / tables instead of
-  // the depthwise input
-  const bh_dwconv_params& dw = F->chain.dw;
-  Q.alg_bytes = F->alg_bytes - static_cast<double>(dw.batch) * dw.in_h * dw.in_w * dw.in_c +
-                static_cast<double>(st.batch) * st.in_h * st.in_w * st.in_c +
-                static_cast<double>(st.out_c) * st.k_pad + 12.0 * st.out_c;
-  Q.alg_ops = F->alg_ops + S.alg_ops;
-  Q.op_index = S.op_index;
-  sg->fused_tensors.insert(S.out_tensor);
-  out->pop_back();
-  *F = Q;
 }
 
 namespace {

@@ -292,19 +292,10 @@ absl::Status HipModelExecutor::EnsureMeta(const HipModel& model) {
   if (f && std::strcmp(f, "nogroup") == 0) allow_group_ = false;
   if (f && std::strcmp(f, "forcechain") == 0) force_chain_ = true;  // parity tests: every feasible chain
   if (f && std::strcmp(f, "forcetile") == 0) force_chain_ = force_tile_chain_ = true;  // ... in the tile form
-  if (f && std::strcmp(f, "forcetilepipe") == 0) {  // ... in the persistent tile form
-    force_chain_ = force_tile_chain_ = true;
-    tile_pipe_ = true;
-  }
   if (f && std::strcmp(f, "notile") == 0) no_tile_chain_ = true;  // A-B: the raster chain forms only
   if (f && std::strcmp(f, "nodeep") == 0) no_deep_chain_ = true;  // A-B: without the deep-issue forms
   if (f && std::strcmp(f, "nosplit") == 0) no_split_chain_ = true;  // A-B: without the phase-C split forms
-  if (f && std::strcmp(f, "novalu") == 0) no_valu_chain_ = true;  // A-B: depthwise phase on MFMA only
-  if (f && std::strcmp(f, "r4forms") == 0) no_split_chain_ = no_valu_chain_ = true;  // A-B: round 4's form set
-  if (f && std::strcmp(f, "forcevalu") == 0) force_chain_ = force_valu_chain_ = true;  // parity: ... VALU depthwise
   if (f && std::strcmp(f, "forcedeep") == 0) force_deep_chain_ = true;  // parity tests: deep form wherever it fits
-  if (f && std::strcmp(f, "nostem") == 0) no_stem_chain_ = true;  // A-B: the stem stays its own launch
-  if (f && std::strcmp(f, "forcestem") == 0) force_chain_ = force_tile_chain_ = force_stem_chain_ = true;  // parity
   if (f && std::strcmp(f, "forcestage") == 0) force_chain_ = force_stage_chain_ = true;  // parity: ... stage form
   if (f && std::strcmp(f, "nostage") == 0) no_stage_chain_ = true;  // A-B: without the stage forms
   const char* at = std::getenv("BAND_HIP_AUTOTUNE");
@@ -584,15 +575,7 @@ absl::Status HipModelExecutor::EnqueueLaunch(const Launch& l) {
     case Launch::kEltwise: rc = bh_eltwise_i8(&l.elt, stream_); break;
     case Launch::kPool: rc = bh_pool_i8(&l.pool, stream_); break;
     case Launch::kIrb: rc = bh_irb_i8(&l.irb, stream_); break;
-    case Launch::kChain:
-      if (l.chain_stem) {
-        bh_chain_params q = l.chain;
-        q.stem = &l.conv;
-        rc = bh_chain_i8(&q, stream_);
-      } else {
-        rc = bh_chain_i8(&l.chain, stream_);
-      }
-      break;
+    case Launch::kChain: rc = bh_chain_i8(&l.chain, stream_); break;
     case Launch::kConvGroup: rc = bh_conv_group_i8(&l.cgroup, stream_); break;
     case Launch::kCopy: {
       // a kernel copy, not a blit: graphs replayed under rocprofv3's kernel

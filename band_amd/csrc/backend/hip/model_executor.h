@@ -48,9 +48,6 @@ struct Launch {
   } kind;
   int op_index = -1;
   int out_tensor = -1;  // tensor this launch materialises (after epilogue fusions)
-  // kChain with the RGB stem fused into its tile form: `conv` holds the
-  // stem (bh_chain_params.stem points at it for the launch)
-  bool chain_stem = false;
   bh_conv_params conv{};
   bh_dwconv_params dw{};
   bh_fc_params fc{};
@@ -206,7 +203,6 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   void FuseBlocks(const HipModel& model, PreparedSubgraph* sg);
   // dw3x3 -> conv1x1 [+ADD] [-> conv1x1] runs into one bh_chain_i8 launch
   bool PackChainTile(bh_chain_params* q, PreparedSubgraph* sg);
-  void TryFuseStem(std::vector<Launch>* out, Launch* F, PreparedSubgraph* sg);
   void FuseChains(const HipModel& model, PreparedSubgraph* sg);
   // 8-bit unary table ops into the producing conv / FC / depthwise epilogue;
   // CONCATENATION with outer size 1 elided (producers write their slices)
@@ -273,15 +269,10 @@ class HipModelExecutor : public interface::IModelExecutor, public IJobBatching {
   bool allow_group_ = true;   // BAND_HIP_FUSION=nogroup: one launch per conv
   bool force_chain_ = false;  // BAND_HIP_FUSION=forcechain
   bool force_tile_chain_ = false;  // BAND_HIP_FUSION=forcetile: every feasible chain in the tile form
-  bool tile_pipe_ = false;         // BAND_HIP_FUSION=forcetilepipe: ... in the persistent tile form
   bool no_tile_chain_ = false;     // BAND_HIP_FUSION=notile: the tuner skips the tile form
   bool no_deep_chain_ = false;     // BAND_HIP_FUSION=nodeep: the tuner skips the deep-issue forms
   bool no_split_chain_ = false;    // BAND_HIP_FUSION=nosplit: the tuner skips the phase-C split forms
-  bool no_valu_chain_ = false;     // BAND_HIP_FUSION=novalu: ... the VALU depthwise forms
-  bool force_valu_chain_ = false;  // BAND_HIP_FUSION=forcevalu: every feasible chain, VALU depthwise (parity)
   bool force_deep_chain_ = false;  // BAND_HIP_FUSION=forcedeep: every feasible chain in the deep form
-  bool no_stem_chain_ = false;     // BAND_HIP_FUSION=nostem: the RGB stem stays its own launch
-  bool force_stem_chain_ = false;  // BAND_HIP_FUSION=forcestem: tile chains, the stem fused wherever it fits
   bool force_stage_chain_ = false; // BAND_HIP_FUSION=forcestage: every chain the stage form takes, in it (parity)
   bool no_stage_chain_ = false;    // BAND_HIP_FUSION=nostage: the tuner skips the stage forms
   bool autotune_ = true;  // BAND_HIP_AUTOTUNE=0: pick fused tiles by the static model

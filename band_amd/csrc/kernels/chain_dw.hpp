@@ -12,7 +12,6 @@ namespace bh {
 
 struct ChainDivs {
   FastDiv out_w, out_h;
-  FastDiv quads;  // dw_valu: C / 4 channel quads per pixel
 };
 
 // The block-diagonal MFMA tile: one v_mfma_i32_16x16x64_i8 contracts 3 taps x

@@ -344,7 +344,7 @@ extern "C" size_t bh_chain_stage_lds_bytes(const bh_chain_params* pp) {
   if (!p.has_pw2 || p.pw2.k_pad > 64 * 5) return 0;
   if (p.px_blocks != 1 && p.px_blocks != 2) return 0;
   if (p.waves != 0 && p.waves != 4 && p.waves != 8) return 0;
-  if (p.tile || p.persist || p.deep || p.dw_valu || p.stage < 0 || p.stage > 2) return 0;
+  if (p.tile || p.persist || p.deep || p.stage < 0 || p.stage > 2) return 0;
   if (p.c_split < 0 || p.c_split > 8 || (p.pw2.out_c + 15) / 16 < std::max(1, p.c_split)) return 0;
   const bh::StageGeom G = bh::stage_geom(p);
   return G.bytes <= 160 * 1024 ? G.bytes : 0;

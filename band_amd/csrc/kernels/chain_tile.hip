@@ -45,11 +45,9 @@
 // fall on distinct LDS banks (the DMA writes LDS linearly; no padding).
 #include <algorithm>
 #include <cstring>
-#include <type_traits>
 
 #include "chain_blob.hpp"
 #include "common.hpp"
-#include "stem_window.hpp"
 
 namespace bh {
 
@@ -67,14 +65,12 @@ struct TileGeom {
   int off_dl, off_pl, off_o1, off_add, off_out;
   int out_pitch;       // bytes per pixel of the second 1x1's staging (N2, or N2 + 16)
   int o1_pitch;        // the same for the first 1x1's staging (N1, or N1 + 16)
-  int buf_bytes;  // patch + residual region (pipe: the second one follows it)
+  int buf_bytes;  // patch + residual region
   TileBlob blob;
   size_t bytes;
 };
 
-// pipe: the persistent form's layout - two patch + residual buffers (the
-// next tile's DMA lands in one while the other is computed), then the rest
-__host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, int TW, bool pipe = false) {
+__host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, int TW) {
   TileGeom g{};
   const bh_dwconv_params& d = p.dw;
   const int C = d.out_c;
@@ -108,8 +104,7 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
   g.off_res = (int)o;
   o += p.pw1.residual ? (size_t)rows * N1 : 0;
   o = (o + 15) / 16 * 16;
-  g.buf_bytes = (int)o;  // one patch + residual buffer
-  if (pipe) o += g.buf_bytes;
+  g.buf_bytes = (int)o;  // the patch + residual buffer
   g.off_blob = (int)o;
   g.blob = tile_blob(p);
   g.blob_units = g.blob.bytes / 16;
@@ -141,8 +136,7 @@ __host__ __device__ inline TileGeom tile_geom(const bh_chain_params& p, int TH, 
 
 struct TileDivs {
   FastDiv tiles_x, txy, patch_ru, res_ru4;
-  FastDiv pw;  // STEM: patch pixels per row
-  int per;     // PIPE: consecutive tiles per workgroup
+  int per;     // RUN: consecutive tiles per workgroup
   int ntiles;  // batch x tiles
 };
 
@@ -211,29 +205,13 @@ __global__ void chain_tile_pack_kernel(bh_chain_params p, TileBlob B, unsigned c
   *(uint32_t*)(blob + o) = v;
 }
 
-// PIPE: the persistent form - a workgroup walks dv.per consecutive tiles,
-// the constant block staged once, and each tile's patch + residual DMA is
-// issued into the other buffer before the current tile's phases run, so it
-// lands under their compute (bh_chain_params.tile == 2)
-//
-// PIPE == 2: the sequential multi-tile form (bh_chain_params.tile == 3) - a
-// workgroup walks dv.per consecutive tiles through ONE patch buffer: the
-// constant block is staged once per workgroup instead of once per tile (for
-// the 112x112 x 32 chain it is 9.2 KB against a 3.2 KB patch), and each
-// further tile's patch is DMA'd after the previous tile is done
-// STEM (bh_chain_params.stem, tile 1): the depthwise input is the RGB stem's
-// output, and the workgroup computes its patch from the image instead of
-// reading it, on MFMA as conv_stem_mfma_kernel does (16-pixel blocks, the
-// channel's bias and requantisation constants from LDS records), writing
-// each pixel's channel quads to the patch at their swizzled chunks.  Pixels
-// outside the image get values phase A never reads (it masks those taps).
-// The stem's output never reaches HBM; halo pixels are computed by both
-// neighbouring tiles (1.56x the stem's arithmetic for 8 x 8 tiles at
-// stride 1).
-struct NoStem {};
-template <int TH, int TW, bool FAST, int KX, int PIPE, typename ST = NoStem>
-__global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv, ST st) {
-  constexpr bool STEM = !std::is_same<ST, NoStem>::value;
+// RUN: a workgroup walks dv.per consecutive tiles through ONE patch buffer
+// (bh_chain_params.tile 3 / 4): the constant block is staged once per
+// workgroup instead of once per tile (for the 112x112 x 32 chain it is 9.2 KB
+// against a 3.2 KB patch), and each further tile's patch is DMA'd after the
+// previous tile is done
+template <int TH, int TW, bool FAST, int KX, bool RUN>
+__global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, TileGeom G, TileDivs dv) {
   static_assert(TH * TW == 64, "4 pixel blocks of 16");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const unsigned long long t_entry = __builtin_amdgcn_s_memtime();  // before any kernarg load
@@ -248,10 +226,10 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   const int OH = d.out_h, OW = d.out_w;
 
   const int logical = xcd_block(blockIdx.x, gridDim.x);
-  // this workgroup's tiles: one (grid = batch x tiles), or PIPE's run of
+  // this workgroup's tiles: one (grid = batch x tiles), or RUN's run of
   // dv.per consecutive ones (neighbours share their halo rows in one L2)
-  const int t_first = PIPE ? logical * dv.per : logical;
-  const int t_count = PIPE ? min(dv.per, dv.ntiles - t_first) : 1;
+  const int t_first = RUN ? logical * dv.per : logical;
+  const int t_count = RUN ? min(dv.per, dv.ntiles - t_first) : 1;
   if (t_count <= 0) return;
   auto tile_xy = [&](int t, int& n, int& oy0, int& ox0) {
     n = dv.txy.div(t);
@@ -274,67 +252,6 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
     tile_xy(t, n, oy0, ox0);
     const int C = d.out_c;
     const int y0 = oy0 * d.stride_h - d.pad_h;  // image coords of patch (0, 0)
-    if constexpr (STEM) {
-      const int xs = ox0 * d.stride_w - d.pad_w;
-      const int npix = G.PH * G.PW;
-      const long img = (long)st.in_h * st.in_w * 3;
-      const uint8_t* im = (const uint8_t*)st.input + n * img;
-      const uint8_t* end = (const uint8_t*)st.input + st.batch * img;
-      // the stem's channel records (filter dwords, bias, ChanQ) in the
-      // depthwise-output region, unused until phase A (C x 64 bytes <= the
-      // region's 64 x (k_pad + 32))
-      StemChan* rec = (StemChan*)(smem + G.off_dl);
-      for (int i = tid; i < C * 16; i += 256)
-        ((int32_t*)rec)[i] = stem_chan_word((const int32_t*)st.weights, st.k_pad >> 2, st.bias_eff, st.mult,
-                                            st.shift, st.out_zp, i >> 4, i & 15);
-      __syncthreads();
-      // the patch on v_mfma_i32_16x16x64_i8, as conv_stem_mfma_kernel: wave w
-      // takes 16-pixel blocks w, w + 4, ...; lane groups 0 / 1 gather the
-      // pixel's window bytes 0-15 / 16-26 (k-ordered), D = X W^T gives a lane
-      // 4 pixels of channel 16b + r16 (one record per lane and block), and a
-      // quad byte-transpose turns them into 4 channels of one pixel for one
-      // dword into the patch at its swizzled chunk
-      const int nblk = (npix + 15) >> 4;
-      const int nbc = C >> 4;
-      const int qi = lane & 3, qj = (lane >> 2) & 3;
-      for (int blk = wave; blk < nblk; blk += 4) {
-        v4i xf = (v4i){0, 0, 0, 0};
-        if (g < 2) {
-          const int pc = min(blk * 16 + r16, npix - 1);
-          const int r = dv.pw.div(pc);
-          const int px = pc - r * G.PW;
-          uint32_t xw[7];
-          stem_window(im, end, (y0 + r) * st.stride_h - st.pad_h, (xs + px) * st.stride_w - st.pad_w, st.dil_h,
-                      st.in_h, st.in_w, (uint32_t)st.in_xor, (uint32_t)st.in_zp, xw);
-          xf = g == 0 ? (v4i){(int)xw[0], (int)xw[1], (int)xw[2], (int)xw[3]}
-                      : (v4i){(int)xw[4], (int)xw[5], (int)xw[6], 0};
-        }
-        const int p2 = blk * 16 + 4 * g + qi;  // this lane's pixel after the transpose
-        const int r2 = dv.pw.div(min(p2, npix - 1));
-        const int px2 = min(p2, npix - 1) - r2 * G.PW;
-        const bool wr = p2 < npix;
-        const int f2 = (3 * r2 + px2) & G.pmask;
-        unsigned char* dst = buf + (r2 * G.patch_ru + px2 * nbc) * 16 + 4 * qj;
-        for (int b = 0; b < nbc; ++b) {
-          const v4i wf = *(const v4i*)(st.weights + (long)(16 * b + r16) * st.k_pad + 16 * g);
-          const v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(xf, wf, (v4i){0, 0, 0, 0}, 0, 0, 0);
-          const StemChan& k = rec[16 * b + r16];
-          const v4i q0 = *(const v4i*)&k.bias, q1 = *(const v4i*)&k.emask;
-          ChanQ q;
-          q.mu = q0.y;
-          q.sh = q0.z;
-          q.e = q0.w;
-          q.emask = q1.x;
-          q.zpe = q1.y;
-          q.c0 = (int64_t)(((uint64_t)(uint32_t)q1.w << 32) | (uint32_t)q1.z);
-          int32_t v[4];
-#pragma unroll
-          for (int t = 0; t < 4; ++t) v[t] = requant_out<FAST>(acc[t] + q0.x, q, st.out_zp, st.act_min, st.act_max);
-          const uint32_t packed = quad_transpose8(pack4_bytes(v));
-          if (wr) *(uint32_t*)(dst + ((b ^ f2) << 4)) = packed;
-        }
-      }
-    } else {
     const uint8_t* in = (const uint8_t*)d.input;
     const long in_last = (long)d.batch * d.in_h * d.in_w * C - 16;
     const long row0 = (long)n * d.in_h;
@@ -351,7 +268,6 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
         dma16(in + off, buf + base * 16);
       }
     }
-    }  // patch DMA
     if (a.residual) {
       const int N1 = a.out_c;
       const uint8_t* res = (const uint8_t*)a.residual;
@@ -398,21 +314,19 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   const int orow = pb * 16 + 4 * g;  // first of this lane's 4 result rows
 
   for (int it = 0; it < t_count; ++it) {
-  if (PIPE == 2 && it > 0) {
+  if (RUN && it > 0) {
     __syncthreads();  // every read of the previous tile's patch / staging is done
     issue_tile(t_first + it, smem);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  unsigned char* cur = smem + (PIPE == 1 ? (it & 1) * G.buf_bytes : 0);
+  unsigned char* cur = smem;
   const unsigned char* patch = cur;
   const unsigned char* resl = cur + G.off_res;
   // the second 1x1's staging: the current patch (dead after phase A) when it fits
   unsigned char* ol = G.off_out == 0 ? cur : smem + G.off_out;
   int n, oy0, ox0;
   tile_xy(t_first + it, n, oy0, ox0);
-  // the next tile's patch + residual into the other buffer, under this one's phases
-  if (PIPE == 1 && it + 1 < t_count) issue_tile(t_first + it + 1, smem + ((it + 1) & 1) * G.buf_bytes);
 
   // ---- phase A: depthwise 3x3 from the patch -> dl ------------------------
   {
@@ -587,23 +501,17 @@ __global__ __launch_bounds__(256) void chain_tile_kernel(bh_chain_params cp, Til
   tile_copy_out(ol, (uint8_t*)b.output, b.out_c, TH, TW, n, oy0, ox0, OH, OW, tid, 256, G.out_pitch);
   TILE_STAMP(6)
   }  // has_pw2
-  if (PIPE == 1 && it + 1 < t_count) {
-    // the next tile's DMA has landed (this wave's part; the barrier covers
-    // every wave's), and every read of this tile's buffers is done
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
   }  // tiles
 #undef TILE_STAMP
 }
 
-template <int TH, int TW, bool FAST, int KX, int PIPE, typename ST = NoStem>
-static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s, ST st = ST{}) {
+template <int TH, int TW, bool FAST, int KX, bool RUN>
+static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t s) {
   static thread_local int opted_device = -1;
   int dev = 0;
   (void)hipGetDevice(&dev);
   if (opted_device != dev) {
-    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>,
+    (void)hipFuncSetAttribute((const void*)chain_tile_kernel<TH, TW, FAST, KX, RUN>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     opted_device = dev;
   }
@@ -612,32 +520,15 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
   dv.txy = FastDiv(G.tiles_x * G.tiles_y);
   dv.patch_ru = FastDiv(G.patch_ru);
   dv.res_ru4 = FastDiv(G.res_ru4 > 0 ? G.res_ru4 : 1);
-  dv.pw = FastDiv(G.PW);
   dv.ntiles = p.dw.batch * G.tiles_y * G.tiles_x;
   dv.per = 1;
   int blocks = dv.ntiles;
-  if (PIPE == 2) {
+  if (RUN) {
     // bh_chain_params.tile 3 / 4: runs of 2 / 4 consecutive tiles
     dv.per = p.tile == 4 ? 4 : 2;
     blocks = (dv.ntiles + dv.per - 1) / dv.per;
-  } else if (PIPE) {
-    // one wave of resident workgroups (LDS and registers permitting, <= 4 per
-    // CU on 256 CUs), each taking a run of consecutive tiles
-    static thread_local size_t cached_lds = 0;
-    static thread_local int cached_per_cu = 1;
-    if (cached_lds != G.bytes) {
-      int nb = 0;
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>, 256, G.bytes) !=
-          hipSuccess)
-        nb = 1;
-      cached_per_cu = std::max(1, std::min(4, nb));
-      cached_lds = G.bytes;
-    }
-    const int slots = 256 * cached_per_cu;
-    dv.per = (dv.ntiles + slots - 1) / slots;
-    blocks = (dv.ntiles + dv.per - 1) / dv.per;
   }
-  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX, PIPE, ST>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv, st);
+  BH_LAUNCH((chain_tile_kernel<TH, TW, FAST, KX, RUN>), dim3(blocks), dim3(256), G.bytes, s, p, G, dv);
 }
 
 }  // namespace bh
@@ -648,26 +539,14 @@ static void launch_tile(const bh_chain_params& p, const TileGeom& G, hipStream_t
 extern "C" size_t bh_chain_tile_lds_bytes(const bh_chain_params* pp) {
   const bh_chain_params& p = *pp;
   const bh_dwconv_params& d = p.dw;
-  // 2: the persistent pipelined form; 3 / 4: runs of 2 / 4 tiles per
-  // workgroup through one buffer
-  if (p.tile < 1 || p.tile > 4) return 0;
-  if (p.stem) {
-    // the fused RGB stem: a 3x3 CONV_2D over 3 channels whose output (int8,
-    // no table / residual) is the depthwise input; one tile per workgroup
-    const bh_conv_params& st = *(const bh_conv_params*)p.stem;
-    if (p.tile != 1 || st.k_h != 3 || st.k_w != 3 || st.in_c != 3 || st.dil_w != 1 || st.dil_h < 1 ||
-        st.out_c != d.in_c || d.in_c % 8 || st.w_zp != 0 || st.residual || st.out_table || st.k_pad < 28 ||
-        st.k_pad % 4 || st.out_img_stride || !st.input || !st.weights || !st.bias_eff || !st.mult || !st.shift ||
-        st.batch != d.batch || st.out_h != d.in_h || st.out_w != d.in_w || st.output != d.input ||
-        st.act_min < -128 || st.act_max > 127 || st.stride_h < 1 || st.stride_w < 1)
-      return 0;
-  }
+  // 1: one tile per workgroup; 3 / 4: runs of 2 / 4 tiles per workgroup
+  if (p.tile != 1 && p.tile != 3 && p.tile != 4) return 0;
   if (d.stride_h < 1 || d.stride_h > 2 || d.stride_w < 1 || d.stride_w > 2 || d.dil_h < 1 || d.dil_h > 2 ||
       d.dil_w < 1 || d.dil_w > 2)
     return 0;
   if (p.has_pw2 && p.pw2.k_pad > 64 * 5) return 0;
   if ((long)d.batch * d.in_h * d.in_w * d.in_c < 16) return 0;
-  const bh::TileGeom G = bh::tile_geom(p, 8, 8, p.tile == 2);
+  const bh::TileGeom G = bh::tile_geom(p, 8, 8);
   // a workgroup's grid index and the DMA unit counts stay in int range
   if ((long)d.batch * G.tiles_y * G.tiles_x >= INT32_MAX / 2) return 0;
   return G.bytes <= 160 * 1024 ? G.bytes : 0;
@@ -701,38 +580,17 @@ extern "C" int bh_chain_tile_launch(const bh_chain_params* pp, bh_stream_t strea
     bh_set_last_error("bh_chain_i8: the tile form needs tile_blob (bh_chain_tile_pack)");
     return BH_EINVAL;
   }
-  const bool pipe = p.tile == 2;
-  const bh::TileGeom G = bh::tile_geom(p, 8, 8, pipe);
-  const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast) &&
-                    (!p.stem || ((const bh_conv_params*)p.stem)->requant_fast);
+  const bh::TileGeom G = bh::tile_geom(p, 8, 8);
+  const bool fast = p.dw.requant_fast && p.pw1.requant_fast && (!p.has_pw2 || p.pw2.requant_fast);
   const bool k2 = !p.has_pw2 || p.pw2.k_pad <= 128;
+  const bool run = p.tile >= 3;
   hipStream_t s = (hipStream_t)stream;
-  if (p.stem) {  // tile 1 (bh_chain_tile_lds_bytes)
-    const bh_conv_params st = *(const bh_conv_params*)p.stem;
-    if (k2) {
-      if (fast) bh::launch_tile<8, 8, true, 2, 0>(p, G, s, st);
-      else bh::launch_tile<8, 8, false, 2, 0>(p, G, s, st);
-    } else {
-      if (fast) bh::launch_tile<8, 8, true, 5, 0>(p, G, s, st);
-      else bh::launch_tile<8, 8, false, 5, 0>(p, G, s, st);
-    }
-    return bh_check_launch("chain_tile_kernel");
-  }
-#define BH_TILE(PIPE)                                                  \
-  if (k2) {                                                            \
-    if (fast) bh::launch_tile<8, 8, true, 2, PIPE>(p, G, s);           \
-    else bh::launch_tile<8, 8, false, 2, PIPE>(p, G, s);               \
-  } else {                                                             \
-    if (fast) bh::launch_tile<8, 8, true, 5, PIPE>(p, G, s);           \
-    else bh::launch_tile<8, 8, false, 5, PIPE>(p, G, s);               \
-  }
-  if (pipe) {
-    BH_TILE(1)
-  } else if (p.tile >= 3) {
-    BH_TILE(2)
+  if (k2) {
+    if (fast) run ? bh::launch_tile<8, 8, true, 2, true>(p, G, s) : bh::launch_tile<8, 8, true, 2, false>(p, G, s);
+    else run ? bh::launch_tile<8, 8, false, 2, true>(p, G, s) : bh::launch_tile<8, 8, false, 2, false>(p, G, s);
   } else {
-    BH_TILE(0)
+    if (fast) run ? bh::launch_tile<8, 8, true, 5, true>(p, G, s) : bh::launch_tile<8, 8, true, 5, false>(p, G, s);
+    else run ? bh::launch_tile<8, 8, false, 5, true>(p, G, s) : bh::launch_tile<8, 8, false, 5, false>(p, G, s);
   }
-#undef BH_TILE
   return bh_check_launch("chain_tile_kernel");
 }

@@ -395,14 +395,9 @@ struct StemPlan {
   bool lds;
 };
 StemPlan stem_plan(const bh_conv_params& p, int M) {
-  static const int min_wg = [] {
-    const char* e = std::getenv("BH_STEM_MIN_WG");  // A-B runs
-    return e ? std::atoi(e) : 512;
-  }();
-  static const bool scalar_env = [] {
-    const char* e = std::getenv("BH_STEM_SCALAR");
-    return e && e[0] == '1';
-  }();
+  // channel groups over grid.y until 512 workgroups (splitting further only
+  // adds waves that repeat the window gather, profiles/r05ax_breakdown_mw*)
+  constexpr int min_wg = 512;
   StemPlan sp;
   sp.gx = (M + 255) / 256;
   const int groups = p.out_c / 8;
@@ -410,7 +405,7 @@ StemPlan stem_plan(const bh_conv_params& p, int M) {
   gy = gy < 1 ? 1 : (gy > groups ? groups : gy);
   sp.ch_per_y = (groups + gy - 1) / gy * 8;
   sp.gy = (p.out_c + sp.ch_per_y - 1) / sp.ch_per_y;
-  sp.lds = !scalar_env && p.kernel_hint != BH_CONV_STEM_SCALAR && sp.ch_per_y <= 64 && p.out_c % 4 == 0 &&
+  sp.lds = p.kernel_hint != BH_CONV_STEM_SCALAR && sp.ch_per_y <= 64 && p.out_c % 4 == 0 &&
            (((uintptr_t)p.output) & 3) == 0 && (sp.gx >= 256 || p.kernel_hint == BH_CONV_STEM_VALU);
   return sp;
 }
@@ -435,23 +430,11 @@ int bh_conv_stem_launch(const bh_conv_params& p, int M, int K, hipStream_t s) {
   const dim3 grid((unsigned)gx, (unsigned)gy);
   const bool lds = sp.lds;
   if (lds) {
-    // pixels per thread: 1; BH_STEM_PX=2 (A-B runs) gives each thread two
-    // pixels sharing the channel records' LDS reads - slower, 17.5 vs 14.7
-    // us at B = 24 (interleaved, profiles/r05x_stem_px{1,2}.txt): half the
-    // waves, each with twice the dependent VALU chains
-    static const int px_env = [] {
-      const char* e = std::getenv("BH_STEM_PX");
-      return e ? std::atoi(e) : 0;
-    }();
-    const int px = px_env == 2 ? 2 : 1;
-    const dim3 g2((unsigned)((M + 256 * px - 1) / (256 * px)), (unsigned)gy);
-    if (px == 2) {
-      if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 2>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
-      else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 2>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
-    } else {
-      if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
-      else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 1>), g2, dim3(256), 0, s, p, M, dv, ch_per_y);
-    }
+    // one pixel per thread (two, sharing the channel records' LDS reads,
+    // was slower: 17.5 vs 14.7 us at B = 24, profiles/r05x_stem_px{1,2}.txt -
+    // half the waves, each with twice the dependent VALU chains)
+    if (p.requant_fast) BH_LAUNCH((bh::conv_stem_lds_kernel<true, 1>), grid, dim3(256), 0, s, p, M, dv, ch_per_y);
+    else BH_LAUNCH((bh::conv_stem_lds_kernel<false, 1>), grid, dim3(256), 0, s, p, M, dv, ch_per_y);
     return bh_check_launch("conv_stem_lds_kernel");
   }
   if (p.requant_fast) BH_LAUNCH(bh::conv_stem_kernel<true>, grid, dim3(256), 0, s, p, M, dv, ch_per_y);

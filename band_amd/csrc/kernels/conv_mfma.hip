@@ -449,15 +449,11 @@ static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t 
   dv.in_c = FastDiv(p.in_c);
   dv.k_w = FastDiv(p.k_w);
   const int gm = (M + TM - 1) / TM, gn = (N + TN - 1) / TN;
-  static const int xcd_env = [] {
-    const char* e = std::getenv("BH_CONV_XCD");  // A-B runs: 0 plain order, 1 / 2 forced
-    return e ? std::atoi(e) : -1;
-  }();
   // replicate the smaller operand over the 8 XCDs' L2s: 8 x filters + input
   // (xcd 1) against filters + 8 x input (xcd 2)
   const long in_bytes = (long)p.batch * p.in_h * p.in_w * p.in_c;
   const long w_bytes = (long)N * K;
-  const int xcd = xcd_env >= 0 ? xcd_env : (w_bytes > in_bytes ? 2 : 1);
+  const int xcd = w_bytes > in_bytes ? 2 : 1;
   BH_LAUNCH((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
                      s, p, M, K, N, kchunk, dv, gn, xcd);
   return bh_check_launch("conv_mfma_kernel");
@@ -611,11 +607,7 @@ static int launch_gemm(const bh_conv_params& p, int M, int K, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   const int gm = (M + BM - 1) / BM, gn = (p.out_c + BN - 1) / BN;
-  static const int xcd_env = [] {
-    const char* e = std::getenv("BH_CONV_XCD");
-    return e ? std::atoi(e) : -1;
-  }();
-  const int xcd = xcd_env >= 0 ? xcd_env : ((long)p.out_c * K > (long)M * K ? 2 : 1);
+  const int xcd = (long)p.out_c * K > (long)M * K ? 2 : 1;
   BH_LAUNCH((conv_gemm_kernel<WM, WN, WAVES_M, WAVES_N, NB>), dim3(gm * gn), dim3(WAVES_M * WAVES_N * 64), 0, s,
             p, M, K, gn, (K + 63) / 64, xcd);
   return bh_check_launch("conv_gemm_kernel");

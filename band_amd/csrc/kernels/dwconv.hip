@@ -507,11 +507,7 @@ static DwDivs dw_divs(const bh_dwconv_params& p, int groups) {
   dv.out_w = FastDiv(p.out_w);
   dv.out_h = FastDiv(p.out_h);
   dv.dm = FastDiv(p.depth_multiplier);
-  static const int xcd = [] {
-    const char* e = std::getenv("BH_DW_XCD");
-    return e ? std::atoi(e) : 1;
-  }();
-  dv.xcd = xcd;
+  dv.xcd = 1;
   return dv;
 }
 
@@ -561,12 +557,8 @@ static bool mfma_ok(const bh_dwconv_params& p) { return p.taps && p.out_c % 16 =
 
 // the run kernel's shapes: tap table, dil 1, equal strides 1 / 2
 static bool run_ok(const bh_dwconv_params& p) {
-  static const int off = [] {
-    const char* e = std::getenv("BH_DW_NO_RUN");
-    return e ? std::atoi(e) : 0;
-  }();
   // dil 1 with stride 1 / 2, or dil 2 with stride 1 (DeepLab's atrous layers)
-  return !off && p.taps && p.dil_h == p.dil_w && p.stride_h == p.stride_w &&
+  return p.taps && p.dil_h == p.dil_w && p.stride_h == p.stride_w &&
          ((p.dil_h == 1 && (p.stride_h == 1 || p.stride_h == 2)) || (p.dil_h == 2 && p.stride_h == 1));
 }
 

@@ -288,8 +288,8 @@ __device__ __forceinline__ void gemm_xs4_nt(const bh_conv_params& c, const unsig
 #endif
 // VAR: compile-time form variants, so the default instantiation carries no
 // code of the others (built as runtime branches they cost 1-3.6 us per
-// launch on every chain at batch 24, profiles/r05m_*): bit 0 = the VALU
-// depthwise phase (dw_valu), bit 1 = the phase-C channel split over grid.y
+// launch on every chain at batch 24, profiles/r05m_*): bit 1 = the phase-C
+// channel split over grid.y
 template <int RB, bool FAST, int KX, int NW, bool AM, int DA = 2, int VAR = 0>
 __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_params cp, int P, int S1, int S2, int off_pl, int off_o1,
                                                     int off_add, ChainDivs dv) {
@@ -338,95 +338,7 @@ __global__ __launch_bounds__(NW * 64) BH_CHAIN_OCC void chain_kernel(bh_chain_pa
 
   // ---- phase A: depthwise 3x3 -> LDS -------------------------------------
   constexpr bool SPLIT = (VAR & 2) != 0;
-  if constexpr ((VAR & 1) != 0) {
-    // VALU form (dw_valu): a thread takes (pixel, 4-channel quad) items; the
-    // nine tap dwords of an item hold 4 CHANNELS of one tap, two 4x4 byte
-    // transposes turn taps 0-3 / 4-7 into dwords of 4 TAPS of one channel
-    // and v_dot4 sums them against the host-packed tap table (taps 0-3,
-    // 4-7, tap 8 in byte c % 4, folded bias), as dwconv3x3_dot_kernel;
-    // the quad's 4 requantised bytes go to LDS [pixel][C] as one dword.
-    // MFMA stays on the 1x1 contractions.  Two items per round, every tap
-    // load issued before either item's arithmetic.
-    const bh_dwconv_params& d = cp.dw;
-    const int C = d.out_c;
-    const int Q = C >> 2;
-    const int items = RB * 16 * Q;
-    const __amdgpu_buffer_rsrc_t rsrc =
-        __builtin_amdgcn_make_buffer_rsrc((void*)d.input, (short)0, d.batch * d.in_h * d.in_w * C, 0x00020000);
-    const uint32_t zfill = splat_byte(d.in_zp);
-    const v4i* tp = (const v4i*)d.taps;
-    for (int i0 = threadIdx.x; i0 < items; i0 += 2 * NW * 64) {
-      uint32_t xv[2][9];
-      int pr[2], q4[2];
-      bool live[2];
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = i0 + u * NW * 64;
-        live[u] = i < items;
-        const int ii = live[u] ? i : 0;
-        pr[u] = (int)dv.quads.div((uint32_t)ii);
-        q4[u] = ii - pr[u] * Q;
-        const int mm = m0 + pr[u];
-        live[u] = live[u] && mm < P;
-        const int mc = live[u] ? mm : 0;
-        const int t = dv.out_w.div(mc);
-        const int ox = mc - t * d.out_w;
-        const int n = dv.out_h.div(t);
-        const int oy = t - n * d.out_h;
-        const int iy = oy * d.stride_h - d.pad_h, ix = ox * d.stride_w - d.pad_w;
-#pragma unroll
-        for (int tap = 0; tap < 9; ++tap) {
-          const int fy = tap / 3, fx = tap - 3 * (tap / 3);
-          const int y = iy + fy * d.dil_h, x = ix + fx * d.dil_w;
-          const bool ok = live[u] && y >= 0 && y < d.in_h && x >= 0 && x < d.in_w;
-          const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rsrc, ok ? (((n * d.in_h + y) * d.in_w + x) * C + 4 * q4[u]) : 0, 0, 0);
-          xv[u][tap] = ok ? v : zfill;
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        if (!live[u]) continue;
-        const uint32_t* X = xv[u];
-        uint32_t T[4], U[4];
-        {
-          const uint32_t l01 = __builtin_amdgcn_perm(X[1], X[0], 0x05010400u);
-          const uint32_t h01 = __builtin_amdgcn_perm(X[1], X[0], 0x07030602u);
-          const uint32_t l23 = __builtin_amdgcn_perm(X[3], X[2], 0x05010400u);
-          const uint32_t h23 = __builtin_amdgcn_perm(X[3], X[2], 0x07030602u);
-          T[0] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
-          T[1] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
-          T[2] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
-          T[3] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
-        }
-        {
-          const uint32_t l01 = __builtin_amdgcn_perm(X[5], X[4], 0x05010400u);
-          const uint32_t h01 = __builtin_amdgcn_perm(X[5], X[4], 0x07030602u);
-          const uint32_t l23 = __builtin_amdgcn_perm(X[7], X[6], 0x05010400u);
-          const uint32_t h23 = __builtin_amdgcn_perm(X[7], X[6], 0x07030602u);
-          U[0] = __builtin_amdgcn_perm(l23, l01, 0x05040100u);
-          U[1] = __builtin_amdgcn_perm(l23, l01, 0x07060302u);
-          U[2] = __builtin_amdgcn_perm(h23, h01, 0x05040100u);
-          U[3] = __builtin_amdgcn_perm(h23, h01, 0x07060302u);
-        }
-        const int c0 = 4 * q4[u];
-        const v4i mm = *(const v4i*)(d.mult + c0);
-        const v4i ss = *(const v4i*)(d.shift + c0);
-        uint32_t o = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const v4i w = tp[c0 + j];  // taps 0-3, 4-7, 8 (byte j), folded bias
-          int32_t acc = __builtin_amdgcn_sdot4((int)T[j], w.x, w.w, false);
-          acc = __builtin_amdgcn_sdot4((int)U[j], w.y, acc, false);
-          acc = __builtin_amdgcn_sdot4((int)X[8], w.z, acc, false);
-          const int32_t v = requant_out<FAST>(acc, chan_q(mm[j], ss[j], d.out_zp), d.out_zp, d.act_min, d.act_max);
-          o |= ((uint32_t)v & 0xffu) << (8 * j);
-        }
-        *(uint32_t*)(dl + pr[u] * S1 + c0) = o;
-      }
-    }
-  } else {
-    chain_dw_mfma<FAST, DA, WPB>(cp.dw, dv, m, mval, lane, r16, g, wsub, dl, S1, orow);
-  }  // phase A (MFMA form)
+  chain_dw_mfma<FAST, DA, WPB>(cp.dw, dv, m, mval, lane, r16, g, wsub, dl, S1, orow);
   __syncthreads();
   CHAIN_STAMP(1)
 
@@ -881,25 +793,18 @@ static void launch_chain_v(const bh_chain_params& p, int P, const ChainLds& L, s
   ChainDivs dv;
   dv.out_w = FastDiv(p.dw.out_w);
   dv.out_h = FastDiv(p.dw.out_h);
-  dv.quads = FastDiv(p.dw.out_c / 4);
   const int blocks = (P + RB * 16 - 1) / (RB * 16);
   const int split = (VAR & 2) ? p.c_split : 1;
   BH_LAUNCH((chain_kernel<RB, FAST, KX, NW, AM, DA, VAR>), dim3(blocks, split), dim3(NW * 64), lds, s, p, P, L.S1,
             L.S2, L.off_pl, L.off_o1, L.off_add, dv);
 }
 
-// the variant instantiations: VALU phase A on the DA = 2 forms; the split on
-// the one- / two-block forms without the amortised GEMMs (bh_chain_lds_bytes
-// admits nothing else)
+// the split variant on the one- / two-block forms without the amortised
+// GEMMs (bh_chain_lds_bytes admits nothing else)
 template <int RB, bool FAST, int KX, int NW = 4, bool AM = false, int DA = 2>
 static void launch_chain(const bh_chain_params& p, int P, const ChainLds& L, size_t lds, hipStream_t s) {
-  const int var = (p.dw_valu ? 1 : 0) | (p.has_pw2 && p.c_split > 1 ? 2 : 0);
-  if constexpr (DA == 2) {
-    if constexpr (!AM && RB <= 2) {
-      if (var == 3) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 3>(p, P, L, lds, s);
-      if (var == 2) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 2>(p, P, L, lds, s);
-    }
-    if (var == 1) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 1>(p, P, L, lds, s);
+  if constexpr (DA == 2 && !AM && RB <= 2) {
+    if (p.has_pw2 && p.c_split > 1) return launch_chain_v<RB, FAST, KX, NW, AM, DA, 2>(p, P, L, lds, s);
   }
   launch_chain_v<RB, FAST, KX, NW, AM, DA, 0>(p, P, L, lds, s);
 }
@@ -970,8 +875,6 @@ extern "C" size_t bh_chain_lds_bytes(const bh_chain_params* pp) {
   if (P * widest >= INT32_MAX || (long)d.batch * d.in_h * d.in_w * d.in_c >= INT32_MAX) return 0;
   if (p.stage) return bh_chain_stage_lds_bytes(pp);
   if (p.c_split < 0 || p.c_split > 4) return 0;
-  // the VALU depthwise phase: raster forms (not persistent / tile / deep)
-  if (p.dw_valu && (p.tile || p.persist || p.deep)) return 0;
   if (p.c_split > 1 && (p.tile || p.persist || p.deep || p.px_blocks > 2 || !p.has_pw2 ||
                         (p.pw2.out_c + 15) / 16 < p.c_split))
     return 0;

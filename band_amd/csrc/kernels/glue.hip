@@ -550,12 +550,8 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
       (long)p.batch * p.out_h < INT32_MAX) {
     // 16-byte stores when every output row starts 16-byte aligned
     const int vec_ok = ((p.out_w * p.channels) % 16 == 0 && ((uintptr_t)p.output & 15) == 0) ? 1 : 0;
-    static const bool rows_only = [] {
-      const char* e = std::getenv("BH_RESIZE_ROWS");  // A-B: the byte-blend row kernel only
-      return e && e[0] == '1';
-    }();
     const size_t lds = ((size_t)p.in_w * p.channels + 3 * (size_t)p.out_w) * sizeof(int32_t);
-    if (!rows_only && p.channels >= 16 && lds <= 64 * 1024) {
+    if (p.channels >= 16 && lds <= 64 * 1024) {
       BH_LAUNCH(bh::resize_bilinear_cols_kernel, dim3(p.batch * p.out_h), dim3(256), lds, (hipStream_t)s, p,
                 bh::FastDiv(p.channels), vec_ok);
       return bh_check_launch("resize_bilinear_cols_kernel");

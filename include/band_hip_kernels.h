@@ -382,10 +382,7 @@ typedef struct bh_chain_params {
    * output pixels and stages its depthwise input patch (tile + halo), the
    * residual tile, both 1x1 filters and every table in LDS with one burst of
    * LDS-DMA; stride / dilation 1 or 2, pw2 K <= 320.  px_blocks, waves and
-   * persist are ignored.  2: the same tile in a persistent workgroup that
-   * walks a run of consecutive tiles, the constant block staged once and
-   * each tile's patch + residual DMA issued into a second buffer under the
-   * previous tile's phases.  3 / 4: runs of 2 / 4 consecutive tiles per
+   * persist are ignored.  3 / 4: runs of 2 / 4 consecutive tiles per
    * workgroup through ONE buffer (the constant block staged once per run) */
   int tile;
   /* tile form: the chain's constant block (both 1x1 filters swizzled for
@@ -406,17 +403,6 @@ typedef struct bh_chain_params {
    * channel slice - more, shorter workgroups for the few-pixel 14x14 / 7x7
    * layers.  2..4 */
   int c_split;
-  /* raster forms (not persistent / tile / deep): the depthwise phase on VALU
-   * (v_dot4 over the tap table, 4 channels of one pixel per item) instead of
-   * the block-diagonal MFMA tile; MFMA then runs only the 1x1 contractions */
-  int dw_valu;
-  /* tile form 1 only: when non-NULL, a const bh_conv_params* of the RGB stem
-   * (CONV_2D 3x3 over 3 channels, int8 symmetric filters, no residual /
-   * table, out_c == dw.in_c) whose output is dw.input.  Each workgroup then
-   * computes its depthwise input patch from the image instead of reading
-   * the stem's output: the stem launch and its output tensor go away.
-   * Read during the bh_chain_i8 / bh_chain_lds_bytes call only. */
-  const void* stem;
   /* 1: raster form with staged filters (chain_stage_kernel) - a workgroup of
    * px_blocks (1 / 2) x 16 pixels and `waves` (4 / 8) waves starts with one
    * burst of LDS-DMA of the first 1x1's filter and tables, its c_split slice

@@ -82,7 +82,7 @@ class ChainCase:
         return y, f
 
     # --- GPU: one fused launch -------------------------------------------
-    def params(self, lib, px_blocks, keep, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0, stage=0):
+    def params(self, lib, px_blocks, keep, waves=4, persist=0, tile=0, deep=0, c_split=0, stage=0):
         from band_amd import _abi
         from band_amd.device import DeviceBuffer
 
@@ -171,7 +171,6 @@ class ChainCase:
         c.tile = tile
         c.deep = deep
         c.c_split = c_split
-        c.dw_valu = dw_valu
         c.stage = stage
         if tile or stage:
             nb = lib.bh_chain_tile_blob_bytes(ctypes.byref(c))
@@ -182,10 +181,10 @@ class ChainCase:
                 c.tile_blob = blob.value
         return c
 
-    def gpu(self, lib, px_blocks, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0, stage=0):
+    def gpu(self, lib, px_blocks, waves=4, persist=0, tile=0, deep=0, c_split=0, stage=0):
         from band_amd import _abi
         keep = []
-        c = self.params(lib, px_blocks, keep, waves, persist, tile, deep, c_split, dw_valu, stage)
+        c = self.params(lib, px_blocks, keep, waves, persist, tile, deep, c_split, stage)
         assert lib.bh_chain_lds_bytes(ctypes.byref(c)) > 0, "chain unsupported"
         _abi.check(lib.bh_chain_i8(ctypes.byref(c), None), "bh_chain_i8")
         y = self._y.download(np.int8, (self.b, self.oh, self.ow, self.cout)) if self._y else None

@@ -21,9 +21,9 @@ from tests.chain_harness import MNV2_CHAINS, ChainCase
 pytestmark = pytest.mark.gpu
 
 
-def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0, dw_valu=0, stage=0):
+def _check(c, lib, px, waves=4, persist=0, tile=0, deep=0, c_split=0, stage=0):
     y_ref, f_ref = c.oracle()
-    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split, dw_valu, stage)
+    y, f = c.gpu(lib, px, waves, persist, tile, deep, c_split, stage)
     if c.store_pw1:
         np.testing.assert_array_equal(y, y_ref, err_msg="first conv, px_blocks %d" % px)
     if c.ce2:
@@ -94,17 +94,12 @@ def test_chain_tile_mnv2(gpu_lib, h, ce, s, cout, res, ce2):
             # stay with the raster forms
             assert ce >= 384, "tile form should cover the %dx%dx%d chain" % (h, h, ce)
             continue
-        pipe = _tile_fits(c, gpu_lib, 2)  # persistent, double-buffered: two patches in LDS
         _check(c, gpu_lib, 4, tile=1)
         _check(c, gpu_lib, 4, tile=3)  # runs of 2 / 4 tiles through one buffer
         _check(c, gpu_lib, 4, tile=4)
-        if pipe:
-            _check(c, gpu_lib, 4, tile=2)
         c.fast = False
         _check(c, gpu_lib, 4, tile=1)
         _check(c, gpu_lib, 4, tile=4)
-        if pipe:
-            _check(c, gpu_lib, 4, tile=2)
 
 
 @pytest.mark.parametrize("args", [
@@ -128,8 +123,6 @@ def test_chain_tile_general(gpu_lib, args):
     _check(c, gpu_lib, 4, tile=1)
     _check(c, gpu_lib, 4, tile=3)
     _check(c, gpu_lib, 4, tile=4)
-    if _tile_fits(c, gpu_lib, 2):
-        _check(c, gpu_lib, 4, tile=2)
 
 
 def test_chain_tile_rejects(gpu_lib):
@@ -175,8 +168,7 @@ def test_chain_rejects_unsupported(gpu_lib):
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(c)) == 0
 
 
-@pytest.fixture(params=["forcechain", "forcetile", "forcetilepipe", "forcedeep", "forcevalu", "forcestem",
-                        "forcestage"])
+@pytest.fixture(params=["forcechain", "forcetile", "forcedeep", "forcestage"])
 def forcechain(request):
     old = os.environ.get("BAND_HIP_FUSION")
     os.environ["BAND_HIP_FUSION"] = request.param
@@ -202,12 +194,10 @@ def test_chain_forced_mix_models(gpu_lib, forcechain, arch):
     key = SubgraphKey(41, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
     assert any(k in kernels for k in ("chain_kernel", "chain_tile_kernel", "chain_stage_kernel")), kernels
-    if forcechain in ("forcetile", "forcetilepipe", "forcestem"):
+    if forcechain == "forcetile":
         assert "chain_tile_kernel" in kernels, kernels
     if forcechain == "forcestage" and arch != "posenet_mobilenet_v1":  # MobileNetV1: pairs, no second 1x1
         assert "chain_stage_kernel" in kernels, kernels
-    if forcechain == "forcestem":  # the RGB stem computed inside the first chain's tiles
-        assert kernels[0] == "chain_tile_kernel" and not any(k.startswith("conv_stem") for k in kernels), kernels
     for rep in range(2):  # eager, then graph replay
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
         assert ex.ExecuteSubgraph(key).ok()
@@ -247,7 +237,7 @@ def test_chain_split_phase_c(gpu_lib, h, ce, s, cout, res, ce2):
 def _stage_fits(c, lib, px, waves, split):
     import ctypes
     keep = []
-    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, px, keep, waves, 0, 0, 0, split, 0, 1))) > 0
+    return lib.bh_chain_lds_bytes(ctypes.byref(c.params(lib, px, keep, waves, 0, 0, 0, split, 1))) > 0
 
 
 @pytest.mark.parametrize("h,ce,s,cout,res,ce2", [c for c in MNV2_CHAINS if c[5]])
@@ -299,9 +289,9 @@ def test_chain_stage_rejects(gpu_lib):
     import ctypes
     keep = []
     c = ChainCase(np.random.default_rng(3), 1, 14, 14, 64, 1, 32, False, 64)
-    q = c.params(gpu_lib, 1, keep, 8, 0, 0, 0, 2, 0, 1)
+    q = c.params(gpu_lib, 1, keep, 8, 0, 0, 0, 2, 1)
     assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) > 0
-    for field, bad in (("px_blocks", 4), ("waves", 16), ("c_split", 9), ("deep", 1), ("dw_valu", 1), ("stage", 3)):
+    for field, bad in (("px_blocks", 4), ("waves", 16), ("c_split", 9), ("deep", 1), ("stage", 3)):
         old = getattr(q, field)
         setattr(q, field, bad)
         assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0, field
@@ -314,28 +304,6 @@ def test_chain_stage_rejects(gpu_lib):
     q.has_pw2 = 1
     q.tile_blob = None
     assert gpu_lib.bh_chain_i8(ctypes.byref(q), None) != 0  # no constant block: refused, nothing launched
-
-
-@pytest.mark.parametrize("h,ce,s,cout,res,ce2", MNV2_CHAINS)
-def test_chain_valu_depthwise(gpu_lib, h, ce, s, cout, res, ce2):
-    """the depthwise phase on VALU (dw_valu: v_dot4 over the tap table, 4
-    channels of one pixel per item; MFMA only on the 1x1 contractions) in
-    every raster form that admits it, with and without the phase-C split,
-    both requant forms, bit-exact"""
-    import ctypes
-    rng = np.random.default_rng(h * 11 + ce + cout + 5)
-    c = ChainCase(rng, 2, h, h, ce, s, cout, res, ce2, store_pw1=True)
-    for px, waves, split in ((4, 4, 0), (2, 4, 0), (1, 4, 0), (1, 8, 0), (1, 16, 0), (1, 8, 2)):
-        keep = []
-        q = c.params(gpu_lib, px, keep, waves, 0, 0, 0, split, 1)
-        if gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
-            continue
-        _check(c, gpu_lib, px, waves, c_split=split, dw_valu=1)
-    c.fast = False
-    _check(c, gpu_lib, 4, 4, dw_valu=1)
-    keep = []
-    q = c.params(gpu_lib, 4, keep, 4, 1, 0, 0, 0, 1)  # persistent: no VALU form
-    assert gpu_lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0
 
 
 def test_chain_split_rejects(gpu_lib):
@@ -356,12 +324,12 @@ def test_chain_split_rejects(gpu_lib):
 @pytest.mark.parametrize("arch,size", [("deeplab_v3_mobilenet_v2", 100), ("deeplab_v3_mobilenet_v2", 57),
                                        ("posenet_mobilenet_v1", 90), ("posenet_mobilenet_v1", 57),
                                        ("ssd_mobilenet_v2", 100)])
-def test_chain_stem_fused_ragged(gpu_lib, monkeypatch, arch, size):
-    """the RGB stem fused into the first tile chain (BAND_HIP_FUSION=
-    forcestem) on image sizes whose stem output is not a multiple of the
-    8 x 8 tile (ragged right / bottom tiles, odd sizes: SAME padding with a
-    one-sided pad); one-job and job-batched passes bit-exact vs the oracle"""
-    monkeypatch.setenv("BAND_HIP_FUSION", "forcestem")
+def test_chain_tile_ragged_models(gpu_lib, monkeypatch, arch, size):
+    """whole models in the tile form (BAND_HIP_FUSION=forcetile) on image
+    sizes whose layers are not multiples of the 8 x 8 tile (ragged right /
+    bottom tiles, odd sizes: SAME padding with a one-sided pad); one-job
+    and job-batched passes bit-exact vs the oracle"""
+    monkeypatch.setenv("BAND_HIP_FUSION", "forcetile")
     buf = getattr(S, arch)(np.int8, size=size)
     om = OModel(buf)
     t = om.tensors[om.inputs[0]]
@@ -374,7 +342,7 @@ def test_chain_stem_fused_ragged(gpu_lib, monkeypatch, arch, size):
     assert ex.PrepareSubgraph(m).ok()
     key = SubgraphKey(43, 1)
     kernels = [r["kernel"] for r in ex.ProfileSubgraph(key, iters=1)]
-    assert kernels[0] == "chain_tile_kernel" and not any(k.startswith("conv_stem") for k in kernels), kernels
+    assert "chain_tile_kernel" in kernels, kernels
     for rep in range(2):
         ex.GetTensorView(key, om.inputs[0]).GetData()[...] = xs[0]
         assert ex.ExecuteSubgraph(key).ok()

@@ -13,7 +13,8 @@ import kernel_resources as kr  # noqa: E402
 
 def test_choice_codes_decode_like_fusion_cc():
     # px_blocks, +10 two-launch form, +100 16 waves, +200 persistent,
-    # +300 8 waves, +400.. tile, +1000 deep, +2000*(s-1) split, +8000 VALU
+    # +300 8 waves, +400.. tile, +1000 deep, +2000*(s-1) split; stage forms
+    # from 100000
     f = co.decode(2101)
     assert (f["c_split"], f["waves"], f["px_blocks"], f["three"], f["tile"]) == (2, 16, 1, True, 0)
     f = co.decode(404)
@@ -26,8 +27,8 @@ def test_choice_codes_decode_like_fusion_cc():
     assert (f["px_blocks"], f["three"], f["waves"]) == (2, False, 4)
     f = co.decode(1001)
     assert (f["deep"], f["px_blocks"]) == (1, 1)
-    f = co.decode(8004)
-    assert (f["dw_valu"], f["px_blocks"], f["three"]) == (1, 4, True)
+    f = co.decode(100000 + 1000 + 200 + 10 + 1)  # stage 2, 2 slices, 1 block, 8 waves
+    assert (f["stage"], f["c_split"], f["px_blocks"], f["waves"], f["three"]) == (2, 2, 1, 8, True)
     assert not co.decode(0)["fused"]
 
 

@@ -21,10 +21,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--iters", type=int, default=50)
-    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,tp,1d,1w8d,2d",
+    ap.add_argument("--px", default="1,2,4,1w16,1w8,4p,t,1d,1w8d,2d,g1w8,G1w8s2",
                     help="forms: px_blocks [wN waves] [p persistent] [d deep-issue]; t = the 2-D tile form, "
-                         "tp = its persistent double-buffered variant, t3 / t4 = runs of 2 / 4 tiles per workgroup; "
-                         "sN suffix = the phase-C split over N workgroups; v suffix = the VALU depthwise phase; "
+                         "t3 / t4 = runs of 2 / 4 tiles per workgroup; "
+                         "sN suffix = the phase-C split over N workgroups; "
                          "g prefix = the stage form (g1w8s2: 1 pixel block, 8 waves, 2 slices)")
     ap.add_argument("--only", default="", help="comma-separated chain indices")
     a = ap.parse_args()
@@ -47,17 +47,15 @@ def main():
             # "g1w8s2": the stage form, 1 block, 8 waves, 2 slices; "G": with loader waves (stage 2)
             stage = 1 if form.startswith("g") else (2 if form.startswith("G") else 0)
             form = form[1:] if stage else form
-            valu = int(form.endswith("v"))
-            form = form[:-1] if valu else form
             if "s" in form and not form.startswith("t"):  # "1s2": the phase-C split over 2 workgroups
                 form, split = form.split("s")[0], int(form.split("s")[1])
-            tile = {"t": 1, "tp": 2, "t3": 3, "t4": 4}.get(form, 0)
+            tile = {"t": 1, "t3": 3, "t4": 4}.get(form, 0)
             persist = int(form.endswith("p") and not tile)
             deep = int(form.endswith("d"))
             f = "4" if tile else form.rstrip("pd")
             px, waves = (int(f.split("w")[0]), int(f.split("w")[1])) if "w" in f else (int(f), 4)
             keep = []
-            q = c.params(lib, px, keep, waves, persist, tile, deep, split, valu, stage)
+            q = c.params(lib, px, keep, waves, persist, tile, deep, split, stage)
             if lib.bh_chain_lds_bytes(ctypes.byref(q)) == 0:
                 row.append("   -   ")
                 continue

@@ -35,8 +35,11 @@ CUS = 256
 
 def decode(choice):
     """fusion.cc FuseChains: choice code -> form fields"""
-    f = dict(dw_valu=int(choice >= 8000))
-    choice %= 8000
+    if choice >= 100000:  # kStageChoice + 1000 (stage - 1) + 100 slices + 10 px_blocks + (8 waves)
+        c = choice - 100000
+        return dict(stage=1 + c // 1000, c_split=(c % 1000) // 100, px_blocks=(c // 10) % 10,
+                    waves=8 if c % 10 else 4, deep=0, three=True, persist=0, tile=0, fused=True)
+    f = dict(stage=0)
     f["c_split"] = choice // 2000 + 1 if choice >= 2000 else 0
     choice %= 2000
     f["deep"] = int(choice >= 1000)

@@ -14,8 +14,9 @@ tensor -> request ring, band/engine.cc:455-529) -> planner thread ->
 scheduler -> worker queue (band/planner.cc:268-365) -> Worker::Work: input
 copy into the executor's view, IModelExecutor::ExecuteSubgraph on the GPU,
 output copy (band/worker.cc:222-323) -> Wait.  A native closed-loop driver
-(BandxEngineRunClosedLoop) keeps 2 x workers x job-batch requests in flight;
-the engine's request rings apply back-pressure beyond 128 per model.
+(BandxEngineRunClosedLoop) keeps 1.25 x workers x job-batch requests in
+flight (2 x workers with one job per pass); the engine's request rings apply
+back-pressure beyond 128 per model.
 
 A STEP is one round of `--jobs-per-step` jobs (default 1024, 256 of each mix
 model): `--steps K --warmup W` times exactly K x 1024 jobs after W x 1024
@@ -23,11 +24,14 @@ warm-up jobs, so the driver's `--steps 20 --warmup 5` times 20,480 jobs in
 steady state.  Job latency = end - enqueue of the planner's job record
 (band/common.h:351-353).
 
-Job batching (--job-batch B, default 24; BANDX_WORKER_MAX_JOB_BATCH): an
+Job batching (--job-batch B, default 32; BANDX_WORKER_MAX_JOB_BATCH): an
 idle GPU worker takes up to B queued requests of one model from round_robin
 and runs them as ONE pass over a batch-B variant of the model's subgraph
 (every job still gets its own input copy, its own outputs, its own job
-record).  Band itself runs one job per ExecuteSubgraph; that configuration
+record).  The pass-size policy (--pass-target-us, default 700;
+BANDX_WORKER_PASS_TARGET_US) caps a model's pass at the jobs whose expected
+pass time fits the target, so the slowest model of the mix (DeepLab, whose
+32-job pass is ~1.3 ms) does not set every job's latency tail.  Band itself runs one job per ExecuteSubgraph; that configuration
 (8 GPU workers, no batching) is measured in the same run and reported as
 "band_one_job_per_pass".
 
@@ -97,7 +101,8 @@ def parse():
     p.add_argument("--scheduler", default="round_robin",
                    choices=["round_robin", "fixed_worker", "shortest_expected_latency",
                             "heterogeneous_earliest_finish_time"])
-    p.add_argument("--inflight", type=int, default=0, help="outstanding requests (default 2 x workers x job batch)")
+    p.add_argument("--inflight", type=int, default=0,
+                   help="outstanding requests (default 1.25 x workers x job batch; 2 x workers without batching)")
     p.add_argument("--device", default="gpu", choices=["gpu", "cpu"],
                    help="cpu: --workers-per-gpu Band CPU workers instead of GPU workers (C1 / CPU tests; no roofline)")
     p.add_argument("--size", type=int, default=0, help="input edge (default 224; EfficientDet 448)")
@@ -105,10 +110,10 @@ def parse():
                    help="skip the one-job-per-pass (Band semantics) line reported beside a job-batched run")
     p.add_argument("--band1-workers", type=int, default=48,
                    help="GPU workers per GPU of the band_one_job_per_pass line (Band's own contract)")
-    p.add_argument("--job-batch", type=int, default=24,
+    p.add_argument("--job-batch", type=int, default=32,
                    help="max queued jobs of one model a GPU worker runs as one batched pass "
                         "(BANDX_WORKER_MAX_JOB_BATCH; 1 = Band's one job per ExecuteSubgraph)")
-    p.add_argument("--pass-target-us", type=int, default=0,
+    p.add_argument("--pass-target-us", type=int, default=700,
                    help="pass-size policy of job batching (BANDX_WORKER_PASS_TARGET_US): a model's pass takes at "
                         "most the jobs whose expected pass time fits this many microseconds (0 = off)")
     p.add_argument("--share-profiles", type=int, default=-1, choices=[-1, 0, 1],
@@ -125,6 +130,17 @@ def parse():
     p.add_argument("--profile-only", action="store_true",
                    help="run only the profiled batch passes (rocprofv3 traces); prints their per-kernel table")
     return p.parse_args()
+
+
+def default_inflight(workers, job_batch):
+    """requests the closed loop keeps in flight: 1.25 x workers x job batch
+    (a pass's worth per worker plus a quarter queued: in-flight 384 -> 320 at
+    8 x 32 cut p99 4.5 -> 4.2 ms at equal throughput, profiles/r06g_*), or
+    2 x workers with one job per pass; the engine's request rings hold back
+    a model's 129th unfinished request"""
+    if job_batch > 1:
+        return max(2 * workers, int(1.25 * workers * job_batch))
+    return 2 * workers
 
 
 def model_list(name, size=0, batch=1):
@@ -739,7 +755,7 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed, names=
             _backend.PinProcessToCpus(sorted(_START_AFFINITY))
     try:
         e, bm, ins = make_engine(args, D, paths, sched, [flag] * n_workers, 0, n_workers, args.job_batch)
-        inflight = args.inflight * n_gpus if args.inflight else 2 * n_workers * max(1, args.job_batch)
+        inflight = args.inflight * n_gpus if args.inflight else default_inflight(n_workers, args.job_batch)
         el, lat, wid = run_closed(e, bm, ins, n_warm, n_timed, inflight, Local())
         per_model = per_model_latency(lat, list(names), len(bm), LAST_MODEL_IDX)
         e.close()
@@ -844,9 +860,7 @@ def main():
     jps = max(M, args.jobs_per_step // M * M)
     args.jobs_per_step = jps
     n_warm, n_timed = max(1, args.warmup) * jps, max(1, args.steps) * jps
-    # 2 x workers x job batch requests in flight (the engine's request rings
-    # hold back a model's 129th unfinished request)
-    inflight = args.inflight or 2 * W * (args.job_batch if batching else 1)
+    inflight = args.inflight or default_inflight(W, args.job_batch)
 
     poisson = None
     single = None
@@ -897,20 +911,25 @@ def main():
     # batching), the same mix and scheduler over 8 GPU workers per GPU
     batch1 = None
     if batching and not poisson and not args.no_batch1 and not args.single_engine:
-        W1 = args.band1_workers
-        e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1, seed_offset=D.rank)
+        def band1_line(W1, n1):
+            e1, bm1, in1 = make_engine(args, D, paths, sched, [DeviceFlag.kGPU] * W1, 0, W1, 1, seed_offset=D.rank)
+            el1, lat1, _ = run_closed(e1, bm1, in1, max(n_warm // 4, 2 * W1 * M), n1, 2 * W1, D)
+            e1.close()
+            l1 = np.array([x for part in D.gather((lat1 * 1e-3).tolist()) for x in part])
+            return {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "jobs": n1,
+                    "p50_job_latency_ms": float(np.percentile(l1, 50)),
+                    "p99_job_latency_ms": float(np.percentile(l1, 99)),
+                    "engine_calls": "band/interface only (max_job_batch 1): TryCopyInputTensors -> "
+                                    "ExecuteSubgraph -> TryCopyOutputTensors per job",
+                    "backend_coalescing": dict(COALESCE),
+                    "process_cpu_cores": HOST_THREADS.get("process_cpu_cores"),
+                    "busiest_threads": HOST_THREADS.get("busiest", [])[:6]}
         n1 = max(n_timed // 4, 16 * M)
-        el1, lat1, _ = run_closed(e1, bm1, in1, max(n_warm // 4, 2 * W1 * M), n1, 2 * W1, D)
-        l1 = np.array([x for part in D.gather((lat1 * 1e-3).tolist()) for x in part])
-        batch1 = {"value": n1 * D.world / el1, "unit": "inferences/s", "workers_per_gpu": W1, "jobs": n1,
-                  "p50_job_latency_ms": float(np.percentile(l1, 50)),
-                  "p99_job_latency_ms": float(np.percentile(l1, 99)),
-                  "engine_calls": "band/interface only (max_job_batch 1): TryCopyInputTensors -> "
-                                  "ExecuteSubgraph -> TryCopyOutputTensors per job",
-                  "backend_coalescing": dict(COALESCE),
-                  "process_cpu_cores": HOST_THREADS.get("process_cpu_cores"),
-                  "busiest_threads": HOST_THREADS.get("busiest", [])[:6]}
-        e1.close()
+        batch1 = band1_line(args.band1_workers, n1)
+        # the same contract at a worker count an 8-GPU engine can carry
+        # (12 per GPU = 96 worker threads on a node)
+        if args.band1_workers > 12:
+            batch1["at_12_workers_per_gpu"] = band1_line(12, max(n1 // 2, 16 * M))
 
     # N > 1: the same C3 workload through ONE engine spanning every GPU, with
     # W workers per GPU and with one worker per GPU (north_star's "One Worker

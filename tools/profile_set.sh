@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# Round-5 profile set (same steps as tools/profile_r04.sh) on an MI355X box (outputs in gpurun_out/<tag>_*;
+# The profile set on an MI355X box (outputs in gpurun_out/<tag>_*;
 # rocprofv3's own directories stay in a scratch dir on the box):
 #   0. the default bench line, untraced; its measured kernel / fusion
 #      choices go to a tune file every later run replays;
@@ -17,7 +17,7 @@
 #   7. the default bench line again, now with the PMC traffic in place.
 # Profile-only passes use eager launches (--no-graph): same kernels, grids
 # and batches as the graph replay.
-# usage: tools/profile_r05.sh <tag>
+# usage: tools/profile_set.sh <tag>
 set -uo pipefail
 TAG=${1:?tag}
 R=${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}

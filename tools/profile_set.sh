@@ -46,8 +46,11 @@ step "3 FETCH_SIZE done"
 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$W/${TAG}_pmcw" -o run -- \
   python3 bench.py --profile-only --no-graph > "$O/${TAG}_pmcw.log" 2> "$O/${TAG}_pmcw.err" || exit $?
 step "4 WRITE_SIZE done"
-python3 tools/pmc_traffic.py "$W/${TAG}_pmcf" "$W/${TAG}_pmcw" "$O/${TAG}_pmc_traffic.json" --batch 24 \
-  --config "bench.py --profile-only: C3 mix batch-24 passes" > "$O/${TAG}_pmc_traffic.txt" || exit $?
+# the batch the profile-only passes ran at (bench.py's default job batch)
+PB=$(python3 -c "import json,sys; print(json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])['pass_batch'])" \
+  "$O/${TAG}_profile_only.json") || exit $?
+python3 tools/pmc_traffic.py "$W/${TAG}_pmcf" "$W/${TAG}_pmcw" "$O/${TAG}_pmc_traffic.json" --batch "$PB" \
+  --config "bench.py --profile-only: C3 mix batch-$PB passes" > "$O/${TAG}_pmc_traffic.txt" || exit $?
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS"
 P2="SQ_INSTS_MFMA SQ_INSTS_VALU_MFMA_I8 SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM"
 n=0

@@ -5,7 +5,7 @@
 out=${1:-gpurun_out/ceiling_sweep.jsonl}
 : > "$out"
 run() {
-  env "$@" PLANNER_CEILING_SAMPLE=1 timeout -k 10 120 python tools/planner_ceiling.py --workers 8 --job-batch 24 \
+  env "$@" PLANNER_CEILING_SAMPLE=1 timeout -k 10 120 python tools/planner_ceiling.py --workers 8 --job-batch ${CEIL_JB:-32} \
     --jobs 400000 $EXTRA >> "$out" 2>/dev/null || return 1
 }
 EXTRA="" run BANDX_DRIVER_READERS=2 &&

@@ -230,6 +230,62 @@ __device__ __forceinline__ int xcd_block(int hw, int total) {
   return hw < (per << 3) ? (hw & 7) * per + (hw >> 3) : hw;
 }
 
+// 2-D XCD split of a GEMM's gm x gn output-block grid: (8 / xb) pixel
+// ranges x xb channel ranges, one per XCD, so each L2 pulls 1 / (8 / xb) of
+// the input and 1 / xb of the filters (xb = 1: the input read once and the
+// filters 8 times; xb = 8: the other way round; 2 / 4 between).  Hardware
+// block i runs on XCD i % 8 and walks that XCD's ranges N-blocks fastest;
+// the ranges are balanced (sizes differ by at most one block), the grid is
+// 8 x the largest range pair, and the blocks past an XCD's share get
+// bm = gm and must exit.  xb 0: the 1-D order of xcd_block over the
+// row-major grid (N-blocks fastest), for grids the split would pad by more
+// than 1/8.
+struct XcdSplit {
+  int xb, sub_m, sub_n;
+};
+__device__ __forceinline__ void xcd_tile(int hw, int total, const XcdSplit& x, int gm, int gn, int& bm, int& bn) {
+  if (x.xb == 0) {
+    const int l = xcd_block(hw, total);
+    bm = l / gn;
+    bn = l - bm * gn;
+    return;
+  }
+  const int a = 8 / x.xb;
+  const int xcd = hw & 7, j = hw >> 3;
+  const int pa = xcd / x.xb, pb = xcd - pa * x.xb;
+  const int m_lo = pa * gm / a, sm = (pa + 1) * gm / a - m_lo;
+  const int n_lo = pb * gn / x.xb, sn = (pb + 1) * gn / x.xb - n_lo;
+  if (j >= sm * sn) {
+    bm = gm;
+    bn = 0;
+    return;
+  }
+  const int jm = j / sn;
+  bm = m_lo + jm;
+  bn = n_lo + (j - jm * sn);
+}
+// host: the split with the fewest L2-fill bytes xb * in + (8 / xb) * w over
+// the splits that give every XCD at least one pixel and one channel block
+// and pad the grid by at most 1/8 (ties: fewer channel ranges); else xb 0
+inline XcdSplit xcd_split(long in_bytes, long w_bytes, int gm, int gn) {
+  XcdSplit best{0, gm, gn};
+  long cost = -1;
+  const long blocks = (long)gm * gn;
+  for (int xb = 1; xb <= 8; xb *= 2) {
+    const int a = 8 / xb;
+    if (xb > gn || a > gm) continue;
+    const int sub_m = (gm + a - 1) / a, sub_n = (gn + xb - 1) / xb;
+    if (8L * sub_m * sub_n * 8 > blocks * 9) continue;
+    const long c = xb * in_bytes + a * w_bytes;
+    if (cost < 0 || c < cost) {
+      cost = c;
+      best = {xb, sub_m, sub_n};
+    }
+  }
+  return best;
+}
+inline int xcd_grid(const XcdSplit& x) { return x.xb ? 8 * x.sub_m * x.sub_n : x.sub_m * x.sub_n; }
+
 }  // namespace bh
 
 // thread-local last-error plumbing for the C ABI (defined in capi_runtime.hip)

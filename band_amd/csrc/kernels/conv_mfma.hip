@@ -230,11 +230,11 @@ __device__ __forceinline__ void conv_epilogue4(const bh_conv_params& p, v4i acc,
 constexpr int KU = 4;  // K-steps whose loads are issued together
 
 // WM x WN 16x16 tiles per wave; waves arranged WAVES_M x WAVES_N x SPLITK.
-// One workgroup's tile: `logical` is its block index in the layer's
-// gm x nblocks grid (conv_mfma_kernel, or a member of a grouped launch).
+// One workgroup's tile: (bm, bn) in the layer's output-block grid
+// (conv_mfma_kernel, or a member of a grouped launch).
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
 __device__ __forceinline__ void conv_mfma_tile(const bh_conv_params& p, int M, int K, int N, int kchunk,
-                                               const ConvDivs& dv, int nblocks, int xcd, int logical, int total) {
+                                               const ConvDivs& dv, int bm, int bn) {
   static_assert(WAVES_M * WAVES_N * SPLITK == 4, "4 waves per workgroup");
   constexpr int TM = WAVES_M * WM * 16;
   constexpr int TN = WAVES_N * WN * 16;
@@ -245,15 +245,6 @@ __device__ __forceinline__ void conv_mfma_tile(const bh_conv_params& p, int M, i
   const int wt = wave % (WAVES_M * WAVES_N);
   const int wave_m = wt % WAVES_M;
   const int wave_n = wt / WAVES_M;
-  int bm, bn;
-  if (xcd == 2) {
-    const int gm = total / nblocks;
-    bn = logical / gm;
-    bm = logical - bn * gm;
-  } else {
-    bm = logical / nblocks;
-    bn = logical - bm * nblocks;
-  }
   const int m0 = bm * TM + wave_m * WM * 16;
   const int n0 = bn * TN + wave_n * WN * 16;
   const int r16 = lane & 15;
@@ -371,16 +362,13 @@ __device__ __forceinline__ void conv_mfma_tile(const bh_conv_params& p, int M, i
 
 template <int WM, int WN, int WAVES_M, int WAVES_N, int SPLITK, bool IS1X1, int VEC>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(bh_conv_params p, int M, int K, int N, int kchunk, ConvDivs dv,
-                                                        int nblocks, int xcd) {
-  // 1-D grid; with xcd each XCD (hardware ids i % 8) runs a contiguous run
-  // of logical blocks.  xcd 1: N-blocks fastest, so all N-blocks of a pixel
-  // block - which read the same input rows - share one L2 (the filters are
-  // read once per XCD).  xcd 2 (filters larger than the input): pixel blocks
-  // fastest, so each XCD reads only its slice of the filters and the small
-  // input is the operand read once per XCD.
-  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-  conv_mfma_tile<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>(p, M, K, N, kchunk, dv, nblocks, xcd, logical,
-                                                               (int)gridDim.x);
+                                                        int gm, int gn, XcdSplit xs) {
+  // 1-D grid in the 2-D XCD split (xcd_tile): each XCD's L2 holds one pixel
+  // range of the input and one channel range of the filters
+  int bm, bn;
+  xcd_tile((int)blockIdx.x, (int)gridDim.x, xs, gm, gn, bm, bn);
+  if (bm >= gm) return;
+  conv_mfma_tile<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>(p, M, K, N, kchunk, dv, bm, bn);
 }
 
 // ---------------------------------------------------------------------------
@@ -430,10 +418,10 @@ __global__ __launch_bounds__(256) void conv_group_kernel(ConvGroupArgs a) {
   const ConvGroupMember& e = tab[i];
   const int local = b - e.blk0;
   switch (e.form) {
-    case 0: conv_mfma_tile<1, 1, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
-    case 1: conv_mfma_tile<1, 1, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
-    case 2: conv_mfma_tile<2, 2, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
-    default: conv_mfma_tile<2, 2, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, e.gn, 0, local, e.blocks); break;
+    case 0: conv_mfma_tile<1, 1, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, local / e.gn, local % e.gn); break;
+    case 1: conv_mfma_tile<1, 1, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, local / e.gn, local % e.gn); break;
+    case 2: conv_mfma_tile<2, 2, 1, 1, 4, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, local / e.gn, local % e.gn); break;
+    default: conv_mfma_tile<2, 2, 2, 2, 1, IS1X1, 16>(e.p, e.M, e.K, e.N, e.kchunk, e.dv, local / e.gn, local % e.gn); break;
   }
 }
 
@@ -449,13 +437,9 @@ static int launch_cfg(const bh_conv_params& p, int M, int K, int N, hipStream_t 
   dv.in_c = FastDiv(p.in_c);
   dv.k_w = FastDiv(p.k_w);
   const int gm = (M + TM - 1) / TM, gn = (N + TN - 1) / TN;
-  // replicate the smaller operand over the 8 XCDs' L2s: 8 x filters + input
-  // (xcd 1) against filters + 8 x input (xcd 2)
-  const long in_bytes = (long)p.batch * p.in_h * p.in_w * p.in_c;
-  const long w_bytes = (long)N * K;
-  const int xcd = w_bytes > in_bytes ? 2 : 1;
-  BH_LAUNCH((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(gm * gn), dim3(256), 0,
-                     s, p, M, K, N, kchunk, dv, gn, xcd);
+  const XcdSplit xs = xcd_split((long)p.batch * p.in_h * p.in_w * p.in_c, (long)N * K, gm, gn);
+  BH_LAUNCH((conv_mfma_kernel<WM, WN, WAVES_M, WAVES_N, SPLITK, IS1X1, VEC>), dim3(xcd_grid(xs)), dim3(256), 0,
+                     s, p, M, K, N, kchunk, dv, gm, gn, xs);
   return bh_check_launch("conv_mfma_kernel");
 }
 
@@ -491,8 +475,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 }
 
 template <int WM, int WN, int WAVES_M, int WAVES_N, int NB>
-__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_conv_params p, int M, int K,
-                                                                          int nblocks, int ksteps, int xcd) {
+__global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_conv_params p, int M, int K, int gm,
+                                                                          int gn, int ksteps, XcdSplit xs) {
   constexpr int W = WAVES_M * WAVES_N;
   static_assert(W == 4 || W == 8, "4 or 8 waves per workgroup");
   static_assert(NB >= 2 && NB <= 4, "LDS ring depth");
@@ -509,17 +493,10 @@ __global__ __launch_bounds__(WAVES_M* WAVES_N * 64) void conv_gemm_kernel(bh_con
   __shared__ __attribute__((aligned(16))) uint8_t lds[NB * STAGE];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  // xcd: as in conv_mfma_kernel (1 = N-blocks fastest, 2 = pixel blocks fastest)
-  const int logical = xcd ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  // the 2-D XCD split, as in conv_mfma_kernel
   int bm, bn;
-  if (xcd == 2) {
-    const int gm = gridDim.x / nblocks;
-    bn = logical / gm;
-    bm = logical - bn * gm;
-  } else {
-    bm = logical / nblocks;
-    bn = logical - bm * nblocks;
-  }
+  xcd_tile((int)blockIdx.x, (int)gridDim.x, xs, gm, gn, bm, bn);
+  if (bm >= gm) return;
   const int tm0 = bm * BM;
   const int tn0 = bn * BN;
   const int N = p.out_c;
@@ -607,9 +584,9 @@ static int launch_gemm(const bh_conv_params& p, int M, int K, hipStream_t s) {
   constexpr int BM = WAVES_M * WM * 16;
   constexpr int BN = WAVES_N * WN * 16;
   const int gm = (M + BM - 1) / BM, gn = (p.out_c + BN - 1) / BN;
-  const int xcd = (long)p.out_c * K > (long)M * K ? 2 : 1;
-  BH_LAUNCH((conv_gemm_kernel<WM, WN, WAVES_M, WAVES_N, NB>), dim3(gm * gn), dim3(WAVES_M * WAVES_N * 64), 0, s,
-            p, M, K, gn, (K + 63) / 64, xcd);
+  const XcdSplit xs = xcd_split((long)M * K, (long)p.out_c * K, gm, gn);
+  BH_LAUNCH((conv_gemm_kernel<WM, WN, WAVES_M, WAVES_N, NB>), dim3(xcd_grid(xs)), dim3(WAVES_M * WAVES_N * 64), 0,
+            s, p, M, K, gm, gn, (K + 63) / 64, xs);
   return bh_check_launch("conv_gemm_kernel");
 }
 

@@ -29,7 +29,23 @@ def test_choice_codes_decode_like_fusion_cc():
     assert (f["deep"], f["px_blocks"]) == (1, 1)
     f = co.decode(100000 + 1000 + 200 + 10 + 1)  # stage 2, 2 slices, 1 block, 8 waves
     assert (f["stage"], f["c_split"], f["px_blocks"], f["waves"], f["three"]) == (2, 2, 1, 8, True)
+    f = co.decode(2000 * 3 + 101)  # 16 waves, 4 slices
+    assert (f["deep"], f["waves"], f["c_split"], f["px_blocks"], f["three"]) == (0, 16, 4, 1, True)
     assert not co.decode(0)["fused"]
+
+
+def test_instantiation_names():
+    # the kernel names chain_occupancy looks up in the resource table
+    class Conv:
+        k_pad = 960
+
+    class Q:
+        has_pw2 = True
+        pw2 = Conv()
+
+    assert co.instantiation(Q, co.decode(2000 * 3 + 101), True)[0] == "chain_kernel<1, true, 5, 16, false, 2, 2>"
+    assert co.instantiation(Q, co.decode(1301), False)[0] == "chain_kernel<1, false, 5, 8, false, 6, 0>"
+    assert co.instantiation(Q, co.decode(100000 + 1000 + 200 + 10 + 1), True) == ("chain_stage_kernel<1, true", 8)
 
 
 def test_waves_per_simd_tables():

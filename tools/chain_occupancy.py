@@ -66,11 +66,13 @@ def load_resources(path):
 
 def instantiation(q, f, fast):
     F = "true" if fast else "false"
+    if f["stage"]:
+        return "chain_stage_kernel<%d, %s" % (f["px_blocks"], F), f["waves"]
     if f["tile"]:
         return "chain_tile_kernel<8, 8, %s" % F, 4
     k2 = (not q.has_pw2) or q.pw2.k_pad <= 128
     kx = 2 if k2 else 5
-    var = (1 if f["dw_valu"] else 0) | (2 if f["c_split"] > 1 else 0)
+    var = 2 if f["c_split"] > 1 else 0
     if f["deep"]:
         rb, nw = (2, 4) if f["px_blocks"] == 2 else (1, f["waves"] if f["waves"] == 8 else 4)
         return "chain_kernel<%d, %s, %d, %d, false, 6, 0>" % (rb, F, kx, nw), nw
@@ -120,7 +122,7 @@ def main():
                          store_pw1=bool(store) if f["three"] else True)
         keep = []
         q = case.params(lib, max(f["px_blocks"], 1), keep, f["waves"], 0, f["tile"], f["deep"], f["c_split"],
-                        f["dw_valu"])
+                        f["stage"])
         lds = lib.bh_chain_lds_bytes(ctypes.byref(q))
         if lds == 0:
             print("%-40s choice %d: not launchable here" % (str(tag), choice))
@@ -154,8 +156,8 @@ def main():
         ms = ctypes.c_float()
         lib.bh_event_elapsed_ms(e0, e1, ctypes.byref(ms))
         us = 1e3 * ms.value / a.iters
-        form = ("t%d" % f["tile"]) if f["tile"] else "%d%s%s%s" % (
-            f["px_blocks"], "w%d" % f["waves"] if f["waves"] != 4 else "", "d" if f["deep"] else "",
+        form = ("t%d" % f["tile"]) if f["tile"] else "%s%d%s%s%s" % (
+            "gG"[f["stage"] - 1] if f["stage"] else "", f["px_blocks"], "w%d" % f["waves"] if f["waves"] != 4 else "", "d" if f["deep"] else "",
             "s%d" % f["c_split"] if f["c_split"] > 1 else "")
         label = "%dx%d x%d s%d d%d -> %d%s -> %d" % (h, w, c, s, dil, cout, "+res" if r else "", nxt)
         print("%-40s %-6s %-44s %7.1f %6d %5s %4d %4d %-14s %6.2f %8.2f" % (

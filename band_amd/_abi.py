@@ -246,10 +246,6 @@ KERNEL_SYMBOLS = {
     "bh_chain_tile_pack": (c_int, [ctypes.POINTER(ChainParams), c_void_p, c_void_p]),
     "bh_chain_stage_lds_bytes": (c_size_t, [ctypes.POINTER(ChainParams)]),
     "bh_chain_stage_launch": (c_int, [ctypes.POINTER(ChainParams), c_void_p]),
-    "bh_chain_seq_lds_bytes": (c_size_t, [ctypes.POINTER(ChainParams), c_int]),
-    "bh_chain_seq_i8": (c_int, [ctypes.POINTER(ChainParams), c_void_p, c_int, c_void_p]),
-    "bh_chain_seq_table_bytes": (c_size_t, []),
-    "bh_chain_seq_plan": (c_int, [ctypes.POINTER(ChainParams), c_int, c_void_p]),
     "bh_last_error": (ctypes.c_char_p, []),
 }
 

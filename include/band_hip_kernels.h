@@ -430,28 +430,6 @@ size_t bh_chain_tile_blob_bytes(const bh_chain_params* p);
 int bh_chain_tile_pack(const bh_chain_params* p, void* blob, bh_stream_t s);
 int bh_chain_i8(const bh_chain_params* p, bh_stream_t s);
 
-/* Image-resident chain sequence (chain_seq_kernel): a run of n (2 ..
- * BH_SEQ_MAX) three-launch chains executed by ONE 8-wave workgroup per
- * image, every block output kept in LDS and every expanded tensor produced
- * and consumed in chunks of <= 256 channels - for the 14x14 / 7x7 stages at
- * small batch, where the per-layer launches are boundary- and latency-bound.
- * chains[i + 1].dw.input must be chains[i].pw2.output and
- * chains[i + 1].pw1.residual NULL or chains[i].pw1.output; those
- * intermediates are NOT written (the caller guarantees nobody else reads
- * them).  Stored: the last chain's pw1.output (when set) and pw2.output.
- * Depthwise 3x3, stride 1 / 2, pad <= 1, images <= 16 x 16, channels a
- * multiple of 64 (<= 1280); every layer int8 with the single-step requant
- * (requant_fast).  bh_chain_seq_plan fills `host_table`
- * (bh_chain_seq_table_bytes() bytes: the run's geometry and a copy of the
- * chains, whose filters and tables the kernel reads); the caller copies it
- * to device memory and passes that as `table`.  The run's input / residual
- * / output pointers are taken from `chains` at each launch. */
-#define BH_SEQ_MAX 12
-size_t bh_chain_seq_lds_bytes(const bh_chain_params* chains, int n);
-size_t bh_chain_seq_table_bytes(void);
-int bh_chain_seq_plan(const bh_chain_params* chains, int n, void* host_table);
-int bh_chain_seq_i8(const bh_chain_params* chains, const void* table, int n, bh_stream_t s);
-
 /* MEAN over one contiguous run of axes (TFLite 2.9.2 reduce.cc EvalMean ->
  * optimized_integer_ops::Mean int8 / optimized_ops::Mean uint8 / float):
  * the input viewed as [outer][reduce][inner]; out[o][i] = for 8-bit types

@@ -356,11 +356,12 @@ def cpu_baseline(args, models, paths, seconds):
 
 
 def kernel_source_tag():
-    """hash of the kernel sources: PMC traffic figures are only reported for
-    the tree they were measured on"""
+    """hash of the kernel sources and their build recipe (compiler flags
+    change the code): PMC traffic figures are only reported for the tree
+    they were measured on"""
     h = hashlib.sha1()
     for f in sorted(glob.glob(os.path.join(ROOT, "band_amd", "csrc", "kernels", "*"))) + \
-            [os.path.join(ROOT, "include", "band_hip_kernels.h")]:
+            [os.path.join(ROOT, "include", "band_hip_kernels.h"), os.path.join(ROOT, "band_amd", "csrc", "Makefile")]:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]

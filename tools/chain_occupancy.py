@@ -16,8 +16,8 @@ of one workgroup, 160 KiB / LDS, 32 waves per CU / waves per workgroup)
 `rounds` = grid / (256 CUs x resident workgroups): below 1 the launch does
 not fill the chip; the launch time is measured here with HIP events.
 
-usage: python tools/chain_occupancy.py --tune profiles/r05g_tune.txt \
-         --resources profiles/r05am_chain_resources.tsv [--batch 24]
+usage: python tools/chain_occupancy.py --tune profiles/r06s_tune.txt \
+         --resources <tools/kernel_resources.py output> [--batch 24]
 """
 import argparse
 import ctypes

@@ -33,7 +33,9 @@ BANDX_WORKER_PASS_TARGET_US) caps a model's pass at the jobs whose expected
 pass time fits the target, so the slowest model of the mix (DeepLab, whose
 32-job pass is ~1.3 ms) does not set every job's latency tail.  Band itself runs one job per ExecuteSubgraph; that configuration
 (8 GPU workers, no batching) is measured in the same run and reported as
-"band_one_job_per_pass".
+"band_one_job_per_pass"; "latency_point" is the same engine with smaller
+passes and fewer requests in flight (--latency-point, default job batch 24,
+500 us pass target, 200 in flight), the tail-latency side of the trade.
 
 N>1 (torchrun, one process per GPU): each rank serves its own job stream
 with its own engine over its GPU; jobs shard across GPUs with no data-path
@@ -116,6 +118,9 @@ def parse():
     p.add_argument("--pass-target-us", type=int, default=700,
                    help="pass-size policy of job batching (BANDX_WORKER_PASS_TARGET_US): a model's pass takes at "
                         "most the jobs whose expected pass time fits this many microseconds (0 = off)")
+    p.add_argument("--latency-point", default="24,500,200",
+                   help="JOB_BATCH,PASS_TARGET_US,INFLIGHT of the latency_point line beside a job-batched N = 1 "
+                        "headline (the same engine with smaller passes and fewer requests in flight); '' = skip")
     p.add_argument("--share-profiles", type=int, default=-1, choices=[-1, 0, 1],
                    help="BANDX_PROFILE_SHARE_IDENTICAL: identical workers share latency estimates; -1 (default) = "
                         "on for the latency-driven schedulers (SEL / HEFT: C4, C5), 0 = the reference's "
@@ -866,6 +871,7 @@ def main():
     poisson = None
     single = None
     host_threads = None
+    head_model_idx = []
     if args.single_engine:
         # headline: one process, one engine over all --gpus GPUs
         assert D.world == 1, "--single-engine runs in one process (no torchrun)"
@@ -897,6 +903,7 @@ def main():
             elapsed = D.max(t1 - t0)
         else:
             elapsed, lat_us, worker_ids = run_closed(engine, band_models, inputs, n_warm, n_timed, inflight, D)
+            head_model_idx = list(LAST_MODEL_IDX)  # the side lines below run their own loops
             host_threads = dict(HOST_THREADS)
             if HOST_THREAD_STATES:
                 host_threads["thread_states"] = dict(HOST_THREAD_STATES)
@@ -931,6 +938,29 @@ def main():
         # (12 per GPU = 96 worker threads on a node)
         if args.band1_workers > 12:
             batch1["at_12_workers_per_gpu"] = band1_line(12, max(n1 // 2, 16 * M))
+
+    # the latency / throughput trade beside the headline: the same workload
+    # and engine shape with smaller passes and fewer requests in flight
+    # (p99 near 3 ms at about 105k inf/s per GPU)
+    latency_point = None
+    if (batching and not poisson and not args.single_engine and D.world == 1 and on_gpu and args.latency_point
+            and not args.no_batch1):
+        jb2, pt2, inf2 = (int(v) for v in args.latency_point.split(","))
+        pt_head = args.pass_target_us
+        args.pass_target_us = pt2
+        try:
+            e2, bm2, in2 = make_engine(args, D, paths, sched, workers, n_cpu, W, jb2, seed_offset=D.rank)
+        finally:
+            args.pass_target_us = pt_head
+        el2, lat2, _ = run_closed(e2, bm2, in2, n_warm, n_timed, inf2, D)
+        e2.close()
+        l2 = np.asarray(lat2) * 1e-3
+        latency_point = {"value": n_timed / el2, "unit": "inferences/s", "job_batch": jb2, "pass_target_us": pt2,
+                         "inflight": inf2, "jobs": n_timed,
+                         "p50_job_latency_ms": float(np.percentile(l2, 50)),
+                         "p99_job_latency_ms": float(np.percentile(l2, 99)),
+                         "job_latency_ms_per_model": per_model_latency(lat2, [m[0] for m in models], M,
+                                                                       LAST_MODEL_IDX)}
 
     # N > 1: the same C3 workload through ONE engine spanning every GPU, with
     # W workers per GPU and with one worker per GPU (north_star's "One Worker
@@ -1031,13 +1061,14 @@ def main():
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
             single["p99_job_latency_ms"],
             "job_latency_ms_per_model": single.get("job_latency_ms_per_model") if single and "value" in single else
-            (per_model_latency(lat_us, [m[0] for m in models], M, LAST_MODEL_IDX)
+            (per_model_latency(lat_us, [m[0] for m in models], M, head_model_idx)
              if lat_us is not None and not poisson else None),
             "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
             "gpu_kernel_us_per_inference_at_mean_pass": dev.get("gpu_us_per_inference_at_mean_pass") if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
             "device_us_per_model": dev["device_us"] if dev else None,
             "band_one_job_per_pass": batch1,
+            "latency_point": latency_point,
             "single_engine": single,
             "per_process": per_process,
             "single_engine_one_worker_per_gpu": single_1wpg,

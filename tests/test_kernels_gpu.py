@@ -122,11 +122,14 @@ def test_conv1x1_gemm_big_residual_table(gpu_lib, b, spatial, ch):
 # the RGB stem kernel (conv_stem_kernel: aligned row gathers + byte path at
 # the image's left / right edge and the tensor's end): SAME / VALID padding,
 # stride 1 / 2, odd widths, batch, uint8 (filter zero point), both
-# requantisation paths
+# requantisation paths; the persistent LDS form's multi-tile workgroups
+# (> 768 tiles: batch 64 at 57x61 mixes staged tiles and tiles that span two
+# images, batch 32 at 224x224 is the bench's shape)
 @pytest.mark.parametrize("b,h,w,oc,stride,same,dtype", [
     (2, 224, 224, 32, 2, True, np.int8), (3, 37, 41, 16, 2, True, np.uint8), (1, 15, 13, 24, 1, True, np.int8),
     (5, 31, 29, 32, 1, True, np.uint8), (24, 224, 224, 32, 2, True, np.int8), (2, 11, 10, 64, 2, False, np.uint8),
-    (2, 20, 23, 8, 1, False, np.uint8), (4, 9, 9, 48, 2, False, np.int8), (1, 224, 224, 64, 2, True, np.uint8)])
+    (2, 20, 23, 8, 1, False, np.uint8), (4, 9, 9, 48, 2, False, np.int8), (1, 224, 224, 64, 2, True, np.uint8),
+    (64, 57, 61, 16, 1, True, np.uint8), (32, 224, 224, 32, 2, True, np.int8)])
 def test_conv_stem(gpu_lib, b, h, w, oc, stride, same, dtype):
     rng = np.random.default_rng(5000 + b * h * w + oc + stride)
     c = ConvCase(rng, b, h, w, 3, oc, 3, 3, stride=(stride, stride), same=same, dtype=dtype, act=3)

@@ -63,8 +63,13 @@ __device__ __forceinline__ void stem_row(const bh_conv_params& p, const uint8_t*
   }
 }
 
+// Launch bound: the 4-block forms of up to 48 channels are held to 64-76
+// VGPRs (>= 6 waves per SIMD: a batch-32 stem's 24.5 waves per CU resident
+// at once; unbounded they took 90-104, 4-5 waves per SIMD, and ran in two
+// rounds: 17.0 vs 15.1 us at batch 32, profiles/r06ag_stem_forms.txt).
+// 64 channels at that bound would spill.
 template <int NB, int PB, bool FAST>
-__global__ __launch_bounds__(256) void conv_stem_mfma_kernel(bh_conv_params p, int M, StemDivs dv) {
+__global__ __launch_bounds__(256, (PB == 4 && NB <= 3 ? 6 : 1)) void conv_stem_mfma_kernel(bh_conv_params p, int M, StemDivs dv) {
   const int lane = threadIdx.x & 63;
   const int r16 = lane & 15;
   const int g = lane >> 4;
@@ -193,21 +198,16 @@ static int launch_stem_mfma(const bh_conv_params& p, int M, hipStream_t s) {
 // 3x3 stems over 3 channels, dilation-1 columns, out_c in {16, 32, 48, 64}
 // (4-byte aligned output), no residual: 1 when this kernel takes the layer
 int bh_conv_stem_mfma_ok(const bh_conv_params& p) {
-  // small grids (batch-1 stems, below 65,536 output pixels; BH_STEM_MFMA_MAX_M
-  // overrides), or forced (BH_CONV_STEM_MFMA).  With the untransposed
-  // epilogue (a lane requantises 4 pixels of one channel) it is the fastest
-  // stem at batch 1: 4.2-4.3 us against 4.9 for the scalar-cache VALU form
-  // and 5.2-5.6 for the LDS-staged one; at B = 24 the LDS-staged VALU form
-  // wins, 14.0 vs 14.6-14.9 us (interleaved, profiles/r05z2_stem_h{4,5}_r*).
+  // every batch unless a VALU form is forced: batch 1 4.2-4.3 us against
+  // 4.9 for the scalar-cache VALU form and 5.2-5.6 for the LDS-staged one
+  // (r05z2_stem_h*); with the launch bound above 9.4 / 11.7 / 15.1 us at
+  // batch 16 / 24 / 32 against 11.9 / 14.0 / 18.9 for the LDS-staged form
+  // (profiles/r06ag_stem_forms.txt; that form's broadcast record reads leave
+  // its waves 48 % of their cycles in memory waits, r06af_stem_*_stall_b32).
   // The round-4 transposed epilogue derived the requantisation constants
   // per value and lost everywhere (r05l_stem_ab.txt).
-  static const long max_m = [] {
-    const char* e = std::getenv("BH_STEM_MFMA_MAX_M");
-    return e ? std::atol(e) : 65535L;
-  }();
-  const long M = (long)p.batch * p.out_h * p.out_w;
   const bool want = p.kernel_hint == BH_CONV_STEM_MFMA ||
-                    (p.kernel_hint != BH_CONV_STEM_VALU && p.kernel_hint != BH_CONV_STEM_SCALAR && M <= max_m);
+                    (p.kernel_hint != BH_CONV_STEM_VALU && p.kernel_hint != BH_CONV_STEM_SCALAR);
   return want && p.k_h == 3 && p.k_w == 3 && p.in_c == 3 && p.dil_w == 1 && p.k_pad == 64 && p.out_c % 16 == 0 &&
          p.out_c >= 16 && p.out_c <= 64 && !p.residual && !p.out_img_stride && (((uintptr_t)p.output) & 3) == 0;
 }

@@ -202,7 +202,7 @@ int bh_conv_group_i8(const bh_conv_group* g, bh_stream_t stream);
 #define BH_CONV_GEMM 2 /* conv_gemm_kernel: LDS-staged GEMM (1x1 s1, int8 in, symmetric filters) */
 #define BH_CONV_GEMM_BIG 3 /* conv_gemm_big_kernel: 256-row tiles on 32x32x32 MFMA (same layers, large M) */
 #define BH_CONV_STEM_VALU 4 /* RGB stems: conv_stem_kernel (VALU dot4) instead of conv_stem_mfma_kernel */
-#define BH_CONV_STEM_MFMA 5 /* RGB stems: conv_stem_mfma_kernel at any size (routed below 65536 output pixels) */
+#define BH_CONV_STEM_MFMA 5 /* RGB stems: conv_stem_mfma_kernel (the routed form wherever its shape rules allow) */
 #define BH_CONV_STEM_SCALAR 6 /* RGB stems: conv_stem_kernel with filters read through the scalar cache (round-4 form) */
 /* the tile configuration conv_gemm_big_kernel takes for an M x N layer when
  * routed automatically (1: 256x256, 2: 256x128; BH_GEMM_BIG_CFG overrides),

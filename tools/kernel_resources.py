@@ -9,7 +9,8 @@ Waves per SIMD allowed by registers follow MI355X_MICROARCH.md "Register
 files": alloc = ceil((VGPR + AGPR) / 8) * 8, min(8, 512 // alloc); by SGPRs:
 800 // (ceil(SGPR / 16) * 16 + 16) ("Residency and cooperative launch").
 
-usage: tools/kernel_resources.py band_amd/csrc/kernels/fused_chain.hip [more.hip] > out.txt
+usage: tools/kernel_resources.py [-DNAME=V ...] band_amd/csrc/kernels/fused_chain.hip [more.hip] > out.txt
+(the Makefile's -amdgpu-mfma-vgpr-form build; -D options are build-time A-B switches)
 """
 import os
 import re
@@ -30,9 +31,10 @@ def demangle(names):
         return names
 
 
-def resources(src):
+def resources(src, defines=()):
     with tempfile.TemporaryDirectory() as td:
         cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "-fPIC", "--offload-arch=gfx950", "--cuda-device-only",
+               "-mllvm", "-amdgpu-mfma-vgpr-form"] + list(defines) + [
                "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(CSRC, "kernels"),
                "-I" + os.path.join(CSRC, "compat"), "-I" + CSRC, "-Rpass-analysis=kernel-resource-usage",
                "-c", src, "-o", os.path.join(td, "k.o")]
@@ -64,8 +66,9 @@ def waves_per_simd(vgpr, agpr, sgpr):
 def main():
     print("%-6s %-5s %-5s %-5s %-7s %-7s %-4s %-5s %-5s  %s" % (
         "sgpr", "vgpr", "agpr", "lds", "scratch", "occ", "v/S", "s/S", "w/S", "kernel (demangled)"))
-    for src in sys.argv[1:]:
-        for r in resources(src):
+    defines = [a for a in sys.argv[1:] if a.startswith("-D")]
+    for src in (a for a in sys.argv[1:] if not a.startswith("-D")):
+        for r in resources(src, defines):
             bv, bs = waves_per_simd(r["vgpr"], r["agpr"], r["sgpr"])
             print("%-6d %-5d %-5d %-5d %-7d %-7d %-4d %-5d %-5d  %s" % (
                 r["sgpr"], r["vgpr"], r["agpr"], r["lds"], r["scratch"], r["occ"], bv, bs, min(bv, bs),

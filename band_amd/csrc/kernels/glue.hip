@@ -273,33 +273,48 @@ __global__ __launch_bounds__(256) void resize_bilinear_rows_kernel(bh_resize_bil
   }
 }
 
-// Column-blend row form for channels >= 16 (DeepLab's 21-class logits):
-// the two input rows are blended VERTICALLY once per workgroup into int32
-// V[xi][c] = r0[xi][c] (1 - fy) + r1[xi][c] fy (dynamic LDS, in_w * C
-// words), so each output byte is (V[x0][c] (1 - fx) + V[x1][c] fx), the same
-// exact integer sum as TFLite's four terms (|s| <= 2^29, no overflow).  With
-// C >= 16 a thread's 16 consecutive bytes span at most two output pixels:
-// their column entries are read once (not per byte) and each byte picks one
-// of the two with a select, so a byte costs 2 LDS reads and ~12 VALU instead
-// of 7 LDS reads and ~30 VALU (the row kernel above was VALU-bound).
+// TFLite's (s + (s > 0 ? 2^19 : -2^19)) / 2^20 (C division, toward zero)
+// for |s| < 2^30 as one arithmetic shift: s > 0 gives floor((s + 2^19) /
+// 2^20); s <= 0 gives trunc((s - 2^19) / 2^20) = floor((s + 2^19 - 1) / 2^20)
+__device__ __forceinline__ int32_t rz_round20(int32_t s) {
+  return (s + ((1 << 19) - 1) + (int32_t)((uint32_t)(-s) >> 31)) >> 20;
+}
+
+// Column-blend form for channels >= 16 (DeepLab's 21-class logits): the two
+// input rows of an output row are blended VERTICALLY once into int32
+// V[xi][c] = r0[xi][c] (1 - fy) + r1[xi][c] fy (dynamic LDS, in_w * C words
+// per row), so each output byte is (V[x0][c] (1 - fx) + V[x1][c] fx), the
+// same exact integer sum as TFLite's four terms (|s| <= 2^29, no overflow).
+// With C >= 16 a thread's 16 consecutive bytes span at most two output
+// pixels: their column entries are read once (not per byte) and each byte
+// picks one of the two with a select, so a byte costs 2 LDS reads and ~12
+// VALU instead of 7 LDS reads and ~30 VALU (the row kernel above was
+// VALU-bound).  A workgroup takes `nr` consecutive output rows of one image
+// (one row each: 7,168 workgroups of 4.7 KB output at DeepLab's batch 32,
+// each paying its own load round trip and a 15 %-occupied second pass).
 __global__ __launch_bounds__(256) void resize_bilinear_cols_kernel(bh_resize_bilinear_params p, FastDiv chans,
-                                                                   int vec_ok) {
+                                                                   int vec_ok, int nr, FastDiv groups,
+                                                                   FastDiv cpr_div) {
   extern __shared__ __attribute__((aligned(16))) int32_t rz_lds[];
-  const int y = blockIdx.x % p.out_h;
-  const int n = blockIdx.x / p.out_h;
+  const int n = groups.div(blockIdx.x);
+  const int y_first = (blockIdx.x - n * (int)groups.d) * nr;
+  const int rows = min(nr, p.out_h - y_first);
   const int C = p.channels;
   const int in_row = p.in_w * C;
-  int32_t* V = rz_lds;                // [in_row]
-  int32_t* X0 = rz_lds + in_row;      // [out_w]: x0 * C
-  int32_t* X1 = X0 + p.out_w;         // [out_w]: x1 * C
-  int32_t* FX = X1 + p.out_w;         // [out_w]: fx
+  int32_t* X0 = rz_lds;          // [out_w]: x0 * C
+  int32_t* X1 = X0 + p.out_w;    // [out_w]: x1 * C
+  int32_t* FX = X1 + p.out_w;    // [out_w]: fx
+  int32_t* V = FX + p.out_w;     // [rows][in_row]
   constexpr int32_t one = 1 << 10;
-  const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1], iy = p.y_tab[3 * y + 2];
-  const int32_t fy = iy - one * y0;
-  const int8_t* src0 = (const int8_t*)p.input + ((long)n * p.in_h + y0) * in_row;
-  const int8_t* src1 = (const int8_t*)p.input + ((long)n * p.in_h + y1) * in_row;
-  for (int i = threadIdx.x; i < in_row; i += 256)
-    V[i] = (int32_t)src0[i] * (one - fy) + (int32_t)src1[i] * fy;
+  for (int i = threadIdx.x; i < rows * in_row; i += 256) {
+    const int r = i / in_row;  // rows <= 8: a short division
+    const int k = i - r * in_row;
+    const int y = y_first + r;
+    const int y0 = p.y_tab[3 * y], y1 = p.y_tab[3 * y + 1];
+    const int32_t fy = p.y_tab[3 * y + 2] - one * y0;
+    const int8_t* in = (const int8_t*)p.input + (long)n * p.in_h * in_row;
+    V[i] = __mul24((int32_t)in[y0 * in_row + k], one - fy) + __mul24((int32_t)in[y1 * in_row + k], fy);
+  }
   for (int x = threadIdx.x; x < p.out_w; x += 256) {
     const int x0 = p.x_tab[3 * x];
     X0[x] = x0 * C;
@@ -308,13 +323,17 @@ __global__ __launch_bounds__(256) void resize_bilinear_cols_kernel(bh_resize_bil
   }
   __syncthreads();
   const int row_bytes = p.out_w * C;
-  int8_t* dst = (int8_t*)p.output + ((long)n * p.out_h + y) * row_bytes;
-  for (int f0 = threadIdx.x * 16; f0 < row_bytes; f0 += 256 * 16) {
+  const int cpr = (int)cpr_div.d;  // 16-byte chunks per output row
+  for (int i = threadIdx.x; i < rows * cpr; i += 256) {
+    const int r = (int)cpr_div.div((uint32_t)i);
+    const int f0 = (i - r * cpr) * 16;
+    const int32_t* Vr = V + r * in_row;
+    int8_t* dst = (int8_t*)p.output + ((long)n * p.out_h + y_first + r) * row_bytes;
     const int x = (int)chans.div((uint32_t)f0);
     const int ch0 = f0 - x * C;
     const int k = C - ch0;  // bytes b < k belong to pixel x, the rest to x + 1
     const int xn = x + 1 < p.out_w ? x + 1 : x;
-    // per-pixel bases with the byte index folded out: byte b reads V[base + b]
+    // per-pixel bases with the byte index folded out: byte b reads Vr[base + b]
     const int a0 = X0[x] + ch0, a1 = X1[x] + ch0, fa = FX[x];
     const int b0 = X0[xn] - k, b1 = X1[xn] - k, fb = FX[xn];
     uint32_t w[4] = {0u, 0u, 0u, 0u};
@@ -323,11 +342,11 @@ __global__ __launch_bounds__(256) void resize_bilinear_cols_kernel(bh_resize_bil
       const bool first = b < k;
       const int o0 = (first ? a0 : b0) + b, o1 = (first ? a1 : b1) + b;
       const int32_t fx = first ? fa : fb;
-      const int32_t v0 = V[o0], v1 = V[o1];
-      const int32_t s = v0 * (one - fx) + v1 * fx;
-      const int32_t rnd = s > 0 ? (1 << 19) : -(1 << 19);
-      const uint32_t v = (uint32_t)(uint8_t)(int8_t)((s + rnd) / (1 << 20));
-      w[b >> 2] |= v << (8 * (b & 3));
+      const int32_t v0 = Vr[o0], v1 = Vr[o1];
+      // |V| <= 2^17, fx <= 2^10: 24-bit multiplies (v_mul_i32_i24, full
+      // rate; v_mul_lo_u32 is quarter rate) are exact
+      const int32_t s = __mul24(v0, one - fx) + __mul24(v1, fx);
+      w[b >> 2] |= ((uint32_t)rz_round20(s) & 0xffu) << (8 * (b & 3));
     }
     if (vec_ok && f0 + 16 <= row_bytes) {
       *(v4i*)(dst + f0) = (v4i){(int)w[0], (int)w[1], (int)w[2], (int)w[3]};
@@ -552,8 +571,23 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
     const int vec_ok = ((p.out_w * p.channels) % 16 == 0 && ((uintptr_t)p.output & 15) == 0) ? 1 : 0;
     const size_t lds = ((size_t)p.in_w * p.channels + 3 * (size_t)p.out_w) * sizeof(int32_t);
     if (p.channels >= 16 && lds <= 64 * 1024) {
-      BH_LAUNCH(bh::resize_bilinear_cols_kernel, dim3(p.batch * p.out_h), dim3(256), lds, (hipStream_t)s, p,
-                bh::FastDiv(p.channels), vec_ok);
+      // output rows per workgroup: up to 8 while >= 1024 workgroups remain
+      // and the blended rows fit 48 KB (BH_RESIZE_ROWS overrides: A-B runs)
+      static const int force = [] {
+        const char* e = std::getenv("BH_RESIZE_ROWS");
+        return e ? std::atoi(e) : 0;
+      }();
+      const size_t row_lds = (size_t)p.in_w * p.channels * sizeof(int32_t);
+      int nr = 1;
+      while (nr < 8 && (long)p.batch * ((p.out_h + 2 * nr - 1) / (2 * nr)) >= 1024 &&
+             lds + (2 * nr - 1) * row_lds <= 48 * 1024)
+        nr *= 2;
+      if (force > 0) nr = std::min(force, 8);
+      const int groups = (p.out_h + nr - 1) / nr;
+      const size_t lds_nr = lds + (size_t)(nr - 1) * row_lds;
+      BH_LAUNCH(bh::resize_bilinear_cols_kernel, dim3(p.batch * groups), dim3(256), lds_nr, (hipStream_t)s, p,
+                bh::FastDiv(p.channels), vec_ok, nr, bh::FastDiv(groups),
+                bh::FastDiv((p.out_w * p.channels + 15) / 16));
       return bh_check_launch("resize_bilinear_cols_kernel");
     }
     BH_LAUNCH(bh::resize_bilinear_rows_kernel, dim3(p.batch * p.out_h), dim3(256), 0, (hipStream_t)s, p,

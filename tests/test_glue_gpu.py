@@ -127,21 +127,25 @@ def test_pad(gpu_lib, shape, pads, elem):
     np.testing.assert_array_equal(dy.download(x.dtype, ref.shape), ref)
 
 
-@pytest.mark.parametrize("ih,iw,oh,ow,c,ac,hp", [
-    (5, 5, 10, 10, 8, 0, 0), (10, 10, 20, 20, 3, 0, 1), (7, 9, 13, 4, 4, 1, 0), (6, 6, 3, 3, 5, 0, 1),
-    (14, 14, 224, 224, 21, 0, 0), (14, 14, 224, 224, 16, 1, 0), (3, 5, 37, 41, 7, 0, 1), (2, 515, 3, 1030, 1, 0, 0),
+# b >= 16 with tall outputs: the column-blend form's multi-row workgroups
+# (DeepLab's batch-32 upsample; 261 rows = 65 groups of 4 + one of 1, with a
+# 493-byte row that takes the byte-store tail)
+@pytest.mark.parametrize("ih,iw,oh,ow,c,ac,hp,b", [
+    (5, 5, 10, 10, 8, 0, 0, 2), (10, 10, 20, 20, 3, 0, 1, 2), (7, 9, 13, 4, 4, 1, 0, 2), (6, 6, 3, 3, 5, 0, 1, 2),
+    (14, 14, 224, 224, 21, 0, 0, 2), (14, 14, 224, 224, 16, 1, 0, 2), (3, 5, 37, 41, 7, 0, 1, 2),
+    (2, 515, 3, 1030, 1, 0, 0, 2), (14, 14, 224, 224, 21, 0, 0, 32), (5, 7, 261, 29, 17, 0, 1, 16),
 ])
-def test_resize(gpu_lib, ih, iw, oh, ow, c, ac, hp):
+def test_resize(gpu_lib, ih, iw, oh, ow, c, ac, hp, b):
     from band_amd import _abi
     from band_amd.device import DeviceBuffer
     rng = np.random.default_rng(ih * 100 + oh)
-    x = rand_q(rng, (2, ih, iw, c), np.int8)
+    x = rand_q(rng, (b, ih, iw, c), np.int8)
     # nearest: host-built index tables, as the executor builds them
     yi = np.array([orc.nearest_index(y, ih, oh, ac, hp) for y in range(oh)], np.int32)
     xi = np.array([orc.nearest_index(v, iw, ow, ac, hp) for v in range(ow)], np.int32)
     ref = orc.resize_nearest(x, (oh, ow), ac, hp)
     dx, dyi, dxi, dy = _dev(x), _dev(yi), _dev(xi), DeviceBuffer(ref.nbytes)
-    p = _abi.ResizeNearestParams(batch=2, in_h=ih, in_w=iw, out_h=oh, out_w=ow, row_bytes=c,
+    p = _abi.ResizeNearestParams(batch=b, in_h=ih, in_w=iw, out_h=oh, out_w=ow, row_bytes=c,
                                  y_index=dyi.value, x_index=dxi.value, input=dx.value, output=dy.value)
     _check(gpu_lib.bh_resize_nearest(ctypes.byref(p), None), "nearest")
     np.testing.assert_array_equal(dy.download(np.int8, ref.shape), ref)
@@ -160,7 +164,7 @@ def test_resize(gpu_lib, ih, iw, oh, ow, c, ac, hp):
             t += [lo, hi, sc]
         return np.array(t, np.int32)
     dty, dtx, dy2 = _dev(tab(ih, oh)), _dev(tab(iw, ow)), DeviceBuffer(ref.nbytes)
-    q = _abi.ResizeBilinearParams(batch=2, in_h=ih, in_w=iw, channels=c, out_h=oh, out_w=ow, y_tab=dty.value,
+    q = _abi.ResizeBilinearParams(batch=b, in_h=ih, in_w=iw, channels=c, out_h=oh, out_w=ow, y_tab=dty.value,
                                   x_tab=dtx.value, input=dx.value, output=dy2.value)
     _check(gpu_lib.bh_resize_bilinear_i8(ctypes.byref(q), None), "bilinear")
     np.testing.assert_array_equal(dy2.download(np.int8, ref.shape), ref)

@@ -572,17 +572,14 @@ extern "C" int bh_resize_bilinear_i8(const bh_resize_bilinear_params* pp, bh_str
     const size_t lds = ((size_t)p.in_w * p.channels + 3 * (size_t)p.out_w) * sizeof(int32_t);
     if (p.channels >= 16 && lds <= 64 * 1024) {
       // output rows per workgroup: up to 8 while >= 1024 workgroups remain
-      // and the blended rows fit 48 KB (BH_RESIZE_ROWS overrides: A-B runs)
-      static const int force = [] {
-        const char* e = std::getenv("BH_RESIZE_ROWS");
-        return e ? std::atoi(e) : 0;
-      }();
+      // and the blended rows fit 48 KB (4 at DeepLab's batch 24 / 32: 26.8
+      // us at batch 32 against 30.0 for one row, 28.3 for 2, 30.1 for 8,
+      // profiles/r06ah_resize_rows.txt)
       const size_t row_lds = (size_t)p.in_w * p.channels * sizeof(int32_t);
       int nr = 1;
       while (nr < 8 && (long)p.batch * ((p.out_h + 2 * nr - 1) / (2 * nr)) >= 1024 &&
              lds + (2 * nr - 1) * row_lds <= 48 * 1024)
         nr *= 2;
-      if (force > 0) nr = std::min(force, 8);
       const int groups = (p.out_h + nr - 1) / nr;
       const size_t lds_nr = lds + (size_t)(nr - 1) * row_lds;
       BH_LAUNCH(bh::resize_bilinear_cols_kernel, dim3(p.batch * groups), dim3(256), lds_nr, (hipStream_t)s, p,

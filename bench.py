@@ -35,7 +35,7 @@ pass time fits the target, so the slowest model of the mix (DeepLab, whose
 (8 GPU workers, no batching) is measured in the same run and reported as
 "band_one_job_per_pass"; "latency_point" is the same engine with smaller
 passes and fewer requests in flight (--latency-point, default job batch 24,
-500 us pass target, 200 in flight), the tail-latency side of the trade.
+450 us pass target, 200 in flight), the tail-latency side of the trade.
 
 N>1 (torchrun, one process per GPU): each rank serves its own job stream
 with its own engine over its GPU; jobs shard across GPUs with no data-path
@@ -118,7 +118,7 @@ def parse():
     p.add_argument("--pass-target-us", type=int, default=700,
                    help="pass-size policy of job batching (BANDX_WORKER_PASS_TARGET_US): a model's pass takes at "
                         "most the jobs whose expected pass time fits this many microseconds (0 = off)")
-    p.add_argument("--latency-point", default="24,500,200",
+    p.add_argument("--latency-point", default="24,450,200",
                    help="JOB_BATCH,PASS_TARGET_US,INFLIGHT of the latency_point line beside a job-batched N = 1 "
                         "headline (the same engine with smaller passes and fewer requests in flight); '' = skip")
     p.add_argument("--share-profiles", type=int, default=-1, choices=[-1, 0, 1],

@@ -251,3 +251,22 @@ def test_dw_tap_table_identity(dtype):
             if zw:
                 acc -= zw * int(xp[:, c].sum())
             assert acc == ref[c], (trial, c)
+
+
+# the conv launcher's routing is host logic (no device call): the RGB stem
+# takes the MFMA form at every batch (r06ag), the LDS-staged VALU form only
+# when forced (BH_CONV_STEM_VALU = 4) or outside the MFMA form's channel
+# range, the scalar-cache form above 64 channels per workgroup; pointers are
+# placeholders, never dereferenced
+@pytest.mark.parametrize("batch,oc,hint,want", [
+    (1, 32, 0, "conv_stem_mfma_kernel"), (32, 32, 0, "conv_stem_mfma_kernel"), (256, 32, 0, "conv_stem_mfma_kernel"),
+    (32, 64, 0, "conv_stem_mfma_kernel"), (32, 32, 4, "conv_stem_lds_kernel"), (32, 24, 0, "conv_stem_lds_kernel"),
+    (32, 80, 0, "conv_stem_kernel")])
+def test_stem_routing(batch, oc, hint, want):
+    import ctypes
+    lib = _abi.load()
+    p = _abi.ConvParams(batch=batch, in_h=224, in_w=224, in_c=3, out_h=112, out_w=112, out_c=oc, k_h=3, k_w=3,
+                        stride_h=2, stride_w=2, dil_h=1, dil_w=1, pad_h=0, pad_w=0, k_pad=64, n_pad=(oc + 63) // 64 * 64,
+                        kernel_hint=hint)
+    p.input, p.output, p.weights = 1 << 20, 2 << 20, 3 << 20
+    assert lib.bh_conv2d_i8_kernel(ctypes.byref(p)).decode() == want

@@ -93,6 +93,10 @@ def parse():
                    help="Band CPU workers (worker ids first); default: 1 when the model has CPU-only ops")
     p.add_argument("--cpu-threads", type=int, default=8, help="num_threads of each CPU worker")
     p.add_argument("--no-graph", action="store_true")
+    p.add_argument("--fresh-tuning", action="store_true",
+                   help="let the fusion tuner measure every choice in this process instead of replaying the "
+                        "committed profile set's decisions (profiles/<tag>_tune.tsv of the PMC traffic file that "
+                        "matches this kernel tree)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--sample-threads", action="store_true",
                    help="diagnostics: sample every thread's /proc state through the timed loop")
@@ -370,6 +374,44 @@ def kernel_source_tag():
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:12]
+
+
+def replay_tuning():
+    """The fusion tuner's decisions of the committed profile set whose PMC
+    traffic file matches this kernel tree (BAND_HIP_TUNE_FILE, copied to a
+    scratch file the tuner may append to): the headline then runs the chain
+    forms the traffic was measured on, so `roofline.traffic` describes the
+    same launches; otherwise close calls between forms flip from process to
+    process.  Returns the source file or None."""
+    if os.environ.get("BAND_HIP_TUNE_FILE"):
+        return None
+    tag = kernel_source_tag()
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json"))):
+        try:
+            with open(f) as fh:
+                meta = json.load(fh).get("_meta", {})
+        except (OSError, ValueError):
+            continue
+        # (.tsv: the committed copy travels to the GPU box, profiles/*.txt do not)
+        tunes = [f[:-len("_pmc_traffic.json")] + "_tune" + ext for ext in (".tsv", ".txt")]
+        tune = next((t for t in tunes if os.path.exists(t)), None)
+        if meta.get("kernel_source_tag") == tag and tune:
+            import shutil
+            import tempfile
+            fd, scratch = tempfile.mkstemp(prefix="band_tune_", suffix=".txt")
+            os.close(fd)
+            shutil.copyfile(tune, scratch)
+            os.environ["BAND_HIP_TUNE_FILE"] = scratch
+
+            def _drop(path=scratch):
+                try:
+                    os.unlink(path)
+                except OSError:
+                    pass
+            import atexit
+            atexit.register(_drop)
+            return os.path.relpath(tune, ROOT)
+    return None
 
 
 def profiled_batch(args):
@@ -817,6 +859,8 @@ def main():
     # running Band GPU worker stream (must be set before libband_hip loads)
     # (explicit assignment: the GPU box exports HIP's default of 4)
     os.environ["GPU_MAX_HW_QUEUES"] = str(max(1, min(32, args.hw_queues)))
+    # before libband_hip loads: the tuner reads the file at its first decision
+    tuning = None if args.fresh_tuning else replay_tuning()
     hinfo = host_info()  # before any GPU runtime is touched
     D = Dist()
     import band_amd
@@ -1064,7 +1108,9 @@ def main():
                        "parallelism": ("one engine, workers over %d GPUs" % max(1, args.gpus, n_ranks)) if one_engine
                        else "job-sharded x%d (no collective)" % n_ranks,
                        "hipgraph": not args.no_graph,
-                       "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))},
+                       "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+                       "fusion_tuning": ("decisions replayed from %s" % tuning) if tuning else
+                                        "measured in this process"},
             "p50_job_latency_ms": float(np.percentile(lat_ms, 50)) if lat_ms is not None else
             single["p50_job_latency_ms"],
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else

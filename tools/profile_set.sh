@@ -2,7 +2,10 @@
 # The profile set on an MI355X box (outputs in gpurun_out/<tag>_*;
 # rocprofv3's own directories stay in a scratch dir on the box):
 #   0. the default bench line, untraced; its measured kernel / fusion
-#      choices go to a tune file every later run replays;
+#      choices go to a tune file every later run replays (commit it as
+#      profiles/<tag>_tune.tsv beside the PMC traffic file: a default
+#      bench.py on the same kernel tree replays it, so its roofline traffic
+#      describes the same launches);
 #   1. the bench itself (direct ring I/O, 8 GPU workers) WITH its roofline
 #      stage under rocprofv3 --kernel-trace --stats, eager launches
 #      (--no-graph: rocprofv3 7.2 faults inside hipGraphLaunch after enough

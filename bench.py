@@ -834,6 +834,25 @@ def single_engine_line(args, D, paths, sched, W, n_gpus, n_warm, n_timed, names=
             "job_latency_ms_per_model": per_model}
 
 
+def latency_tail(lat_us, worker_ids, model_idx, names, ms=10.0):
+    """where an open-loop stream's slow jobs (> `ms`) fall: how many, per
+    model and worker, and how they cluster in arrival order (runs of slow
+    jobs at most 64 arrivals apart) - one tight cluster is a stall of the
+    whole engine, a spread is a scheduling effect"""
+    lat = np.asarray(lat_us) * 1e-3
+    slow = np.flatnonzero(lat > ms)
+    if slow.size == 0:
+        return {"threshold_ms": ms, "jobs": 0}
+    runs = np.split(slow, np.flatnonzero(np.diff(slow) > 64) + 1)
+    mid, wid = np.asarray(model_idx), np.asarray(worker_ids)
+    return {"threshold_ms": ms, "jobs": int(slow.size), "max_ms": round(float(lat.max()), 2),
+            "per_model": {names[int(m)] if int(m) < len(names) else str(int(m)): int(c)
+                          for m, c in zip(*np.unique(mid[slow], return_counts=True))},
+            "per_worker": {str(int(w)): int(c) for w, c in zip(*np.unique(wid[slow], return_counts=True))},
+            "clusters": [{"first_job": int(r[0]), "last_job": int(r[-1]), "jobs": int(r.size),
+                          "max_ms": round(float(lat[r].max()), 2)} for r in runs[:8]]}
+
+
 def per_model_latency(lat_us, names, n_models, model_idx):
     """rank 0's p50 / p99 job latency per model of the closed loop, keyed on
     the model index the driver reports for every job
@@ -946,8 +965,10 @@ def main():
             D.barrier()
             cg0 = cgroup_cpu_stat()
             t0 = time.perf_counter()
-            lat_us, worker_ids, _, _ = engine.RunPoisson(band_models, n_timed, rate, seed=poisson["seed"],
-                                                         max_inflight=1 << 20, inputs=inputs)
+            lat_us, worker_ids, poisson_mid, _ = engine.RunPoisson(band_models, n_timed, rate, seed=poisson["seed"],
+                                                                   max_inflight=1 << 20, inputs=inputs)
+            head_model_idx = [int(v) for v in poisson_mid]
+            poisson["tail"] = latency_tail(lat_us, worker_ids, poisson_mid, [m[0] for m in models])
             t1 = time.perf_counter()
             cg1 = cgroup_cpu_stat()
             if cg0 and cg1:  # CFS throttling inside the stream (a p99 tail's suspect)
@@ -1111,13 +1132,14 @@ def main():
                        "gpu_max_hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
                        "fusion_tuning": ("decisions replayed from %s" % tuning) if tuning else
                                         "measured in this process"},
+            "latency_tail": poisson.get("tail") if poisson else None,
             "p50_job_latency_ms": float(np.percentile(lat_ms, 50)) if lat_ms is not None else
             single["p50_job_latency_ms"],
             "p99_job_latency_ms": float(np.percentile(lat_ms, 99)) if lat_ms is not None else
             single["p99_job_latency_ms"],
             "job_latency_ms_per_model": single.get("job_latency_ms_per_model") if single and "value" in single else
             (per_model_latency(lat_us, [m[0] for m in models], M, head_model_idx)
-             if lat_us is not None and not poisson else None),
+             if lat_us is not None else None),
             "gpu_kernel_us_per_inference": dev["gpu_us_per_inference"] if dev else None,
             "gpu_kernel_us_per_inference_at_mean_pass": dev.get("gpu_us_per_inference_at_mean_pass") if dev else None,
             "device_us_per_inference": float(np.mean(list(dev["device_us"].values()))) if dev else None,
